@@ -1,0 +1,129 @@
+// fp32 MFMA tile machinery for gfx950 (CDNA4).
+//
+// All training math in this package is exact fp32 (the reference trains in
+// fp32, examples/mnist/mnist.py), so GEMM-shaped work runs on
+// v_mfma_f32_16x16x4_f32: 16x16 output tile per wave, K=4 per instruction,
+// 32-cycle issue / 40-cycle dependent latency -> every wave keeps two
+// independent accumulator chains so the matrix pipe never waits on itself.
+//
+// Operand lane maps (cdna_hip_programming.md §3):
+//   A: lane l holds A[i = l&15][k = l>>4]
+//   B: lane l holds B[k = l>>4][j = l&15]
+//   C/D: lane l, reg r -> row (l>>4)*4 + r, col l&15
+//
+// The K order inside a group of four MFMAs is free (a sum is a sum), so a
+// lane streams FOUR CONSECUTIVE k of its own row/col per group:
+//   MFMA j of a group uses k = k0 + 4*(l>>4) + j
+// which turns K-contiguous operands into one 16-byte load per lane per
+// group instead of four strided 4-byte loads.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define PTO_DEV __device__ __forceinline__
+
+PTO_DEV f32x4 mfma16x16x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+PTO_DEV f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// Operand layouts.  For A ("rows" = M): MK = a[m*ld + k] (K contiguous),
+// KM = a[k*ld + m].  For B ("rows" = N): NK = b[n*ld + k], KN = b[k*ld + n].
+enum { LAY_ROWK = 0, LAY_KROW = 1 };
+
+// Load the 4 consecutive-k operand values for one lane.  `row` is the
+// M index (A) or N index (B) this lane owns; rows >= R and k >= K read 0.
+template <int LAY>
+PTO_DEV void load4(const float* __restrict__ p, int ld, int row, int R, int k0, int K, float v[4]) {
+  if (row >= R) {
+    v[0] = v[1] = v[2] = v[3] = 0.f;
+    return;
+  }
+  if (LAY == LAY_ROWK) {
+    const float* q = p + (size_t)row * ld + k0;
+    if (k0 + 3 < K && ((ld & 3) == 0) && ((((uintptr_t)q) & 15) == 0)) {
+      const float4 t = *reinterpret_cast<const float4*>(q);
+      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (k0 + j < K) ? q[j] : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (k0 + j < K) ? p[(size_t)(k0 + j) * ld + row] : 0.f;
+  }
+}
+
+// One wave: 16x16 tile at (m0, n0) of C = A * B over k in [kb, ke).
+// kb must be a multiple of 4 (it is always a multiple of 16 here).
+template <int AL, int BL>
+PTO_DEV f32x4 wave_tile_16x16(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb,
+                              int M, int N, int K, int m0, int n0, int kb, int ke) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  f32x4 acc0 = zero4(), acc1 = zero4();
+  const int kend = ke < K ? ke : K;
+  for (int k = kb; k < kend; k += 16) {
+    float a[4], b[4];
+    load4<AL>(A, lda, m0 + r, M, k + 4 * g, kend, a);
+    load4<BL>(B, ldb, n0 + r, N, k + 4 * g, kend, b);
+    acc0 = mfma16x16x4(a[0], b[0], acc0);
+    acc1 = mfma16x16x4(a[1], b[1], acc1);
+    acc0 = mfma16x16x4(a[2], b[2], acc0);
+    acc1 = mfma16x16x4(a[3], b[3], acc1);
+  }
+  return acc0 + acc1;
+}
+
+// Block of 4 waves, each wave an independent 16x16 tile over the full K.
+// `vbid` is the virtual block id inside a multi-part launch.
+template <int AL, int BL, class Epi>
+PTO_DEV void block_gemm_4tiles(const float* A, int lda, const float* B, int ldb, int M, int N, int K, int vbid,
+                               Epi epi) {
+  const int mtiles = (M + 15) >> 4, ntiles = (N + 15) >> 4;
+  const int tile = vbid * 4 + (threadIdx.x >> 6);
+  if (tile >= mtiles * ntiles) return;
+  const int mt = tile % mtiles, nt = tile / mtiles;
+  f32x4 acc = wave_tile_16x16<AL, BL>(A, lda, B, ldb, M, N, K, mt * 16, nt * 16, 0, K);
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int m = mt * 16 + (lane >> 4) * 4 + rr, n = nt * 16 + (lane & 15);
+    if (m < M && n < N) epi(m, n, acc[rr]);
+  }
+}
+
+// Block of 4 waves cooperating on ONE 16x16 tile: K split four ways,
+// partial tiles reduced through LDS, epilogue by all 256 threads (one
+// output element each).  `red` is a 4*256-float LDS scratch.
+template <int AL, int BL, class Epi>
+PTO_DEV void block_gemm_splitk4(const float* A, int lda, const float* B, int ldb, int M, int N, int K, int vbid,
+                                float* red, Epi epi) {
+  const int mtiles = (M + 15) >> 4;
+  const int mt = vbid % mtiles, nt = vbid / mtiles;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int kc = (((K + 3) / 4) + 15) & ~15;
+  f32x4 acc = wave_tile_16x16<AL, BL>(A, lda, B, ldb, M, N, K, mt * 16, nt * 16, w * kc, (w + 1) * kc);
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) red[w * 256 + ((lane >> 4) * 4 + rr) * 16 + (lane & 15)] = acc[rr];
+  __syncthreads();
+  const int t = threadIdx.x;
+  const float v = red[t] + red[256 + t] + red[512 + t] + red[768 + t];
+  const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
+  if (m < M && n < N) epi(m, n, v);
+}
+
+PTO_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+PTO_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}

@@ -1,0 +1,110 @@
+"""Rendezvous / process-group helpers for one-process-per-GPU training.
+
+The operator injects the same env contract as the reference
+(``pkg/controller.v1/pytorch/pod.go:234-281``): ``MASTER_ADDR``,
+``MASTER_PORT``, ``WORLD_SIZE``, ``RANK``.  torchrun additionally provides
+``LOCAL_RANK``; the node agent provides ``LOCAL_RANK=0`` plus
+``HIP_VISIBLE_DEVICES`` pinning, so device selection always goes through
+``LOCAL_RANK``.
+
+Backend names: ``rccl`` is accepted as an alias of torch's ``nccl`` (which
+*is* RCCL on ROCm builds); ``gloo`` is kept for the CPU configuration.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+BACKEND_ALIASES = {"rccl": "nccl", "nccl": "nccl", "gloo": "gloo", "mpi": "mpi"}
+
+
+@dataclass
+class DistEnv:
+    rank: int
+    world_size: int
+    local_rank: int
+    master_addr: str
+    master_port: int
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1
+
+    @property
+    def is_master(self) -> bool:
+        return self.rank == 0
+
+
+def read_env() -> DistEnv:
+    return DistEnv(
+        rank=int(os.environ.get("RANK", "0")),
+        world_size=int(os.environ.get("WORLD_SIZE", "1")),
+        local_rank=int(os.environ.get("LOCAL_RANK", "0")),
+        master_addr=os.environ.get("MASTER_ADDR", "127.0.0.1"),
+        master_port=int(os.environ.get("MASTER_PORT", "23456")),
+    )
+
+
+def resolve_backend(name: str | None, use_gpu: bool) -> str:
+    if not name:
+        return "nccl" if use_gpu else "gloo"
+    try:
+        return BACKEND_ALIASES[name.lower()]
+    except KeyError as e:
+        raise ValueError(f"unknown backend {name!r}; choose from {sorted(BACKEND_ALIASES)}") from e
+
+
+def init_distributed(backend: str | None = None, use_gpu: bool | None = None,
+                     timeout_s: float = 300.0) -> tuple[DistEnv, torch.device]:
+    """Initialise the default process group from the env contract and pick
+    this rank's device.  Safe to call with ``WORLD_SIZE`` unset (single
+    process, no process group).
+
+    RCCL failures must surface as a retryable exit instead of a hang
+    (SURVEY §5.3), so async error handling is switched on and a finite
+    timeout is used.
+    """
+    env = read_env()
+    if use_gpu is None:
+        use_gpu = torch.cuda.is_available()
+    if use_gpu:
+        n = torch.cuda.device_count()
+        device = torch.device("cuda", env.local_rank % max(n, 1))
+        torch.cuda.set_device(device)
+    else:
+        device = torch.device("cpu")
+    if env.is_distributed and not dist.is_initialized():
+        be = resolve_backend(backend, use_gpu)
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        kwargs = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
+        if be == "nccl":
+            kwargs["device_id"] = device
+        dist.init_process_group(**kwargs)
+    return env, device
+
+
+def barrier(device: torch.device | None = None) -> None:
+    if dist.is_available() and dist.is_initialized():
+        if device is not None and device.type == "cuda" and dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[device.index])
+        else:
+            dist.barrier()
+
+
+def all_reduce_max(value: float, device: torch.device) -> float:
+    """MAX of a host scalar over ranks (bench reports the slowest rank)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return value
+    dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cleanup() -> None:
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
