@@ -1,0 +1,181 @@
+// Generic fp32 kernels shared by the fused trainer and the nn.Module path:
+//   * multi-tensor fused SGD (momentum, weight decay, nesterov, grad scale,
+//     grad zeroing) — one launch for every parameter tensor (K8+K10 of
+//     SURVEY §2.9, incl. the DDP 1/world scale of K9),
+//   * row-wise log_softmax forward/backward and fused cross-entropy
+//     (log_softmax + NLL, forward and dlogits in one pass) (K7).
+#include "mfma_f32.h"
+
+struct SgdTensor {
+  float* p;
+  float* g;
+  float* m;
+  long long n;
+};
+
+namespace {
+
+constexpr int SGD_CHUNK = 256 * 4;  // elements per block (one float4 per thread: max parallelism)
+
+// buf = momentum*buf + (gscale*g + wd*p);  p -= lr * (nesterov ? d + momentum*buf : buf);  g = 0
+// Matches torch.optim.SGD with dampening = 0 (torch's first step sets
+// buf = d, identical to momentum*0 + d with a zero-initialised buffer).
+PTO_DEV void sgd_elem(float& p, float& g, float& m, float lr, float mom, float wd, float gs, int nesterov) {
+  float d = g * gs;
+  if (wd != 0.f) d = fmaf(wd, p, d);
+  if (mom != 0.f) {
+    m = fmaf(mom, m, d);
+    d = nesterov ? fmaf(mom, m, d) : m;
+  }
+  p = fmaf(-lr, d, p);
+}
+
+__global__ __launch_bounds__(256) void k_sgd_multi(const SgdTensor* __restrict__ ts,
+                                                   const int* __restrict__ block_start, int ntensors,
+                                                   const float* __restrict__ lr_ptr, float lr, float mom, float wd,
+                                                   float gscale, int nesterov, int zero_grad,
+                                                   long long* __restrict__ bidx, long long nbatches) {
+  // The optimizer is the last launch of a training step: it also advances
+  // the device-side batch cursor read by the next step's kernels.
+  if (bidx && blockIdx.x == 0 && threadIdx.x == 0) *bidx = (*bidx + 1) % nbatches;
+  // locate the tensor of this block (ntensors is small; binary search)
+  int lo = 0, hi = ntensors - 1;
+  const int bid = blockIdx.x;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (block_start[mid] <= bid) lo = mid; else hi = mid - 1;
+  }
+  const SgdTensor t = ts[lo];
+  if (lr_ptr) lr = *lr_ptr;
+  const long long base = (long long)(bid - block_start[lo]) * SGD_CHUNK;
+  const bool vec = ((((uintptr_t)t.p) | ((uintptr_t)t.g) | ((uintptr_t)t.m)) & 15) == 0;
+  {
+    const long long i = base + (long long)threadIdx.x * 4;
+    if (i >= t.n) return;
+    if (vec && i + 3 < t.n) {
+      float4 p = *reinterpret_cast<float4*>(t.p + i);
+      float4 g = *reinterpret_cast<float4*>(t.g + i);
+      float4 m = t.m ? *reinterpret_cast<float4*>(t.m + i) : float4{0.f, 0.f, 0.f, 0.f};
+      sgd_elem(p.x, g.x, m.x, lr, mom, wd, gscale, nesterov);
+      sgd_elem(p.y, g.y, m.y, lr, mom, wd, gscale, nesterov);
+      sgd_elem(p.z, g.z, m.z, lr, mom, wd, gscale, nesterov);
+      sgd_elem(p.w, g.w, m.w, lr, mom, wd, gscale, nesterov);
+      *reinterpret_cast<float4*>(t.p + i) = p;
+      if (t.m) *reinterpret_cast<float4*>(t.m + i) = m;
+      if (zero_grad) *reinterpret_cast<float4*>(t.g + i) = float4{0.f, 0.f, 0.f, 0.f};
+    } else {
+      for (long long e = i; e < i + 4 && e < t.n; ++e) {
+        float m = t.m ? t.m[e] : 0.f;
+        float p = t.p[e], g = t.g[e];
+        sgd_elem(p, g, m, lr, mom, wd, gscale, nesterov);
+        t.p[e] = p;
+        if (t.m) t.m[e] = m;
+        if (zero_grad) t.g[e] = 0.f;
+      }
+    }
+  }
+}
+
+// One wave per row of x[R, C].  mode 0: log_softmax -> y.  mode 1: fused
+// cross-entropy: loss_rows[r] = lse - x[r, t[r]], dx = (softmax - onehot) *
+// gscale (so backward is a single scale of the saved dx).
+__global__ __launch_bounds__(256) void k_rowwise_softmax(const float* __restrict__ x, float* __restrict__ y,
+                                                         const int64_t* __restrict__ target,
+                                                         float* __restrict__ loss_rows, float* __restrict__ dx,
+                                                         int R, int C, float gscale, int mode) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= R) return;
+  const float* xr = x + (size_t)row * C;
+  float mx = -INFINITY;
+  for (int c = lane; c < C; c += 64) mx = fmaxf(mx, xr[c]);
+  mx = wave_max(mx);
+  float se = 0.f;
+  for (int c = lane; c < C; c += 64) se += __expf(xr[c] - mx);
+  se = wave_sum(se);
+  const float lse = mx + __logf(se);
+  if (mode == 0) {
+    for (int c = lane; c < C; c += 64) y[(size_t)row * C + c] = xr[c] - lse;
+    return;
+  }
+  const int t = (int)target[row];
+  if (lane == 0) loss_rows[row] = lse - xr[t];
+  if (dx)
+    for (int c = lane; c < C; c += 64)
+      dx[(size_t)row * C + c] = (__expf(xr[c] - lse) - (c == t ? 1.f : 0.f)) * gscale;
+}
+
+// log_softmax backward: dx = dy - exp(y) * sum(dy)
+__global__ __launch_bounds__(256) void k_log_softmax_bwd(const float* __restrict__ dy, const float* __restrict__ y,
+                                                         float* __restrict__ dx, int R, int C) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= R) return;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += dy[(size_t)row * C + c];
+  s = wave_sum(s);
+  for (int c = lane; c < C; c += 64) {
+    const size_t i = (size_t)row * C + c;
+    dx[i] = dy[i] - __expf(y[i]) * s;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_scale(float* __restrict__ x, const float* __restrict__ s, float c,
+                                               long long n) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) x[i] *= (s ? *s : 1.f) * c;
+}
+
+// sum of n floats into out[0] (block partials + atomics; out pre-zeroed)
+__global__ __launch_bounds__(256) void k_sum(const float* __restrict__ x, float* __restrict__ out, long long n,
+                                             float scale) {
+  float s = 0.f;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) s += x[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, s * scale);
+}
+
+}  // namespace
+
+#define PTO_API extern "C" __attribute__((visibility("default")))
+
+PTO_API int pto_sgd_block_count(long long n) { return (int)((n + SGD_CHUNK - 1) / SGD_CHUNK); }
+
+// ts / block_start live in device memory (prepared once by the caller and
+// reused every step, so the launch is graph-capturable).
+PTO_API int pto_sgd_multi(const SgdTensor* ts, const int* block_start, int ntensors, int nblocks,
+                          const float* lr_ptr, float lr, float mom, float wd, float gscale, int nesterov,
+                          int zero_grad, long long* bidx, long long nbatches, hipStream_t s) {
+  if (nblocks <= 0) return 0;
+  hipLaunchKernelGGL(k_sgd_multi, dim3(nblocks), dim3(256), 0, s, ts, block_start, ntensors, lr_ptr, lr, mom, wd,
+                     gscale, nesterov, zero_grad, bidx, nbatches);
+  return (int)hipGetLastError();
+}
+
+PTO_API int pto_log_softmax_fwd(const float* x, float* y, int R, int C, hipStream_t s) {
+  hipLaunchKernelGGL(k_rowwise_softmax, dim3((R + 3) / 4), dim3(256), 0, s, x, y, nullptr, nullptr, nullptr, R, C,
+                     1.f, 0);
+  return (int)hipGetLastError();
+}
+
+PTO_API int pto_log_softmax_bwd(const float* dy, const float* y, float* dx, int R, int C, hipStream_t s) {
+  hipLaunchKernelGGL(k_log_softmax_bwd, dim3((R + 3) / 4), dim3(256), 0, s, dy, y, dx, R, C);
+  return (int)hipGetLastError();
+}
+
+PTO_API int pto_cross_entropy_fwd(const float* x, const int64_t* target, float* loss_rows, float* dx, int R, int C,
+                                  float gscale, hipStream_t s) {
+  hipLaunchKernelGGL(k_rowwise_softmax, dim3((R + 3) / 4), dim3(256), 0, s, x, nullptr, target, loss_rows, dx, R, C,
+                     gscale, 1);
+  return (int)hipGetLastError();
+}
+
+PTO_API int pto_scale(float* x, const float* sptr, float c, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_scale, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, sptr, c, n);
+  return (int)hipGetLastError();
+}
+
+PTO_API int pto_sum(const float* x, float* out, long long n, float scale, hipStream_t s) {
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(k_sum, dim3(blocks), dim3(256), 0, s, x, out, n, scale);
+  return (int)hipGetLastError();
+}

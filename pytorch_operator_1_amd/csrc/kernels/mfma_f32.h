@@ -36,8 +36,17 @@ enum { LAY_ROWK = 0, LAY_KROW = 1 };
 
 // Load the 4 consecutive-k operand values for one lane.  `row` is the
 // M index (A) or N index (B) this lane owns; rows >= R and k >= K read 0.
-template <int LAY>
+// VEC (ROWK only): the caller guarantees ld % 4 == 0, K % 4 == 0 and a
+// 16-byte aligned base, so every group is one float4 load with no per-lane
+// alignment branch (a divergent branch there serialises the prefetch).
+template <int LAY, bool VEC = false>
 PTO_DEV void load4(const float* __restrict__ p, int ld, int row, int R, int k0, int K, float v[4]) {
+  if (LAY == LAY_ROWK && VEC) {
+    const bool ok = row < R && k0 < K;
+    const float4 t = *reinterpret_cast<const float4*>(p + (ok ? (size_t)row * ld + k0 : 0));
+    v[0] = ok ? t.x : 0.f; v[1] = ok ? t.y : 0.f; v[2] = ok ? t.z : 0.f; v[3] = ok ? t.w : 0.f;
+    return;
+  }
   if (row >= R) {
     v[0] = v[1] = v[2] = v[3] = 0.f;
     return;
@@ -59,35 +68,47 @@ PTO_DEV void load4(const float* __restrict__ p, int ld, int row, int R, int k0, 
 
 // One wave: 16x16 tile at (m0, n0) of C = A * B over k in [kb, ke).
 // kb must be a multiple of 4 (it is always a multiple of 16 here).
-template <int AL, int BL>
+//
+// These GEMMs are tiny and their operands were just written by the
+// previous kernel (often on another XCD), so every load is a ~1 us trip to
+// the Infinity Cache.  The loop therefore issues the operands of NG
+// 16-deep k-groups (NG*8 loads per lane) before the first MFMA: one memory
+// round trip per 16*NG of K instead of one per 16.
+template <int AL, int BL, int NG = 8, bool AV = false, bool BV = false>
 PTO_DEV f32x4 wave_tile_16x16(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb,
                               int M, int N, int K, int m0, int n0, int kb, int ke) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
   f32x4 acc0 = zero4(), acc1 = zero4();
   const int kend = ke < K ? ke : K;
-  for (int k = kb; k < kend; k += 16) {
-    float a[4], b[4];
-    load4<AL>(A, lda, m0 + r, M, k + 4 * g, kend, a);
-    load4<BL>(B, ldb, n0 + r, N, k + 4 * g, kend, b);
-    acc0 = mfma16x16x4(a[0], b[0], acc0);
-    acc1 = mfma16x16x4(a[1], b[1], acc1);
-    acc0 = mfma16x16x4(a[2], b[2], acc0);
-    acc1 = mfma16x16x4(a[3], b[3], acc1);
+  for (int k = kb; k < kend; k += 16 * NG) {
+    float a[NG][4], b[NG][4];
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      load4<AL, AV>(A, lda, m0 + r, M, k + 16 * q + 4 * g, kend, a[q]);
+      load4<BL, BV>(B, ldb, n0 + r, N, k + 16 * q + 4 * g, kend, b[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      acc0 = mfma16x16x4(a[q][0], b[q][0], acc0);
+      acc1 = mfma16x16x4(a[q][1], b[q][1], acc1);
+      acc0 = mfma16x16x4(a[q][2], b[q][2], acc0);
+      acc1 = mfma16x16x4(a[q][3], b[q][3], acc1);
+    }
   }
   return acc0 + acc1;
 }
 
 // Block of 4 waves, each wave an independent 16x16 tile over the full K.
 // `vbid` is the virtual block id inside a multi-part launch.
-template <int AL, int BL, class Epi>
+template <int AL, int BL, class Epi, int NG = 8>
 PTO_DEV void block_gemm_4tiles(const float* A, int lda, const float* B, int ldb, int M, int N, int K, int vbid,
                                Epi epi) {
   const int mtiles = (M + 15) >> 4, ntiles = (N + 15) >> 4;
   const int tile = vbid * 4 + (threadIdx.x >> 6);
   if (tile >= mtiles * ntiles) return;
   const int mt = tile % mtiles, nt = tile / mtiles;
-  f32x4 acc = wave_tile_16x16<AL, BL>(A, lda, B, ldb, M, N, K, mt * 16, nt * 16, 0, K);
+  f32x4 acc = wave_tile_16x16<AL, BL, NG>(A, lda, B, ldb, M, N, K, mt * 16, nt * 16, 0, K);
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
@@ -96,24 +117,58 @@ PTO_DEV void block_gemm_4tiles(const float* A, int lda, const float* B, int ldb,
   }
 }
 
-// Block of 4 waves cooperating on ONE 16x16 tile: K split four ways,
-// partial tiles reduced through LDS, epilogue by all 256 threads (one
-// output element each).  `red` is a 4*256-float LDS scratch.
-template <int AL, int BL, class Epi>
-PTO_DEV void block_gemm_splitk4(const float* A, int lda, const float* B, int ldb, int M, int N, int K, int vbid,
-                                float* red, Epi epi) {
+// Block of KS waves (blockDim = 64*KS) cooperating on ONE 16x16 tile: K
+// split KS ways, partial tiles reduced through LDS, epilogue by the first
+// 256 threads (one output element each).  `red` >= KS*256 floats.
+template <int AL, int BL, class Epi, int KS = 4, bool AV = false, bool BV = false>
+PTO_DEV void block_gemm_splitk(const float* A, int lda, const float* B, int ldb, int M, int N, int K, int vbid,
+                               float* red, Epi epi) {
   const int mtiles = (M + 15) >> 4;
   const int mt = vbid % mtiles, nt = vbid / mtiles;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int kc = (((K + 3) / 4) + 15) & ~15;
-  f32x4 acc = wave_tile_16x16<AL, BL>(A, lda, B, ldb, M, N, K, mt * 16, nt * 16, w * kc, (w + 1) * kc);
+  const int kc = (((K + KS - 1) / KS) + 15) & ~15;
+  f32x4 acc = wave_tile_16x16<AL, BL, 8, AV, BV>(A, lda, B, ldb, M, N, K, mt * 16, nt * 16, w * kc, (w + 1) * kc);
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) red[w * 256 + ((lane >> 4) * 4 + rr) * 16 + (lane & 15)] = acc[rr];
   __syncthreads();
   const int t = threadIdx.x;
-  const float v = red[t] + red[256 + t] + red[512 + t] + red[768 + t];
-  const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
-  if (m < M && n < N) epi(m, n, v);
+  if (t < 256) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < KS; ++q) v += red[q * 256 + t];
+    const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
+    if (m < M && n < N) epi(m, n, v);
+  }
+}
+
+template <int AL, int BL, class Epi>
+PTO_DEV void block_gemm_splitk4(const float* A, int lda, const float* B, int ldb, int M, int N, int K, int vbid,
+                                float* red, Epi epi) {
+  block_gemm_splitk<AL, BL, Epi, 4>(A, lda, B, ldb, M, N, K, vbid, red, epi);
+}
+
+// Column sums out[n] = sum_m x[m*ld + n] for 64 consecutive columns per
+// block of 256 threads: 4 row-groups x 64 columns, loads issued 16 rows at
+// a time, LDS combine.  `red` >= 256 floats.
+PTO_DEV void block_colsum64(const float* __restrict__ x, int ld, int M, int N, int col0, float* red,
+                            float* __restrict__ out, float scale = 1.f) {
+  const int t = threadIdx.x, c = col0 + (t & 63), rg = t >> 6;
+  float s = 0.f;
+  if (c < N) {
+    for (int m0 = rg; m0 < M; m0 += 64) {
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = m0 + 4 * q;
+        v[q] = m < M ? x[(size_t)m * ld + c] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s += v[q];
+    }
+  }
+  red[t] = s;
+  __syncthreads();
+  if (t < 64 && c < N) out[c] = (red[t] + red[t + 64] + red[t + 128] + red[t + 192]) * scale;
 }
 
 PTO_DEV float wave_sum(float v) {

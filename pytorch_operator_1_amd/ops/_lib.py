@@ -1,0 +1,149 @@
+"""Build and load the package's gfx950 HIP kernel library.
+
+All device code is compiled by ``hipcc --offload-arch=gfx950`` into ONE
+in-tree shared object, ``pytorch_operator_1_amd/_lib/libpto_hip.so``, that
+exposes a plain C ABI (``extern "C" pto_*`` launchers taking raw device
+pointers and a ``hipStream_t``).  It is loaded with ``ctypes`` — no torch
+C++ headers in the kernel build, so a rebuild takes seconds and the object
+works with any torch-ROCm of the same HIP major version.
+
+On a GPU box the library is REQUIRED: :func:`lib` raises if it cannot be
+built or loaded (no silent eager fallback).  On a CPU-only host it is only
+needed by the ``build()`` check.
+"""
+from __future__ import annotations
+
+import ctypes
+import glob
+import hashlib
+import os
+import shutil
+import subprocess
+import threading
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_DIR = os.path.join(PKG_DIR, "_lib")
+LIB_PATH = os.path.join(LIB_DIR, "libpto_hip.so")
+ARCH = os.environ.get("PTO_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+
+HIP_SOURCES = ("kernels/mnist_kernels.hip", "kernels/common_kernels.hip", "comm/xgmi_allreduce.hip")
+
+_lock = threading.Lock()
+_lib = None
+
+
+def _sources():
+    return [os.path.join(CSRC, s) for s in HIP_SOURCES if os.path.exists(os.path.join(CSRC, s))]
+
+
+def _digest() -> str:
+    h = hashlib.sha256()
+    h.update(ARCH.encode())
+    for p in sorted(_sources() + glob.glob(os.path.join(CSRC, "kernels", "*.h")) +
+                    glob.glob(os.path.join(CSRC, "comm", "*.h"))):
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile every HIP source for gfx950 into the in-tree library."""
+    os.makedirs(LIB_DIR, exist_ok=True)
+    stamp = LIB_PATH + ".stamp"
+    dig = _digest()
+    if not force and os.path.exists(LIB_PATH) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read().strip() == dig:
+                return LIB_PATH
+    tmp = LIB_PATH + f".tmp{os.getpid()}"
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-I", os.path.join(CSRC, "kernels"), "-o", tmp] + _sources()
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    with open(stamp, "w") as f:
+        f.write(dig)
+    return LIB_PATH
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_L = ctypes.c_longlong
+
+_SIGS = {
+    "pto_conv1_fwd": [_P, _P, _P, _P, _P, _I, _P, _P],
+    "pto_conv2_fwd": [_P, _P, _P, _P, _P, _I, _P],
+    "pto_linear_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
+    "pto_linear_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "pto_relu_bwd": [_P, _P, _P, _I, _P],
+    "pto_fc2_ce": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _P, _P],
+    "pto_fc_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P],
+    "pto_conv2_bwd": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _P],
+    "pto_conv1_bwd": [_P, _P, _P, _P, _P, _I, _P, _P],
+    "pto_conv1_bwd_data": [_P, _P, _P, _P, _I, _P],
+    "pto_eval_head": [_P, _P, _P, _I, _P],
+    "pto_sgd_block_count": [_L],
+    "pto_sgd_multi": [_P, _P, _I, _I, _P, _F, _F, _F, _F, _I, _I, _P, _L, _P],
+    "pto_log_softmax_fwd": [_P, _P, _I, _I, _P],
+    "pto_log_softmax_bwd": [_P, _P, _P, _I, _I, _P],
+    "pto_cross_entropy_fwd": [_P, _P, _P, _P, _I, _I, _F, _P],
+    "pto_scale": [_P, _P, _F, _L, _P],
+    "pto_sum": [_P, _P, _L, _F, _P],
+    # xGMI peer all-reduce (csrc/comm)
+    "pto_ar_ipc_handle_size": [],
+    "pto_ar_get_ipc_handle": [_P, _P],
+    "pto_ar_open_ipc_handle": [_P, ctypes.POINTER(ctypes.c_void_p)],
+    "pto_ar_close_ipc_handle": [_P],
+    "pto_ar_allreduce": [_P, _P, _L, _I, _I, _P, _P, _I, _F, _P],
+    "pto_ar_flag_bytes": [_I],
+}
+
+
+def lib():
+    """Return the loaded ctypes library, building it on first use."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        # build() is a no-op when the stamp matches the current sources, and
+        # recompiles a stale library (e.g. sources edited after a build).
+        try:
+            path = build(force=os.environ.get("PTO_REBUILD") == "1")
+        except (OSError, subprocess.CalledProcessError):
+            if not os.path.exists(LIB_PATH):
+                raise
+            path = LIB_PATH
+        L = ctypes.CDLL(path)
+        for name, args in _SIGS.items():
+            fn = getattr(L, name, None)
+            if fn is None:
+                continue
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        _lib = L
+        return _lib
+
+
+def loaded_path() -> str | None:
+    return LIB_PATH if _lib is not None else None
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with hipError {rc}")
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,183 @@
+"""Autograd wrappers over the gfx950 kernels (the ``nn.Module`` path).
+
+These give PyTorch-compatible ops for users who keep the reference's
+``model(x) -> F.nll_loss -> backward -> optimizer.step()`` loop
+(``examples/mnist/mnist.py:35-43``) but want the HIP kernels:
+
+* :func:`conv2d_bias_relu_maxpool` — fused conv(5x5, stride 1) + bias +
+  ReLU + 2x2 maxpool for the two MNIST conv shapes (1→20 @28², 20→50 @12²).
+* :func:`linear` — fp32 MFMA GEMM with fused bias (+ReLU).
+* :func:`log_softmax`, :func:`cross_entropy` — one wave per row.
+
+All ops require CUDA(HIP) fp32 contiguous tensors and raise on anything
+else: there is deliberately no silent fallback to stock kernels.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def _check(t, name):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name}: pytorch_operator_1_amd HIP ops need a HIP device tensor")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name}: fp32 only (got {t.dtype})")
+
+
+def _c(t):
+    return t.contiguous()
+
+
+class _ConvReluPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        _check(x, "conv2d_bias_relu_maxpool")
+        L, s = _lib.lib(), _lib.stream_ptr(x.device)
+        x, w, b = _c(x), _c(w), _c(b)
+        B = x.shape[0]
+        if tuple(w.shape) == (20, 1, 5, 5) and tuple(x.shape[1:]) == (1, 28, 28):
+            out = torch.empty(B, 20, 12, 12, device=x.device)
+            code = torch.empty(B, 20, 12, 12, device=x.device, dtype=torch.uint8)
+            _lib.check(L.pto_conv1_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), out.data_ptr(), code.data_ptr(), B,
+                                       None, s), "conv1_fwd")
+            ctx.kind = 1
+        elif tuple(w.shape) == (50, 20, 5, 5) and tuple(x.shape[1:]) == (20, 12, 12):
+            out = torch.empty(B, 50, 4, 4, device=x.device)
+            code = torch.empty(B, 50, 4, 4, device=x.device, dtype=torch.uint8)
+            _lib.check(L.pto_conv2_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), out.data_ptr(), code.data_ptr(), B,
+                                       s), "conv2_fwd")
+            ctx.kind = 2
+        else:
+            raise NotImplementedError(
+                f"conv2d_bias_relu_maxpool: kernel specialised for the MNIST shapes, got x{tuple(x.shape)} "
+                f"w{tuple(w.shape)}")
+        ctx.save_for_backward(x, w, code)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, w, code = ctx.saved_tensors
+        L, s = _lib.lib(), _lib.stream_ptr(x.device)
+        gout = _c(gout)
+        B = x.shape[0]
+        gw = torch.zeros_like(w)
+        gb = torch.zeros(w.shape[0], device=x.device)
+        gx = None
+        if ctx.kind == 2:
+            parts = 1 | 4
+            if ctx.needs_input_grad[0]:
+                gx = torch.empty_like(x)
+                parts |= 2
+            _lib.check(L.pto_conv2_bwd(gout.data_ptr(), code.data_ptr(), x.data_ptr(), w.data_ptr(), gw.data_ptr(),
+                                       gb.data_ptr(), None if gx is None else gx.data_ptr(), B, parts, s),
+                       "conv2_bwd")
+        else:
+            _lib.check(L.pto_conv1_bwd(gout.data_ptr(), code.data_ptr(), x.data_ptr(), gw.data_ptr(), gb.data_ptr(),
+                                       B, None, s), "conv1_bwd")
+            if ctx.needs_input_grad[0]:
+                gx = torch.empty_like(x)
+                _lib.check(L.pto_conv1_bwd_data(gout.data_ptr(), code.data_ptr(), w.data_ptr(), gx.data_ptr(), B, s),
+                           "conv1_bwd_data")
+        return gx, gw, gb
+
+
+def conv2d_bias_relu_maxpool(x, w, b):
+    return _ConvReluPool.apply(x, w, b)
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, relu):
+        _check(x, "linear")
+        L, s = _lib.lib(), _lib.stream_ptr(x.device)
+        x2 = _c(x.reshape(-1, x.shape[-1]))
+        w = _c(w)
+        M, K = x2.shape
+        N = w.shape[0]
+        y = torch.empty(M, N, device=x.device)
+        _lib.check(L.pto_linear_fwd(x2.data_ptr(), w.data_ptr(), None if b is None else _c(b).data_ptr(),
+                                    y.data_ptr(), M, N, K, int(relu), s), "linear_fwd")
+        ctx.relu = relu
+        ctx.has_bias = b is not None
+        ctx.in_shape = x.shape
+        ctx.save_for_backward(x2, w, y if relu else None)
+        return y.reshape(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w, y = ctx.saved_tensors
+        L, s = _lib.lib(), _lib.stream_ptr(x2.device)
+        M, K = x2.shape
+        N = w.shape[0]
+        g = _c(gy.reshape(M, N))
+        if ctx.relu:
+            gm = torch.empty_like(g)
+            _lib.check(L.pto_relu_bwd(g.data_ptr(), y.data_ptr(), gm.data_ptr(), g.numel(), s), "relu_bwd")
+            g = gm
+        gx = torch.empty(M, K, device=x2.device) if ctx.needs_input_grad[0] else None
+        gw = torch.empty(N, K, device=x2.device) if ctx.needs_input_grad[1] else None
+        gb = torch.empty(N, device=x2.device) if (ctx.has_bias and ctx.needs_input_grad[2]) else None
+        _lib.check(L.pto_linear_bwd(g.data_ptr(), x2.data_ptr(), w.data_ptr(), _lib.ptr(gx), _lib.ptr(gw),
+                                    _lib.ptr(gb), M, N, K, s), "linear_bwd")
+        if gx is not None:
+            gx = gx.reshape(ctx.in_shape)
+        return gx, gw, gb, None
+
+
+def linear(x, w, b=None, relu: bool = False):
+    return _Linear.apply(x, w, b, relu)
+
+
+class _LogSoftmax(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        _check(x, "log_softmax")
+        L, s = _lib.lib(), _lib.stream_ptr(x.device)
+        x2 = _c(x.reshape(-1, x.shape[-1]))
+        y = torch.empty_like(x2)
+        _lib.check(L.pto_log_softmax_fwd(x2.data_ptr(), y.data_ptr(), x2.shape[0], x2.shape[1], s), "log_softmax")
+        ctx.save_for_backward(y)
+        return y.reshape(x.shape)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (y,) = ctx.saved_tensors
+        L, s = _lib.lib(), _lib.stream_ptr(y.device)
+        g = _c(gy.reshape(y.shape))
+        gx = torch.empty_like(y)
+        _lib.check(L.pto_log_softmax_bwd(g.data_ptr(), y.data_ptr(), gx.data_ptr(), y.shape[0], y.shape[1], s),
+                   "log_softmax_bwd")
+        return gx.reshape(gy.shape)
+
+
+def log_softmax(x):
+    """log_softmax over the last dim."""
+    return _LogSoftmax.apply(x)
+
+
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target):
+        _check(logits, "cross_entropy")
+        L, s = _lib.lib(), _lib.stream_ptr(logits.device)
+        x = _c(logits)
+        R, C = x.shape
+        t = _c(target.to(torch.int64))
+        loss_rows = torch.empty(R, device=x.device)
+        dx = torch.empty_like(x) if logits.requires_grad else None
+        _lib.check(L.pto_cross_entropy_fwd(x.data_ptr(), t.data_ptr(), loss_rows.data_ptr(), _lib.ptr(dx), R, C,
+                                           1.0 / R, s), "cross_entropy")
+        ctx.save_for_backward(dx)
+        return loss_rows.mean()
+
+    @staticmethod
+    def backward(ctx, g):
+        (dx,) = ctx.saved_tensors
+        return dx * g, None
+
+
+def cross_entropy(logits, target):
+    """Fused log_softmax + mean NLL; dlogits computed in the forward pass."""
+    return _CrossEntropy.apply(logits, target)

@@ -1,0 +1,105 @@
+"""Fused multi-tensor SGD (momentum / weight decay / nesterov) on gfx950.
+
+One launch updates every parameter tensor: a device-resident table of
+``(param, grad, momentum, numel)`` records plus a block-prefix array lets
+each workgroup find its tensor with a binary search.  The table is built
+once and reused, so the launch is HIP-graph capturable.  The learning rate
+may live in device memory (``lr_dev``) so LR schedules keep working under
+graph replay.
+
+Semantics: ``torch.optim.SGD`` with ``dampening=0`` (the reference uses
+``SGD(lr, momentum)``, ``examples/mnist/mnist.py:140``), plus an optional
+gradient pre-scale (DDP 1/world) and gradient zeroing after the update
+(``zero_grad`` folded into the step).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+
+class _SgdTensor(ctypes.Structure):
+    _fields_ = [("p", ctypes.c_void_p), ("g", ctypes.c_void_p), ("m", ctypes.c_void_p), ("n", ctypes.c_longlong)]
+
+
+class SgdTable:
+    def __init__(self, triples, device):
+        L = _lib.lib()
+        self.L = L
+        recs, starts, nb = [], [], 0
+        self._keep = []
+        for p, g, m in triples:
+            assert p.dtype == torch.float32 and p.is_contiguous() and g.is_contiguous()
+            recs.append((p.data_ptr(), g.data_ptr(), 0 if m is None else m.data_ptr(), p.numel()))
+            starts.append(nb)
+            nb += L.pto_sgd_block_count(p.numel())
+            self._keep.append((p, g, m))
+        self.nblocks = nb
+        self.ntensors = len(recs)
+        raw = (_SgdTensor * len(recs))(*[_SgdTensor(*r) for r in recs])
+        host = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(raw), ctypes.sizeof(raw))),
+                                dtype=torch.uint8)
+        self.table = host.to(device)
+        self.starts = torch.tensor(starts, dtype=torch.int32, device=device)
+
+    def step(self, lr_dev, lr, momentum, weight_decay, grad_scale, nesterov, zero_grad=True, stream=None,
+             batch_cursor=None, n_batches=1):
+        """``batch_cursor``: optional int64 device scalar advanced modulo
+        ``n_batches`` by the same launch (fused trainer data cursor)."""
+        s = stream if stream is not None else _lib.stream_ptr()
+        _lib.check(self.L.pto_sgd_multi(self.table.data_ptr(), self.starts.data_ptr(), self.ntensors, self.nblocks,
+                                        None if lr_dev is None else lr_dev.data_ptr(), float(lr), float(momentum),
+                                        float(weight_decay), float(grad_scale), int(bool(nesterov)),
+                                        int(bool(zero_grad)), _lib.ptr(batch_cursor), int(n_batches), s),
+                   "sgd_multi")
+
+
+class FusedSGD(torch.optim.Optimizer):
+    """Drop-in ``torch.optim.SGD`` (dampening=0) backed by one HIP launch.
+
+    Grads are consumed and zeroed in the same launch when ``zero_grad=True``
+    is passed to :meth:`step` (set_to_none semantics are emulated by zeros).
+    """
+
+    def __init__(self, params, lr=0.01, momentum=0.0, weight_decay=0.0, nesterov=False):
+        if nesterov and momentum <= 0:
+            raise ValueError("Nesterov momentum requires a momentum")
+        super().__init__(params, dict(lr=lr, momentum=momentum, weight_decay=weight_decay, nesterov=nesterov))
+        self._tables = None
+
+    def _build(self):
+        self._tables = []
+        for group in self.param_groups:
+            triples = []
+            for p in group["params"]:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+                st = self.state[p]
+                if group["momentum"] != 0 and "momentum_buffer" not in st:
+                    st["momentum_buffer"] = torch.zeros_like(p)
+                triples.append((p.data, p.grad, st.get("momentum_buffer")))
+            dev = group["params"][0].device
+            self._tables.append(SgdTable(triples, dev))
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_scale: float = 1.0, zero_grad: bool = False):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        if self._tables is None or any(p.grad is None for g in self.param_groups for p in g["params"]):
+            self._build()
+        for group, table in zip(self.param_groups, self._tables):
+            table.step(None, group["lr"], group["momentum"], group["weight_decay"], grad_scale, group["nesterov"],
+                       zero_grad=zero_grad)
+        return loss
+
+    def zero_grad(self, set_to_none: bool = False):
+        # keep grad tensors alive: the launch table holds their pointers
+        for g in self.param_groups:
+            for p in g["params"]:
+                if p.grad is not None:
+                    p.grad.zero_()

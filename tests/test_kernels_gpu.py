@@ -1,0 +1,179 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of
+the same op (MI355X only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _lib_loaded():
+    from pytorch_operator_1_amd.ops import _lib
+
+    _lib.lib()
+    assert _lib.loaded_path() is not None
+
+
+def rel_err(a, b):
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+def test_library_is_native():
+    _lib_loaded()
+    import os
+
+    from pytorch_operator_1_amd.ops import _lib
+
+    maps = open(f"/proc/{os.getpid()}/maps").read()
+    assert os.path.basename(_lib.LIB_PATH) in maps
+
+
+@pytest.mark.parametrize("B", [64, 7, 100])
+def test_conv1_relu_pool(B):
+    from pytorch_operator_1_amd import ops
+
+    torch.manual_seed(0)
+    x = torch.randn(B, 1, 28, 28, device=DEV, requires_grad=True)
+    w = (torch.randn(20, 1, 5, 5, device=DEV) * 0.2).requires_grad_()
+    b = (torch.randn(20, device=DEV) * 0.1).requires_grad_()
+    y = ops.conv2d_bias_relu_maxpool(x, w, b)
+    yr = F.max_pool2d(F.relu(F.conv2d(x, w, b)), 2, 2)
+    assert rel_err(y, yr) < 1e-5
+    g = torch.randn_like(y)
+    gx, gw, gb = torch.autograd.grad(y, (x, w, b), g)
+    gxr, gwr, gbr = torch.autograd.grad(yr, (x, w, b), g)
+    assert rel_err(gw, gwr) < 1e-4
+    assert rel_err(gb, gbr) < 1e-4
+    assert rel_err(gx, gxr) < 1e-4
+
+
+@pytest.mark.parametrize("B", [64, 5])
+def test_conv2_relu_pool(B):
+    from pytorch_operator_1_amd import ops
+
+    torch.manual_seed(1)
+    x = torch.relu(torch.randn(B, 20, 12, 12, device=DEV)).requires_grad_()
+    w = (torch.randn(50, 20, 5, 5, device=DEV) * 0.05).requires_grad_()
+    b = (torch.randn(50, device=DEV) * 0.1).requires_grad_()
+    y = ops.conv2d_bias_relu_maxpool(x, w, b)
+    yr = F.max_pool2d(F.relu(F.conv2d(x, w, b)), 2, 2)
+    assert rel_err(y, yr) < 1e-5
+    g = torch.randn_like(y)
+    gx, gw, gb = torch.autograd.grad(y, (x, w, b), g)
+    gxr, gwr, gbr = torch.autograd.grad(yr, (x, w, b), g)
+    assert rel_err(gw, gwr) < 1e-4
+    assert rel_err(gb, gbr) < 1e-4
+    assert rel_err(gx, gxr) < 1e-4
+
+
+@pytest.mark.parametrize("M,N,K,relu", [(64, 500, 800, True), (64, 10, 500, False), (33, 70, 129, True),
+                                        (1, 16, 4, False)])
+def test_linear(M, N, K, relu):
+    from pytorch_operator_1_amd import ops
+
+    torch.manual_seed(2)
+    x = torch.randn(M, K, device=DEV, requires_grad=True)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).requires_grad_()
+    b = torch.randn(N, device=DEV, requires_grad=True)
+    y = ops.linear(x, w, b, relu=relu)
+    yr = F.linear(x, w, b)
+    if relu:
+        yr = F.relu(yr)
+    assert rel_err(y, yr) < 1e-5
+    g = torch.randn_like(y)
+    gs = torch.autograd.grad(y, (x, w, b), g)
+    grs = torch.autograd.grad(yr, (x, w, b), g)
+    for a, r in zip(gs, grs):
+        assert rel_err(a, r) < 1e-5
+
+
+def test_log_softmax_and_ce():
+    from pytorch_operator_1_amd import ops
+
+    torch.manual_seed(3)
+    x = torch.randn(64, 10, device=DEV, requires_grad=True)
+    t = torch.randint(0, 10, (64,), device=DEV)
+    y = ops.log_softmax(x)
+    yr = F.log_softmax(x, dim=1)
+    assert rel_err(y, yr) < 1e-6
+    g = torch.randn_like(y)
+    assert rel_err(torch.autograd.grad(y, x, g)[0], torch.autograd.grad(yr, x, g)[0]) < 1e-5
+    l = ops.cross_entropy(x, t)
+    lr_ = F.cross_entropy(x, t)
+    assert abs(l.item() - lr_.item()) < 1e-5
+    assert rel_err(torch.autograd.grad(l, x)[0], torch.autograd.grad(lr_, x)[0]) < 1e-5
+
+
+def test_fused_sgd_matches_torch():
+    from pytorch_operator_1_amd.ops import FusedSGD
+
+    torch.manual_seed(4)
+    ps = [torch.randn(s, device=DEV, requires_grad=True) for s in [(7,), (1000, 3), (5001,)]]
+    qs = [p.detach().clone().requires_grad_() for p in ps]
+    o1 = FusedSGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-3, nesterov=True)
+    o2 = torch.optim.SGD(qs, lr=0.1, momentum=0.9, weight_decay=1e-3, nesterov=True)
+    for _ in range(3):
+        gs = [torch.randn_like(p) for p in ps]
+        for p, q, g in zip(ps, qs, gs):
+            if p.grad is None:
+                p.grad = g.clone()
+            else:
+                p.grad.copy_(g)
+            q.grad = g.clone()
+        o1.step()
+        o2.step()
+    for p, q in zip(ps, qs):
+        assert rel_err(p.detach(), q.detach()) < 1e-6
+
+
+def test_mnist_module_hip_matches_torch():
+    from pytorch_operator_1_amd.models.mnist import MnistNet
+
+    torch.manual_seed(5)
+    m1 = MnistNet(impl="hip").to(DEV)
+    m2 = MnistNet(impl="torch").to(DEV)
+    m2.load_state_dict(m1.state_dict())
+    x = torch.randn(64, 1, 28, 28, device=DEV)
+    t = torch.randint(0, 10, (64,), device=DEV)
+    l1 = F.nll_loss(m1(x), t)
+    l2 = F.nll_loss(m2(x), t)
+    assert abs(l1.item() - l2.item()) < 1e-5
+    l1.backward()
+    l2.backward()
+    for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert rel_err(p1.grad, p2.grad) < 1e-4, n
+
+
+@pytest.mark.parametrize("graph", ["none", "full"])
+def test_fused_trainer_matches_eager(graph):
+    """Fused step == stock PyTorch step (same init, same batches) over 5
+    SGD-momentum steps."""
+    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+    from pytorch_operator_1_amd.train.runner import EagerMnistTrainer
+
+    dev = torch.device(DEV)
+    fused = FusedMnistTrainer(dev, batch_size=64, dataset_size=640, seed=1, graph=graph)
+    eager = EagerMnistTrainer(dev, batch_size=64, dataset_size=640, seed=1)
+    for name, t in eager.model.state_dict().items():
+        assert torch.equal(fused.p[name], t), name
+    for _ in range(5):
+        fused.step()
+        eager.step()
+    torch.cuda.synchronize()
+    assert abs(fused.last_loss() - eager.last_loss()) < 1e-4
+    for name, t in eager.model.state_dict().items():
+        assert rel_err(fused.p[name], t) < 1e-4, name
+
+
+def test_fused_trainer_converges():
+    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+
+    tr = FusedMnistTrainer(torch.device(DEV), batch_size=64, dataset_size=6400, seed=3)
+    first = None
+    for i in range(300):
+        tr.step()
+        if i == 0:
+            first = tr.last_loss()
+    assert tr.last_loss() < 0.5 * first
