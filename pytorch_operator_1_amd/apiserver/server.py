@@ -72,7 +72,7 @@ class ApiServer:
         self.host, self.port = host, port
         self.token = token
         self.app = web.Application(middlewares=[self._errors])
-        self.app.router.add_get("/healthz", lambda r: web.Response(text="ok"))
+        self.app.router.add_get("/healthz", self._healthz)
         self.app.router.add_get("/version", self._version)
         self.app.router.add_route("*", "/{tail:.*}", self._dispatch)
         self._runner = None
@@ -91,6 +91,9 @@ class ApiServer:
             return _json(e.status(), e.code)
         except json.JSONDecodeError as e:
             return _json(ApiError(400, "BadRequest", f"invalid JSON body: {e}").status(), 400)
+
+    async def _healthz(self, request):
+        return web.Response(text="ok")
 
     async def _version(self, request):
         from .. import __version__
