@@ -105,7 +105,7 @@ class RateLimitingQueue:
             if item in self._processing:
                 return
             self._queue.append(item)
-            self._cond.notify()
+            self._cond.notify_all()  # the delay thread waits on the same condition
 
     def __len__(self):
         with self._cond:
@@ -132,7 +132,7 @@ class RateLimitingQueue:
             self._processing.discard(item)
             if item in self._dirty:
                 self._queue.append(item)
-                self._cond.notify()
+                self._cond.notify_all()  # the delay thread waits on the same condition
 
     def shutdown(self):
         with self._cond:

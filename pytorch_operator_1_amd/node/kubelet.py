@@ -1,0 +1,491 @@
+"""Node manager: turns Pod objects into supervised processes on the
+MI355X node (the kubelet + device plugin + cluster DNS of the reference's
+substrate), using the native agent for process control.
+
+Per pod:
+  1. admission — ``amd.com/gpu`` allocation by the agent's exclusive
+     allocator; with gang scheduling (``scheduling.k8s.io/group-name``
+     annotation + PodGroup ``minMember``) all members are admitted at once
+     or none (kube-batch semantics, C30); unschedulable pods stay Pending
+     with ``PodScheduled=False/Unschedulable``.
+  2. init containers — the reference's ``init-pytorch`` DNS wait
+     (``until nslookup <job>-master-0``) runs natively: wait until the
+     master Service exists (and, on request, its port accepts
+     connections); other init containers run as processes.
+  3. containers — spawned through the agent with kubelet restart semantics;
+     env = container env + ``HIP_VISIBLE_DEVICES`` (GPU pinning),
+     ``LOCAL_RANK=0``; Service names in ``MASTER_ADDR`` resolve to the node
+     address (single-node "DNS"), and ``MASTER_PORT`` is virtualised per job
+     so concurrent jobs can all ask for 23456 (pods share the host network).
+  4. status — phase, containerStatuses (state, restartCount, exitCode),
+     podIP/hostIP, written back through the status subresource.
+  5. deletion — SIGTERM the process group, SIGKILL after the grace period,
+     free the GPUs.
+"""
+from __future__ import annotations
+
+import copy
+import json
+import logging
+import os
+import re
+import shlex
+import socket
+import sys
+import threading
+import time
+
+from ..api import constants as C
+from ..api.types import key_of, name_of, namespace_of, now_rfc3339
+from ..api.validation import gpus_requested
+from ..apiserver.server import LOG_ANNOTATION
+from ..apiserver.store import ApiError
+from ..controller.informer import Informer
+from .native import AgentClient
+
+log = logging.getLogger("pto-kubelet")
+
+REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+# "container images" -> entrypoints in the node's Python environment.  The
+# reference images are mapped onto this package's runtimes.
+DEFAULT_IMAGES = {
+    "pto/pytorch-mnist:rocm": [sys.executable, "-m", "pytorch_operator_1_amd.train.mnist"],
+    "gcr.io/kubeflow-ci/pytorch-dist-mnist-test:v1.0": [sys.executable, "-m", "pytorch_operator_1_amd.train.mnist"],
+    "pto/pytorch-sendrecv:rocm": [sys.executable, "-m", "pytorch_operator_1_amd.train.sendrecv"],
+    "gcr.io/kubeflow-ci/pytorch-dist-sendrecv-test:1.0": [sys.executable, "-m",
+                                                          "pytorch_operator_1_amd.train.sendrecv"],
+    "pto/bench:rocm": [sys.executable, os.path.join(REPO_ROOT, "bench.py")],
+    "pto/python:rocm": [sys.executable],
+}
+FIRST_STEP_ANNOTATION = "pto.amd.com/first-step-unix"
+THROUGHPUT_ANNOTATION = "pto.amd.com/samples-per-sec"
+GPUS_ANNOTATION = "pto.amd.com/gpus"
+NODE_ADDRESS = "127.0.0.1"
+
+
+def _port_free(port: int) -> bool:
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    try:
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        s.bind(("0.0.0.0", port))
+        return True
+    except OSError:
+        return False
+    finally:
+        s.close()
+
+
+class PodRuntime:
+    def __init__(self, pod):
+        self.key = key_of(pod)
+        self.uid = pod["metadata"].get("uid")
+        self.stage = "admit"  # admit -> init -> run -> done
+        self.gpus: list[int] = []
+        self.init_index = 0
+        self.started_at = None
+        self.proc_ids: list[str] = []
+        self.deleted = False
+        self.last_status = None
+        self.metrics_pos = 0
+        self.annotated_first_step = False
+
+
+class Kubelet:
+    def __init__(self, client, agent: AgentClient | None = None, node_name: str = "mi355x-0",
+                 log_dir: str | None = None, images: dict | None = None, gpus: int | None = None,
+                 poll_interval: float = 0.05, grace_seconds: float = 5.0, extra_env: dict | None = None,
+                 hbm_per_gpu: float = C.HBM_PER_GPU_BYTES):
+        self.client = client
+        self.agent = agent or AgentClient(gpus=gpus, hbm_per_gpu=hbm_per_gpu)
+        self.node_name = node_name
+        self.log_dir = log_dir or os.path.join(os.environ.get("TMPDIR", "/tmp"), "pto-pods")
+        os.makedirs(self.log_dir, exist_ok=True)
+        self.images = dict(DEFAULT_IMAGES, **(images or {}))
+        self.poll = poll_interval
+        self.grace = grace_seconds
+        self.extra_env = extra_env or {}
+        self.pods: dict[str, PodRuntime] = {}
+        self.job_ports: dict[str, int] = {}
+        self.pod_informer = Informer(client, "pods")
+        self.svc_informer = Informer(client, "services")
+        self.pod_informer.add_event_handler(on_delete=self._on_pod_delete)
+        self._stop = threading.Event()
+        self._thread = None
+        self._lock = threading.RLock()
+
+    # ------------------------------------------------------------ lifecycle
+    def start(self):
+        self.pod_informer.start()
+        self.svc_informer.start()
+        self.pod_informer.wait_for_sync(10)
+        self.svc_informer.wait_for_sync(10)
+        self._register_node()
+        self._thread = threading.Thread(target=self._loop, name="pto-kubelet", daemon=True)
+        self._thread.start()
+        return self
+
+    def stop(self, kill_pods: bool = True):
+        self._stop.set()
+        if self._thread:
+            self._thread.join(5)
+        if kill_pods:
+            for rt in list(self.pods.values()):
+                for pid in rt.proc_ids:
+                    self.agent.kill(pid, signal=9)
+        self.pod_informer.stop()
+        self.svc_informer.stop()
+        self.agent.close()
+
+    def _register_node(self):
+        n = self.agent.gpus()["count"]
+        node = {"metadata": {"name": self.node_name, "labels": {"kubernetes.io/hostname": self.node_name,
+                                                                 "amd.com/gpu.product": "MI355X"}},
+                "status": {"capacity": {C.GPU_RESOURCE: n, "cpu": os.cpu_count()},
+                           "allocatable": {C.GPU_RESOURCE: n, "cpu": os.cpu_count()},
+                           "addresses": [{"type": "InternalIP", "address": NODE_ADDRESS}]}}
+        try:
+            self.client.create("nodes", node)
+        except ApiError:
+            pass
+
+    def _loop(self):
+        while not self._stop.is_set():
+            try:
+                self.sync_once()
+            except Exception:
+                log.exception("kubelet sync failed")
+            self._stop.wait(self.poll)
+
+    # ------------------------------------------------------------ sync
+    def sync_once(self):
+        pods = self.pod_informer.list()
+        procs = self.agent.status()
+        with self._lock:
+            for pod in pods:
+                k = key_of(pod)
+                rt = self.pods.get(k)
+                if rt is None or rt.uid != pod["metadata"].get("uid"):
+                    if rt is not None:  # same name, new incarnation
+                        self._teardown(rt)
+                    if (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
+                        continue  # finished before we knew it (e.g. kubelet restart)
+                    rt = self.pods[k] = PodRuntime(pod)
+                self._advance(pod, rt, procs)
+            live = {key_of(p) for p in pods}
+            for k in [k for k in self.pods if k not in live]:
+                self._teardown(self.pods.pop(k))
+
+    def _on_pod_delete(self, pod):
+        with self._lock:
+            rt = self.pods.pop(key_of(pod), None)
+            if rt is not None:
+                self._teardown(rt)
+
+    def _teardown(self, rt: PodRuntime):
+        for pid in rt.proc_ids:
+            try:
+                self.agent.kill(pid, signal=15, grace=self.grace)
+            except Exception:
+                pass
+        threading.Thread(target=self._reap_later, args=(list(rt.proc_ids), rt.key), daemon=True).start()
+        rt.deleted = True
+
+    def _reap_later(self, ids, owner):
+        try:
+            end = time.time() + self.grace + 5
+            while time.time() < end and not self._stop.is_set():
+                st = self.agent.status()
+                if all(st.get(i, {}).get("state") != "running" for i in ids):
+                    break
+                time.sleep(0.1)
+            for i in ids:
+                self.agent.remove(i)
+            self.agent.free(owner)
+        except Exception:  # agent already shut down (node stopping)
+            pass
+
+    # ------------------------------------------------------------ stages
+    def _advance(self, pod, rt: PodRuntime, procs):
+        if rt.stage == "done":
+            return
+        if rt.stage == "admit":
+            if not self._admit(pod, rt):
+                return
+            rt.stage = "init"
+            rt.started_at = now_rfc3339()
+            self._annotate(pod, {LOG_ANNOTATION: self._log_path(pod), GPUS_ANNOTATION:
+                                 ",".join(map(str, rt.gpus))})
+        if rt.stage == "init":
+            if not self._run_init(pod, rt, procs):
+                return
+            self._start_containers(pod, rt)
+            rt.stage = "run"
+            procs = self.agent.status()
+        if rt.stage == "run":
+            self._report(pod, rt, procs)
+
+    def _admit(self, pod, rt) -> bool:
+        n = sum(gpus_requested(c) for c in pod.get("spec", {}).get("containers") or [])
+        ann = pod["metadata"].get("annotations") or {}
+        group = ann.get(C.ANNOTATION_GANG_GROUP)
+        if n == 0 and not group:
+            return True
+        requests = [{"owner": rt.key, "count": n}]
+        if group:
+            members = [p for p in self.pod_informer.list(namespace_of(pod))
+                       if (p["metadata"].get("annotations") or {}).get(C.ANNOTATION_GANG_GROUP) == group]
+            try:
+                pg = self.client.get("podgroups", namespace_of(pod), group)
+                min_member = int(pg.get("spec", {}).get("minMember", len(members)))
+            except ApiError:
+                min_member = len(members)
+            if len(members) < min_member:
+                self._set_unschedulable(pod, rt, f"{len(members)}/{min_member} gang members present")
+                return False
+            requests = [{"owner": key_of(m), "count": sum(gpus_requested(c) for c in m["spec"].get("containers", []))}
+                        for m in members]
+        r = self.agent.alloc(requests)
+        if not r.get("ok"):
+            self._set_unschedulable(pod, rt, r.get("error", "insufficient amd.com/gpu"))
+            return False
+        rt.gpus = list(r["assigned"].get(rt.key, []))
+        return True
+
+    def _set_unschedulable(self, pod, rt, msg):
+        st = {"phase": "Pending", "conditions": [{"type": "PodScheduled", "status": "False",
+                                                 "reason": "Unschedulable", "message": msg}]}
+        self._write_status(pod, rt, st)
+
+    def _run_init(self, pod, rt, procs) -> bool:
+        inits = pod.get("spec", {}).get("initContainers") or []
+        while rt.init_index < len(inits):
+            c = inits[rt.init_index]
+            cmd = " ".join(c.get("command") or []) + " " + " ".join(c.get("args") or [])
+            m = re.search(r"nslookup\s+([\w.-]+)", cmd)
+            if c.get("name") == "init-pytorch" or m:
+                svc = m.group(1) if m else None
+                if svc and self.svc_informer.get_by_key(f"{namespace_of(pod)}/{svc}") is None:
+                    self._write_status(pod, rt, self._pending_status(pod, "PodInitializing"))
+                    return False
+                rt.init_index += 1
+                continue
+            pid = f"{rt.key}/init/{c.get('name')}"
+            st = procs.get(pid)
+            if st is None:
+                self._spawn(pod, rt, c, pid, restart_policy="Never")
+                self._write_status(pod, rt, self._pending_status(pod, "PodInitializing"))
+                return False
+            if st["state"] != "terminated":
+                return False
+            if st["exit_code"] != 0:
+                if pod["spec"].get("restartPolicy") == "Never":
+                    self._write_status(pod, rt, {"phase": "Failed", "reason": "InitContainerFailed"})
+                    rt.stage = "done"
+                    return False
+                self.agent.remove(pid)  # retry
+                return False
+            rt.init_index += 1
+        return True
+
+    def _pending_status(self, pod, reason):
+        return {"phase": "Pending", "hostIP": NODE_ADDRESS, "podIP": NODE_ADDRESS,
+                "conditions": [{"type": "PodScheduled", "status": "True"},
+                               {"type": "Initialized", "status": "False", "reason": reason}]}
+
+    def _log_path(self, pod, container=None):
+        base = f"{namespace_of(pod)}_{name_of(pod)}"
+        return os.path.join(self.log_dir, base + (f".{container}" if container else "") + ".log")
+
+    def _job_port(self, pod, wanted: int) -> int:
+        job = (pod["metadata"].get("labels") or {}).get(C.LABEL_JOB_NAME) or name_of(pod)
+        jk = f"{namespace_of(pod)}/{job}"
+        if jk in self.job_ports:
+            return self.job_ports[jk]
+        used = set(self.job_ports.values())
+        port = wanted
+        while port in used or not _port_free(port):
+            port += 1
+        self.job_ports[jk] = port
+        return port
+
+    def _resolve_env(self, pod, c, rt) -> dict:
+        env = {k: v for k, v in os.environ.items() if not k.startswith(("MASTER_", "RANK", "WORLD_SIZE",
+                                                                          "LOCAL_RANK", "GROUP_RANK"))}
+        pp = env.get("PYTHONPATH", "")
+        env["PYTHONPATH"] = REPO_ROOT + (os.pathsep + pp if pp else "")
+        env.update(self.extra_env)
+        for e in c.get("env") or []:
+            if "value" in e:
+                env[e["name"]] = str(e["value"])
+            elif "valueFrom" in e:  # fieldRef subset
+                fr = (e["valueFrom"] or {}).get("fieldRef", {}).get("fieldPath", "")
+                env[e["name"]] = {"metadata.name": name_of(pod), "metadata.namespace": namespace_of(pod),
+                                  "status.podIP": NODE_ADDRESS, "spec.nodeName": self.node_name}.get(fr, "")
+        # single-node service "DNS" + per-job port virtualisation
+        addr = env.get("MASTER_ADDR")
+        if addr and addr != "localhost" and self.svc_informer.get_by_key(f"{namespace_of(pod)}/{addr}"):
+            env["PTO_MASTER_SERVICE"] = addr
+            env["MASTER_ADDR"] = NODE_ADDRESS
+        if addr == "localhost":
+            env["MASTER_ADDR"] = NODE_ADDRESS
+        if "MASTER_PORT" in env:
+            env["PTO_MASTER_PORT_REQUESTED"] = env["MASTER_PORT"]
+            env["MASTER_PORT"] = str(self._job_port(pod, int(env["MASTER_PORT"])))
+        # GPU pinning: one process per GPU, the process sees only its GPUs
+        if gpus_requested(c) > 0 or rt.gpus:
+            env["HIP_VISIBLE_DEVICES"] = ",".join(map(str, rt.gpus))
+        else:
+            env["HIP_VISIBLE_DEVICES"] = ""
+            env["PTO_NO_GPU"] = "1"
+        env.setdefault("LOCAL_RANK", "0")
+        env.setdefault("LOCAL_WORLD_SIZE", "1")
+        env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+        env["PTO_POD_NAME"] = name_of(pod)
+        env["PTO_NAMESPACE"] = namespace_of(pod)
+        env["PTO_JOB_NAME"] = (pod["metadata"].get("labels") or {}).get(C.LABEL_JOB_NAME, "")
+        env["PTO_METRICS_FILE"] = self._log_path(pod, "metrics").replace(".log", ".jsonl")
+        return env
+
+    def _argv(self, c) -> list[str]:
+        if c.get("command"):
+            argv = list(c["command"])
+        else:
+            image = c.get("image", "")
+            if image not in self.images:
+                raise KeyError(f"image {image!r} is not available on this node")
+            argv = list(self.images[image])
+        argv += [str(a) for a in c.get("args") or []]
+        if argv and argv[0] in ("python", "python3"):
+            argv[0] = sys.executable
+        return argv
+
+    def _spawn(self, pod, rt, c, pid, restart_policy):
+        log_path = self._log_path(pod) if c.get("name") == C.DEFAULT_CONTAINER_NAME else \
+            self._log_path(pod, c.get("name"))
+        try:
+            argv = self._argv(c)
+        except KeyError as e:
+            self._write_status(pod, rt, {"phase": "Pending", "containerStatuses": [
+                {"name": c.get("name"), "ready": False, "restartCount": 0, "image": c.get("image"),
+                 "state": {"waiting": {"reason": "ErrImagePull", "message": str(e)}}}]})
+            return
+        self.agent.spawn(pid, argv, env=self._resolve_env(pod, c, rt), cwd=c.get("workingDir") or REPO_ROOT,
+                         log=log_path, restart_policy=restart_policy)
+        rt.proc_ids.append(pid)
+
+    def _start_containers(self, pod, rt):
+        policy = pod.get("spec", {}).get("restartPolicy") or "Always"
+        for c in pod["spec"].get("containers") or []:
+            self._spawn(pod, rt, c, f"{rt.key}/{c.get('name')}", restart_policy=policy)
+
+    def _report(self, pod, rt, procs):
+        statuses = []
+        running = terminated_ok = terminated_bad = waiting = 0
+        for c in pod["spec"].get("containers") or []:
+            st = procs.get(f"{rt.key}/{c.get('name')}")
+            cs = {"name": c.get("name"), "image": c.get("image"), "restartCount": 0, "ready": False}
+            if st is None:
+                cs["state"] = {"waiting": {"reason": "ContainerCreating"}}
+                waiting += 1
+            else:
+                cs["restartCount"] = st["restart_count"]
+                if st["state"] == "running":
+                    cs["state"] = {"running": {"startedAt": _ts(st["started_at"])}}
+                    cs["ready"] = True
+                    running += 1
+                elif st["state"] == "terminated":
+                    cs["state"] = {"terminated": {"exitCode": st["exit_code"], "signal": st["signal"],
+                                                  "reason": st["reason"], "startedAt": _ts(st["started_at"]),
+                                                  "finishedAt": _ts(st["finished_at"])}}
+                    if st["exit_code"] == 0:
+                        terminated_ok += 1
+                    else:
+                        terminated_bad += 1
+                else:
+                    cs["state"] = {"waiting": {"reason": st["reason"]}}
+                    waiting += 1
+                if st["restart_count"] > 0:
+                    cs["lastState"] = {"terminated": {"exitCode": st["last_exit_code"],
+                                                      "finishedAt": _ts(st["last_finished_at"])}}
+            statuses.append(cs)
+        n = len(statuses)
+        if terminated_ok == n and n:
+            phase = "Succeeded"
+        elif terminated_ok + terminated_bad == n and terminated_bad:
+            phase = "Failed"
+        elif running or waiting:
+            phase = "Running" if (running or any(s["restartCount"] for s in statuses)) else "Pending"
+        else:
+            phase = "Pending"
+        status = {"phase": phase, "hostIP": NODE_ADDRESS, "podIP": NODE_ADDRESS, "startTime": rt.started_at,
+                  "containerStatuses": statuses,
+                  "conditions": [{"type": "PodScheduled", "status": "True"},
+                                 {"type": "Initialized", "status": "True"},
+                                 {"type": "Ready", "status": "True" if phase == "Running" else "False"}]}
+        if pod["spec"].get("initContainers"):
+            status["initContainerStatuses"] = [{"name": c.get("name"), "restartCount": 0, "ready": True,
+                                                "state": {"terminated": {"exitCode": 0, "reason": "Completed"}}}
+                                               for c in pod["spec"]["initContainers"]]
+        self._write_status(pod, rt, status)
+        self._read_metrics(pod, rt)
+        if phase in ("Succeeded", "Failed"):
+            rt.stage = "done"
+            self.agent.free(rt.key)
+
+    def _read_metrics(self, pod, rt):
+        path = self._log_path(pod, "metrics").replace(".log", ".jsonl")
+        if not os.path.exists(path):
+            return
+        ann = {}
+        with open(path) as f:
+            f.seek(rt.metrics_pos)
+            for line in f:
+                try:
+                    rec = json.loads(line)
+                except json.JSONDecodeError:
+                    break
+                if rec.get("event") == "first_step" and not rt.annotated_first_step:
+                    ann[FIRST_STEP_ANNOTATION] = repr(float(rec["t"]))
+                    rt.annotated_first_step = True
+                if "samples_per_sec" in rec:
+                    ann[THROUGHPUT_ANNOTATION] = str(rec["samples_per_sec"])
+            rt.metrics_pos = f.tell()
+        if ann:
+            self._annotate(pod, ann)
+
+    def _annotate(self, pod, ann):
+        try:
+            self.client.patch("pods", namespace_of(pod), name_of(pod), {"metadata": {"annotations": ann}})
+        except ApiError:
+            pass
+
+    def _write_status(self, pod, rt, status):
+        if status == rt.last_status:
+            return
+        try:
+            cur = self.client.get("pods", namespace_of(pod), name_of(pod))
+        except ApiError:
+            return
+        if cur["metadata"].get("uid") != rt.uid:
+            return
+        cur["status"] = status
+        try:
+            self.client.update_status("pods", cur)
+            rt.last_status = copy.deepcopy(status)
+        except ApiError as e:
+            log.debug("pod status write failed: %s", e)
+
+    # ------------------------------------------------------------ faults
+    def inject_fault(self, namespace, name, container="pytorch", signal=9):
+        """SIGKILL (or other signal) a running replica: the fault-injection
+        hook for the kill/rejoin path.  The process may be
+        restarted by its restart policy (exit 137 is retryable)."""
+        pid = f"{namespace}/{name}/{container}"
+        return self.agent.kill(pid, signal=signal, restartable=True)
+
+
+def _ts(t):
+    if not t:
+        return None
+    return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(t))

@@ -195,6 +195,40 @@ class FusedMnistTrainer:
     def last_loss(self):
         return float(self.loss_rows.mean().item())
 
+    @torch.no_grad()
+    def evaluate(self, data: torch.Tensor, target: torch.Tensor, batch_size: int = 1000):
+        """Test pass with the same kernels (forward + fused argmax/NLL-sum
+        eval head, K11).  Returns ``(mean_loss, accuracy)`` like the
+        reference's ``test()`` (examples/mnist/mnist.py:51-65)."""
+        L, s, P = self.L, self._s(), self.p
+        n = data.shape[0]
+        Bm = min(batch_size, n)
+        f32 = dict(device=self.device, dtype=torch.float32)
+        a1p = torch.empty(Bm * 2880, **f32)
+        c1 = torch.empty(Bm * 2880, device=self.device, dtype=torch.uint8)
+        a2p = torch.empty(Bm * 800, **f32)
+        c2 = torch.empty(Bm * 800, device=self.device, dtype=torch.uint8)
+        h1 = torch.empty(Bm * 500, **f32)
+        logp = torch.empty(Bm * 10, **f32)
+        stats = torch.zeros(2, **f32)
+        x = data.reshape(n, 784).contiguous()
+        y = target.to(torch.int64).contiguous()
+        c = _lib.check
+        for i in range(0, n, Bm):
+            B = min(Bm, n - i)
+            xb, yb = x[i:i + B], y[i:i + B]
+            c(L.pto_conv1_fwd(xb.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
+                              a1p.data_ptr(), c1.data_ptr(), B, None, s), "conv1_fwd")
+            c(L.pto_conv2_fwd(a1p.data_ptr(), P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(),
+                              a2p.data_ptr(), c2.data_ptr(), B, s), "conv2_fwd")
+            c(L.pto_linear_fwd(a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(), h1.data_ptr(),
+                               B, 500, 800, 1, s), "fc1_fwd")
+            c(L.pto_fc2_ce(h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(), yb.data_ptr(),
+                           logp.data_ptr(), None, None, None, B, 1.0, None, s), "fc2_ce")
+            c(L.pto_eval_head(logp.data_ptr(), yb.data_ptr(), stats.data_ptr(), B, s), "eval_head")
+        loss_sum, correct = stats.tolist()
+        return loss_sum / n, correct / n
+
     def set_lr(self, lr: float):
         self.lr = float(lr)
         self.lr_dev.fill_(self.lr)

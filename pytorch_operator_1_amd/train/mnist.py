@@ -1,0 +1,218 @@
+"""MNIST DDP trainer — the workload container of a PyTorchJob.
+
+CLI-compatible with the reference trainer (``examples/mnist/mnist.py:78-103``:
+``--batch-size 64 --test-batch-size 1000 --epochs 1 --lr 0.01
+--momentum 0.5 --no-cuda --seed 1 --log-interval 10 --save-model --dir logs
+--backend gloo|nccl|mpi``), same log lines (``Train Epoch: ...
+loss=...``, ``accuracy=...``), same env:// rendezvous from the operator's
+``MASTER_ADDR/MASTER_PORT/WORLD_SIZE/RANK``.
+
+MI355X additions: ``--backend rccl`` (alias of torch's ``nccl`` = RCCL),
+``--impl fused`` (hand-written gfx950 kernels + HIP graph, default on GPU)
+or ``eager`` (stock PyTorch DDP), synthetic HBM-resident data (no
+network), ``--sampler`` for true global throughput, periodic atomic
+checkpoints with auto-resume (``--checkpoint-dir``), ``--max-steps``,
+and a metrics stream (``$PTO_METRICS_FILE``: first optimizer step time and
+samples/s) that the node agent turns into pod annotations for the
+submit -> first-step latency metric.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+from ..models.mnist import synthetic_mnist
+from ..utils import dist as pdist
+from . import checkpoint as ckpt
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description="PyTorch MNIST Example (MI355X)")
+    p.add_argument("--batch-size", type=int, default=64, metavar="N")
+    p.add_argument("--test-batch-size", type=int, default=1000, metavar="N")
+    p.add_argument("--epochs", type=int, default=1, metavar="N")
+    p.add_argument("--lr", type=float, default=0.01, metavar="LR")
+    p.add_argument("--momentum", type=float, default=0.5, metavar="M")
+    p.add_argument("--no-cuda", action="store_true", default=False)
+    p.add_argument("--seed", type=int, default=1, metavar="S")
+    p.add_argument("--log-interval", type=int, default=10, metavar="N")
+    p.add_argument("--save-model", action="store_true", default=False)
+    p.add_argument("--dir", default="logs", metavar="L")
+    p.add_argument("--backend", type=str, default="gloo", choices=["gloo", "nccl", "rccl", "mpi"])
+    # MI355X runtime extensions
+    p.add_argument("--impl", choices=["fused", "eager"], default=None)
+    p.add_argument("--synthetic", action="store_true", default=True)
+    p.add_argument("--data", default=None, help="optional .npz with x_train/y_train/x_test/y_test (no pickle)")
+    p.add_argument("--train-size", type=int, default=60000)
+    p.add_argument("--test-size", type=int, default=10000)
+    p.add_argument("--sampler", action="store_true", help="DistributedSampler: shard the data over ranks")
+    p.add_argument("--max-steps", type=int, default=0, help="stop after N optimizer steps (0 = full epochs)")
+    p.add_argument("--no-test", action="store_true")
+    p.add_argument("--checkpoint-dir", default=None)
+    p.add_argument("--checkpoint-interval", type=int, default=0)
+    p.add_argument("--fail-at-step", type=int, default=int(os.environ.get("PTO_FAIL_AT_STEP", "0")),
+                   help="fault injection: SIGKILL self at this step (once)")
+    p.add_argument("--fail-rank", type=int, default=int(os.environ.get("PTO_FAIL_RANK", "1")))
+    return p.parse_args(argv)
+
+
+class Metrics:
+    def __init__(self):
+        self.path = os.environ.get("PTO_METRICS_FILE")
+        self.f = open(self.path, "a", buffering=1) if self.path else None
+
+    def emit(self, **rec):
+        if self.f:
+            self.f.write(json.dumps(rec) + "\n")
+
+
+def load_data(args, device, rank):
+    if args.data:
+        import numpy as np
+
+        z = np.load(args.data, allow_pickle=False)
+        mean, std = 0.1307, 0.3081
+
+        def prep(x):
+            t = torch.from_numpy(x.astype("float32"))
+            if t.max() > 1.5:
+                t = t / 255.0
+            return ((t - mean) / std).reshape(-1, 1, 28, 28).to(device)
+
+        return (prep(z["x_train"]), torch.from_numpy(z["y_train"]).long().to(device),
+                prep(z["x_test"]), torch.from_numpy(z["y_test"]).long().to(device))
+    # reference-equivalent: every rank uses the same seed/order (no sampler)
+    xtr, ytr = synthetic_mnist(args.train_size, device, seed=args.seed)
+    xte, yte = synthetic_mnist(args.test_size, device, seed=args.seed + 7)
+    return xtr, ytr, xte, yte
+
+
+# Exit code for "a peer died under me": 138 (128+SIGUSR1) is retryable in
+# the operator's exit-code table (train_util.go:18-53), so with
+# restartPolicy ExitCode the survivors are recreated too and every rank
+# resumes from the latest checkpoint (kill/rejoin).
+RETRYABLE_EXIT = 138
+_COMM_ERRORS = ("Connection closed by peer", "Connection reset by peer", "NCCL", "RCCL", "Broken pipe",
+                "timed out", "Timeout", "DistBackendError", "ProcessGroup", "Gloo", "gloo")
+
+
+def main(argv=None):
+    try:
+        return _main(argv)
+    except Exception as e:  # noqa: BLE001
+        msg = f"{type(e).__name__}: {e}"
+        if any(k in msg for k in _COMM_ERRORS) or isinstance(e, getattr(dist, "DistError", ())):
+            print(f"[pto] collective failed ({msg.splitlines()[0][:200]}); exiting {RETRYABLE_EXIT} for restart",
+                  flush=True)
+            os._exit(RETRYABLE_EXIT)
+        raise
+
+
+def _main(argv=None):
+    args = parse_args(argv)
+    use_cuda = not args.no_cuda and torch.cuda.is_available() and os.environ.get("PTO_NO_GPU") != "1"
+    if use_cuda:
+        print("Using CUDA (HIP) on", torch.cuda.get_device_name(0))
+    torch.manual_seed(args.seed)
+    env, device = pdist.init_distributed(args.backend, use_gpu=use_cuda)
+    if env.is_distributed:
+        print(f"Using distributed PyTorch with {dist.get_backend()} backend")
+    rank, world = env.rank, env.world_size
+    metrics = Metrics()
+    xtr, ytr, xte, yte = load_data(args, device, rank)
+    if args.sampler and world > 1:  # DistributedSampler semantics: disjoint shards
+        n = xtr.shape[0] // world
+        xtr, ytr = xtr[rank * n:(rank + 1) * n], ytr[rank * n:(rank + 1) * n]
+
+    impl = args.impl or ("fused" if use_cuda else "eager")
+    from .runner import build_trainer
+
+    trainer = build_trainer(impl, device=device, batch_size=args.batch_size, lr=args.lr, momentum=args.momentum,
+                            dataset_size=xtr.shape[0], seed=args.seed, rank=rank, data=xtr, target=ytr)
+    start_step = 0
+    if args.checkpoint_dir:
+        path = ckpt.latest(args.checkpoint_dir)
+        if path:
+            st = ckpt.load(path, map_location="cpu")
+            trainer.load_state_dict(st["trainer"])
+            start_step = int(st["step"])
+            print(f"Resumed from {path} at step {start_step}")
+            sys.stdout.flush()
+
+    n_batches = xtr.shape[0] // args.batch_size
+    total_steps = args.epochs * n_batches
+    if args.max_steps:
+        total_steps = min(total_steps, args.max_steps)
+    step = start_step
+    t_epoch = time.time()
+    samples_since = 0
+    t_last = time.time()
+    first = True
+    while step < total_steps:
+        epoch = step // n_batches + 1
+        batch_idx = step % n_batches
+        if args.fail_at_step and step == args.fail_at_step and rank == args.fail_rank and not start_step:
+            print(f"[fault-injection] rank {rank} SIGKILL at step {step}", flush=True)
+            os.kill(os.getpid(), signal.SIGKILL)
+        trainer.step()
+        step += 1
+        samples_since += args.batch_size
+        if first:
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            metrics.emit(event="first_step", t=time.time(), rank=rank)
+            first = False
+        if batch_idx % args.log_interval == 0:
+            loss = trainer.last_loss()
+            now = time.time()
+            sps = samples_since / max(now - t_last, 1e-9)
+            samples_since, t_last = 0, now
+            print("Train Epoch: {} [{}/{} ({:.0f}%)]\tloss={:.4f}".format(
+                epoch, batch_idx * args.batch_size, n_batches * args.batch_size, 100.0 * batch_idx / n_batches, loss))
+            metrics.emit(event="train", step=step, loss=loss, samples_per_sec=round(sps * world, 1), rank=rank)
+        if args.checkpoint_dir and args.checkpoint_interval and step % args.checkpoint_interval == 0 and rank == 0:
+            ckpt.save(args.checkpoint_dir, step, {"trainer": trainer.state_dict(), "rng": ckpt.rng_state()})
+        end_of_epoch = step % n_batches == 0 or step == total_steps
+        if end_of_epoch and not args.no_test:
+            if hasattr(trainer, "evaluate"):
+                test_loss, acc = trainer.evaluate(xte, yte, args.test_batch_size)
+            else:
+                test_loss, acc = evaluate_module(trainer.model, xte, yte, args.test_batch_size)
+            print("\naccuracy={:.4f}\n".format(acc))
+            metrics.emit(event="test", epoch=epoch, accuracy=acc, loss=test_loss, rank=rank,
+                         epoch_seconds=round(time.time() - t_epoch, 3))
+            t_epoch = time.time()
+        sys.stdout.flush()
+    if args.checkpoint_dir and rank == 0:
+        ckpt.save(args.checkpoint_dir, step, {"trainer": trainer.state_dict(), "rng": ckpt.rng_state()})
+    if args.save_model and rank == 0:
+        sd = trainer.state_dict()["model"]
+        prefix = "module." if world > 1 else ""
+        torch.save({prefix + k: v.cpu() for k, v in sd.items()}, "mnist_cnn.pt")
+    pdist.cleanup()
+    return 0
+
+
+@torch.no_grad()
+def evaluate_module(model, x, y, bs):
+    import torch.nn.functional as F
+
+    model.eval()
+    loss, correct = 0.0, 0
+    for i in range(0, x.shape[0], bs):
+        out = model(x[i:i + bs])
+        loss += F.nll_loss(out, y[i:i + bs], reduction="sum").item()
+        correct += (out.argmax(1) == y[i:i + bs]).sum().item()
+    model.train()
+    return loss / x.shape[0], correct / x.shape[0]
+
+
+if __name__ == "__main__":
+    sys.exit(main())

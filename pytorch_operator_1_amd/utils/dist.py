@@ -79,7 +79,11 @@ def init_distributed(backend: str | None = None, use_gpu: bool | None = None,
         device = torch.device("cpu")
     if env.is_distributed and not dist.is_initialized():
         be = resolve_backend(backend, use_gpu)
-        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        # 2 = clean up the communicator and raise in the caller instead of
+        # abort() (SIGABRT = exit 134, which the operator treats as
+        # permanent); the trainer maps the exception to a retryable exit.
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
+        timeout_s = float(os.environ.get("PTO_PG_TIMEOUT", timeout_s))
         kwargs = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kwargs["device_id"] = device

@@ -1,0 +1,117 @@
+"""End to end on CPU: API server + controller + native node agent running
+real multi-process gloo jobs (BASELINE config 1 and the sendrecv smoke),
+restart semantics, fault injection and checkpoint resume."""
+import os
+import signal
+import time
+
+import pytest
+
+from pytorch_operator_1_amd.api.types import new_job
+from pytorch_operator_1_amd.cluster import LocalCluster
+
+pytestmark = pytest.mark.slow
+
+
+@pytest.fixture(scope="module")
+def cluster(tmp_path_factory):
+    d = tmp_path_factory.mktemp("pods")
+    c = LocalCluster(gpus=0, log_dir=str(d), extra_env={"OMP_NUM_THREADS": "2"}).start()
+    yield c
+    c.stop()
+
+
+def _mnist_job(name, workers, extra=(), restart="OnFailure"):
+    args = ["--backend", "gloo", "--no-cuda", "--max-steps", "30", "--log-interval", "10", "--train-size", "2560",
+            "--test-size", "500"] + list(extra)
+    return new_job(name, image="pto/pytorch-mnist:rocm", master_args=args, workers=workers, restart_policy=restart)
+
+
+def test_mnist_gloo_master_worker_succeeds(cluster):
+    cluster.submit(_mnist_job("mnist-gloo", 1))
+    j = cluster.wait_for_condition("mnist-gloo", timeout=180)
+    types = [c["type"] for c in j["status"]["conditions"]]
+    assert types[-1] == "Succeeded", j["status"]
+    assert "Created" in types and "Running" in types
+    log0 = cluster.pod_log("default", "mnist-gloo-master-0")
+    assert "Using distributed PyTorch with gloo backend" in log0
+    assert "Train Epoch: 1 [0/2560 (0%)]\tloss=" in log0
+    assert "accuracy=" in log0
+    w = cluster.pod_log("default", "mnist-gloo-worker-0")
+    assert "Train Epoch" in w
+    pod = cluster.store.get("pods", "default", "mnist-gloo-master-0")
+    assert pod["status"]["phase"] == "Succeeded"
+    assert "pto.amd.com/first-step-unix" in pod["metadata"]["annotations"]
+    env = {e["name"]: e["value"] for e in pod["spec"]["containers"][0]["env"]}
+    assert env["WORLD_SIZE"] == "2" and env["RANK"] == "0" and env["MASTER_ADDR"] == "localhost"
+    svc = cluster.store.get("services", "default", "mnist-gloo-master-0")
+    assert svc["spec"]["clusterIP"] == "None"
+    assert j["status"]["replicaStatuses"]["Master"]["succeeded"] == 1
+
+
+def test_sendrecv_master_3_workers(cluster):
+    cluster.submit(new_job("sendrecv", image="pto/pytorch-sendrecv:rocm", workers=3))
+    j = cluster.wait_for_condition("sendrecv", timeout=120)
+    assert j["status"]["conditions"][-1]["type"] == "Succeeded", j["status"]
+    log0 = cluster.pod_log("default", "sendrecv-master-0")
+    assert "Result from worker 3" in log0 and "sendrecv OK" in log0
+
+
+def test_never_policy_failure_fails_job(cluster):
+    job = new_job("failing", image="pto/python:rocm", master_args=["-c", "import sys; sys.exit(1)"], workers=0,
+                  restart_policy="Never")
+    cluster.submit(job)
+    j = cluster.wait_for_condition("failing", timeout=60)
+    c = j["status"]["conditions"][-1]
+    assert c["type"] == "Failed" and "1 Master replica(s) failed" in c["message"]
+
+
+def test_onfailure_restarts_in_place(cluster):
+    # exits 3 on the first run, 0 on the second (state kept in a file)
+    flag = f"/tmp/pto-onfailure-{os.getpid()}"
+    code = f"import os,sys; f='{flag}'; first=not os.path.exists(f); open(f,'w').close(); sys.exit(3 if first else 0)"
+    cluster.submit(new_job("retry", image="pto/python:rocm", master_args=["-c", code], workers=0,
+                           restart_policy="OnFailure"))
+    j = cluster.wait_for_condition("retry", timeout=60)
+    assert j["status"]["conditions"][-1]["type"] == "Succeeded"
+    pod = cluster.store.get("pods", "default", "retry-master-0")
+    assert pod["status"]["containerStatuses"][0]["restartCount"] == 1
+    os.unlink(flag)
+
+
+def test_exitcode_policy_kill_rejoin_resume(cluster, tmp_path):
+    """Config 5 on CPU: SIGKILL a worker mid-run (137, retryable) -> the
+    operator deletes and recreates it (Restarting), survivors fail fast on
+    the broken collective and are restarted too, training resumes from the
+    checkpoint and the job succeeds."""
+    ck = str(tmp_path / "ckpt")
+    job = _mnist_job("elastic", 1, extra=["--checkpoint-dir", ck, "--checkpoint-interval", "5", "--fail-at-step",
+                                          "12", "--fail-rank", "1", "--max-steps", "30"], restart="ExitCode")
+    job["spec"]["backoffLimit"] = 6
+    cluster.submit(job)
+    j = cluster.wait_for_condition("elastic", timeout=300)
+    types = [c["type"] for c in j["status"]["conditions"]]
+    assert types[-1] == "Succeeded", j["status"]
+    evs = [e["reason"] for e in cluster.store.list("events")["items"]
+           if e["involvedObject"]["name"] == "elastic"]
+    assert "PyTorchJobRestarting" in evs or "ExitedWithCode" in evs
+    assert any(f.startswith("ckpt-") for f in os.listdir(ck))
+    log0 = cluster.pod_log("default", "elastic-worker-0")
+    assert "Resumed from" in log0
+
+
+def test_clean_pod_policy_running_and_delete_cascade(cluster):
+    job = new_job("cleanup", image="pto/python:rocm", master_args=["-c", "print('done')"], workers=1,
+                  worker_args=["-c", "import time; time.sleep(600)"], clean_pod_policy="Running")
+    cluster.submit(job)
+    cluster.wait_for_condition("cleanup", timeout=60)
+    end = time.time() + 30
+    while time.time() < end:
+        names = [p["metadata"]["name"] for p in cluster.store.list("pods")["items"]
+                 if p["metadata"]["labels"].get("job-name") == "cleanup"]
+        if "cleanup-worker-0" not in names:
+            break
+        time.sleep(0.1)
+    assert "cleanup-worker-0" not in names and "cleanup-master-0" in names
+    cluster.store.delete("pytorchjobs", "default", "cleanup")
+    assert not [p for p in cluster.store.list("pods")["items"] if p["metadata"]["labels"].get("job-name") == "cleanup"]
