@@ -97,6 +97,8 @@ class Kubelet:
                  poll_interval: float = 0.05, grace_seconds: float = 5.0, extra_env: dict | None = None,
                  hbm_per_gpu: float = C.HBM_PER_GPU_BYTES):
         self.client = client
+        if gpus is None and agent is None:
+            gpus = _visible_gpu_count()
         self.agent = agent or AgentClient(gpus=gpus, hbm_per_gpu=hbm_per_gpu)
         self.node_name = node_name
         self.log_dir = log_dir or os.path.join(os.environ.get("TMPDIR", "/tmp"), "pto-pods")
@@ -334,7 +336,7 @@ class Kubelet:
             env["MASTER_PORT"] = str(self._job_port(pod, int(env["MASTER_PORT"])))
         # GPU pinning: one process per GPU, the process sees only its GPUs
         if gpus_requested(c) > 0 or rt.gpus:
-            env["HIP_VISIBLE_DEVICES"] = ",".join(map(str, rt.gpus))
+            env["HIP_VISIBLE_DEVICES"] = _physical_ids(rt.gpus)
         else:
             env["HIP_VISIBLE_DEVICES"] = ""
             env["PTO_NO_GPU"] = "1"
@@ -483,6 +485,28 @@ class Kubelet:
         restarted by its restart policy (exit 137 is retryable)."""
         pid = f"{namespace}/{name}/{container}"
         return self.agent.kill(pid, signal=signal, restartable=True)
+
+
+def _visible_gpu_count() -> int:
+    """GPUs this node manager may hand out: the HIP-visible devices of its
+    own process (torch.cuda.device_count() does not initialise the GPU)."""
+    try:
+        import torch
+
+        return int(torch.cuda.device_count())
+    except Exception:
+        return 0
+
+
+def _physical_ids(idx: list[int]) -> str:
+    """Allocator indices are relative to this process's visible devices;
+    translate through an inherited HIP/CUDA_VISIBLE_DEVICES list so the
+    child sees exactly the allocated physical GPUs."""
+    parent = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+    if parent:
+        plist = [p.strip() for p in parent.split(",") if p.strip()]
+        return ",".join(plist[i] for i in idx if i < len(plist))
+    return ",".join(map(str, idx))
 
 
 def _ts(t):
