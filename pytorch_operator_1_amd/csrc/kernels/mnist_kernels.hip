@@ -181,6 +181,122 @@ __global__ __launch_bounds__(256) void k_conv2_fwd(const float* __restrict__ a1p
   code2[oi] = cd;
 }
 
+// -------------------------------------------------------------- F1+F2 ----
+// conv1 and conv2 forward in ONE launch.  Block = (sample, 16-channel conv2
+// tile); each block recomputes the sample's whole pooled conv1 map straight
+// into LDS (2880 outputs x 100 FMAs, ~1 us of VALU: cheaper than a kernel
+// boundary) and the nt == 0 block also writes it (+ argmax codes) to HBM
+// for the backward pass.  Then the conv2 implicit GEMM of k_conv2_fwd.
+__global__ __launch_bounds__(256) void k_conv12_fwd(const float* __restrict__ x, const float* __restrict__ w1,
+                                                    const float* __restrict__ b1, const float* __restrict__ w2,
+                                                    const float* __restrict__ b2, float* __restrict__ a1p,
+                                                    uint8_t* __restrict__ code1, float* __restrict__ a2p,
+                                                    uint8_t* __restrict__ code2, int B,
+                                                    const long long* __restrict__ bidx) {
+  __shared__ float ws[16 * WS_LD];
+  __shared__ __attribute__((aligned(16))) float in_s[A1P];
+  __shared__ __attribute__((aligned(16))) float xs[784];
+  __shared__ float w1s[C1 * 25 + C1];
+  const int b = blockIdx.x >> 2, nt = blockIdx.x & 3;
+  const int tid = threadIdx.x;
+  {
+    x = batch_ptr(x, bidx, B * 784);
+    const int nrows = min(16, C2 - nt * 16);
+    const float4* wsrc = reinterpret_cast<const float4*>(w2 + nt * 16 * 500);
+    float4 wv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + 256 * q;
+      wv[q] = (e < nrows * 125) ? wsrc[e] : float4{0.f, 0.f, 0.f, 0.f};
+    }
+    const float4 xv = tid < 196 ? reinterpret_cast<const float4*>(x + b * 784)[tid] : float4{0.f, 0.f, 0.f, 0.f};
+    float wq[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int e = tid + 256 * q;
+      wq[q] = e < C1 * 25 ? w1[e] : (e < C1 * 26 ? b1[e - C1 * 25] : 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + 256 * q;
+      if (e < 2000) {
+        const int row = e / 125, col = (e - row * 125) * 4;
+        float* d = ws + row * WS_LD + col;
+        d[0] = wv[q].x; d[1] = wv[q].y; d[2] = wv[q].z; d[3] = wv[q].w;
+      }
+    }
+    if (tid < 196) reinterpret_cast<float4*>(xs)[tid] = xv;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (tid + 256 * q < C1 * 26) w1s[tid + 256 * q] = wq[q];
+  }
+  __syncthreads();
+  // conv1 + bias + ReLU + pool: item = (4-channel group, pooled pixel)
+  for (int it = tid; it < 5 * 144; it += 256) {
+    const int cg = it / 144, pix = it - cg * 144;
+    const int ph = pix / 12, pw = pix - ph * 12;
+    float p[6][6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) p[r][c] = xs[(2 * ph + r) * 28 + 2 * pw + c];
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      const int oc = cg * 4 + cc;
+      const float* wc = w1s + oc * 25;
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int dy = q >> 1, dx = q & 1;
+        float sacc = w1s[C1 * 25 + oc];
+#pragma unroll
+        for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw) sacc = fmaf(p[dy + kh][dx + kw], wc[kh * 5 + kw], sacc);
+        v[q] = sacc;
+      }
+      float o;
+      uint8_t cd;
+      relu_pool4(v, o, cd);
+      in_s[oc * 144 + pix] = o;
+      if (nt == 0) {
+        a1p[b * A1P + oc * 144 + pix] = o;
+        code1[b * A1P + oc * 144 + pix] = cd;
+      }
+    }
+  }
+  __syncthreads();
+  const int t = tid >> 6, lane = tid & 63;
+  const int i = lane & 15, g = lane >> 4;
+  const int pw = i >> 2, dy = (i >> 1) & 1, dx = i & 1;
+  const int n = nt * 16 + (lane & 15);
+  const float* wl = ws + (lane & 15) * WS_LD + 5 * g;
+  const float* il = in_s + (2 * t + dy) * 12 + 2 * pw + dx;
+  f32x4 acc0 = zero4(), acc1 = zero4();
+#pragma unroll
+  for (int G = 0; G < 25; ++G) {
+    const int R = 4 * G + g;
+    const int ic = R / 5, kh = R - ic * 5;
+    const float* arow = il + ic * 144 + kh * 12;
+    const float* brow = wl + 20 * G;
+    acc0 = mfma16x16x4(arow[0], brow[0], acc0);
+    acc1 = mfma16x16x4(arow[1], brow[1], acc1);
+    acc0 = mfma16x16x4(arow[2], brow[2], acc0);
+    acc1 = mfma16x16x4(arow[3], brow[3], acc1);
+    acc0 = mfma16x16x4(arow[4], brow[4], acc0);
+  }
+  const f32x4 acc = acc0 + acc1;
+  if (n >= C2 || b >= B) return;
+  const float bn = b2[n];
+  float v[4] = {acc[0] + bn, acc[1] + bn, acc[2] + bn, acc[3] + bn};
+  float o;
+  uint8_t cd;
+  relu_pool4(v, o, cd);
+  const int oi = b * F1IN + n * 16 + t * 4 + (lane >> 4);
+  a2p[oi] = o;
+  code2[oi] = cd;
+}
+
 // ---------------------------------------------------------------- F3 ----
 struct EpiBiasRelu {
   const float* bias; float* out; int ld; bool relu;
@@ -365,77 +481,84 @@ __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ dh1, c
 //          entries.  Deterministic, no atomics, 3.4x fewer MFMAs than the
 //          dense full-convolution GEMM.
 //  part C: db2[oc] = sum of unmasked pooled grads (one wave per channel).
-constexpr int B2_CHUNK = 8;  // samples per weight-grad block
-constexpr int B2_INFLIGHT = 4;
+constexpr int B2_CHUNK = 4;  // samples per weight-grad block
+constexpr int B2_ICG = 10;   // input-channel pairs per sample in the dgrad part
 
 __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2, const uint8_t* __restrict__ code2,
                                                    const float* __restrict__ a1p, const float* __restrict__ w2,
                                                    float* __restrict__ gw2, float* __restrict__ gb2,
-                                                   float* __restrict__ da1p, int B, int nA, int nB, int nC) {
+                                                   float* __restrict__ da1p, int B, int nA, int nB, int nC,
+                                                   const float* __restrict__ x, const long long* __restrict__ bidx,
+                                                   const uint8_t* __restrict__ code1, float* __restrict__ gw1,
+                                                   float* __restrict__ gb1) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int bid = blockIdx.x;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (bid < nA) {
-    // ---- part A: weight gradient.  The block walks its sample chunk with
-    // a double-buffered LDS stage per sample (pooled conv1 map 11.5 KB +
-    // pooled grads + codes, all coalesced float4 loads; the next sample is
-    // loaded into registers while the current one is consumed).
+    // ---- part A: weight gradient.  ONE staging round: the block's K-tile
+    // (16 (ic,kh,kw) columns) touches at most 2 input channels, so for all 8
+    // samples of the chunk it stages 2x144 pooled conv1 values + the 800
+    // pooled grads + 800 codes (41 KB) with coalesced 16-byte loads, then
+    // runs its 128 MFMAs from LDS.
     const int nt = bid % 32, chunk = bid / 32;
     const int oc = wv * 16 + (lane & 15);
     const int g = lane >> 4;
     const int kk = nt * 16 + (lane & 15);
     const bool kvalid = kk < 500;
-    const int ic = kvalid ? kk / 25 : 0, r25 = kvalid ? kk - ic * 25 : 0;
+    const int ic0 = (nt * 16) / 25;
+    const int ic = kvalid ? kk / 25 : ic0, r25 = kvalid ? kk - ic * 25 : 0;
     const int kh = r25 / 5, kw = r25 - kh * 5;
     const bool ocvalid = oc < C2;
-    const int b0 = chunk * B2_CHUNK, b1 = min(B, b0 + B2_CHUNK);
-    constexpr int STG = A1P + F1IN + F1IN / 4;  // floats per stage buffer
-    float* stage = smem;                         // [2][STG]
+    const int b0 = chunk * B2_CHUNK, nb = min(B, b0 + B2_CHUNK) - b0;
+    float* as = smem;                                   // [8][2][144]
+    float* gs = smem + B2_CHUNK * 288;                  // [8][800]
+    uint8_t* cs = reinterpret_cast<uint8_t*>(gs + B2_CHUNK * F1IN);  // [8][800] bytes
     const int tid = threadIdx.x;
-    float4 ra[3], rg;
-    uint32_t rc = 0;
-    auto fetch = [&](int b) {
-      const float4* sa = reinterpret_cast<const float4*>(a1p + b * A1P);
+    {
+      float4 va[3], vg[7];
+      uint32_t vc[7];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int e = tid + 256 * q;  // float4 index over [s][ch][36]
+        const int smp = e / 72, rr = e - smp * 72, ch = rr / 36, off = (rr - ch * 36) * 4;
+        const bool ok = e < nb * 72 && ic0 + ch < C1;
+        va[q] = ok ? *reinterpret_cast<const float4*>(a1p + (b0 + smp) * A1P + (ic0 + ch) * 144 + off)
+                   : float4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int q = 0; q < 7; ++q) {
+        const int e = tid + 256 * q;
+        const bool ok = e < nb * (F1IN / 4);
+        vg[q] = ok ? reinterpret_cast<const float4*>(g2 + b0 * F1IN)[e] : float4{0.f, 0.f, 0.f, 0.f};
+        vc[q] = ok ? reinterpret_cast<const uint32_t*>(code2 + b0 * F1IN)[e] : 0x04040404u;
+      }
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         const int e = tid + 256 * q;
-        ra[q] = e < A1P / 4 ? sa[e] : float4{0.f, 0.f, 0.f, 0.f};
+        if (e < B2_CHUNK * 72) reinterpret_cast<float4*>(as)[e] = va[q];
       }
-      rg = tid < F1IN / 4 ? reinterpret_cast<const float4*>(g2 + b * F1IN)[tid] : float4{0.f, 0.f, 0.f, 0.f};
-      rc = tid < F1IN / 4 ? reinterpret_cast<const uint32_t*>(code2 + b * F1IN)[tid] : 0u;
-    };
-    auto put = [&](float* buf) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
+      for (int q = 0; q < 7; ++q) {
         const int e = tid + 256 * q;
-        if (e < A1P / 4) reinterpret_cast<float4*>(buf)[e] = ra[q];
+        if (e < B2_CHUNK * (F1IN / 4)) {
+          reinterpret_cast<float4*>(gs)[e] = vg[q];
+          reinterpret_cast<uint32_t*>(cs)[e] = vc[q];
+        }
       }
-      if (tid < F1IN / 4) {
-        reinterpret_cast<float4*>(buf + A1P)[tid] = rg;
-        reinterpret_cast<uint32_t*>(buf + A1P + F1IN)[tid] = rc;
-      }
-    };
-    f32x4 acc0 = zero4(), acc1 = zero4();
-    if (b0 < b1) {
-      fetch(b0);
-      put(stage);
     }
     __syncthreads();
-    const int koff = ic * 144 + kh * 12 + kw;
-    for (int b = b0; b < b1; ++b) {
-      float* cur = stage + ((b - b0) & 1) * STG;
-      if (b + 1 < b1) fetch(b + 1);
-      const float* as = cur;
-      const float* gs = cur + A1P;
-      const uint8_t* cs = reinterpret_cast<const uint8_t*>(cur + A1P + F1IN);
+    f32x4 acc0 = zero4(), acc1 = zero4();
+    const int koff = (ic - ic0) * 144 + kh * 12 + kw;
+    const int goff = (ocvalid ? oc : 0) * 16;
+#pragma unroll 2
+    for (int smp = 0; smp < nb; ++smp) {
+      const float* ap0 = as + smp * 288 + koff;
 #pragma unroll
       for (int G = 0; G < 4; ++G) {
         const int pp = 4 * G + g;
-        const int gi = (ocvalid ? oc : 0) * 16 + pp;
-        const float gv = ocvalid ? gs[gi] : 0.f;
-        const int cd = ocvalid ? (int)cs[gi] : 4;
-        const int oh0 = 2 * (pp >> 2), ow0 = 2 * (pp & 3);
-        const float* ap = as + koff + oh0 * 12 + ow0;
+        const float gv = ocvalid ? gs[smp * F1IN + goff + pp] : 0.f;
+        const int cd = ocvalid ? (int)cs[smp * F1IN + goff + pp] : 4;
+        const float* ap = ap0 + 2 * (pp >> 2) * 12 + 2 * (pp & 3);
         const float bv0 = kvalid ? ap[0] : 0.f, bv1 = kvalid ? ap[1] : 0.f;
         const float bv2 = kvalid ? ap[12] : 0.f, bv3 = kvalid ? ap[13] : 0.f;
         acc0 = mfma16x16x4(cd == 0 ? gv : 0.f, bv0, acc0);
@@ -443,8 +566,6 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
         acc0 = mfma16x16x4(cd == 2 ? gv : 0.f, bv2, acc0);
         acc1 = mfma16x16x4(cd == 3 ? gv : 0.f, bv3, acc1);
       }
-      if (b + 1 < b1) put(stage + ((b + 1 - b0) & 1) * STG);
-      __syncthreads();
     }
     const f32x4 acc = acc0 + acc1;
 #pragma unroll
@@ -457,71 +578,103 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
   }
   bid -= nA;
   if (bid < nB) {
-    // ---- part B: data gradient via col2im
-    const int b = bid >> 2, icg = bid & 3;
-    float* dys = smem;               // [64 pos][52 oc]
-    float* ts = smem + 64 * 52;      // [64 pos][129]
+    // ---- part B: data gradient via col2im.  Block = (sample, pair of input
+    // channels): 640 blocks at B=64, so each block's serial chain (one
+    // staging round -> dY2 expansion -> 64x64x52 GEMM -> col2im) is short.
+    // Staged: the W2 slice of the two channels (50 x 50, coalesced) + the
+    // sample's pooled grads and codes.
+    const int b = bid / B2_ICG, icg = bid - b * B2_ICG;
+    constexpr int WLD = 68;   // 64 + 4: the 4 k-rows of a wave hit disjoint banks
+    constexpr int TLD = 65;
+    float* ws = smem;                      // [52][68]
+    float* dys = ws + 52 * WLD;            // [64 pos][52 oc]
+    float* ts = dys + 64 * 52;             // [64 pos][65]
+    float* xs = ts + 64 * TLD;             // [784] input image (conv1 wgrad fusion)
+    uint8_t* c1s = reinterpret_cast<uint8_t*>(xs + 784);  // [2][144] conv1 codes
+    const bool fuse1 = gw1 != nullptr;
     const int r = lane & 15, gg = lane >> 4;
-    // prefetch this lane's W2 operands (128 values) for the GEMM below
-    const float* wb = w2 + icg * 125;
-    float wreg[4][8][4];
-#pragma unroll
-    for (int k0 = 0; k0 < 4; ++k0)
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int k = 16 * k0 + 4 * gg + j, n = q * 16 + r;
-          wreg[k0][q][j] = (k < C2 && n < 125) ? wb[k * 500 + n] : 0.f;
-        }
-    // dY2 gather: stage the sample's pooled grads + codes (coalesced), then
-    // entry (pos, oc) of dys is the pooled grad iff pos is the argmax.
-    float* gst = ts;  // ts is free until the GEMM epilogue: reuse it
-    uint8_t* cst = reinterpret_cast<uint8_t*>(ts + F1IN);
-    if (threadIdx.x < F1IN / 4) {
-      reinterpret_cast<float4*>(gst)[threadIdx.x] = reinterpret_cast<const float4*>(g2 + b * F1IN)[threadIdx.x];
-      reinterpret_cast<uint32_t*>(cst)[threadIdx.x] =
-          reinterpret_cast<const uint32_t*>(code2 + b * F1IN)[threadIdx.x];
+    const int tid = threadIdx.x;
+    if (fuse1) {
+      const float* xb = batch_ptr(x, bidx, B * 784) + b * 784;
+      if (tid < 196) reinterpret_cast<float4*>(xs)[tid] = reinterpret_cast<const float4*>(xb)[tid];
+      if (tid < 72)
+        reinterpret_cast<uint32_t*>(c1s)[tid] =
+            reinterpret_cast<const uint32_t*>(code1 + (b * C1 + icg * 2) * 144)[tid];
     }
-    __syncthreads();
-    for (int e = threadIdx.x; e < 64 * 52; e += 256) {
-      const int pos = e / 52, oc = e - pos * 52;
-      float v = 0.f;
-      if (oc < C2) {
-        const int oh = pos >> 3, ow = pos & 7;
-        const int gi = oc * 16 + (oh >> 1) * 4 + (ow >> 1);
-        v = (cst[gi] == ((oh & 1) * 2 + (ow & 1))) ? gst[gi] : 0.f;
+    {
+      constexpr int NW = (C2 * 50 + 255) / 256;  // 10
+      float wv_[NW];
+      const float* wb = w2 + icg * 50;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const int e = tid + 256 * q, k = e / 50, n = e - k * 50;
+        wv_[q] = e < C2 * 50 ? wb[k * 500 + n] : 0.f;
       }
-      dys[e] = v;
+      float4 gv4 = float4{0.f, 0.f, 0.f, 0.f};
+      uint32_t cv = 0;
+      if (tid < F1IN / 4) {
+        gv4 = reinterpret_cast<const float4*>(g2 + b * F1IN)[tid];
+        cv = reinterpret_cast<const uint32_t*>(code2 + b * F1IN)[tid];
+      }
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const int e = tid + 256 * q, k = e / 50, n = e - k * 50;
+        if (e < C2 * 50) ws[k * WLD + n] = wv_[q];
+      }
+      for (int e = tid; e < 2 * WLD; e += 256) ws[50 * WLD + e] = 0.f;     // rows 50,51
+      for (int e = tid; e < 50 * 14; e += 256) ws[(e / 14) * WLD + 50 + e % 14] = 0.f;  // cols 50..63
+      if (tid < F1IN / 4) {
+        reinterpret_cast<float4*>(ts)[tid] = gv4;                  // grads staged in ts
+        reinterpret_cast<uint32_t*>(ts + F1IN)[tid] = cv;          // codes after them
+      }
     }
     __syncthreads();
     {
-      f32x4 acc[8];
+      const float* gst = ts;
+      const uint8_t* cst = reinterpret_cast<const uint8_t*>(ts + F1IN);
+      for (int e = tid; e < 64 * 52; e += 256) {
+        const int pos = e / 52, oc = e - pos * 52;
+        float v = 0.f;
+        if (oc < C2) {
+          const int oh = pos >> 3, ow = pos & 7;
+          const int gi = oc * 16 + (oh >> 1) * 4 + (ow >> 1);
+          v = (cst[gi] == ((oh & 1) * 2 + (ow & 1))) ? gst[gi] : 0.f;
+        }
+        dys[e] = v;
+      }
+    }
+    __syncthreads();
+    {
+      f32x4 acc[4];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) acc[q] = zero4();
+      for (int q = 0; q < 4; ++q) acc[q] = zero4();
 #pragma unroll
       for (int k0 = 0; k0 < 4; ++k0) {
-        float av[4];
+        float av[4], bv[4][4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int k = 16 * k0 + 4 * gg + j;
           av[j] = k < 52 ? dys[(wv * 16 + r) * 52 + k] : 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) bv[q][j] = k < 52 ? ws[k * WLD + q * 16 + r] : 0.f;
         }
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
+        for (int q = 0; q < 4; ++q)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[q] = mfma16x16x4(av[j], wreg[k0][q][j], acc[q]);
+          for (int j = 0; j < 4; ++j) acc[q] = mfma16x16x4(av[j], bv[q][j], acc[q]);
       }
+      __syncthreads();  // ts (staged grads) is overwritten below
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr)
-          ts[(wv * 16 + gg * 4 + rr) * 129 + q * 16 + r] = acc[q][rr];
+          ts[(wv * 16 + gg * 4 + rr) * TLD + q * 16 + r] = acc[q][rr];
     }
     __syncthreads();
-    for (int o = threadIdx.x; o < 5 * 144; o += 256) {
+    float* dsum = dys;  // free after the GEMM
+    for (int o = tid; o < 2 * 144; o += 256) {
       const int icl = o / 144, pix = o - icl * 144;
-      const int y = pix / 12, x = pix - y * 12;
+      const int y = pix / 12, xx = pix - y * 12;
       float s = 0.f;
 #pragma unroll
       for (int kh = 0; kh < 5; ++kh) {
@@ -529,12 +682,46 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
         if (sy < 0 || sy >= 8) continue;
 #pragma unroll
         for (int kw = 0; kw < 5; ++kw) {
-          const int sx = x - kw;
+          const int sx = xx - kw;
           if (sx < 0 || sx >= 8) continue;
-          s += ts[(sy * 8 + sx) * 129 + icl * 25 + kh * 5 + kw];
+          s += ts[(sy * 8 + sx) * TLD + icl * 25 + kh * 5 + kw];
         }
       }
-      da1p[b * A1P + (icg * 5 + icl) * 144 + pix] = s;
+      da1p[b * A1P + (icg * 2 + icl) * 144 + pix] = s;
+      dsum[o] = s;
+    }
+    if (!fuse1) return;
+    // ---- conv1 weight+bias grad of this sample's 2 channels (replaces the
+    // separate conv1-backward launch): thread = (channel, tap, pixel
+    // quarter); pooled grad expanded through the conv1 argmax code.
+    __syncthreads();
+    float* red = ws;  // free after the GEMM
+    {
+      float acc = 0.f;
+      if (tid < 208) {
+        const int pair = tid >> 2, qtr = tid & 3;
+        const int icl = pair / 26, k = pair - icl * 26;
+        const int kh = k / 5, kw = k - kh * 5;
+        for (int pix = qtr * 36; pix < qtr * 36 + 36; ++pix) {
+          const int cd = c1s[icl * 144 + pix];
+          if (cd >= 4) continue;
+          const float v = dsum[icl * 144 + pix];
+          if (k == 25) {
+            acc += v;
+          } else {
+            const int oh = 2 * (pix / 12) + (cd >> 1), ow = 2 * (pix % 12) + (cd & 1);
+            acc = fmaf(v, xs[(oh + kh) * 28 + ow + kw], acc);
+          }
+        }
+      }
+      red[tid] = acc;
+    }
+    __syncthreads();
+    if (tid < 52) {
+      const float v = red[4 * tid] + red[4 * tid + 1] + red[4 * tid + 2] + red[4 * tid + 3];
+      const int icl = tid / 26, k = tid - icl * 26, oc1 = icg * 2 + icl;
+      if (k < 25) atomicAdd(gw1 + oc1 * 25 + k, v);
+      else atomicAdd(gb1 + oc1, v);
     }
     return;
   }
@@ -574,14 +761,25 @@ __global__ __launch_bounds__(256) void k_conv1_bwd(const float* __restrict__ g1,
                                                    const float* __restrict__ x, float* __restrict__ gw1,
                                                    float* __restrict__ gb1, int B,
                                                    const long long* __restrict__ bidx) {
+  // One memory round: the chunk's 4 input images (12.5 KB, coalesced
+  // float4) go to LDS together with each thread's (grad, code) pairs; the
+  // 25-tap patches are then read from LDS.
+  __shared__ __attribute__((aligned(16))) float xs[B1_CHUNK * 784];
   __shared__ float part[4][26];
   x = batch_ptr(x, bidx, B * 784);
   const int oc = blockIdx.x % C1, chunk = blockIdx.x / C1;
-  const int b0 = chunk * B1_CHUNK, b1 = min(B, b0 + B1_CHUNK);
-  const int nitems = (b1 - b0) * 144;
+  const int b0 = chunk * B1_CHUNK, nb = min(B, b0 + B1_CHUNK) - b0;
+  const int nitems = nb * 144;
   constexpr int PER = (B1_CHUNK * 144 + 255) / 256;
+  constexpr int XPER = (B1_CHUNK * 196 + 255) / 256;
   float gv[PER];
   int cd[PER];
+  float4 xv[XPER];
+#pragma unroll
+  for (int q = 0; q < XPER; ++q) {
+    const int e = threadIdx.x + 256 * q;
+    xv[q] = e < nb * 196 ? reinterpret_cast<const float4*>(x + b0 * 784)[e] : float4{0.f, 0.f, 0.f, 0.f};
+  }
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const int it = threadIdx.x + 256 * q;
@@ -590,27 +788,27 @@ __global__ __launch_bounds__(256) void k_conv1_bwd(const float* __restrict__ g1,
     gv[q] = ok ? g1[idx] : 0.f;
     cd[q] = ok ? (int)code1[idx] : 4;
   }
-  float xv[PER][25];
 #pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const int it = threadIdx.x + 256 * q;
-    const int c = cd[q] < 4 ? cd[q] : 0;
-    const int b = b0 + (it < nitems ? it / 144 : 0), pix = it < nitems ? it % 144 : 0;
-    const int oh = 2 * (pix / 12) + (c >> 1), ow = 2 * (pix % 12) + (c & 1);
-    const float* xp = x + b * 784 + oh * 28 + ow;
-#pragma unroll
-    for (int kh = 0; kh < 5; ++kh)
-#pragma unroll
-      for (int kw = 0; kw < 5; ++kw) xv[q][kh * 5 + kw] = xp[kh * 28 + kw];
+  for (int q = 0; q < XPER; ++q) {
+    const int e = threadIdx.x + 256 * q;
+    if (e < B1_CHUNK * 196) reinterpret_cast<float4*>(xs)[e] = xv[q];
   }
+  __syncthreads();
   float acc[26];
 #pragma unroll
   for (int k = 0; k < 26; ++k) acc[k] = 0.f;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
-    const float gq = cd[q] < 4 ? gv[q] : 0.f;
+    const int it = threadIdx.x + 256 * q;
+    if (cd[q] >= 4) continue;
+    const int smp = it / 144, pix = it - smp * 144;
+    const int oh = 2 * (pix / 12) + (cd[q] >> 1), ow = 2 * (pix % 12) + (cd[q] & 1);
+    const float* xp = xs + smp * 784 + oh * 28 + ow;
+    const float gq = gv[q];
 #pragma unroll
-    for (int k = 0; k < 25; ++k) acc[k] = fmaf(gq, xv[q][k], acc[k]);
+    for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) acc[kh * 5 + kw] = fmaf(gq, xp[kh * 28 + kw], acc[kh * 5 + kw]);
     acc[25] += gq;
   }
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -702,6 +900,13 @@ PTO_API int pto_conv2_fwd(const float* a1p, const float* w, const float* b, floa
   LAUNCH_CHECK();
 }
 
+PTO_API int pto_conv12_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
+                           float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B, const long long* bidx,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_conv12_fwd, dim3(B * 4), dim3(256), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B, bidx);
+  LAUNCH_CHECK();
+}
+
 PTO_API int pto_linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int N, int K, int relu,
                            hipStream_t s) {
   const int tiles = ((M + 15) / 16) * ((N + 15) / 16);
@@ -753,17 +958,20 @@ PTO_API int pto_fc_bwd(const float* dh1, const float* a2p, const float* w1, cons
 
 // parts: bit0 = weight grad (atomic-accumulated: gw2 must be zeroed by the
 // caller), bit1 = data grad, bit2 = bias grad.
+// With gw1 != nullptr the dgrad part also accumulates conv1's weight/bias
+// grads (gw1/gb1 zeroed by the caller) from x (+ batch cursor) and code1.
 PTO_API int pto_conv2_bwd(const float* g2, const uint8_t* code2, const float* a1p, const float* w2, float* gw2,
-                          float* gb2, float* da1p, int B, int parts, hipStream_t s) {
+                          float* gb2, float* da1p, int B, int parts, const float* x, const long long* bidx,
+                          const uint8_t* code1, float* gw1, float* gb1, hipStream_t s) {
   const int nA = (parts & 1) ? ((B + B2_CHUNK - 1) / B2_CHUNK) * 32 : 0;
-  const int nB = (parts & 2) ? B * 4 : 0;
+  const int nB = (parts & 2) ? B * B2_ICG : 0;
   const int nC = (parts & 4) ? (C2 + 3) / 4 : 0;
-  const size_t ldsA = (parts & 1) ? 2 * (A1P + F1IN + F1IN / 4) * sizeof(float) : 0;
-  const size_t ldsB = (parts & 2) ? (64 * 52 + 64 * 129) * sizeof(float) : 0;
+  const size_t ldsA = (parts & 1) ? B2_CHUNK * (288 + F1IN + F1IN / 4) * sizeof(float) : 0;
+  const size_t ldsB = (parts & 2) ? (52 * 68 + 64 * 52 + 64 * 65 + 784 + 72) * sizeof(float) : 0;
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;
   if (nA + nB + nC == 0) return 0;
   hipLaunchKernelGGL(k_conv2_bwd, dim3(nA + nB + nC), dim3(256), lds, s, g2, code2, a1p, w2, gw2, gb2, da1p, B, nA,
-                     nB, nC);
+                     nB, nC, x, bidx, code1, (parts & 2) ? gw1 : nullptr, gb1);
   LAUNCH_CHECK();
 }
 

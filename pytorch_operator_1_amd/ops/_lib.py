@@ -77,12 +77,13 @@ _L = ctypes.c_longlong
 _SIGS = {
     "pto_conv1_fwd": [_P, _P, _P, _P, _P, _I, _P, _P],
     "pto_conv2_fwd": [_P, _P, _P, _P, _P, _I, _P],
+    "pto_conv12_fwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     "pto_linear_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
     "pto_linear_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "pto_relu_bwd": [_P, _P, _P, _I, _P],
     "pto_fc2_ce": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _P, _P],
     "pto_fc_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P],
-    "pto_conv2_bwd": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _P],
+    "pto_conv2_bwd": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P],
     "pto_conv1_bwd": [_P, _P, _P, _P, _P, _I, _P, _P],
     "pto_conv1_bwd_data": [_P, _P, _P, _P, _I, _P],
     "pto_eval_head": [_P, _P, _P, _I, _P],

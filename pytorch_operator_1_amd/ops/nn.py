@@ -71,7 +71,8 @@ class _ConvReluPool(torch.autograd.Function):
                 gx = torch.empty_like(x)
                 parts |= 2
             _lib.check(L.pto_conv2_bwd(gout.data_ptr(), code.data_ptr(), x.data_ptr(), w.data_ptr(), gw.data_ptr(),
-                                       gb.data_ptr(), None if gx is None else gx.data_ptr(), B, parts, s),
+                                       gb.data_ptr(), None if gx is None else gx.data_ptr(), B, parts, None, None,
+                                       None, None, None, s),
                        "conv2_bwd")
         else:
             _lib.check(L.pto_conv1_bwd(gout.data_ptr(), code.data_ptr(), x.data_ptr(), gw.data_ptr(), gb.data_ptr(),

@@ -20,9 +20,26 @@ def watch(api, name=None, namespace=None, timeout_seconds=600, out=None, retries
         namespace = utils.get_default_target_namespace()
     _row("NAME", "STATE", "TIME", out)
     end = time.time() + timeout_seconds
+    def rows(job):
+        jname = job["metadata"]["name"]
+        conds = job.get("status", {}).get("conditions", []) or []
+        status = conds[-1].get("type", "") if conds else ""
+        t = conds[-1].get("lastTransitionTime", "") if conds else ""
+        return jname, status, t
+
     for attempt in range(retries):
         try:
-            stream = api.watch(constants.PYTORCHJOB_PLURAL, namespace, resource_version=0,
+            # list first (current state), then stream changes from that version
+            lst = api.list(constants.PYTORCHJOB_PLURAL, namespace)
+            for job in lst.get("items", []):
+                jname, status, t = rows(job)
+                if name and name != jname:
+                    continue
+                _row(jname, status, t, out)
+                if name == jname and status in ("Succeeded", "Failed"):
+                    return job
+            stream = api.watch(constants.PYTORCHJOB_PLURAL, namespace,
+                               resource_version=lst.get("metadata", {}).get("resourceVersion"),
                                timeout_seconds=max(1, int(end - time.time())))
             for _, job in stream:
                 jname = job["metadata"]["name"]

@@ -121,10 +121,9 @@ class FusedMnistTrainer:
         L, s, B, P, G = self.L, self._s(), self.B, self.p, self.g
         c = _lib.check
         bi = self.batch_idx.data_ptr()
-        c(L.pto_conv1_fwd(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
-                          self.a1p.data_ptr(), self.code1.data_ptr(), B, bi, s), "conv1_fwd")
-        c(L.pto_conv2_fwd(self.a1p.data_ptr(), P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(),
-                          self.a2p.data_ptr(), self.code2.data_ptr(), B, s), "conv2_fwd")
+        c(L.pto_conv12_fwd(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
+                           P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
+                           self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi, s), "conv12_fwd")
         c(L.pto_linear_fwd(self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
                            self.h1.data_ptr(), B, 500, 800, 1, s), "fc1_fwd")
         c(L.pto_fc2_ce(self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
@@ -138,9 +137,14 @@ class FusedMnistTrainer:
         L, s, B, P, G = self.L, self._s(), self.B, self.p, self.g
         c = _lib.check
         bi = self.batch_idx.data_ptr()
+        # conv2 wgrad + dgrad(col2im) + bias in one launch.  (Folding conv1's
+        # wgrad into the dgrad blocks is supported by the kernel — pass gw1 —
+        # but measured break-even: every sample-block adds into the same 520
+        # addresses, 64-way atomic contention.  The separate 320-block conv1
+        # launch below adds each address only 16 times.)
         c(L.pto_conv2_bwd(self.da2p.data_ptr(), self.code2.data_ptr(), self.a1p.data_ptr(),
                           P["conv2.weight"].data_ptr(), G["conv2.weight"].data_ptr(), G["conv2.bias"].data_ptr(),
-                          self.da1p.data_ptr(), B, 7, s), "conv2_bwd")
+                          self.da1p.data_ptr(), B, 7, None, None, None, None, None, s), "conv2_bwd")
         c(L.pto_conv1_bwd(self.da1p.data_ptr(), self.code1.data_ptr(), self.data.data_ptr(),
                           G["conv1.weight"].data_ptr(), G["conv1.bias"].data_ptr(), B, bi, s), "conv1_bwd")
 

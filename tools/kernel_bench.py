@@ -38,6 +38,10 @@ def main():
                                              bi, s),
         "conv2_fwd": lambda: L.pto_conv2_fwd(tr.a1p.data_ptr(), P["conv2.weight"].data_ptr(),
                                              P["conv2.bias"].data_ptr(), tr.a2p.data_ptr(), tr.code2.data_ptr(), B, s),
+        "conv12_fwd": lambda: L.pto_conv12_fwd(tr.data.data_ptr(), P["conv1.weight"].data_ptr(),
+                                               P["conv1.bias"].data_ptr(), P["conv2.weight"].data_ptr(),
+                                               P["conv2.bias"].data_ptr(), tr.a1p.data_ptr(), tr.code1.data_ptr(),
+                                               tr.a2p.data_ptr(), tr.code2.data_ptr(), B, bi, s),
         "fc1_fwd": lambda: L.pto_linear_fwd(tr.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
                                             tr.h1.data_ptr(), B, 500, 800, 1, s),
         "fc2_ce": lambda: L.pto_fc2_ce(tr.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
@@ -48,10 +52,13 @@ def main():
                                        G["fc1.bias"].data_ptr(), G["fc2.weight"].data_ptr(), G["fc2.bias"].data_ptr(),
                                        tr.da2p.data_ptr(), B, s),
     }
-    for parts, nm in ((1, "conv2_bwd_wgrad"), (2, "conv2_bwd_dgrad"), (4, "conv2_bwd_bias"), (7, "conv2_bwd_all")):
-        launches[nm] = (lambda p=parts: L.pto_conv2_bwd(tr.da2p.data_ptr(), tr.code2.data_ptr(), tr.a1p.data_ptr(),
-                                                         P["conv2.weight"].data_ptr(), G["conv2.weight"].data_ptr(),
-                                                         G["conv2.bias"].data_ptr(), tr.da1p.data_ptr(), B, p, s))
+    for parts, nm, fuse in ((1, "conv2_bwd_wgrad", 0), (2, "conv2_bwd_dgrad", 0), (4, "conv2_bwd_bias", 0),
+                            (7, "conv2_bwd_all", 0), (7, "conv2_bwd_all+conv1", 1)):
+        launches[nm] = (lambda p=parts, f=fuse: L.pto_conv2_bwd(
+            tr.da2p.data_ptr(), tr.code2.data_ptr(), tr.a1p.data_ptr(), P["conv2.weight"].data_ptr(),
+            G["conv2.weight"].data_ptr(), G["conv2.bias"].data_ptr(), tr.da1p.data_ptr(), B, p,
+            tr.data.data_ptr() if f else None, bi if f else None, tr.code1.data_ptr() if f else None,
+            G["conv1.weight"].data_ptr() if f else None, G["conv1.bias"].data_ptr() if f else None, s))
     launches["conv1_bwd"] = lambda: L.pto_conv1_bwd(tr.da1p.data_ptr(), tr.code1.data_ptr(), tr.data.data_ptr(),
                                                     G["conv1.weight"].data_ptr(), G["conv1.bias"].data_ptr(), B, bi, s)
     launches["sgd"] = lambda: tr.sgd.step(tr.lr_dev, 0.0, 0.0, 0.0, 1.0, False, zero_grad=False, stream=s)
