@@ -11,7 +11,12 @@ Weak scaling: per-rank batch is fixed at 64, ``value`` is the aggregate
 samples/s over all ranks (reference-equivalent mode: no sampler, every
 rank runs its own batch stream, exactly like the reference's mnist.py).
 
+Other configs of BASELINE.json (same contract, same timing bracket):
+``--model resnet50`` (config 3: ResNet-50 224x224 bf16 DDP, images/s) and
+``--model llama3-8b`` (config 4: Llama-3-8B bf16 DDP, tokens/s + MFU).
+
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--impl fused|eager]
+                        [--model mnist|resnet50|llama3-8b|llama3-1b]
 """
 from __future__ import annotations
 
@@ -31,9 +36,13 @@ BASELINE_SAMPLES_PER_SEC_PER_RANK = 210.0
 def parse_args(argv=None):
     p = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=2000)
-    p.add_argument("--warmup", type=int, default=200)
-    p.add_argument("--batch-size", type=int, default=64)
+    p.add_argument("--steps", type=int, default=None, help="timed steps (default 2000 mnist, 20 others)")
+    p.add_argument("--warmup", type=int, default=None, help="untimed steps (default 200 mnist, 3 others)")
+    p.add_argument("--model", default=os.environ.get("BENCH_MODEL", "mnist"),
+                   choices=["mnist", "resnet50", "llama3-8b", "llama3-1b", "llama3-tiny"])
+    p.add_argument("--batch-size", type=int, default=None, help="per-rank batch (64 mnist, 256 resnet50, 2 llama)")
+    p.add_argument("--seq-len", type=int, default=4096, help="llama sequence length")
+    p.add_argument("--checkpoint", choices=["none", "full"], default="none", help="llama activation checkpointing")
     p.add_argument("--lr", type=float, default=0.01)
     p.add_argument("--momentum", type=float, default=0.5)
     p.add_argument("--impl", choices=["fused", "eager"], default=os.environ.get("BENCH_IMPL", "fused"))
@@ -45,12 +54,22 @@ def parse_args(argv=None):
 
 def main(argv=None):
     args = parse_args(argv)
+    mnist = args.model == "mnist"
+    if args.steps is None:
+        args.steps = 2000 if mnist else 20
+    if args.warmup is None:
+        args.warmup = 200 if mnist else 3
+    if args.batch_size is None:
+        args.batch_size = 64 if mnist else (256 if args.model == "resnet50" else 2)
     from pytorch_operator_1_amd.utils import dist as pdist
 
     use_gpu = torch.cuda.is_available() and not args.cpu
     env, device = pdist.init_distributed(use_gpu=use_gpu)
     if env.world_size != args.gpus and env.rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
+
+    if not mnist:
+        return run_model_bench(args, env, device, pdist)
 
     from pytorch_operator_1_amd.train.runner import build_trainer
 
@@ -62,14 +81,13 @@ def main(argv=None):
         if device.type == "cuda":
             torch.cuda.synchronize(device)
 
-    for _ in range(args.warmup):
-        trainer.step()
+    run = getattr(trainer, "run", None) or (lambda n: [trainer.step() for _ in range(n)])
+    run(args.warmup)
     sync()
     pdist.barrier(device)
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        trainer.step()
+    run(args.steps)  # exactly K optimizer steps
     sync()
     pdist.barrier(device)
     sync()
@@ -109,6 +127,57 @@ def main(argv=None):
             },
         }
         print(json.dumps(out), flush=True)
+    pdist.cleanup()
+
+
+# Dense bf16 MFMA peak of one MI355X (no sparsity), for MFU reporting.
+MI355X_BF16_DENSE_FLOPS = 2.5e15
+
+
+def run_model_bench(args, env, device, pdist):
+    """BASELINE configs 3/4: ResNet-50 / Llama-3 DDP, full optimizer steps."""
+    from pytorch_operator_1_amd.train.bench_models import LlamaTrainer, ResNetTrainer
+
+    if device.type != "cuda":
+        raise SystemExit(f"--model {args.model} needs a GPU")
+    if args.model == "resnet50":
+        trainer = ResNetTrainer(device, batch_size=args.batch_size, seed=env.rank)
+    else:
+        trainer = LlamaTrainer(device, model=args.model, batch_size=args.batch_size, seq_len=args.seq_len,
+                               seed=env.rank, checkpoint=args.checkpoint)
+    trainer.run(args.warmup)
+    torch.cuda.synchronize(device)
+    pdist.barrier(device)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    trainer.run(args.steps)
+    torch.cuda.synchronize(device)
+    pdist.barrier(device)
+    torch.cuda.synchronize(device)
+    elapsed = pdist.all_reduce_max(time.perf_counter() - t0, device)
+    n = env.world_size
+    per_step = trainer.samples_per_step()
+    value = per_step * n * args.steps / elapsed
+    if env.rank == 0:
+        cfg = {"model": args.model, "global_batch": args.batch_size * n, "per_rank_batch": args.batch_size,
+               "seq_len": args.seq_len if args.model.startswith("llama") else None,
+               "parallelism": f"dp{n}", "backend": (torch.distributed.get_backend() if n > 1 else "none"),
+               "bucket_mb": trainer.bucketer.buckets and round(
+                   max((b["hi"] - b["lo"]) for b in trainer.bucketer.buckets)
+                   * next(iter(trainer.bucketer.flat.values())).element_size() / 2**20, 1),
+               "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 1),
+               "final_loss": trainer.last_loss()}
+        cfg.update(trainer.describe())
+        if hasattr(trainer, "flops_per_step"):
+            cfg["mfu"] = round(trainer.flops_per_step() * args.steps / elapsed / MI355X_BF16_DENSE_FLOPS, 4)
+        unit = "images/s" if args.model == "resnet50" else "tokens/s"
+        metric = "images/sec ResNet-50 DDP bf16" if args.model == "resnet50" else f"tokens/sec {args.model} DDP bf16"
+        print(json.dumps({"metric": metric, "value": round(value, 1), "unit": unit, "n_gpus": n,
+                          "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+                          "data": "synthetic (random tokens / ImageNet-shaped images), random-init weights",
+                          "config": cfg}), flush=True)
     pdist.cleanup()
 
 

@@ -1,0 +1,430 @@
+// Memory-bound kernels of the Llama-3 / ResNet DDP configs (BASELINE
+// configs 3-4), bf16 activations with fp32 math.  GEMMs go to hipBLASLt;
+// everything between the GEMMs is fused here so each activation tensor
+// crosses HBM once per direction:
+//
+//   add_rmsnorm_fwd   h = x + r (optional), y = h * rstd(h) * w      1 read x,r  1 write h,y
+//   rmsnorm_bwd       dx = rstd*(dy*w) - h*rstd^3/D*<dy*w,h> + dres  (dres = grad flowing
+//                     into h from the residual stream -> add fused), dw partials
+//   swiglu_fwd/bwd    gu = [gate | up] from one fused W13 GEMM
+//   rope_fwd/bwd      in place on the q,k heads of the fused QKV GEMM output
+//   ce_fwd/bwd        vocab-wide cross entropy on bf16 logits (128256 columns),
+//                     gradient written in place into the logits buffer
+//
+// Rows are processed by one 256-thread block (4 waves); each thread moves
+// 8 bf16 (16 bytes) per access (Guideline 13).  bf16 is raw uint16_t.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+__device__ __forceinline__ float bf2f(uint16_t x) { return __uint_as_float(((uint32_t)x) << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)(u >> 16) | ((u & 0xffff) ? 0x40 : 0);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+struct V8 {
+  float v[8];
+};
+__device__ __forceinline__ V8 ld8(const uint16_t* p) {
+  const uint4 q = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  V8 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    r.v[2 * i] = __uint_as_float(w[i] << 16);
+    r.v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+  return r;
+}
+__device__ __forceinline__ void st8(uint16_t* p, const V8& r) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(r.v[2 * i]) | ((uint32_t)f2bf(r.v[2 * i + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = uint4{w[0], w[1], w[2], w[3]};
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// 256-thread block reduction (4 waves); red must hold 4 floats.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+constexpr int NT = 256;
+constexpr int RMS_MAXV = 4;  // up to 4 x 8 x 256 = 8192 columns held in registers
+
+// ---------------------------------------------------------------- RMSNorm
+template <bool RES>
+__global__ __launch_bounds__(NT) void k_add_rmsnorm_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ r,
+                                                         const uint16_t* __restrict__ w, uint16_t* __restrict__ h,
+                                                         uint16_t* __restrict__ y, float* __restrict__ rstd, int D,
+                                                         float eps) {
+  __shared__ float red[4];
+  const long long row = blockIdx.x;
+  const uint16_t* xr = x + row * D;
+  V8 hv[RMS_MAXV];
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < RMS_MAXV; ++j) {
+    const int c = (j * NT + threadIdx.x) * 8;
+    if (c < D) {
+      hv[j] = ld8(xr + c);
+      if (RES) {
+        const V8 rv = ld8(r + row * D + c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) hv[j].v[e] += rv.v[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ss += hv[j].v[e] * hv[j].v[e];
+      }
+    }
+  }
+  // Residual sum is rounded to bf16 (it is the stored residual stream);
+  // normalise the rounded value so forward and backward agree.
+  if (RES) {
+    ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < RMS_MAXV; ++j) {
+      const int c = (j * NT + threadIdx.x) * 8;
+      if (c < D) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          hv[j].v[e] = bf2f(f2bf(hv[j].v[e]));
+          ss += hv[j].v[e] * hv[j].v[e];
+        }
+        st8(h + row * D + c, hv[j]);
+      }
+    }
+  }
+  const float rs = rsqrtf(block_sum(ss, red) / (float)D + eps);
+  if (threadIdx.x == 0) rstd[row] = rs;
+#pragma unroll
+  for (int j = 0; j < RMS_MAXV; ++j) {
+    const int c = (j * NT + threadIdx.x) * 8;
+    if (c < D) {
+      const V8 wv = ld8(w + c);
+      V8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o.v[e] = bf2f(f2bf(hv[j].v[e] * rs)) * wv.v[e];  // HF: w * (x*rstd).to(bf16)
+      st8(y + row * D + c, o);
+    }
+  }
+}
+
+// One block per group of rows; dw partial sums in registers -> part[G][D].
+__global__ __launch_bounds__(NT) void k_rmsnorm_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ h,
+                                                    const uint16_t* __restrict__ w, const float* __restrict__ rstd,
+                                                    const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
+                                                    float* __restrict__ part, int M, int D) {
+  __shared__ float red[4];
+  V8 wv[RMS_MAXV], dwacc[RMS_MAXV];
+#pragma unroll
+  for (int j = 0; j < RMS_MAXV; ++j) {
+    const int c = (j * NT + threadIdx.x) * 8;
+    if (c < D) wv[j] = ld8(w + c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dwacc[j].v[e] = 0.f;
+  }
+  for (long long row = blockIdx.x; row < M; row += gridDim.x) {
+    const float rs = rstd[row];
+    V8 hv[RMS_MAXV], gv[RMS_MAXV];
+    float dot = 0.f;
+#pragma unroll
+    for (int j = 0; j < RMS_MAXV; ++j) {
+      const int c = (j * NT + threadIdx.x) * 8;
+      if (c < D) {
+        hv[j] = ld8(h + row * D + c);
+        gv[j] = ld8(dy + row * D + c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float n = bf2f(f2bf(hv[j].v[e] * rs));
+          dwacc[j].v[e] += gv[j].v[e] * n;
+          gv[j].v[e] *= wv[j].v[e];  // g = dy * w
+          dot += gv[j].v[e] * hv[j].v[e];
+        }
+      }
+    }
+    const float k = block_sum(dot, red) * rs * rs * rs / (float)D;
+#pragma unroll
+    for (int j = 0; j < RMS_MAXV; ++j) {
+      const int c = (j * NT + threadIdx.x) * 8;
+      if (c < D) {
+        V8 o;
+        if (dres) {
+          o = ld8(dres + row * D + c);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o.v[e] = 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o.v[e] += rs * gv[j].v[e] - k * hv[j].v[e];
+        st8(dx + row * D + c, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < RMS_MAXV; ++j) {
+    const int c = (j * NT + threadIdx.x) * 8;
+    if (c < D) {
+      float4* pp = reinterpret_cast<float4*>(part + (long long)blockIdx.x * D + c);
+      pp[0] = float4{dwacc[j].v[0], dwacc[j].v[1], dwacc[j].v[2], dwacc[j].v[3]};
+      pp[1] = float4{dwacc[j].v[4], dwacc[j].v[5], dwacc[j].v[6], dwacc[j].v[7]};
+    }
+  }
+}
+
+// dw[c] = sum_g part[g][c]; 64 columns x 4 row-slices per block.
+__global__ __launch_bounds__(NT) void k_colsum_bf16(const float* __restrict__ part, uint16_t* __restrict__ dw, int G,
+                                                    int D) {
+  __shared__ float s[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int sl = threadIdx.x >> 6;
+  float a = 0.f;
+  if (c < D)
+    for (int g = sl; g < G; g += 4) a += part[(long long)g * D + c];
+  s[sl][threadIdx.x & 63] = a;
+  __syncthreads();
+  if (sl == 0 && c < D) dw[c] = f2bf(s[0][threadIdx.x] + s[1][threadIdx.x] + s[2][threadIdx.x] + s[3][threadIdx.x]);
+}
+
+// ---------------------------------------------------------------- SwiGLU
+__device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// gu [M][2F] (gate | up) -> out [M][F];  8 columns per thread.
+__global__ __launch_bounds__(NT) void k_swiglu_fwd(const uint16_t* __restrict__ gu, uint16_t* __restrict__ out,
+                                                   long long M, int F) {
+  const int F8 = F >> 3;
+  const long long total = M * F8;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const long long m = i / F8;
+    const int c = (int)(i - m * F8) * 8;
+    const V8 g = ld8(gu + m * 2 * F + c), u = ld8(gu + m * 2 * F + F + c);
+    V8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o.v[e] = bf2f(f2bf(g.v[e] * sigmoidf(g.v[e]))) * u.v[e];
+    st8(out + m * F + c, o);
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_swiglu_bwd(const uint16_t* __restrict__ gu, const uint16_t* __restrict__ dout,
+                                                   uint16_t* __restrict__ dgu, long long M, int F) {
+  const int F8 = F >> 3;
+  const long long total = M * F8;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const long long m = i / F8;
+    const int c = (int)(i - m * F8) * 8;
+    const V8 g = ld8(gu + m * 2 * F + c), u = ld8(gu + m * 2 * F + F + c), d = ld8(dout + m * F + c);
+    V8 dg, du;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float s = sigmoidf(g.v[e]);
+      const float silu = g.v[e] * s;
+      du.v[e] = d.v[e] * silu;
+      dg.v[e] = d.v[e] * u.v[e] * s * (1.f + g.v[e] * (1.f - s));
+    }
+    st8(dgu + m * 2 * F + c, dg);
+    st8(dgu + m * 2 * F + F + c, du);
+  }
+}
+
+// ---------------------------------------------------------------- RoPE
+// qkv row m = (b*S + s) has nh heads of D at stride row_stride; rotate the
+// first nrot heads (q and k).  rotate_half convention: pairs (i, i + D/2).
+// cs = [S][D/2] cos, sn = [S][D/2] sin (fp32).  sign = +1 fwd, -1 bwd.
+__global__ __launch_bounds__(NT) void k_rope(uint16_t* __restrict__ qkv, const float* __restrict__ cs,
+                                             const float* __restrict__ sn, long long M, int S, int nrot, int D,
+                                             long long row_stride, float sign) {
+  const int H2 = D >> 1, Q = H2 >> 2;  // 4 pairs per thread
+  const long long total = M * nrot * Q;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int q = (int)(i % Q);
+    const long long t = i / Q;
+    const int hd = (int)(t % nrot);
+    const long long m = t / nrot;
+    const int s = (int)(m % S);
+    uint16_t* base = qkv + m * row_stride + (long long)hd * D + q * 4;
+    const uint2 lo = *reinterpret_cast<const uint2*>(base), hi = *reinterpret_cast<const uint2*>(base + H2);
+    const float4 c = *reinterpret_cast<const float4*>(cs + (long long)s * H2 + q * 4);
+    const float4 n = *reinterpret_cast<const float4*>(sn + (long long)s * H2 + q * 4);
+    const float x1[4] = {__uint_as_float(lo.x << 16), __uint_as_float(lo.x & 0xffff0000u), __uint_as_float(lo.y << 16),
+                         __uint_as_float(lo.y & 0xffff0000u)};
+    const float x2[4] = {__uint_as_float(hi.x << 16), __uint_as_float(hi.x & 0xffff0000u), __uint_as_float(hi.y << 16),
+                         __uint_as_float(hi.y & 0xffff0000u)};
+    const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sign * n.x, sign * n.y, sign * n.z, sign * n.w};
+    uint16_t o1[4], o2[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o1[e] = f2bf(x1[e] * cc[e] - x2[e] * ss[e]);
+      o2[e] = f2bf(x2[e] * cc[e] + x1[e] * ss[e]);
+    }
+    *reinterpret_cast<uint2*>(base) = uint2{(uint32_t)o1[0] | ((uint32_t)o1[1] << 16), (uint32_t)o1[2] | ((uint32_t)o1[3] << 16)};
+    *reinterpret_cast<uint2*>(base + H2) =
+        uint2{(uint32_t)o2[0] | ((uint32_t)o2[1] << 16), (uint32_t)o2[2] | ((uint32_t)o2[3] << 16)};
+  }
+}
+
+// ---------------------------------------------------------------- cross entropy
+// One block per row of V logits (bf16).  fwd: lse[m], loss[m] (0 for ignored).
+__global__ __launch_bounds__(NT) void k_ce_fwd(const uint16_t* __restrict__ logits, const long long* __restrict__ labels,
+                                               float* __restrict__ lse, float* __restrict__ loss, int V,
+                                               long long ignore_index) {
+  __shared__ float red[4];
+  const long long row = blockIdx.x;
+  const uint16_t* z = logits + row * V;
+  float mx = -INFINITY, sum = 0.f;
+  const int V8n = V >> 3;
+  for (int i = threadIdx.x; i < V8n; i += NT) {  // online max/sum, 8 logits at a time
+    const V8 a = ld8(z + i * 8);
+    float lm = a.v[0];
+#pragma unroll
+    for (int e = 1; e < 8; ++e) lm = fmaxf(lm, a.v[e]);
+    if (lm > mx) {
+      sum *= __expf(mx - lm);
+      mx = lm;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sum += __expf(a.v[e] - mx);
+  }
+  for (int c = V8n * 8 + threadIdx.x; c < V; c += NT) {
+    const float a = bf2f(z[c]);
+    if (a > mx) {
+      sum *= __expf(mx - a);
+      mx = a;
+    }
+    sum += __expf(a - mx);
+  }
+  const float gmx = block_max(mx, red);
+  sum = (mx == -INFINITY) ? 0.f : sum * __expf(mx - gmx);
+  const float l = gmx + __logf(block_sum(sum, red));
+  if (threadIdx.x == 0) {
+    const long long y = labels[row];
+    lse[row] = l;
+    loss[row] = (y == ignore_index) ? 0.f : l - bf2f(z[y]);
+  }
+}
+
+// dz = (softmax(z) - onehot(y)) * scale[0], in place on z.
+__global__ __launch_bounds__(NT) void k_ce_bwd(uint16_t* __restrict__ logits, const long long* __restrict__ labels,
+                                               const float* __restrict__ lse, const float* __restrict__ scale, int V,
+                                               long long ignore_index) {
+  const long long row = blockIdx.x;
+  uint16_t* z = logits + row * V;
+  const long long y = labels[row];
+  const float sc = (y == ignore_index) ? 0.f : scale[0];
+  const float l = lse[row];
+  const int V8n = V >> 3;
+  for (int i = threadIdx.x; i < V8n; i += NT) {
+    V8 a = ld8(z + i * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = i * 8 + e;
+      a.v[e] = (__expf(a.v[e] - l) - (c == y ? 1.f : 0.f)) * sc;
+    }
+    st8(z + i * 8, a);
+  }
+  for (int c = V8n * 8 + threadIdx.x; c < V; c += NT) z[c] = f2bf((__expf(bf2f(z[c]) - l) - (c == y ? 1.f : 0.f)) * sc);
+}
+
+inline unsigned grid_for(long long work, int per_block = NT) {
+  long long g = (work + per_block - 1) / per_block;
+  if (g > 256 * 64) g = 256 * 64;  // grid-stride beyond 64 blocks per CU
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+}  // namespace
+
+#define PTO_API extern "C" __attribute__((visibility("default")))
+
+// Errors: -1 = unsupported shape (D % 8 != 0 or D > 8192).
+PTO_API int pto_add_rmsnorm_fwd(const void* x, const void* r, const void* w, void* h, void* y, float* rstd, long long M,
+                                int D, float eps, hipStream_t s) {
+  if (D % 8 || D > RMS_MAXV * NT * 8) return -1;
+  if (M <= 0) return 0;
+  if (r)
+    hipLaunchKernelGGL(k_add_rmsnorm_fwd<true>, dim3((unsigned)M), dim3(NT), 0, s, (const uint16_t*)x,
+                       (const uint16_t*)r, (const uint16_t*)w, (uint16_t*)h, (uint16_t*)y, rstd, D, eps);
+  else
+    hipLaunchKernelGGL(k_add_rmsnorm_fwd<false>, dim3((unsigned)M), dim3(NT), 0, s, (const uint16_t*)x, nullptr,
+                       (const uint16_t*)w, nullptr, (uint16_t*)y, rstd, D, eps);
+  return (int)hipGetLastError();
+}
+
+// part must hold G*D floats with G = pto_rmsnorm_bwd_groups(M).
+PTO_API int pto_rmsnorm_bwd_groups(long long M) { return (int)(M < 1024 ? (M < 1 ? 1 : M) : 1024); }
+
+PTO_API int pto_rmsnorm_bwd(const void* dy, const void* h, const void* w, const float* rstd, const void* dres, void* dx,
+                            void* dw, float* part, long long M, int D, hipStream_t s) {
+  if (D % 8 || D > RMS_MAXV * NT * 8) return -1;
+  if (M <= 0) return 0;
+  const int G = pto_rmsnorm_bwd_groups(M);
+  hipLaunchKernelGGL(k_rmsnorm_bwd, dim3(G), dim3(NT), 0, s, (const uint16_t*)dy, (const uint16_t*)h,
+                     (const uint16_t*)w, rstd, (const uint16_t*)dres, (uint16_t*)dx, part, (int)M, D);
+  hipLaunchKernelGGL(k_colsum_bf16, dim3((D + 63) / 64), dim3(NT), 0, s, part, (uint16_t*)dw, G, D);
+  return (int)hipGetLastError();
+}
+
+PTO_API int pto_swiglu_fwd(const void* gu, void* out, long long M, int F, hipStream_t s) {
+  if (F % 8) return -1;
+  hipLaunchKernelGGL(k_swiglu_fwd, dim3(grid_for(M * (F / 8))), dim3(NT), 0, s, (const uint16_t*)gu, (uint16_t*)out,
+                     M, F);
+  return (int)hipGetLastError();
+}
+
+PTO_API int pto_swiglu_bwd(const void* gu, const void* dout, void* dgu, long long M, int F, hipStream_t s) {
+  if (F % 8) return -1;
+  hipLaunchKernelGGL(k_swiglu_bwd, dim3(grid_for(M * (F / 8))), dim3(NT), 0, s, (const uint16_t*)gu,
+                     (const uint16_t*)dout, (uint16_t*)dgu, M, F);
+  return (int)hipGetLastError();
+}
+
+PTO_API int pto_rope(void* qkv, const float* cs, const float* sn, long long M, int S, int nrot, int D,
+                     long long row_stride, int backward, hipStream_t s) {
+  if (D % 8) return -1;
+  hipLaunchKernelGGL(k_rope, dim3(grid_for(M * nrot * (D / 8))), dim3(NT), 0, s, (uint16_t*)qkv, cs, sn, M, S, nrot,
+                     D, row_stride, backward ? -1.f : 1.f);
+  return (int)hipGetLastError();
+}
+
+PTO_API int pto_ce_fwd(const void* logits, const long long* labels, float* lse, float* loss, long long M, int V,
+                       long long ignore_index, hipStream_t s) {
+  if (V % 8) return -1;
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(k_ce_fwd, dim3((unsigned)M), dim3(NT), 0, s, (const uint16_t*)logits, labels, lse, loss, V,
+                     ignore_index);
+  return (int)hipGetLastError();
+}
+
+PTO_API int pto_ce_bwd(void* logits, const long long* labels, const float* lse, const float* scale, long long M, int V,
+                       long long ignore_index, hipStream_t s) {
+  if (V % 8) return -1;
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(k_ce_bwd, dim3((unsigned)M), dim3(NT), 0, s, (uint16_t*)logits, labels, lse, scale, V,
+                     ignore_index);
+  return (int)hipGetLastError();
+}

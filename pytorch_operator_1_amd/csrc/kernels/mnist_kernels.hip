@@ -481,7 +481,7 @@ __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ dh1, c
 //          entries.  Deterministic, no atomics, 3.4x fewer MFMAs than the
 //          dense full-convolution GEMM.
 //  part C: db2[oc] = sum of unmasked pooled grads (one wave per channel).
-constexpr int B2_CHUNK = 4;  // samples per weight-grad block
+constexpr int B2_CHUNK = 7;  // samples per weight-grad block (7: LDS <= 40 KB -> 4 blocks/CU, all parts co-resident)
 constexpr int B2_ICG = 10;   // input-channel pairs per sample in the dgrad part
 
 __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2, const uint8_t* __restrict__ code2,
@@ -587,9 +587,10 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
     constexpr int WLD = 68;   // 64 + 4: the 4 k-rows of a wave hit disjoint banks
     constexpr int TLD = 65;
     float* ws = smem;                      // [52][68]
-    float* dys = ws + 52 * WLD;            // [64 pos][52 oc]
-    float* ts = dys + 64 * 52;             // [64 pos][65]
-    float* xs = ts + 64 * TLD;             // [784] input image (conv1 wgrad fusion)
+    float* dys = ws + 52 * WLD;            // [64 pos][52 oc]   } union: ts is written
+    float* ts = dys;                       // [64 pos][65]      } after the GEMM's last dys read
+    float* gstage = dys + 64 * TLD;        // [800] grads + [800 B] codes
+    float* xs = gstage + F1IN + F1IN / 4;  // [784] input image (conv1 wgrad fusion only)
     uint8_t* c1s = reinterpret_cast<uint8_t*>(xs + 784);  // [2][144] conv1 codes
     const bool fuse1 = gw1 != nullptr;
     const int r = lane & 15, gg = lane >> 4;
@@ -624,14 +625,14 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
       for (int e = tid; e < 2 * WLD; e += 256) ws[50 * WLD + e] = 0.f;     // rows 50,51
       for (int e = tid; e < 50 * 14; e += 256) ws[(e / 14) * WLD + 50 + e % 14] = 0.f;  // cols 50..63
       if (tid < F1IN / 4) {
-        reinterpret_cast<float4*>(ts)[tid] = gv4;                  // grads staged in ts
-        reinterpret_cast<uint32_t*>(ts + F1IN)[tid] = cv;          // codes after them
+        reinterpret_cast<float4*>(gstage)[tid] = gv4;
+        reinterpret_cast<uint32_t*>(gstage + F1IN)[tid] = cv;
       }
     }
     __syncthreads();
     {
-      const float* gst = ts;
-      const uint8_t* cst = reinterpret_cast<const uint8_t*>(ts + F1IN);
+      const float* gst = gstage;
+      const uint8_t* cst = reinterpret_cast<const uint8_t*>(gstage + F1IN);
       for (int e = tid; e < 64 * 52; e += 256) {
         const int pos = e / 52, oc = e - pos * 52;
         float v = 0.f;
@@ -663,7 +664,7 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[q] = mfma16x16x4(av[j], bv[q][j], acc[q]);
       }
-      __syncthreads();  // ts (staged grads) is overwritten below
+      __syncthreads();  // ts aliases dys: every wave's dys reads are done
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -671,7 +672,7 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
           ts[(wv * 16 + gg * 4 + rr) * TLD + q * 16 + r] = acc[q][rr];
     }
     __syncthreads();
-    float* dsum = dys;  // free after the GEMM
+    float* dsum = gstage;  // free after the dY2 expansion
     for (int o = tid; o < 2 * 144; o += 256) {
       const int icl = o / 144, pix = o - icl * 144;
       const int y = pix / 12, xx = pix - y * 12;
@@ -967,7 +968,7 @@ PTO_API int pto_conv2_bwd(const float* g2, const uint8_t* code2, const float* a1
   const int nB = (parts & 2) ? B * B2_ICG : 0;
   const int nC = (parts & 4) ? (C2 + 3) / 4 : 0;
   const size_t ldsA = (parts & 1) ? B2_CHUNK * (288 + F1IN + F1IN / 4) * sizeof(float) : 0;
-  const size_t ldsB = (parts & 2) ? (52 * 68 + 64 * 52 + 64 * 65 + 784 + 72) * sizeof(float) : 0;
+  const size_t ldsB = (parts & 2) ? (52 * 68 + 64 * 65 + F1IN + F1IN / 4 + (gw1 ? 784 + 72 : 0)) * sizeof(float) : 0;
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;
   if (nA + nB + nC == 0) return 0;
   hipLaunchKernelGGL(k_conv2_bwd, dim3(nA + nB + nC), dim3(256), lds, s, g2, code2, a1p, w2, gw2, gb2, da1p, B, nA,

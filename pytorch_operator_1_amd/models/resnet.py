@@ -1,0 +1,88 @@
+"""ResNet-50 (BASELINE config 3: "ResNet-50 ImageNet-shape DDP bf16, 8
+replicas over xGMI").  torchvision is not a dependency; this is the
+standard v1.5 architecture (stride on the 3x3 conv of each bottleneck),
+25,557,032 parameters at 1000 classes.
+
+MI355X-first choices: activations in ``channels_last`` (NHWC, what the
+MIOpen/hipBLASLt implicit-GEMM convolutions want for bf16 MFMA), bf16
+autocast for convs/GEMMs with fp32 master parameters and fp32 BN
+statistics, zero-init of the last BN gamma in each residual branch, and
+the optimizer step as one multi-tensor HIP launch (``FusedSGD``).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin: int, width: int, stride: int = 1, down: bool = False):
+        super().__init__()
+        cout = width * self.expansion
+        self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(cout)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = (nn.Sequential(nn.Conv2d(cin, cout, 1, stride=stride, bias=False), nn.BatchNorm2d(cout))
+                           if down else None)
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        y = self.relu(self.bn1(self.conv1(x)))
+        y = self.relu(self.bn2(self.conv2(y)))
+        y = self.bn3(self.conv3(y))
+        return self.relu(y + idt)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes: int = 1000, zero_init_residual: bool = True):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        cin, stages = 64, []
+        for i, (n, width) in enumerate(zip(layers, (64, 128, 256, 512))):
+            stride = 1 if i == 0 else 2
+            blocks = [Bottleneck(cin, width, stride, down=True)]
+            cin = width * Bottleneck.expansion
+            blocks += [Bottleneck(cin, width) for _ in range(n - 1)]
+            stages.append(nn.Sequential(*blocks))
+        self.layer1, self.layer2, self.layer3, self.layer4 = stages
+        self.avgpool = nn.AdaptiveAvgPool2d(1)
+        self.fc = nn.Linear(cin, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.zeros_(m.bn3.weight)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return self.fc(torch.flatten(self.avgpool(x), 1))
+
+
+def resnet50(num_classes: int = 1000) -> ResNet:
+    return ResNet((3, 4, 6, 3), num_classes)
+
+
+def synthetic_images(batch: int, device, size: int = 224, num_classes: int = 1000, seed: int = 0,
+                     channels_last: bool = True, dtype=torch.float32):
+    """ImageNet-shaped synthetic batch (no dataset access)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(batch, 3, size, size, generator=g).to(device=device, dtype=dtype)
+    if channels_last:
+        x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, num_classes, (batch,), generator=g).to(device)
+    return x, y

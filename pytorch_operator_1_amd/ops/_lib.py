@@ -28,7 +28,8 @@ LIB_PATH = os.path.join(LIB_DIR, "libpto_hip.so")
 ARCH = os.environ.get("PTO_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 
-HIP_SOURCES = ("kernels/mnist_kernels.hip", "kernels/common_kernels.hip", "comm/xgmi_allreduce.hip")
+HIP_SOURCES = ("kernels/mnist_kernels.hip", "kernels/common_kernels.hip", "kernels/optim_kernels.hip",
+               "kernels/llm_kernels.hip", "comm/xgmi_allreduce.hip")
 
 _lock = threading.Lock()
 _lib = None
@@ -94,6 +95,18 @@ _SIGS = {
     "pto_cross_entropy_fwd": [_P, _P, _P, _P, _I, _I, _F, _P],
     "pto_scale": [_P, _P, _F, _L, _P],
     "pto_sum": [_P, _P, _L, _F, _P],
+    "pto_adamw_block_count": [_L],
+    "pto_adamw_multi": [_P, _P, _I, _I, _I, _P, _F, _F, _F, _F, _F, _I, _F, _I, _P],
+    "pto_bf16_to_f32": [_P, _P, _L, _P],
+    # LLM memory-bound kernels (csrc/kernels/llm_kernels.hip)
+    "pto_add_rmsnorm_fwd": [_P, _P, _P, _P, _P, _P, _L, _I, _F, _P],
+    "pto_rmsnorm_bwd_groups": [_L],
+    "pto_rmsnorm_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
+    "pto_swiglu_fwd": [_P, _P, _L, _I, _P],
+    "pto_swiglu_bwd": [_P, _P, _P, _L, _I, _P],
+    "pto_rope": [_P, _P, _P, _L, _I, _I, _I, _L, _I, _P],
+    "pto_ce_fwd": [_P, _P, _P, _P, _L, _I, _L, _P],
+    "pto_ce_bwd": [_P, _P, _P, _P, _L, _I, _L, _P],
     # xGMI peer all-reduce (csrc/comm)
     "pto_ar_ipc_handle_size": [],
     "pto_ar_get_ipc_handle": [_P, _P],

@@ -1,0 +1,199 @@
+"""Autograd wrappers over the bf16 transformer kernels
+(``csrc/kernels/llm_kernels.hip``) used by :mod:`..models.llama`.
+
+The ops take bf16 HIP tensors and raise on anything else (no silent
+fallback): :func:`add_rmsnorm` (residual add + RMSNorm, the residual
+gradient add fused into the RMSNorm backward), :func:`swiglu`,
+:func:`rope_` (in place on the fused QKV projection), and
+:func:`cross_entropy` (vocab-wide CE on bf16 logits, gradient written in
+place into the logits buffer so no fp32 ``[tokens, 128256]`` tensor ever
+exists).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def _req(t: torch.Tensor, name: str):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name}: HIP device tensor required")
+    if t.dtype != torch.bfloat16:
+        raise TypeError(f"{name}: bf16 only (got {t.dtype})")
+    return t.contiguous()
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+class _AddRMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, r, w, eps):
+        x = _req(x, "add_rmsnorm")
+        w = _req(w, "add_rmsnorm")
+        D = x.shape[-1]
+        M = x.numel() // D
+        y = torch.empty_like(x)
+        rstd = torch.empty(M, device=x.device, dtype=torch.float32)
+        if r is not None:
+            r = _req(r, "add_rmsnorm")
+            h = torch.empty_like(x)
+        else:
+            h = x
+        _lib.check(_lib.lib().pto_add_rmsnorm_fwd(x.data_ptr(), _p(r), w.data_ptr(), _p(h if r is not None else None),
+                                                   y.data_ptr(), rstd.data_ptr(), M, D, float(eps),
+                                                   _lib.stream_ptr(x.device)), "add_rmsnorm_fwd")
+        ctx.save_for_backward(h, w, rstd)
+        ctx.has_res = r is not None
+        ctx.set_materialize_grads(False)  # an unused h output costs no zero tensor
+        if r is None:
+            return y
+        return h, y
+
+    @staticmethod
+    def backward(ctx, *grads):
+        h, w, rstd = ctx.saved_tensors
+        if ctx.has_res:
+            dh, dy = grads
+        else:
+            dh, dy = None, grads[0]
+        D = h.shape[-1]
+        M = h.numel() // D
+        L = _lib.lib()
+        dy = torch.zeros_like(h) if dy is None else dy.contiguous()
+        if dh is not None:
+            dh = dh.contiguous()
+        dx = torch.empty_like(h)
+        dw = torch.empty_like(w)
+        part = torch.empty(L.pto_rmsnorm_bwd_groups(M), D, device=h.device, dtype=torch.float32)
+        _lib.check(L.pto_rmsnorm_bwd(dy.data_ptr(), h.data_ptr(), w.data_ptr(), rstd.data_ptr(), _p(dh), dx.data_ptr(),
+                                     dw.data_ptr(), part.data_ptr(), M, D, _lib.stream_ptr(h.device)), "rmsnorm_bwd")
+        return dx, (dx if ctx.has_res else None), dw, None
+
+
+def add_rmsnorm(x, residual, weight, eps: float = 1e-5):
+    """``h = x + residual; y = rmsnorm(h) * weight`` -> ``(h, y)``."""
+    return _AddRMSNorm.apply(x, residual, weight, eps)
+
+
+def rmsnorm(x, weight, eps: float = 1e-5):
+    return _AddRMSNorm.apply(x, None, weight, eps)
+
+
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        gu = _req(gu, "swiglu")
+        F2 = gu.shape[-1]
+        M = gu.numel() // F2
+        out = torch.empty(*gu.shape[:-1], F2 // 2, device=gu.device, dtype=gu.dtype)
+        _lib.check(_lib.lib().pto_swiglu_fwd(gu.data_ptr(), out.data_ptr(), M, F2 // 2, _lib.stream_ptr(gu.device)),
+                   "swiglu_fwd")
+        ctx.save_for_backward(gu)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (gu,) = ctx.saved_tensors
+        F2 = gu.shape[-1]
+        M = gu.numel() // F2
+        dout = dout.contiguous()
+        dgu = torch.empty_like(gu)
+        _lib.check(_lib.lib().pto_swiglu_bwd(gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), M, F2 // 2,
+                                             _lib.stream_ptr(gu.device)), "swiglu_bwd")
+        return dgu
+
+
+def swiglu(gu):
+    """``silu(gu[..., :F]) * gu[..., F:]`` for the fused gate|up projection."""
+    return _SwiGLU.apply(gu)
+
+
+class _RoPE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, seq_len, n_rot, head_dim):
+        if not qkv.is_contiguous():
+            raise ValueError("rope_: qkv must be contiguous")
+        _req(qkv, "rope_")
+        M = qkv.numel() // qkv.shape[-1]
+        _lib.check(_lib.lib().pto_rope(qkv.data_ptr(), cos.data_ptr(), sin.data_ptr(), M, seq_len, n_rot, head_dim,
+                                       qkv.shape[-1], 0, _lib.stream_ptr(qkv.device)), "rope_fwd")
+        ctx.mark_dirty(qkv)
+        ctx.save_for_backward(cos, sin)
+        ctx.cfg = (seq_len, n_rot, head_dim)
+        return qkv
+
+    @staticmethod
+    def backward(ctx, g):
+        cos, sin = ctx.saved_tensors
+        S, n_rot, D = ctx.cfg
+        # rotate in place when autograd handed us a fresh buffer of our own
+        if not g.is_contiguous():
+            g = g.contiguous()
+        elif g._base is not None:
+            g = g.clone()
+        M = g.numel() // g.shape[-1]
+        _lib.check(_lib.lib().pto_rope(g.data_ptr(), cos.data_ptr(), sin.data_ptr(), M, S, n_rot, D, g.shape[-1], 1,
+                                       _lib.stream_ptr(g.device)), "rope_bwd")
+        return g, None, None, None, None, None
+
+
+def rope_(qkv, cos, sin, seq_len: int, n_rot: int, head_dim: int):
+    """Rotate (HF rotate_half convention) the first ``n_rot`` heads of every
+    ``[.., heads*head_dim]`` row of ``qkv`` in place; rows are ordered
+    ``(batch, position)`` and ``cos``/``sin`` are fp32 ``[seq_len, head_dim/2]``."""
+    return _RoPE.apply(qkv, cos, sin, seq_len, n_rot, head_dim)
+
+
+def rope_tables(seq_len: int, head_dim: int, theta: float, device, scaling: dict | None = None):
+    """fp32 cos/sin tables ``[seq_len, head_dim/2]`` (Llama-3 frequency
+    scaling applied when ``scaling`` is given, as in the Llama-3.1 recipe)."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling:
+        import math
+
+        factor, lo, hi, old = (scaling["factor"], scaling["low_freq_factor"], scaling["high_freq_factor"],
+                               scaling["original_max_position_embeddings"])
+        wl = 2 * math.pi / inv
+        smooth = ((old / wl) - lo) / (hi - lo)
+        scaled = torch.where(wl > old / lo, inv / factor, inv)
+        mid = (wl <= old / lo) & (wl >= old / hi)
+        inv = torch.where(mid, (1 - smooth) * inv / factor + smooth * inv, scaled)
+    ang = torch.outer(torch.arange(seq_len, dtype=torch.float64), inv)
+    return ang.cos().float().to(device), ang.sin().float().to(device)
+
+
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        logits = _req(logits, "cross_entropy")
+        V = logits.shape[-1]
+        M = logits.numel() // V
+        labels = labels.reshape(M).to(torch.int64).contiguous()
+        lse = torch.empty(M, device=logits.device, dtype=torch.float32)
+        rows = torch.empty(M, device=logits.device, dtype=torch.float32)
+        _lib.check(_lib.lib().pto_ce_fwd(logits.data_ptr(), labels.data_ptr(), lse.data_ptr(), rows.data_ptr(), M, V,
+                                         ignore_index, _lib.stream_ptr(logits.device)), "ce_fwd")
+        count = (labels != ignore_index).sum().clamp_min(1).float()
+        ctx.save_for_backward(logits, labels, lse, count)
+        ctx.ignore_index = ignore_index
+        return rows.sum() / count
+
+    @staticmethod
+    def backward(ctx, gout):
+        logits, labels, lse, count = ctx.saved_tensors
+        V = logits.shape[-1]
+        M = logits.numel() // V
+        scale = (gout.float() / count).reshape(1)
+        # logits is an intermediate owned by this op (the producing GEMM's
+        # backward needs only its inputs), so the gradient overwrites it.
+        _lib.check(_lib.lib().pto_ce_bwd(logits.data_ptr(), labels.data_ptr(), lse.data_ptr(), scale.data_ptr(), M, V,
+                                         ctx.ignore_index, _lib.stream_ptr(logits.device)), "ce_bwd")
+        return logits, None, None
+
+
+def cross_entropy(logits, labels, ignore_index: int = -100):
+    """Mean token cross-entropy over non-ignored labels on bf16 logits."""
+    return _CrossEntropy.apply(logits, labels, ignore_index)

@@ -103,3 +103,83 @@ class FusedSGD(torch.optim.Optimizer):
             for p in g["params"]:
                 if p.grad is not None:
                     p.grad.zero_()
+
+
+class _AdamTensor(ctypes.Structure):
+    _fields_ = [("p", ctypes.c_void_p), ("g", ctypes.c_void_p), ("master", ctypes.c_void_p), ("m", ctypes.c_void_p),
+                ("v", ctypes.c_void_p), ("n", ctypes.c_longlong)]
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    """Multi-tensor AdamW in one HIP launch (csrc/kernels/optim_kernels.hip).
+
+    bf16 parameters get fp32 master weights and fp32 moments inside the
+    optimizer (``mixed``); fp32 parameters are updated in place.  Matches
+    ``torch.optim.AdamW`` (decoupled weight decay, bias correction) up to
+    the bf16 rounding of the exported parameter.  ``grad_scale`` folds a
+    DDP 1/world (or loss-scale) factor into the same pass.
+    """
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self._tables = None
+        self._step = 0
+
+    def _build(self):
+        L = _lib.lib()
+        self._tables = []
+        for group in self.param_groups:
+            recs, starts, nb, keep = [], [], 0, []
+            mixed = None
+            for p in group["params"]:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+                st = self.state[p]
+                is_mixed = p.dtype == torch.bfloat16
+                if mixed is None:
+                    mixed = is_mixed
+                if mixed != is_mixed:
+                    raise ValueError("FusedAdamW: a param group must be all-bf16 or all-fp32")
+                if "exp_avg" not in st:
+                    st["exp_avg"] = torch.zeros(p.shape, dtype=torch.float32, device=p.device)
+                    st["exp_avg_sq"] = torch.zeros(p.shape, dtype=torch.float32, device=p.device)
+                    if is_mixed:
+                        st["master"] = p.detach().float()
+                master = st.get("master")
+                recs.append(_AdamTensor(p.data_ptr(), p.grad.data_ptr(), 0 if master is None else master.data_ptr(),
+                                        st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), p.numel()))
+                starts.append(nb)
+                nb += L.pto_adamw_block_count(p.numel())
+                keep.append((p, p.grad, master, st["exp_avg"], st["exp_avg_sq"]))
+            raw = (_AdamTensor * len(recs))(*recs)
+            dev = group["params"][0].device
+            table = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(raw), ctypes.sizeof(raw))),
+                                     dtype=torch.uint8).to(dev)
+            self._tables.append((table, torch.tensor(starts, dtype=torch.int32, device=dev), len(recs), nb,
+                                 int(bool(mixed)), keep))
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_scale: float = 1.0, zero_grad: bool = False):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        ptrs_changed = self._tables is not None and any(
+            k[1] is not k[0].grad for t in self._tables for k in t[5])
+        if self._tables is None or ptrs_changed:
+            self._build()
+        self._step += 1
+        L = _lib.lib()
+        for group, (table, starts, nt, nb, mixed, _) in zip(self.param_groups, self._tables):
+            b1, b2 = group["betas"]
+            _lib.check(L.pto_adamw_multi(table.data_ptr(), starts.data_ptr(), nt, nb, mixed, None,
+                                         float(group["lr"]), float(b1), float(b2), float(group["eps"]),
+                                         float(group["weight_decay"]), self._step, float(grad_scale),
+                                         int(bool(zero_grad)), _lib.stream_ptr()), "adamw_multi")
+        return loss
+
+    def zero_grad(self, set_to_none: bool = False):
+        for g in self.param_groups:
+            for p in g["params"]:
+                if p.grad is not None:
+                    p.grad.zero_()

@@ -1,0 +1,139 @@
+"""Bucketed gradient all-reduce overlapped with backward, for the large
+DDP configs (ResNet-50, Llama-3-8B).
+
+Reference parity: the reference workload wraps its model in
+``nn.parallel.DistributedDataParallel`` (``examples/mnist/mnist.py:130-134``)
+and relies on its bucketing.  This is the MI355X-first replacement:
+
+* Gradients live in ONE flat buffer per dtype, laid out in reverse
+  registration order (the order backward produces them), and every
+  ``param.grad`` is a view into it: autograd accumulates straight into the
+  bucket, there is no copy-in/copy-out as in stock DDP buckets.
+* A ``post_accumulate_grad`` hook counts ready params per bucket; a full
+  bucket is all-reduced (SUM) at once on a dedicated comm stream after an
+  event on the compute stream, so RCCL runs over xGMI while backward keeps
+  computing the earlier layers.
+* The 1/world average is NOT a separate pass: the fused optimizers take
+  ``grad_scale`` and fold it into their single read of the gradient
+  (:meth:`grad_scale`), and zero the buffer in the same pass.
+* Bucket size defaults to 256 MB: xGMI is point-to-point (7 links x
+  ~150 GB/s per GPU), a ring all-reduce on 8 GPUs moves 2*(7/8)*size per
+  GPU, so large buckets amortise the per-collective latency
+  (~30-50 us) while still leaving >60 buckets to overlap with Llama-8B's
+  16 GB of bf16 gradients.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class GradBucketer:
+    def __init__(self, module: torch.nn.Module, bucket_mb: float | None = None, process_group=None,
+                 overlap: bool = True):
+        self.module = module
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.overlap = overlap and self.world > 1
+        bucket_mb = bucket_mb if bucket_mb is not None else float(os.environ.get("PTO_BUCKET_MB", "256"))
+        cap = int(bucket_mb * 1024 * 1024)
+        params = [p for p in module.parameters() if p.requires_grad]
+        if not params:
+            raise ValueError("GradBucketer: module has no trainable parameters")
+        dev = params[0].device
+        # one flat buffer per dtype, reverse registration order
+        self.flat: dict[torch.dtype, torch.Tensor] = {}
+        self.buckets: list[dict] = []
+        by_dtype: dict[torch.dtype, list] = {}
+        for p in reversed(params):
+            by_dtype.setdefault(p.dtype, []).append(p)
+        for dt, ps in by_dtype.items():
+            align = max(1, 256 // torch.empty((), dtype=dt).element_size())  # 256-byte aligned views
+            offs, total = [], 0
+            for p in ps:
+                offs.append(total)
+                total += (p.numel() + align - 1) // align * align
+            buf = torch.zeros(total, dtype=dt, device=dev)
+            self.flat[dt] = buf
+            cur, start = [], 0
+            for j, (p, o) in enumerate(zip(ps, offs)):
+                p.grad = buf[o:o + p.numel()].view_as(p)
+                cur.append(p)
+                end = offs[j + 1] if j + 1 < len(ps) else total  # include alignment padding
+                if (end - start) * buf.element_size() >= cap or j + 1 == len(ps):
+                    self.buckets.append(dict(params=cur, dtype=dt, lo=start, hi=end))
+                    cur, start = [], end
+        self._bucket_of = {}
+        for i, b in enumerate(self.buckets):
+            for p in b["params"]:
+                self._bucket_of[p] = i
+        self._pending = [0] * len(self.buckets)
+        self._works: list = []
+        self.comm_stream = torch.cuda.Stream(dev) if (self.overlap and dev.type == "cuda") else None
+        self._handles = []
+        if self.overlap:
+            for p in params:
+                self._handles.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        self.reset()
+
+    # ------------------------------------------------------------------
+    def reset(self):
+        self._pending = [len(b["params"]) for b in self.buckets]
+        self._works = []
+
+    def _bucket_view(self, b):
+        return self.flat[b["dtype"]][b["lo"]:b["hi"]]
+
+    def _launch(self, i):
+        b = self.buckets[i]
+        t = self._bucket_view(b)
+        if self.comm_stream is not None:
+            ev = torch.cuda.current_stream(t.device).record_event()
+            self.comm_stream.wait_event(ev)
+            with torch.cuda.stream(self.comm_stream):
+                self._works.append(dist.all_reduce(t, group=self.pg, async_op=True))
+        else:
+            self._works.append(dist.all_reduce(t, group=self.pg, async_op=True))
+
+    def _on_grad(self, p):
+        i = self._bucket_of[p]
+        self._pending[i] -= 1
+        if self._pending[i] == 0:
+            self._launch(i)
+
+    def finish(self):
+        """Call after ``loss.backward()``: launches any bucket whose params
+        produced no gradient, waits for all collectives, joins the streams."""
+        if self.world > 1:
+            if not self.overlap:
+                for i in range(len(self.buckets)):
+                    self._launch(i)
+            else:
+                for i, n in enumerate(self._pending):
+                    if n > 0:
+                        self._pending[i] = 0
+                        self._launch(i)
+            for w in self._works:
+                w.wait()
+            if self.comm_stream is not None:
+                torch.cuda.current_stream(self.comm_stream.device).wait_stream(self.comm_stream)
+        self.reset()
+
+    @property
+    def grad_scale(self) -> float:
+        """Factor the optimizer folds into its gradient read (SUM -> mean)."""
+        return 1.0 / self.world
+
+    def zero_(self):
+        for buf in self.flat.values():
+            buf.zero_()
+
+    def remove(self):
+        for h in self._handles:
+            h.remove()
+        self._handles = []
+
+    def grad_bytes(self) -> int:
+        return sum(b.numel() * b.element_size() for b in self.flat.values())

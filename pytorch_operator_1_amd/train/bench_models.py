@@ -1,0 +1,107 @@
+"""Large-model DDP training steps for BASELINE configs 3 and 4.
+
+* :class:`ResNetTrainer` — ResNet-50, ImageNet-shaped 224x224 synthetic
+  batches, channels_last + bf16 autocast, fp32 master params, SGD
+  momentum 0.9 / wd 1e-4 as one HIP launch (``FusedSGD``).
+* :class:`LlamaTrainer` — Llama-3-8B (or a smaller preset), bf16 params,
+  mixed-precision AdamW (fp32 master/m/v) as one HIP launch
+  (``FusedAdamW``), HIP kernels between the hipBLASLt GEMMs.
+
+Both use :class:`..parallel.ddp.GradBucketer`: grads accumulate straight
+into flat buckets that are all-reduced over RCCL/xGMI on a comm stream
+while backward continues; the 1/world average and grad zeroing are folded
+into the optimizer's single pass.  Each ``step()`` is a complete optimizer
+step (forward, backward, all-reduce, update) — nothing is skipped.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ..ops.optim import FusedAdamW, FusedSGD
+from ..parallel.ddp import GradBucketer
+
+
+class ResNetTrainer:
+    def __init__(self, device, batch_size: int = 256, image_size: int = 224, lr: float = 0.1,
+                 momentum: float = 0.9, weight_decay: float = 1e-4, seed: int = 0, bucket_mb: float | None = None):
+        from ..models.resnet import resnet50, synthetic_images
+
+        torch.manual_seed(seed)
+        self.device = device
+        self.batch_size = batch_size
+        self.model = resnet50().to(device=device, memory_format=torch.channels_last)
+        self.model.train()
+        self.bucketer = GradBucketer(self.model, bucket_mb=bucket_mb)
+        self.opt = FusedSGD(self.model.parameters(), lr=lr, momentum=momentum, weight_decay=weight_decay)
+        self.x, self.y = synthetic_images(batch_size, device, image_size, seed=seed)
+        self._loss = None
+
+    def step(self):
+        with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+            out = self.model(self.x)
+        loss = F.cross_entropy(out.float(), self.y)
+        loss.backward()
+        self.bucketer.finish()
+        self.opt.step(grad_scale=self.bucketer.grad_scale, zero_grad=True)
+        self._loss = loss.detach()
+
+    def run(self, n: int):
+        for _ in range(n):
+            self.step()
+
+    def last_loss(self):
+        return None if self._loss is None else float(self._loss)
+
+    def samples_per_step(self) -> int:
+        return self.batch_size
+
+    def describe(self) -> dict:
+        return {"model": "resnet50 (v1.5, 25.6M params)", "input_shape": [3, 224, 224],
+                "optimizer": "SGD momentum=0.9 wd=1e-4 (FusedSGD HIP)", "amp": "bf16 autocast, fp32 master"}
+
+
+class LlamaTrainer:
+    def __init__(self, device, model: str = "llama3-8b", batch_size: int = 2, seq_len: int = 4096,
+                 lr: float = 3e-4, weight_decay: float = 0.1, seed: int = 0, checkpoint: str = "none",
+                 impl: str = "hip", bucket_mb: float | None = None):
+        from ..models.llama import CONFIGS, Llama, synthetic_tokens
+
+        torch.manual_seed(seed)
+        self.cfg = CONFIGS[model]
+        self.name = model
+        self.device = device
+        self.batch_size, self.seq_len = batch_size, seq_len
+        self.model = Llama(self.cfg, impl=impl, device=device, checkpoint=checkpoint)
+        self.model.train()
+        self.bucketer = GradBucketer(self.model, bucket_mb=bucket_mb)
+        self.opt = FusedAdamW(self.model.parameters(), lr=lr, betas=(0.9, 0.95), eps=1e-8,
+                              weight_decay=weight_decay)
+        self.tokens, self.labels = synthetic_tokens(batch_size, seq_len, self.cfg.vocab_size, device, seed=seed)
+        self._loss = None
+
+    def step(self):
+        loss = self.model(self.tokens, self.labels)
+        loss.backward()
+        self.bucketer.finish()
+        self.opt.step(grad_scale=self.bucketer.grad_scale, zero_grad=True)
+        self._loss = loss.detach()
+
+    def run(self, n: int):
+        for _ in range(n):
+            self.step()
+
+    def last_loss(self):
+        return None if self._loss is None else float(self._loss)
+
+    def samples_per_step(self) -> int:
+        return self.batch_size * self.seq_len  # tokens
+
+    def flops_per_step(self) -> float:
+        return self.cfg.train_flops_per_token(self.seq_len) * self.samples_per_step()
+
+    def describe(self) -> dict:
+        return {"model": f"{self.name} ({self.cfg.num_params() / 1e9:.2f}B params)",
+                "optimizer": "AdamW betas=(0.9,0.95) wd=0.1 (FusedAdamW HIP, fp32 master/m/v)",
+                "amp": "bf16 params/activations, fp32 optimizer state",
+                "checkpoint": self.model.checkpoint}

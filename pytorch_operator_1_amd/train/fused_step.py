@@ -37,8 +37,10 @@ from ..ops import _lib
 class FusedMnistTrainer:
     def __init__(self, device, batch_size=64, lr=0.01, momentum=0.5, dataset_size=60000, seed=1, rank=0,
                  weight_decay=0.0, nesterov=False, graph: str | None = None, comm: str | None = None,
-                 data=None, target=None):
+                 data=None, target=None, unroll: int | None = None, force_ddp: bool = False):
         assert device.type == "cuda", "FusedMnistTrainer runs on a HIP device"
+        import os
+
         self.L = _lib.lib()
         self.device = device
         self.B = int(batch_size)
@@ -47,7 +49,21 @@ class FusedMnistTrainer:
         self.weight_decay = float(weight_decay)
         self.nesterov = bool(nesterov)
         self.world = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
-        self.graph_mode = graph or ("full" if self.world == 1 else "split")
+        # DDP code path (bucketed, overlapped all-reduce); forced for tests
+        # of the collective path at world size 1
+        self.ddp = self.world > 1 or force_ddp
+        # graph modes: "full" = the whole step (collectives included) is one
+        # HIP graph; "split" = collectives issued eagerly between graphs;
+        # "none" = eager launches.  RCCL all-reduces are captured into the
+        # graph by default (validated by tests/test_graph_gpu.py); gloo
+        # collectives are host-side and cannot be captured, so they always
+        # use "split" (PTO_CAPTURE_COMM=0 forces it for RCCL too).
+        capture_comm = os.environ.get("PTO_CAPTURE_COMM", "1") == "1"
+        if self.ddp and dist.is_initialized() and dist.get_backend() != "nccl":
+            capture_comm = False
+        self.graph_mode = graph or ("full" if (not self.ddp or capture_comm) else "split")
+        # steps per graph replay in run(): amortises the host launch gap
+        self.unroll = int(unroll if unroll is not None else os.environ.get("PTO_GRAPH_UNROLL", "8"))
         self.comm = comm or "rccl"
 
         offs, total = param_offsets()
@@ -97,6 +113,7 @@ class FusedMnistTrainer:
         self.sgd = SgdTable([(self.params, self.grads, self.mom)], device)
         self.lr_dev = torch.tensor([self.lr], **f32)
         self._graphs = None
+        self._graph_unrolled = None
         self._static_ar = None
         self.steps_done = 0
         if self.world > 1 and self.comm == "xgmi":
@@ -168,8 +185,24 @@ class FusedMnistTrainer:
                       zero_grad=True, stream=self._s(), batch_cursor=self.batch_idx, n_batches=self.n_batches)
 
     def _eager_step(self):
+        if self.ddp and self._xgmi is None:
+            self._ddp_step()
+            return
         self.forward_backward()
         self.allreduce()
+        self.optimizer_step()
+
+    def _ddp_step(self):
+        """Bucket 0 (fc grads, 94% of the bytes) all-reduces on RCCL's
+        stream while the conv backward runs; bucket 1 follows; the
+        optimizer waits for both.  Valid eagerly and under graph capture."""
+        fc_b, conv_b = self._bucket_views()
+        self.forward_fc_backward()
+        w0 = dist.all_reduce(fc_b, async_op=True)
+        self.conv_backward()
+        w1 = dist.all_reduce(conv_b, async_op=True)
+        w0.wait()
+        w1.wait()
         self.optimizer_step()
 
     def _capture(self):
@@ -192,6 +225,12 @@ class FusedMnistTrainer:
             with torch.cuda.graph(g):
                 self._eager_step()
             graphs = [g]
+            if self.unroll > 1:  # U consecutive steps in one graph (device batch cursor)
+                gu = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gu):
+                    for _ in range(self.unroll):
+                        self._eager_step()
+                self._graph_unrolled = gu
         else:  # split: collectives outside the graphs, overlapped with conv bwd
             ga, gb, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(ga):
@@ -203,15 +242,41 @@ class FusedMnistTrainer:
             graphs = [ga, gb, gc]
         self._graphs = graphs
 
+    def _ensure_captured(self):
+        if self._graphs is not None:
+            return
+        try:
+            self._capture()
+        except Exception as e:  # noqa: BLE001 - capture of collectives unsupported
+            if self.graph_mode != "full" or not self.ddp:
+                raise
+            import warnings
+
+            warnings.warn(f"HIP-graph capture of the DDP step failed ({e}); using split graphs")
+            torch.cuda.synchronize(self.device)
+            self.graph_mode = "split"
+            self._capture()
+
+    def run(self, n: int):
+        """Run exactly ``n`` training steps (replaying the U-step graph
+        n // U times, then single-step graphs for the remainder)."""
+        if self.graph_mode == "full" and self.unroll > 1:
+            self._ensure_captured()
+            for _ in range(n // self.unroll):
+                self._graph_unrolled.replay()
+            self.steps_done += (n // self.unroll) * self.unroll
+            n %= self.unroll
+        for _ in range(n):
+            self.step()
+
     def step(self):
         if self.graph_mode == "none":
             self._eager_step()
         else:
-            if self._graphs is None:
-                self._capture()
+            self._ensure_captured()
             if self.graph_mode == "full":
                 self._graphs[0].replay()
-            elif self.world == 1:
+            elif not self.ddp:
                 for g in self._graphs:
                     g.replay()
             else:

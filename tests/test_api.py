@@ -133,3 +133,13 @@ def test_example_manifests_validate():
                         assert crd.openapi_check(doc) is None
                         n += 1
     assert n >= 3
+
+
+def test_generated_artifacts_up_to_date():
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "hack", "gen_manifests.py"), "--verify"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
