@@ -256,19 +256,28 @@ __global__ __launch_bounds__(NT) void k_swiglu_bwd(const uint16_t* __restrict__ 
 // qkv row m = (b*S + s) has nh heads of D at stride row_stride; rotate the
 // first nrot heads (q and k).  rotate_half convention: pairs (i, i + D/2).
 // cs = [S][D/2] cos, sn = [S][D/2] sin (fp32).  sign = +1 fwd, -1 bwd.
-__global__ __launch_bounds__(NT) void k_rope(uint16_t* __restrict__ qkv, const float* __restrict__ cs,
-                                             const float* __restrict__ sn, long long M, int S, int nrot, int D,
+// src == dst: in place over the nrot heads only (nh == nrot).  src != dst:
+// all nh heads are written, heads >= nrot copied unchanged (backward: the
+// incoming gradient is never modified).
+__global__ __launch_bounds__(NT) void k_rope(const uint16_t* src, uint16_t* dst, const float* __restrict__ cs,
+                                             const float* __restrict__ sn, long long M, int S, int nrot, int nh, int D,
                                              long long row_stride, float sign) {
   const int H2 = D >> 1, Q = H2 >> 2;  // 4 pairs per thread
-  const long long total = M * nrot * Q;
+  const long long total = M * nh * Q;
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
     const int q = (int)(i % Q);
     const long long t = i / Q;
-    const int hd = (int)(t % nrot);
-    const long long m = t / nrot;
+    const int hd = (int)(t % nh);
+    const long long m = t / nh;
     const int s = (int)(m % S);
-    uint16_t* base = qkv + m * row_stride + (long long)hd * D + q * 4;
-    const uint2 lo = *reinterpret_cast<const uint2*>(base), hi = *reinterpret_cast<const uint2*>(base + H2);
+    const long long off = m * row_stride + (long long)hd * D + q * 4;
+    const uint2 lo = *reinterpret_cast<const uint2*>(src + off), hi = *reinterpret_cast<const uint2*>(src + off + H2);
+    uint16_t* base = dst + off;
+    if (hd >= nrot) {
+      *reinterpret_cast<uint2*>(base) = lo;
+      *reinterpret_cast<uint2*>(base + H2) = hi;
+      continue;
+    }
     const float4 c = *reinterpret_cast<const float4*>(cs + (long long)s * H2 + q * 4);
     const float4 n = *reinterpret_cast<const float4*>(sn + (long long)s * H2 + q * 4);
     const float x1[4] = {__uint_as_float(lo.x << 16), __uint_as_float(lo.x & 0xffff0000u), __uint_as_float(lo.y << 16),
@@ -403,11 +412,15 @@ PTO_API int pto_swiglu_bwd(const void* gu, const void* dout, void* dgu, long lon
   return (int)hipGetLastError();
 }
 
-PTO_API int pto_rope(void* qkv, const float* cs, const float* sn, long long M, int S, int nrot, int D,
-                     long long row_stride, int backward, hipStream_t s) {
+// out == nullptr: in place on the first nrot heads.  Otherwise out receives
+// every one of the nh heads (rotated or copied).
+PTO_API int pto_rope(const void* qkv, void* out, const float* cs, const float* sn, long long M, int S, int nrot,
+                     int nh, int D, long long row_stride, int backward, hipStream_t s) {
   if (D % 8) return -1;
-  hipLaunchKernelGGL(k_rope, dim3(grid_for(M * nrot * (D / 8))), dim3(NT), 0, s, (uint16_t*)qkv, cs, sn, M, S, nrot,
-                     D, row_stride, backward ? -1.f : 1.f);
+  const int heads = out ? nh : nrot;
+  hipLaunchKernelGGL(k_rope, dim3(grid_for(M * heads * (D / 8))), dim3(NT), 0, s, (const uint16_t*)qkv,
+                     out ? (uint16_t*)out : (uint16_t*)qkv, cs, sn, M, S, nrot, heads, D, row_stride,
+                     backward ? -1.f : 1.f);
   return (int)hipGetLastError();
 }
 

@@ -118,8 +118,8 @@ class _RoPE(torch.autograd.Function):
             raise ValueError("rope_: qkv must be contiguous")
         _req(qkv, "rope_")
         M = qkv.numel() // qkv.shape[-1]
-        _lib.check(_lib.lib().pto_rope(qkv.data_ptr(), cos.data_ptr(), sin.data_ptr(), M, seq_len, n_rot, head_dim,
-                                       qkv.shape[-1], 0, _lib.stream_ptr(qkv.device)), "rope_fwd")
+        _lib.check(_lib.lib().pto_rope(qkv.data_ptr(), None, cos.data_ptr(), sin.data_ptr(), M, seq_len, n_rot, 0,
+                                       head_dim, qkv.shape[-1], 0, _lib.stream_ptr(qkv.device)), "rope_fwd")
         ctx.mark_dirty(qkv)
         ctx.save_for_backward(cos, sin)
         ctx.cfg = (seq_len, n_rot, head_dim)
@@ -129,15 +129,13 @@ class _RoPE(torch.autograd.Function):
     def backward(ctx, g):
         cos, sin = ctx.saved_tensors
         S, n_rot, D = ctx.cfg
-        # rotate in place when autograd handed us a fresh buffer of our own
-        if not g.is_contiguous():
-            g = g.contiguous()
-        elif g._base is not None:
-            g = g.clone()
+        # out of place: the incoming gradient may be referenced elsewhere
+        g = g.contiguous()
+        dg = torch.empty_like(g)
         M = g.numel() // g.shape[-1]
-        _lib.check(_lib.lib().pto_rope(g.data_ptr(), cos.data_ptr(), sin.data_ptr(), M, S, n_rot, D, g.shape[-1], 1,
-                                       _lib.stream_ptr(g.device)), "rope_bwd")
-        return g, None, None, None, None, None
+        _lib.check(_lib.lib().pto_rope(g.data_ptr(), dg.data_ptr(), cos.data_ptr(), sin.data_ptr(), M, S, n_rot,
+                                       g.shape[-1] // D, D, g.shape[-1], 1, _lib.stream_ptr(g.device)), "rope_bwd")
+        return dg, None, None, None, None, None
 
 
 def rope_(qkv, cos, sin, seq_len: int, n_rot: int, head_dim: int):
