@@ -124,6 +124,7 @@ def main(argv=None):
                 "backend": (torch.distributed.get_backend() if n > 1 else "none"),
                 "baseline": "210 samples/s/rank (BASELINE.md, derived lower bound); vs_baseline = value/(210*n_gpus)",
                 "final_loss": round(loss, 4) if loss is not None else None,
+                "grad_allreduce": getattr(trainer, "comm_info", None),
             },
         }
         print(json.dumps(out), flush=True)

@@ -1,0 +1,190 @@
+// Single-node gradient all-reduce over xGMI peer memory (IPC-mapped HBM
+// of the other ranks), for the small/medium DDP buckets where RCCL's
+// per-collective latency dominates (MNIST: 1.7 MB of fp32 gradients per
+// step; RCCL ring/tree setup costs tens of microseconds for that size).
+//
+// Algorithm: two-stage "pull" all-reduce, every write local:
+//   barrier 1   every rank's input is complete (stream order) and published
+//   stage 1     rank r sums chunk r of ALL ranks' inputs (fixed rank order, so
+//               every rank ends with bit-identical results) -> own tmp[chunk r]
+//   barrier 2   all partial sums published
+//   stage 2     rank r pulls chunk q from rank q's tmp for every q -> own input
+// Per rank that is 2 x (W-1)/W x bytes read over xGMI (the same as a
+// reduce-scatter + all-gather ring) but in ONE launch with two barriers,
+// no ring steps.  The barriers are per workgroup: workgroup b of every rank
+// owns the same sub-range of every chunk, so block b only waits for block b
+// of the peers (no grid-wide sync).
+//
+// Hazards covered by construction: a rank only overwrites its input in
+// stage 2 (after every peer finished reading it in stage 1 = barrier 2),
+// and only overwrites tmp in the NEXT call's stage 1 (after barrier 1 of
+// that call, which peers only reach once their previous launch, including
+// its stage-2 reads of this tmp, has completed).
+//
+// Visibility (MI355X_MICROARCH.md "inter-workgroup visibility", applied at
+// system scope because readers are other devices): producer = stores ->
+// s_waitcnt vmcnt(0) -> barrier -> release fence (system: L2 write-back) ->
+// s_waitcnt vmcnt(0) -> relaxed system flag store; consumer = relaxed poll ->
+// system acquire (L1/L2 invalidate) -> s_waitcnt -> barrier -> loads.
+// Flags live in uncached memory; every spin is bounded (2 s) and reports a
+// timeout through *err instead of hanging the device.
+//
+// Two independent "channels" (flag sets + epochs) let two buckets be in
+// flight at once on different streams (fc bucket overlapped with the conv
+// backward, then the conv bucket).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#define PTO_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int AR_MAX_RANKS = 8;
+constexpr int AR_MAX_BLOCKS = 64;
+constexpr int AR_CHANNELS = 2;
+constexpr int AR_THREADS = 512;
+constexpr long long AR_TIMEOUT_TICKS = 200000000LL;  // wall_clock64 runs at 100 MHz: 2 s
+
+struct ArPeers {
+  float* in[AR_MAX_RANKS];
+  float* tmp[AR_MAX_RANKS];
+  uint32_t* flags[AR_MAX_RANKS];
+};
+
+__host__ __device__ constexpr int flag_index(int chan, int phase, int block, int src) {
+  return ((chan * 2 + phase) * AR_MAX_BLOCKS + block) * AR_MAX_RANKS + src;
+}
+constexpr int AR_FLAG_WORDS = AR_CHANNELS * 2 * AR_MAX_BLOCKS * AR_MAX_RANKS;
+
+__device__ __forceinline__ bool block_barrier(const ArPeers& P, int chan, int phase, int rank, int world, uint32_t e,
+                                              int* err) {
+  const int t = threadIdx.x, b = blockIdx.x;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  bool ok = true;
+  if (t < world) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back this XCD's L2
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(P.flags[t] + flag_index(chan, phase, b, rank), e, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* f = P.flags[rank] + flag_index(chan, phase, b, t);
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+      if (wall_clock64() - t0 > AR_TIMEOUT_TICKS) {
+        atomicOr(err, 1 << phase);
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // invalidate L1/L2 before reading peer data
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  return ok;
+}
+
+// n4 float4 elements starting at float offset `off` of every rank's buffers.
+__global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce(const ArPeers* __restrict__ peers, long long off,
+                                                               long long n4, int rank, int world, int chan,
+                                                               uint32_t* __restrict__ epochs, int* err) {
+  __shared__ uint32_t s_epoch;
+  const ArPeers P = *peers;
+  if (threadIdx.x == 0) s_epoch = epochs[chan * AR_MAX_BLOCKS + blockIdx.x] + 1;
+  __syncthreads();
+  const uint32_t e = s_epoch;
+  const long long cs = (n4 + world - 1) / world;  // chunk length (float4)
+  const long long stride = (long long)gridDim.x * AR_THREADS;
+
+  block_barrier(P, chan, 0, rank, world, e, err);
+  // stage 1: reduce my chunk over all ranks (rank order 0..W-1 everywhere)
+  {
+    const long long c0 = (long long)rank * cs, c1 = min(n4, c0 + cs);
+    for (long long i = c0 + (long long)blockIdx.x * AR_THREADS + threadIdx.x; i < c1; i += stride) {
+      float4 v[AR_MAX_RANKS];
+#pragma unroll
+      for (int q = 0; q < AR_MAX_RANKS; ++q)
+        if (q < world) v[q] = reinterpret_cast<const float4*>(P.in[q] + off)[i];
+      float4 a = v[0];
+#pragma unroll
+      for (int q = 1; q < AR_MAX_RANKS; ++q)
+        if (q < world) {
+          a.x += v[q].x;
+          a.y += v[q].y;
+          a.z += v[q].z;
+          a.w += v[q].w;
+        }
+      reinterpret_cast<float4*>(P.tmp[rank] + off)[i] = a;
+    }
+  }
+  block_barrier(P, chan, 1, rank, world, e, err);
+  // stage 2: gather every chunk into my input
+  for (long long j = (long long)blockIdx.x * AR_THREADS + threadIdx.x; j < cs; j += stride) {
+    float4 v[AR_MAX_RANKS];
+#pragma unroll
+    for (int q = 0; q < AR_MAX_RANKS; ++q)
+      if (q < world && (long long)q * cs + j < n4) v[q] = reinterpret_cast<const float4*>(P.tmp[q] + off)[q * cs + j];
+#pragma unroll
+    for (int q = 0; q < AR_MAX_RANKS; ++q)
+      if (q < world && (long long)q * cs + j < n4) reinterpret_cast<float4*>(P.in[rank] + off)[q * cs + j] = v[q];
+  }
+  if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blockIdx.x] = e;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- host API
+PTO_API int pto_ar_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+PTO_API int pto_ar_flag_bytes(int) { return AR_FLAG_WORDS * (int)sizeof(uint32_t); }
+PTO_API int pto_ar_max_ranks() { return AR_MAX_RANKS; }
+PTO_API int pto_ar_peers_bytes() { return (int)sizeof(ArPeers); }
+PTO_API int pto_ar_epoch_words() { return AR_CHANNELS * AR_MAX_BLOCKS; }
+
+// Flags: uncached device memory, zeroed.
+PTO_API int pto_ar_alloc_flags(void** out) {
+  hipError_t e = hipExtMallocWithFlags(out, (size_t)AR_FLAG_WORDS * sizeof(uint32_t), hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipMemset(*out, 0, (size_t)AR_FLAG_WORDS * sizeof(uint32_t));
+}
+PTO_API int pto_ar_free(void* p) { return (int)hipFree(p); }
+
+// IPC handle of the allocation containing ptr, plus ptr's byte offset in it.
+PTO_API int pto_ar_get_ipc_handle(void* ptr, void* handle_out, long long* offset_out) {
+  void* base = nullptr;
+  size_t size = 0;
+  hipError_t e = hipMemGetAddressRange(&base, &size, ptr);
+  if (e != hipSuccess) return (int)e;
+  *offset_out = (long long)((char*)ptr - (char*)base);
+  return (int)hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle_out), base);
+}
+PTO_API int pto_ar_open_ipc_handle(const void* handle, void** ptr_out) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof h);
+  return (int)hipIpcOpenMemHandle(ptr_out, h, hipIpcMemLazyEnablePeerAccess);
+}
+PTO_API int pto_ar_close_ipc_handle(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
+
+// Workgroups used for n floats (identical on every rank: derived from n, W).
+PTO_API int pto_ar_blocks(long long n, int world) {
+  const long long cs = ((n / 4) + world - 1) / world;
+  long long b = (cs + AR_THREADS - 1) / AR_THREADS;
+  if (b < 1) b = 1;
+  if (b > AR_MAX_BLOCKS) b = AR_MAX_BLOCKS;
+  return (int)b;
+}
+
+// In-place SUM all-reduce of n floats at float offset `off` of the registered
+// input buffers.  peers: device copy of ArPeers.  Requires n % 4 == 0,
+// off % 4 == 0, 1 < world <= 8, chan < 2.
+PTO_API int pto_ar_allreduce(const void* peers, long long off, long long n, int rank, int world, int chan,
+                             void* epochs, void* err, hipStream_t s) {
+  if (n % 4 || off % 4 || world < 2 || world > AR_MAX_RANKS || chan < 0 || chan >= AR_CHANNELS || rank < 0 ||
+      rank >= world)
+    return -1;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_xgmi_allreduce, dim3(pto_ar_blocks(n, world)), dim3(AR_THREADS), 0, s,
+                     reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,
+                     reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err));
+  return (int)hipGetLastError();
+}

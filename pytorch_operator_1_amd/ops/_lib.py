@@ -107,13 +107,19 @@ _SIGS = {
     "pto_rope": [_P, _P, _P, _P, _L, _I, _I, _I, _I, _L, _I, _P],
     "pto_ce_fwd": [_P, _P, _P, _P, _L, _I, _L, _P],
     "pto_ce_bwd": [_P, _P, _P, _P, _L, _I, _L, _P],
-    # xGMI peer all-reduce (csrc/comm)
+    # xGMI peer all-reduce (csrc/comm/xgmi_allreduce.hip)
     "pto_ar_ipc_handle_size": [],
-    "pto_ar_get_ipc_handle": [_P, _P],
+    "pto_ar_flag_bytes": [_I],
+    "pto_ar_max_ranks": [],
+    "pto_ar_peers_bytes": [],
+    "pto_ar_epoch_words": [],
+    "pto_ar_alloc_flags": [ctypes.POINTER(ctypes.c_void_p)],
+    "pto_ar_free": [_P],
+    "pto_ar_get_ipc_handle": [_P, _P, ctypes.POINTER(ctypes.c_longlong)],
     "pto_ar_open_ipc_handle": [_P, ctypes.POINTER(ctypes.c_void_p)],
     "pto_ar_close_ipc_handle": [_P],
-    "pto_ar_allreduce": [_P, _P, _L, _I, _I, _P, _P, _I, _F, _P],
-    "pto_ar_flag_bytes": [_I],
+    "pto_ar_blocks": [_L, _I],
+    "pto_ar_allreduce": [_P, _L, _L, _I, _I, _I, _P, _P, _P],
 }
 
 

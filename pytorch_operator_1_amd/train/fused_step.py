@@ -52,19 +52,12 @@ class FusedMnistTrainer:
         # DDP code path (bucketed, overlapped all-reduce); forced for tests
         # of the collective path at world size 1
         self.ddp = self.world > 1 or force_ddp
-        # graph modes: "full" = the whole step (collectives included) is one
-        # HIP graph; "split" = collectives issued eagerly between graphs;
-        # "none" = eager launches.  RCCL all-reduces are captured into the
-        # graph by default (validated by tests/test_graph_gpu.py); gloo
-        # collectives are host-side and cannot be captured, so they always
-        # use "split" (PTO_CAPTURE_COMM=0 forces it for RCCL too).
-        capture_comm = os.environ.get("PTO_CAPTURE_COMM", "1") == "1"
-        if self.ddp and dist.is_initialized() and dist.get_backend() != "nccl":
-            capture_comm = False
-        self.graph_mode = graph or ("full" if (not self.ddp or capture_comm) else "split")
         # steps per graph replay in run(): amortises the host launch gap
         self.unroll = int(unroll if unroll is not None else os.environ.get("PTO_GRAPH_UNROLL", "8"))
-        self.comm = comm or "rccl"
+        # gradient all-reduce transport: "rccl", "xgmi" (peer-memory kernel,
+        # parallel/xgmi.py) or "auto" (xGMI if it verifies and beats RCCL on
+        # these buckets, measured at startup; same choice on every rank)
+        self.comm = comm or os.environ.get("PTO_COMM", "auto")
 
         offs, total = param_offsets()
         self.numel = total
@@ -116,12 +109,46 @@ class FusedMnistTrainer:
         self._graph_unrolled = None
         self._static_ar = None
         self.steps_done = 0
-        if self.world > 1 and self.comm == "xgmi":
-            from ..parallel.xgmi import XgmiAllReduce
+        self._xgmi, self.comm_info = None, {"transport": "none" if self.world == 1 else "rccl"}
+        if self.world > 1 and self.comm in ("xgmi", "auto"):
+            self._setup_xgmi()
+        self._side = torch.cuda.Stream(device) if self._xgmi is not None else None
+        # graph modes: "full" = the whole step (collectives included) is one
+        # HIP graph; "split" = collectives issued eagerly between graphs;
+        # "none" = eager launches.  The xGMI kernel and RCCL all-reduces are
+        # captured into the graph by default (validated by
+        # tests/test_graph_gpu.py); gloo collectives are host-side and cannot
+        # be captured, so they use "split" (PTO_CAPTURE_COMM=0 forces it).
+        capture_comm = os.environ.get("PTO_CAPTURE_COMM", "1") == "1"
+        if (self.ddp and self._xgmi is None and dist.is_initialized() and dist.get_backend() != "nccl"):
+            capture_comm = False
+        self.graph_mode = graph or ("full" if (not self.ddp or capture_comm) else "split")
+        if self._xgmi is not None and self.graph_mode == "split":
+            self.graph_mode = "full"  # the xGMI kernel is plain stream work
 
-            self._xgmi = XgmiAllReduce(self.grads, device)
+    def _setup_xgmi(self):
+        from ..parallel.xgmi import XgmiAllReduce
+
+        try:
+            ar = XgmiAllReduce(self.grads)
+        except (RuntimeError, ValueError) as e:  # collective failure: every rank raises
+            if self.comm == "xgmi":
+                raise
+            self.comm_info = {"transport": "rccl", "xgmi_error": str(e)}
+            return
+        split = self._split()
+        tune = ar.autotune([(0, split), (split, self.numel - split)])
+        if self.comm == "xgmi" and not tune["correct"]:
+            raise RuntimeError(f"xGMI all-reduce failed verification: {tune}")
+        if self.comm == "xgmi" or tune["use_xgmi"]:
+            self._xgmi = ar
+            self.comm_info = dict(tune, transport="xgmi")
         else:
-            self._xgmi = None
+            ar.close()
+            self.comm_info = dict(tune, transport="rccl")
+
+    def _split(self) -> int:
+        return param_offsets()[0]["conv2.weight"][0]
 
     # ------------------------------------------------------------------
     def _s(self):
@@ -169,14 +196,14 @@ class FusedMnistTrainer:
         if self.world == 1:
             return
         if self._xgmi is not None:
-            self._xgmi(self._s())
+            self._xgmi.allreduce_(0, self.numel)
         else:
             dist.all_reduce(self.grads)
 
     def _bucket_views(self):
         """Two DDP buckets in backward order: fc grads, conv grads."""
         if not hasattr(self, "_buckets"):
-            split = param_offsets()[0]["conv2.weight"][0]
+            split = self._split()
             self._buckets = (self.grads[:split], self.grads[split:])
         return self._buckets
 
@@ -185,11 +212,27 @@ class FusedMnistTrainer:
                       zero_grad=True, stream=self._s(), batch_cursor=self.batch_idx, n_batches=self.n_batches)
 
     def _eager_step(self):
-        if self.ddp and self._xgmi is None:
+        if self.ddp and self._xgmi is not None:
+            self._xgmi_step()
+            return
+        if self.ddp:
             self._ddp_step()
             return
         self.forward_backward()
-        self.allreduce()
+        self.optimizer_step()
+
+    def _xgmi_step(self):
+        """fc bucket all-reduced by the xGMI kernel on a side stream while
+        the conv backward runs, conv bucket after it; the optimizer joins
+        both.  Pure stream work: capturable into one graph."""
+        split = self._split()
+        cur = torch.cuda.current_stream(self.device)
+        self.forward_fc_backward()
+        self._side.wait_stream(cur)
+        self._xgmi.allreduce_(0, split, chan=0, stream=self._side)
+        self.conv_backward()
+        self._xgmi.allreduce_(split, self.numel - split, chan=1)
+        cur.wait_stream(self._side)
         self.optimizer_step()
 
     def _ddp_step(self):

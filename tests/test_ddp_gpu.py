@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, comm):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import torch.distributed as dist
 
@@ -34,7 +34,8 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=N, seed=1, rank=rank)
+    tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=N, seed=1, rank=rank, comm=comm)
+    assert comm != "xgmi" or (tr.comm_info["transport"] == "xgmi" and tr.graph_mode == "full")
     for _ in range(STEPS):
         tr.step()
     torch.cuda.synchronize()
@@ -43,11 +44,14 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_fused_ddp_two_ranks_matches_reference():
+@pytest.mark.parametrize("comm", ["rccl", "xgmi"])
+def test_fused_ddp_two_ranks_matches_reference(comm):
+    """comm=rccl: host collectives (gloo here) between split graphs;
+    comm=xgmi: peer-memory all-reduce kernel inside the whole-step graph."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, comm)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in range(2))
