@@ -25,6 +25,14 @@ class _SgdTensor(ctypes.Structure):
     _fields_ = [("p", ctypes.c_void_p), ("g", ctypes.c_void_p), ("m", ctypes.c_void_p), ("n", ctypes.c_longlong)]
 
 
+def _same_dense_layout(*ts) -> bool:
+    """Elementwise multi-tensor kernels walk the raw storage, so every tensor
+    of a record must be dense (contiguous or channels_last) with equal strides."""
+    t0 = ts[0]
+    dense = t0.is_contiguous() or (t0.dim() == 4 and t0.is_contiguous(memory_format=torch.channels_last))
+    return dense and all(t is None or (t.shape == t0.shape and t.stride() == t0.stride()) for t in ts)
+
+
 class SgdTable:
     def __init__(self, triples, device):
         L = _lib.lib()
@@ -32,7 +40,8 @@ class SgdTable:
         recs, starts, nb = [], [], 0
         self._keep = []
         for p, g, m in triples:
-            assert p.dtype == torch.float32 and p.is_contiguous() and g.is_contiguous()
+            if p.dtype != torch.float32 or not _same_dense_layout(p, g, m):
+                raise ValueError("SgdTable: fp32 params with grads/momentum of the same dense layout required")
             recs.append((p.data_ptr(), g.data_ptr(), 0 if m is None else m.data_ptr(), p.numel()))
             starts.append(nb)
             nb += L.pto_sgd_block_count(p.numel())
@@ -141,11 +150,13 @@ class FusedAdamW(torch.optim.Optimizer):
                 if mixed != is_mixed:
                     raise ValueError("FusedAdamW: a param group must be all-bf16 or all-fp32")
                 if "exp_avg" not in st:
-                    st["exp_avg"] = torch.zeros(p.shape, dtype=torch.float32, device=p.device)
-                    st["exp_avg_sq"] = torch.zeros(p.shape, dtype=torch.float32, device=p.device)
+                    st["exp_avg"] = torch.zeros_like(p, dtype=torch.float32)  # keeps p's layout
+                    st["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32)
                     if is_mixed:
                         st["master"] = p.detach().float()
                 master = st.get("master")
+                if not _same_dense_layout(p, p.grad, master, st["exp_avg"], st["exp_avg_sq"]):
+                    raise ValueError("FusedAdamW: param, grad and state must share one dense layout")
                 recs.append(_AdamTensor(p.data_ptr(), p.grad.data_ptr(), 0 if master is None else master.data_ptr(),
                                         st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), p.numel()))
                 starts.append(nb)

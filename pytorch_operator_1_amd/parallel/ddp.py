@@ -59,7 +59,8 @@ class GradBucketer:
             self.flat[dt] = buf
             cur, start = [], 0
             for j, (p, o) in enumerate(zip(ps, offs)):
-                p.grad = buf[o:o + p.numel()].view_as(p)
+                # same strides as the param (channels_last convs stay NHWC)
+                p.grad = buf[o:o + p.numel()].as_strided(p.shape, p.stride())
                 cur.append(p)
                 end = offs[j + 1] if j + 1 < len(ps) else total  # include alignment padding
                 if (end - start) * buf.element_size() >= cap or j + 1 == len(ps):

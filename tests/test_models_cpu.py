@@ -119,3 +119,30 @@ def test_grad_bucketer_two_rank_gloo():
     for _, err, scale in res:
         assert err < 1e-4
         assert scale == 0.5
+
+
+def test_grad_bucketer_channels_last_views_accumulate_in_place():
+    import torch.nn as nn
+
+    from pytorch_operator_1_amd.parallel.ddp import GradBucketer
+
+    torch.manual_seed(0)
+
+    def net():
+        return nn.Sequential(nn.Conv2d(3, 8, 3), nn.BatchNorm2d(8), nn.ReLU(),
+                             nn.Conv2d(8, 4, 3)).to(memory_format=torch.channels_last)
+
+    m, ref = net(), net()
+    ref.load_state_dict(m.state_dict())
+    bk = GradBucketer(m, bucket_mb=0.001)
+    x = torch.randn(2, 3, 10, 10).contiguous(memory_format=torch.channels_last)
+    flat_ptr = next(iter(bk.flat.values())).data_ptr()
+    for _ in range(2):  # grads accumulate across backward calls like .grad does
+        m(x).sum().backward()
+        bk.finish()
+        ref(x).sum().backward()
+    for p, q in zip(m.parameters(), ref.parameters()):
+        torch.testing.assert_close(p.grad, q.grad, atol=1e-5, rtol=1e-5)
+        assert p.grad.stride() == p.stride()
+    w = m[0].weight.grad
+    assert w.untyped_storage().data_ptr() == flat_ptr  # still a view of the bucket buffer
