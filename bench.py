@@ -43,6 +43,9 @@ def parse_args(argv=None):
     p.add_argument("--batch-size", type=int, default=None, help="per-rank batch (64 mnist, 256 resnet50, 2 llama)")
     p.add_argument("--seq-len", type=int, default=4096, help="llama sequence length")
     p.add_argument("--checkpoint", choices=["none", "full"], default="none", help="llama activation checkpointing")
+    p.add_argument("--breakdown", action="store_true",
+                   help="large models: time forward/backward/allreduce-wait/optimizer with HIP events "
+                        "(extra pass after the timed steps; printed to stderr)")
     p.add_argument("--lr", type=float, default=0.01)
     p.add_argument("--momentum", type=float, default=0.5)
     p.add_argument("--impl", choices=["fused", "eager"], default=os.environ.get("BENCH_IMPL", "fused"))
@@ -156,6 +159,13 @@ def run_model_bench(args, env, device, pdist):
     pdist.barrier(device)
     torch.cuda.synchronize(device)
     elapsed = pdist.all_reduce_max(time.perf_counter() - t0, device)
+    breakdown = None
+    if args.breakdown:  # separate, untimed pass so event records do not perturb the measurement
+        trainer.timer.enabled = True
+        trainer.run(max(2, min(args.steps, 5)))
+        breakdown = trainer.timer.summary()
+        trainer.timer.enabled = False
+        print(f"[bench] phase ms/step: {breakdown}", file=sys.stderr)
     n = env.world_size
     per_step = trainer.samples_per_step()
     value = per_step * n * args.steps / elapsed
@@ -169,6 +179,8 @@ def run_model_bench(args, env, device, pdist):
                "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 1),
                "final_loss": trainer.last_loss()}
         cfg.update(trainer.describe())
+        if breakdown:
+            cfg["phase_ms"] = breakdown
         if hasattr(trainer, "flops_per_step"):
             cfg["mfu"] = round(trainer.flops_per_step() * args.steps / elapsed / MI355X_BF16_DENSE_FLOPS, 4)
         unit = "images/s" if args.model == "resnet50" else "tokens/s"

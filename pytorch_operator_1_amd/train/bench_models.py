@@ -20,6 +20,7 @@ import torch.nn.functional as F
 
 from ..ops.optim import FusedAdamW, FusedSGD
 from ..parallel.ddp import GradBucketer
+from ..utils.profiling import StepTimer
 
 
 class ResNetTrainer:
@@ -36,14 +37,20 @@ class ResNetTrainer:
         self.opt = FusedSGD(self.model.parameters(), lr=lr, momentum=momentum, weight_decay=weight_decay)
         self.x, self.y = synthetic_images(batch_size, device, image_size, seed=seed)
         self._loss = None
+        self.timer = StepTimer(device, enabled=False)
 
     def step(self):
-        with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+        t = self.timer
+        with t.phase("forward"), torch.autocast(device_type="cuda", dtype=torch.bfloat16):
             out = self.model(self.x)
-        loss = F.cross_entropy(out.float(), self.y)
-        loss.backward()
-        self.bucketer.finish()
-        self.opt.step(grad_scale=self.bucketer.grad_scale, zero_grad=True)
+        with t.phase("forward"):
+            loss = F.cross_entropy(out.float(), self.y)
+        with t.phase("backward"):
+            loss.backward()
+        with t.phase("allreduce_wait"):
+            self.bucketer.finish()
+        with t.phase("optimizer"):
+            self.opt.step(grad_scale=self.bucketer.grad_scale, zero_grad=True)
         self._loss = loss.detach()
 
     def run(self, n: int):
@@ -79,12 +86,18 @@ class LlamaTrainer:
                               weight_decay=weight_decay)
         self.tokens, self.labels = synthetic_tokens(batch_size, seq_len, self.cfg.vocab_size, device, seed=seed)
         self._loss = None
+        self.timer = StepTimer(device, enabled=False)
 
     def step(self):
-        loss = self.model(self.tokens, self.labels)
-        loss.backward()
-        self.bucketer.finish()
-        self.opt.step(grad_scale=self.bucketer.grad_scale, zero_grad=True)
+        t = self.timer
+        with t.phase("forward"):
+            loss = self.model(self.tokens, self.labels)
+        with t.phase("backward"):
+            loss.backward()
+        with t.phase("allreduce_wait"):
+            self.bucketer.finish()
+        with t.phase("optimizer"):
+            self.opt.step(grad_scale=self.bucketer.grad_scale, zero_grad=True)
         self._loss = loss.detach()
 
     def run(self, n: int):

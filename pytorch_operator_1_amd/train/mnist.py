@@ -30,6 +30,7 @@ import torch.distributed as dist
 
 from ..models.mnist import synthetic_mnist
 from ..utils import dist as pdist
+from ..utils.profiling import torch_trace
 from . import checkpoint as ckpt
 
 
@@ -60,6 +61,10 @@ def parse_args(argv=None):
     p.add_argument("--fail-at-step", type=int, default=int(os.environ.get("PTO_FAIL_AT_STEP", "0")),
                    help="fault injection: SIGKILL self at this step (once)")
     p.add_argument("--fail-rank", type=int, default=int(os.environ.get("PTO_FAIL_RANK", "1")))
+    p.add_argument("--profile", default=os.environ.get("PTO_PROFILE_DIR"),
+                   help="torch.profiler Chrome trace (HIP kernels + host) of 10 steps into this directory")
+    p.add_argument("--comm", choices=["auto", "rccl", "xgmi"], default=None,
+                   help="fused trainer gradient all-reduce transport (default: auto = measured at startup)")
     return p.parse_args(argv)
 
 
@@ -134,8 +139,11 @@ def _main(argv=None):
     impl = args.impl or ("fused" if use_cuda else "eager")
     from .runner import build_trainer
 
+    extra = {"comm": args.comm} if (args.comm and impl == "fused") else {}
     trainer = build_trainer(impl, device=device, batch_size=args.batch_size, lr=args.lr, momentum=args.momentum,
-                            dataset_size=xtr.shape[0], seed=args.seed, rank=rank, data=xtr, target=ytr)
+                            dataset_size=xtr.shape[0], seed=args.seed, rank=rank, data=xtr, target=ytr, **extra)
+    if getattr(trainer, "comm_info", None) and world > 1:
+        print(f"[pto] gradient all-reduce: {trainer.comm_info}", flush=True)
     start_step = 0
     if args.checkpoint_dir:
         path = ckpt.latest(args.checkpoint_dir)
@@ -155,6 +163,8 @@ def _main(argv=None):
     samples_since = 0
     t_last = time.time()
     first = True
+    trace = torch_trace(args.profile, rank)
+    prof_step = trace.__enter__()
     while step < total_steps:
         epoch = step // n_batches + 1
         batch_idx = step % n_batches
@@ -162,6 +172,7 @@ def _main(argv=None):
             print(f"[fault-injection] rank {rank} SIGKILL at step {step}", flush=True)
             os.kill(os.getpid(), signal.SIGKILL)
         trainer.step()
+        prof_step()
         step += 1
         samples_since += args.batch_size
         if first:
@@ -190,6 +201,7 @@ def _main(argv=None):
                          epoch_seconds=round(time.time() - t_epoch, 3))
             t_epoch = time.time()
         sys.stdout.flush()
+    trace.__exit__(None, None, None)
     if args.checkpoint_dir and rank == 0:
         ckpt.save(args.checkpoint_dir, step, {"trainer": trainer.state_dict(), "rng": ckpt.rng_state()})
     if args.save_model and rank == 0:
