@@ -79,6 +79,8 @@ REASON_POD_TEMPLATE_SCHEDULER_NAME = "SettedPodTemplateSchedulerName"
 GPU_RESOURCE = "amd.com/gpu"
 LEGACY_GPU_RESOURCES = ("nvidia.com/gpu",)
 HBM_PER_GPU_BYTES = 288 * 1000 ** 3  # MI355X: 288 GB HBM3E
+# per-replica HBM request (bytes per GPU, k8s quantity), checked against the GPU's HBM
+HBM_RESOURCE = "amd.com/hbm"
 
 # controller tunables (reference values)
 EXPECTATIONS_TIMEOUT_S = 5 * 60

@@ -57,8 +57,34 @@ def gpus_requested(container: Obj) -> int:
     return n
 
 
-def validate_resources(job: Obj, gpus_per_node: int = 8) -> None:
-    """MI355X extension: per-replica ``amd.com/gpu`` sanity."""
+_SUFFIX = {"Ki": 2 ** 10, "Mi": 2 ** 20, "Gi": 2 ** 30, "Ti": 2 ** 40, "Pi": 2 ** 50,
+           "k": 10 ** 3, "K": 10 ** 3, "M": 10 ** 6, "G": 10 ** 9, "T": 10 ** 12, "P": 10 ** 15}
+
+
+def parse_quantity(q) -> float:
+    """Kubernetes resource quantity -> number ("288Gi", "200G", "1.5e11", 7)."""
+    if isinstance(q, (int, float)):
+        return float(q)
+    s = str(q).strip()
+    for suf in sorted(_SUFFIX, key=len, reverse=True):
+        if s.endswith(suf):
+            return float(s[: -len(suf)]) * _SUFFIX[suf]
+    return float(s)
+
+
+def hbm_requested(container: Obj) -> float:
+    """Bytes of HBM per GPU requested via ``amd.com/hbm`` (0 = unspecified)."""
+    res = container.get("resources") or {}
+    n = 0.0
+    for section in ("limits", "requests"):
+        v = (res.get(section) or {}).get(C.HBM_RESOURCE)
+        if v is not None:
+            n = max(n, parse_quantity(v))
+    return n
+
+
+def validate_resources(job: Obj, gpus_per_node: int = 8, hbm_per_gpu: float = C.HBM_PER_GPU_BYTES) -> None:
+    """MI355X extension: per-replica ``amd.com/gpu`` / ``amd.com/hbm`` sanity."""
     for rtype, rspec in (job.get("spec", {}).get("pytorchReplicaSpecs") or {}).items():
         for c in rspec.get("template", {}).get("spec", {}).get("containers", []):
             try:
@@ -68,3 +94,10 @@ def validate_resources(job: Obj, gpus_per_node: int = 8) -> None:
             if g < 0 or g > gpus_per_node:
                 raise ValidationError(
                     f"PyTorchJobSpec is not valid: {rtype} requests {g} {C.GPU_RESOURCE}, node has {gpus_per_node}")
+            try:
+                h = hbm_requested(c)
+            except ValueError:
+                raise ValidationError(f"PyTorchJobSpec is not valid: bad {C.HBM_RESOURCE} quantity in {rtype}")
+            if h > hbm_per_gpu:
+                raise ValidationError(f"PyTorchJobSpec is not valid: {rtype} requests {h / 1e9:.0f} GB "
+                                      f"{C.HBM_RESOURCE} per GPU, an MI355X has {hbm_per_gpu / 1e9:.0f} GB")

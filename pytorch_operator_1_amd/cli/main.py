@@ -181,13 +181,25 @@ def cmd_apiserver(args):
     return 0
 
 
+def _hbm(args) -> float:
+    from ..api.validation import parse_quantity
+
+    return parse_quantity(args.hbm_per_gpu)
+
+
 def cmd_node(args):
     setup_logging(False)
     stop = setup_signal_handler()
     from ..apiserver.client import RestClient
     from ..node.kubelet import Kubelet
 
-    kl = Kubelet(RestClient(_server_url(args)), gpus=args.gpus, log_dir=args.log_dir, node_name=args.node_name)
+    agent = None
+    if args.node_agent_socket:
+        from ..node.native import AgentClient
+
+        agent = AgentClient(socket_path=args.node_agent_socket)
+    kl = Kubelet(RestClient(_server_url(args)), agent=agent, gpus=args.gpus, log_dir=args.log_dir,
+                 node_name=args.node_name, hbm_per_gpu=_hbm(args))
     kl.start()
     stop.wait()
     kl.stop()
@@ -201,7 +213,7 @@ def cmd_up(args):
     from ..controller.metrics import serve_metrics
 
     c = LocalCluster(gpus=args.gpus, port=args.port, wal_path=args.wal, log_dir=args.log_dir,
-                     enable_gang_scheduling=args.enable_gang_scheduling)
+                     enable_gang_scheduling=args.enable_gang_scheduling, hbm_per_gpu=_hbm(args))
     c.start()
     serve_metrics(c.metrics, args.monitoring_port)
     print(f"pto: API server {c.url}  metrics :{args.monitoring_port}/metrics  "
@@ -371,7 +383,11 @@ def main(argv=None):
     ap.set_defaults(fn=cmd_apiserver)
 
     nd = sub.add_parser("node", help="run the node manager + native agent")
-    nd.add_argument("--gpus", type=int, default=None)
+    nd.add_argument("--gpus", "--gpus-per-node", dest="gpus", type=int, default=None,
+                    help="GPUs managed by this node (default: all visible)")
+    nd.add_argument("--hbm-per-gpu", default="288G", help="HBM per GPU for amd.com/hbm admission (quantity)")
+    nd.add_argument("--node-agent-socket", default=None,
+                    help="attach to a running pto-node-agent on this Unix socket instead of spawning one")
     nd.add_argument("--log-dir", default=None)
     nd.add_argument("--node-name", default="mi355x-0")
     nd.add_argument("--master", default="")
@@ -379,7 +395,8 @@ def main(argv=None):
 
     up = sub.add_parser("up", help="all-in-one single-node cluster")
     up.add_argument("--port", type=int, default=8080)
-    up.add_argument("--gpus", type=int, default=None)
+    up.add_argument("--gpus", "--gpus-per-node", dest="gpus", type=int, default=None)
+    up.add_argument("--hbm-per-gpu", default="288G", help="HBM per GPU for amd.com/hbm admission (quantity)")
     up.add_argument("--wal", default=None)
     up.add_argument("--log-dir", default=None)
     up.add_argument("--monitoring-port", type=int, default=8443)

@@ -27,7 +27,7 @@ log = logging.getLogger("pto-cluster")
 class LocalCluster:
     def __init__(self, gpus: int | None = None, port: int = 0, wal_path: str | None = None,
                  log_dir: str | None = None, enable_gang_scheduling: bool = False, serve_http: bool = True,
-                 extra_env: dict | None = None, threadiness: int = 2):
+                 extra_env: dict | None = None, threadiness: int = 2, hbm_per_gpu: float | None = None):
         self.store = Store(wal_path=wal_path)
         self.client = LocalClient(self.store)
         self.server = ApiServer(self.store, port=port) if serve_http else None
@@ -35,7 +35,8 @@ class LocalCluster:
         self.controller = PyTorchController(
             self.client, ControllerConfig(enable_gang_scheduling=enable_gang_scheduling, threadiness=threadiness,
                                           job_resync_period=5.0), metrics=self.metrics)
-        self.kubelet = Kubelet(self.client, gpus=gpus, log_dir=log_dir, extra_env=extra_env)
+        kw = {"hbm_per_gpu": hbm_per_gpu} if hbm_per_gpu else {}
+        self.kubelet = Kubelet(self.client, gpus=gpus, log_dir=log_dir, extra_env=extra_env, **kw)
 
     def start(self):
         if self.server:

@@ -91,6 +91,13 @@ class PodRuntime:
         self.annotated_first_step = False
 
 
+def _pod_hbm(pod) -> float:
+    """Per-GPU HBM bytes a pod asks for (max over its containers)."""
+    from ..api.validation import hbm_requested
+
+    return max([hbm_requested(c) for c in pod.get("spec", {}).get("containers", [])] or [0.0])
+
+
 class Kubelet:
     def __init__(self, client, agent: AgentClient | None = None, node_name: str = "mi355x-0",
                  log_dir: str | None = None, images: dict | None = None, gpus: int | None = None,
@@ -233,7 +240,7 @@ class Kubelet:
         group = ann.get(C.ANNOTATION_GANG_GROUP)
         if n == 0 and not group:
             return True
-        requests = [{"owner": rt.key, "count": n}]
+        requests = [{"owner": rt.key, "count": n, "hbm": _pod_hbm(pod)}]
         if group:
             members = [p for p in self.pod_informer.list(namespace_of(pod))
                        if (p["metadata"].get("annotations") or {}).get(C.ANNOTATION_GANG_GROUP) == group]
@@ -245,8 +252,8 @@ class Kubelet:
             if len(members) < min_member:
                 self._set_unschedulable(pod, rt, f"{len(members)}/{min_member} gang members present")
                 return False
-            requests = [{"owner": key_of(m), "count": sum(gpus_requested(c) for c in m["spec"].get("containers", []))}
-                        for m in members]
+            requests = [{"owner": key_of(m), "count": sum(gpus_requested(c) for c in m["spec"].get("containers", [])),
+                         "hbm": _pod_hbm(m)} for m in members]
         r = self.agent.alloc(requests)
         if not r.get("ok"):
             self._set_unschedulable(pod, rt, r.get("error", "insufficient amd.com/gpu"))

@@ -143,3 +143,21 @@ def test_generated_artifacts_up_to_date():
     r = subprocess.run([sys.executable, os.path.join(root, "hack", "gen_manifests.py"), "--verify"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("q,v", [("288Gi", 288 * 2 ** 30), ("200G", 200e9), ("1.5e3", 1500.0), (7, 7.0),
+                                 ("512Mi", 512 * 2 ** 20), ("1k", 1000.0)])
+def test_parse_quantity(q, v):
+    from pytorch_operator_1_amd.api.validation import parse_quantity
+
+    assert parse_quantity(q) == v
+
+
+def test_hbm_request_validation():
+    job = new_job("h", workers=1, gpus=1)
+    c = job["spec"]["pytorchReplicaSpecs"]["Worker"]["template"]["spec"]["containers"][0]
+    c.setdefault("resources", {}).setdefault("limits", {})[C.HBM_RESOURCE] = "200G"
+    validate_resources(job)
+    c["resources"]["limits"][C.HBM_RESOURCE] = "300G"
+    with pytest.raises(ValidationError, match="an MI355X has 288 GB"):
+        validate_resources(job)
