@@ -6,6 +6,8 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 R="$GRAFT_REPO_ROOT"
 cd /tmp
+timeout -k 10 300 python3 "$R/tools/llama_ops_bench.py" --json "$R/gpurun_out/llama_ops.json" > "$R/gpurun_out/llama_ops.log" 2>&1 || { tail -20 "$R/gpurun_out/llama_ops.log"; exit 1; }
+cat "$R/gpurun_out/llama_ops.log"
 timeout -k 10 300 python3 "$R/bench.py" --model llama3-8b --steps 4 --warmup 2 --breakdown > "$R/gpurun_out/llama8b_bd.json" 2> "$R/gpurun_out/llama8b_bd.err" || { tail -20 "$R/gpurun_out/llama8b_bd.err"; exit 1; }
 grep "phase ms" "$R/gpurun_out/llama8b_bd.err"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_llama8b" -o run -- python3 "$R/bench.py" --model llama3-8b --steps 3 --warmup 1 > "$R/gpurun_out/llama8b_prof.log" 2>&1 || { tail -30 "$R/gpurun_out/llama8b_prof.log"; exit 1; }
