@@ -5,6 +5,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 R="$GRAFT_REPO_ROOT"
+export PYTHONPATH="$R${PYTHONPATH:+:$PYTHONPATH}"
 cd /tmp
 timeout -k 10 300 python3 "$R/tools/llama_ops_bench.py" --json "$R/gpurun_out/llama_ops.json" > "$R/gpurun_out/llama_ops.log" 2>&1 || { tail -20 "$R/gpurun_out/llama_ops.log"; exit 1; }
 cat "$R/gpurun_out/llama_ops.log"

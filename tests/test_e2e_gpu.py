@@ -53,3 +53,24 @@ def test_gang_admission_unschedulable_when_gpus_exhausted(cluster):
     assert pod["status"]["phase"] == "Pending"
     assert any(c.get("reason") == "Unschedulable" for c in pod["status"]["conditions"])
     cluster.store.delete("pytorchjobs", "default", "too-big")
+
+
+def test_gpu_kill_rejoin_resumes_fused_trainer(cluster, tmp_path):
+    """Config 5 on the GPU: the fused HIP trainer is SIGKILLed mid-run
+    (exit 137, retryable) -> ExitCode policy recreates the pod on the same
+    GPU -> it resumes from the flat-buffer checkpoint and the job succeeds."""
+    import os
+
+    ck = str(tmp_path / "ckpt")
+    job = new_job("mnist-gpu-kill", image="pto/pytorch-mnist:rocm",
+                  master_args=["--backend", "rccl", "--impl", "fused", "--max-steps", "200", "--log-interval", "50",
+                               "--checkpoint-dir", ck, "--checkpoint-interval", "50", "--fail-at-step", "120",
+                               "--fail-rank", "0", "--no-test"],
+                  workers=0, gpus=1, restart_policy="ExitCode")
+    job["spec"]["backoffLimit"] = 3
+    cluster.submit(job)
+    j = cluster.wait_for_condition("mnist-gpu-kill", timeout=300)
+    log = cluster.pod_log("default", "mnist-gpu-kill-master-0")
+    assert j["status"]["conditions"][-1]["type"] == "Succeeded", (j["status"], log[-2000:])
+    assert "Resumed from" in log and "at step 100" in log
+    assert any(f.startswith("ckpt-") for f in os.listdir(ck))
