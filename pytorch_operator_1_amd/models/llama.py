@@ -99,11 +99,9 @@ class LlamaBlock(nn.Module):
         q = v4[:, :, :c.n_heads].transpose(1, 2)
         k = v4[:, :, c.n_heads:c.n_heads + c.n_kv_heads].transpose(1, 2)
         v = v4[:, :, c.n_heads + c.n_kv_heads:].transpose(1, 2)
-        if c.n_kv_heads != c.n_heads:
-            rep = c.n_heads // c.n_kv_heads
-            k = k[:, :, None].expand(B, c.n_kv_heads, rep, S, hd).reshape(B, c.n_heads, S, hd)
-            v = v[:, :, None].expand(B, c.n_kv_heads, rep, S, hd).reshape(B, c.n_heads, S, hd)
-        o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        # GQA without materialising repeated K/V (measured 0.70 vs 0.87 ms fwd
+        # at 2x4096 tokens, plus no expand copies: profiles/llama8b_ops_r1.json)
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=c.n_kv_heads != c.n_heads)
         return o.transpose(1, 2).reshape(B * S, c.n_heads * hd)
 
     def forward_hip(self, h, delta, rope, B, S):

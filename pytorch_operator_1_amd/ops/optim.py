@@ -33,8 +33,24 @@ def _same_dense_layout(*ts) -> bool:
     return dense and all(t is None or (t.shape == t0.shape and t.stride() == t0.stride()) for t in ts)
 
 
+def _grad_ptrs(groups):
+    return tuple(p.grad.data_ptr() for g in groups for p in g["params"])
+
+
+class _TableMixin:
+    """Rebuild the device launch table when any gradient tensor changed
+    (grads handed over fresh each step by autograd, GradBucketer "none")."""
+
+    def _refresh(self):
+        if self._tables is not None and all(p.grad is not None for g in self.param_groups for p in g["params"]):
+            if _grad_ptrs(self.param_groups) == self._gptrs:
+                return
+        self._build()  # also materialises missing grads as zeros
+        self._gptrs = _grad_ptrs(self.param_groups)
+
+
 class SgdTable:
-    def __init__(self, triples, device):
+    def __init__(self, triples, device, keep_grads: bool = True):
         L = _lib.lib()
         self.L = L
         recs, starts, nb = [], [], 0
@@ -45,7 +61,9 @@ class SgdTable:
             recs.append((p.data_ptr(), g.data_ptr(), 0 if m is None else m.data_ptr(), p.numel()))
             starts.append(nb)
             nb += L.pto_sgd_block_count(p.numel())
-            self._keep.append((p, g, m))
+            # the fused trainer owns its flat buffers; an Optimizer must not pin
+            # gradients autograd will replace (pointers re-checked every step)
+            self._keep.append((p, g if keep_grads else None, m))
         self.nblocks = nb
         self.ntensors = len(recs)
         raw = (_SgdTensor * len(recs))(*[_SgdTensor(*r) for r in recs])
@@ -66,7 +84,7 @@ class SgdTable:
                    "sgd_multi")
 
 
-class FusedSGD(torch.optim.Optimizer):
+class FusedSGD(_TableMixin, torch.optim.Optimizer):
     """Drop-in ``torch.optim.SGD`` (dampening=0) backed by one HIP launch.
 
     Grads are consumed and zeroed in the same launch when ``zero_grad=True``
@@ -78,6 +96,7 @@ class FusedSGD(torch.optim.Optimizer):
             raise ValueError("Nesterov momentum requires a momentum")
         super().__init__(params, dict(lr=lr, momentum=momentum, weight_decay=weight_decay, nesterov=nesterov))
         self._tables = None
+        self._gptrs = None
 
     def _build(self):
         self._tables = []
@@ -91,7 +110,7 @@ class FusedSGD(torch.optim.Optimizer):
                     st["momentum_buffer"] = torch.zeros_like(p)
                 triples.append((p.data, p.grad, st.get("momentum_buffer")))
             dev = group["params"][0].device
-            self._tables.append(SgdTable(triples, dev))
+            self._tables.append(SgdTable(triples, dev, keep_grads=False))
 
     @torch.no_grad()
     def step(self, closure=None, grad_scale: float = 1.0, zero_grad: bool = False):
@@ -99,8 +118,7 @@ class FusedSGD(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        if self._tables is None or any(p.grad is None for g in self.param_groups for p in g["params"]):
-            self._build()
+        self._refresh()
         for group, table in zip(self.param_groups, self._tables):
             table.step(None, group["lr"], group["momentum"], group["weight_decay"], grad_scale, group["nesterov"],
                        zero_grad=zero_grad)
@@ -119,7 +137,7 @@ class _AdamTensor(ctypes.Structure):
                 ("v", ctypes.c_void_p), ("n", ctypes.c_longlong)]
 
 
-class FusedAdamW(torch.optim.Optimizer):
+class FusedAdamW(_TableMixin, torch.optim.Optimizer):
     """Multi-tensor AdamW in one HIP launch (csrc/kernels/optim_kernels.hip).
 
     bf16 parameters get fp32 master weights and fp32 moments inside the
@@ -132,6 +150,7 @@ class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self._tables = None
+        self._gptrs = None
         self._step = 0
 
     def _build(self):
@@ -161,7 +180,7 @@ class FusedAdamW(torch.optim.Optimizer):
                                         st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), p.numel()))
                 starts.append(nb)
                 nb += L.pto_adamw_block_count(p.numel())
-                keep.append((p, p.grad, master, st["exp_avg"], st["exp_avg_sq"]))
+                keep.append((p, master, st["exp_avg"], st["exp_avg_sq"]))  # not the grad: see _grad_ptrs
             raw = (_AdamTensor * len(recs))(*recs)
             dev = group["params"][0].device
             table = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(raw), ctypes.sizeof(raw))),
@@ -175,10 +194,7 @@ class FusedAdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        ptrs_changed = self._tables is not None and any(
-            k[1] is not k[0].grad for t in self._tables for k in t[5])
-        if self._tables is None or ptrs_changed:
-            self._build()
+        self._refresh()
         self._step += 1
         L = _lib.lib()
         for group, (table, starts, nt, nb, mixed, _) in zip(self.param_groups, self._tables):

@@ -31,18 +31,37 @@ import torch.distributed as dist
 
 
 class GradBucketer:
+    """Modes (``mode=None`` picks ``copy`` for world > 1, ``none`` for 1):
+
+    * ``view`` — every ``param.grad`` is a persistent view of the flat
+      buffer; autograd ACCUMULATES into it (read+read+write), so the
+      optimizer must zero it (``zero_grad=True`` in the fused step).
+    * ``copy`` — autograd hands each gradient over as a fresh tensor
+      (``grad is None`` before backward, so AccumulateGrad steals it with no
+      add); the hook copies it into its bucket slot (read+write) and points
+      ``param.grad`` at the slot; buckets all-reduce from the slots.
+    * ``none`` — single process: no buckets, gradients stay the tensors
+      autograd produced (zero extra passes).
+    After the optimizer step call :meth:`release` (``copy``/``none``).
+    """
+
     def __init__(self, module: torch.nn.Module, bucket_mb: float | None = None, process_group=None,
-                 overlap: bool = True):
+                 overlap: bool = True, mode: str | None = None):
         self.module = module
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         self.overlap = overlap and self.world > 1
+        self.mode = mode or os.environ.get("PTO_GRAD_MODE") or ("copy" if self.world > 1 else "none")
+        if self.mode not in ("view", "copy", "none"):
+            raise ValueError(f"GradBucketer: unknown mode {self.mode}")
         bucket_mb = bucket_mb if bucket_mb is not None else float(os.environ.get("PTO_BUCKET_MB", "256"))
         cap = int(bucket_mb * 1024 * 1024)
         params = [p for p in module.parameters() if p.requires_grad]
         if not params:
             raise ValueError("GradBucketer: module has no trainable parameters")
+        self.params = params
         dev = params[0].device
+        self._views: dict = {}
         # one flat buffer per dtype, reverse registration order
         self.flat: dict[torch.dtype, torch.Tensor] = {}
         self.buckets: list[dict] = []
@@ -55,12 +74,15 @@ class GradBucketer:
             for p in ps:
                 offs.append(total)
                 total += (p.numel() + align - 1) // align * align
+            if self.mode == "none":
+                continue
             buf = torch.zeros(total, dtype=dt, device=dev)
             self.flat[dt] = buf
             cur, start = [], 0
             for j, (p, o) in enumerate(zip(ps, offs)):
                 # same strides as the param (channels_last convs stay NHWC)
-                p.grad = buf[o:o + p.numel()].as_strided(p.shape, p.stride())
+                self._views[p] = buf[o:o + p.numel()].as_strided(p.shape, p.stride())
+                p.grad = self._views[p] if self.mode == "view" else None
                 cur.append(p)
                 end = offs[j + 1] if j + 1 < len(ps) else total  # include alignment padding
                 if (end - start) * buf.element_size() >= cap or j + 1 == len(ps):
@@ -74,7 +96,7 @@ class GradBucketer:
         self._works: list = []
         self.comm_stream = torch.cuda.Stream(dev) if (self.overlap and dev.type == "cuda") else None
         self._handles = []
-        if self.overlap:
+        if self.mode == "copy" or (self.overlap and self.mode == "view"):
             for p in params:
                 self._handles.append(p.register_post_accumulate_grad_hook(self._on_grad))
         self.reset()
@@ -99,14 +121,27 @@ class GradBucketer:
             self._works.append(dist.all_reduce(t, group=self.pg, async_op=True))
 
     def _on_grad(self, p):
+        if self.mode == "copy":
+            v = self._views[p]
+            if p.grad is not v:
+                v.copy_(p.grad)
+                p.grad = v
         i = self._bucket_of[p]
         self._pending[i] -= 1
-        if self._pending[i] == 0:
+        if self._pending[i] == 0 and self.overlap:
             self._launch(i)
 
     def finish(self):
         """Call after ``loss.backward()``: launches any bucket whose params
         produced no gradient, waits for all collectives, joins the streams."""
+        if self.mode == "copy":
+            for p, v in self._views.items():  # params that got no gradient this step
+                if p.grad is not v:
+                    if p.grad is None:
+                        v.zero_()
+                    else:
+                        v.copy_(p.grad)
+                    p.grad = v
         if self.world > 1:
             if not self.overlap:
                 for i in range(len(self.buckets)):
@@ -121,6 +156,18 @@ class GradBucketer:
             if self.comm_stream is not None:
                 torch.cuda.current_stream(self.comm_stream.device).wait_stream(self.comm_stream)
         self.reset()
+
+    @property
+    def optimizer_zeroes_grads(self) -> bool:
+        """``view`` mode needs the fused optimizer to zero the grads in its pass."""
+        return self.mode == "view"
+
+    def release(self):
+        """After the optimizer step: drop the gradients (``copy``/``none``) so
+        the next backward hands fresh tensors over instead of accumulating."""
+        if self.mode != "view":
+            for p in self.params:
+                p.grad = None
 
     @property
     def grad_scale(self) -> float:

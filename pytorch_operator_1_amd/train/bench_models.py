@@ -50,7 +50,8 @@ class ResNetTrainer:
         with t.phase("allreduce_wait"):
             self.bucketer.finish()
         with t.phase("optimizer"):
-            self.opt.step(grad_scale=self.bucketer.grad_scale, zero_grad=True)
+            self.opt.step(grad_scale=self.bucketer.grad_scale, zero_grad=self.bucketer.optimizer_zeroes_grads)
+            self.bucketer.release()
         self._loss = loss.detach()
 
     def run(self, n: int):
@@ -97,7 +98,8 @@ class LlamaTrainer:
         with t.phase("allreduce_wait"):
             self.bucketer.finish()
         with t.phase("optimizer"):
-            self.opt.step(grad_scale=self.bucketer.grad_scale, zero_grad=True)
+            self.opt.step(grad_scale=self.bucketer.grad_scale, zero_grad=self.bucketer.optimizer_zeroes_grads)
+            self.bucketer.release()
         self._loss = loss.detach()
 
     def run(self, n: int):

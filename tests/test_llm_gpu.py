@@ -186,4 +186,5 @@ def test_resnet_trainer_steps():
     torch.cuda.synchronize()
     assert tr.last_loss() == tr.last_loss()  # finite
     w = tr.model.fc.weight
-    assert w.grad is not None and float(w.grad.abs().sum()) == 0.0  # zeroed by the fused step
+    # single process: gradients are autograd's own tensors, dropped after the fused step
+    assert tr.bucketer.mode == "none" and w.grad is None
