@@ -1,0 +1,621 @@
+// Causal GQA flash attention for gfx950 (bf16 in/out, fp32 accumulate),
+// head_dim 128: forward, and backward as dK/dV + dQ kernels.  Replaces the
+// ROCm SDPA path in the Llama-3 config (profiles/llama8b_step_rocprof.md:
+// attention fwd+bwd was 4.3 ms/layer, 26 % of the step).
+//
+// Layout: Q/K/V are read in place from the fused QKV projection output
+// ([tokens][(H + 2 Hkv) * 128], any row stride), O is written as
+// [tokens][H * 128] (what the output projection consumes, no transpose),
+// gradients dQ/dK/dV are written into a dQKV buffer of the QKV layout.
+//
+// MFMA: v_mfma_f32_32x32x16_bf16.  Lane maps (cdna_hip_programming.md §3):
+// A[row l&31][k 8(l>>5)+j], B[k 8(l>>5)+j][col l&31], C col = l&31,
+// row = (i&3) + 8(i>>2) + 4(l>>5).
+//
+// Forward / dQ structure ("swapped" products, every softmax quantity
+// lane-local): a wave owns 32 query rows of one head; the block's 4 waves
+// are the 4 query heads sharing one KV head (GQA group), so one K/V tile in
+// LDS serves all of them.  S^T = K Q^T puts the query on the lane: row max /
+// sum are 32 in-lane ops + one cross-half exchange.  O^T = V^T P^T keeps the
+// query on the lane too, so the online-softmax rescale is a per-lane scalar.
+// P^T's B operand is built in registers with v_cvt_pk_bf16_f32 +
+// v_permlane32_swap; V^T's A operand comes from ds_read_b64_tr_b16
+// transposed reads of the row-major V tile.  K/V tiles (64 keys) are
+// register-staged from global memory one tile ahead into a 2-deep LDS ring
+// with an XOR-swizzled image (conflict-free for b128 row reads and the
+// transposed reads).
+//
+// dK/dV structure: a wave owns 32 keys (K and V fragments in registers,
+// dK^T / dV^T accumulated in registers over every query row of the 4 heads
+// of the group); S and dP are computed with the key on the lane, so their
+// accumulators feed the dV^T / dK^T products through the same cvt+swap;
+// the row constants -LSE and -delta are the accumulators' initial values.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int HD = 128;            // head dim
+constexpr int QT = 32;             // query rows per wave
+constexpr int KT = 64;             // keys per tile
+constexpr int NW = 4;              // waves per block
+constexpr int NT = NW * 64;
+constexpr int TILE_B = KT * HD * 2;  // 16 KiB per K or V tile
+constexpr float LOG2E = 1.4426950408889634f;
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// XOR-swizzled [rows][256 B] image (cdna_hip_programming.md T10 image (b)):
+// byte offset of 16-byte chunk ch (0..15) of row r.
+__device__ __forceinline__ int swz(int r, int ch) { return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); }
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ unsigned pack2(float a, float b) {
+  bf16x2 t = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, t);
+}
+
+// Accumulator regs [8s .. 8s+7] of a 32x32 C tile whose row index runs
+// over the MFMA k dimension of the next product -> that product's operand
+// fragment for k-slot s (16 rows): lanes 0-31 need rows 16s+0..7, lanes
+// 32-63 rows 16s+8..15; each half holds 4 of them, the partner the rest.
+__device__ __forceinline__ bf16x8 acc_to_operand(const float* r) {
+  unsigned x0 = pack2(r[0], r[1]), x1 = pack2(r[2], r[3]);
+  unsigned y0 = pack2(r[4], r[5]), y1 = pack2(r[6], r[7]);
+  auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+  auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+  u32x4 o = {s0[0], s1[0], s0[1], s1[1]};
+  return __builtin_bit_cast(bf16x8, o);
+}
+
+// A (or B) operand with k running along the ROWS of a row-major LDS tile
+// (keys for V^T, queries for dO^T / Q^T): two transposed reads.  Operand
+// row index (d) = col0 + (lane & 31); k = krow0 + 8*(lane>>5) + j.
+__device__ __forceinline__ bf16x8 tr_operand(const char* tile, int krow0, int col0) {
+  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  const int row = krow0 + 8 * (g >> 1) + (li >> 2);
+  const int ch = ((col0 + 16 * (g & 1)) >> 3) + ((li & 3) >> 1);
+  const char* p0 = tile + swz(row, ch) + 8 * (li & 1);
+  const char* p1 = tile + swz(row + 4, ch) + 8 * (li & 1);
+  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
+  u32x2 ua = __builtin_bit_cast(u32x2, a), ub = __builtin_bit_cast(u32x2, b);
+  u32x4 o = {ua[0], ua[1], ub[0], ub[1]};
+  return __builtin_bit_cast(bf16x8, o);
+}
+
+// Row operand (k along the columns = head dim): 16 bytes of row
+// r0 + (lane&31), chunk 2*ks + (lane>>5).
+__device__ __forceinline__ bf16x8 row_operand(const char* tile, int r0, int ks) {
+  const int lane = threadIdx.x & 63;
+  return *reinterpret_cast<const bf16x8*>(tile + swz(r0 + (lane & 31), 2 * ks + (lane >> 5)));
+}
+
+// Cooperative tile copy global -> registers -> LDS (64 rows x 256 B).
+struct TileRegs {
+  uint4 v[4];
+};
+__device__ __forceinline__ void tile_load(TileRegs& t, const __bf16* base, long long rs) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int c = threadIdx.x + NT * p, r = c >> 4, ch = c & 15;
+    t.v[p] = *reinterpret_cast<const uint4*>(base + (long long)r * rs + ch * 8);
+  }
+}
+__device__ __forceinline__ void tile_store(const TileRegs& t, char* tile) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int c = threadIdx.x + NT * p, r = c >> 4, ch = c & 15;
+    *reinterpret_cast<uint4*>(tile + swz(r, ch)) = t.v[p];
+  }
+}
+
+struct AttnShape {
+  int B, S, H, Hkv;
+  long long q_rs, k_rs, v_rs;  // row strides (elements) of the Q/K/V sources
+  long long o_rs;              // row stride of O / dO
+  float scale;                 // softmax scale (1/sqrt(128))
+};
+
+// Block -> (batch, kv head, block-of-4-units); unit u = qt*G + g.
+// XCD-aware: consecutive linear indices (same batch/kv head, i.e. the same
+// K/V working set) land on one XCD; heaviest causal tiles first.
+struct BlockMap {
+  int b, kvh, bi;
+};
+__device__ __forceinline__ BlockMap map_block(const AttnShape& sh, int per_pair) {
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  int lin = bid;
+  if ((nblk & 7) == 0) lin = (bid & 7) * (nblk >> 3) + (bid >> 3);
+  const int pair = lin / per_pair;
+  BlockMap m;
+  m.b = pair / sh.Hkv;
+  m.kvh = pair % sh.Hkv;
+  m.bi = per_pair - 1 - (lin % per_pair);
+  return m;
+}
+
+// ------------------------------------------------------------------ forward
+__global__ __launch_bounds__(NT, 2) void k_attn_fwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                    const __bf16* __restrict__ v, __bf16* __restrict__ o,
+                                                    float* __restrict__ lse, AttnShape sh) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [2 stages][K | V]
+  const int G = sh.H / sh.Hkv;
+  const int per_pair = (sh.S / QT) * G / NW;
+  const BlockMap bm = map_block(sh, per_pair);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, hi = lane >> 5, ql = lane & 31;
+  const int u = bm.bi * NW + w, qt = u / G, h = bm.kvh * G + (u % G);
+  const int q0 = qt * QT;
+  const int qt_max = (bm.bi * NW + NW - 1) / G;
+  const int ntiles = (qt_max * QT + QT + KT - 1) / KT;
+  const long long tok0 = (long long)bm.b * sh.S;
+
+  const __bf16* kb = k + tok0 * sh.k_rs + (long long)bm.kvh * HD;
+  const __bf16* vb = v + tok0 * sh.v_rs + (long long)bm.kvh * HD;
+
+  // Q fragments (B operand of S^T = K Q^T): row q0+ql, d = 16ks + 8hi .. +7
+  bf16x8 qf[8];
+  {
+    const __bf16* qr = q + (tok0 + q0 + ql) * sh.q_rs + (long long)h * HD + 8 * hi;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qr + 16 * ks);
+  }
+  f32x16 acc_o[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) acc_o[db] = (f32x16){};
+  float m_run = -INFINITY, l_run = 0.f;
+  const float sl = sh.scale * LOG2E;
+  const int qrow = q0 + ql;
+
+  TileRegs tk, tv;
+  tile_load(tk, kb, sh.k_rs);
+  tile_load(tv, vb, sh.v_rs);
+  tile_store(tk, smem);
+  tile_store(tv, smem + TILE_B);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int k0 = t * KT;
+    const char* ktile = smem + (t & 1) * 2 * TILE_B;
+    const char* vtile = ktile + TILE_B;
+    if (t + 1 < ntiles) {  // next tile in flight during this tile's math
+      tile_load(tk, kb + (long long)(k0 + KT) * sh.k_rs, sh.k_rs);
+      tile_load(tv, vb + (long long)(k0 + KT) * sh.v_rs, sh.v_rs);
+    }
+    if (k0 <= q0 + QT - 1) {  // wave-uniform: this tile has unmasked keys for this wave
+      // S^T (keys on registers, query on the lane)
+      f32x16 st[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        st[kt] = (f32x16){};
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) st[kt] = mfma(row_operand(ktile, 32 * kt, ks), qf[ks], st[kt]);
+      }
+      const bool diag = k0 + KT - 1 > q0;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float s = st[kt][i] * sl;
+          if (diag) {
+            const int key = k0 + 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hi;
+            if (key > qrow) s = -INFINITY;
+          }
+          st[kt][i] = s;
+          mx = fmaxf(mx, s);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      float rs = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = __builtin_amdgcn_exp2f(st[kt][i] - m_new);
+          st[kt][i] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 32);
+      l_run = l_run * alpha + rs;
+      m_run = m_new;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) acc_o[db] *= alpha;
+      bf16x8 pf[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        float tmp[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tmp[j] = st[ks >> 1][8 * (ks & 1) + j];
+        pf[ks] = acc_to_operand(tmp);
+      }
+      // O^T += V^T P^T
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) acc_o[db] = mfma(tr_operand(vtile, 16 * ks, 32 * db), pf[ks], acc_o[db]);
+    }
+    if (t + 1 < ntiles) {
+      char* nt = smem + ((t + 1) & 1) * 2 * TILE_B;
+      tile_store(tk, nt);
+      tile_store(tv, nt + TILE_B);
+    }
+    __syncthreads();
+  }
+  // epilogue: O[q][d] = O^T[d][q] / l ; lane holds d = 32db + 8g + 4hi + (0..3)
+  const float inv = 1.f / l_run;
+  __bf16* orow = o + (tok0 + qrow) * sh.o_rs + (long long)h * HD + 4 * hi;
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      u32x2 pk = {pack2(acc_o[db][4 * g] * inv, acc_o[db][4 * g + 1] * inv),
+                  pack2(acc_o[db][4 * g + 2] * inv, acc_o[db][4 * g + 3] * inv)};
+      *reinterpret_cast<u32x2*>(orow + 32 * db + 8 * g) = pk;
+    }
+  if (hi == 0) lse[((long long)bm.b * sh.H + h) * sh.S + qrow] = m_run + __log2f(l_run);
+}
+
+// ------------------------------------------------------------ backward prep
+// delta[b][h][s] = sum_d dO * O (fp32), one wave per (token, head) row pair.
+__global__ __launch_bounds__(256) void k_attn_bwd_delta(const __bf16* __restrict__ o, const __bf16* __restrict__ dout,
+                                                        float* __restrict__ delta, AttnShape sh) {
+  const long long row = (long long)blockIdx.x * 8 + (threadIdx.x >> 5);  // 32 lanes x 4 elements per row
+  const long long nrows = (long long)sh.B * sh.S * sh.H;
+  if (row >= nrows) return;
+  const long long tok = row / sh.H;
+  const int h = (int)(row % sh.H);
+  const int l = threadIdx.x & 31;
+  const __bf16* a = o + tok * sh.o_rs + (long long)h * HD + 4 * l;
+  const __bf16* b = dout + tok * sh.o_rs + (long long)h * HD + 4 * l;
+  const u32x2 ua = *reinterpret_cast<const u32x2*>(a), ub = *reinterpret_cast<const u32x2*>(b);
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    s += __uint_as_float(ua[e] << 16) * __uint_as_float(ub[e] << 16);
+    s += __uint_as_float(ua[e] & 0xffff0000u) * __uint_as_float(ub[e] & 0xffff0000u);
+  }
+#pragma unroll
+  for (int off = 16; off > 0; off >>= 1) s += __shfl_xor(s, off, 32);
+  if (l == 0) {
+    const int b_ = (int)(tok / sh.S), s_ = (int)(tok % sh.S);
+    delta[((long long)b_ * sh.H + h) * sh.S + s_] = s;
+  }
+}
+
+// --------------------------------------------------------------- dQ kernel
+// Same decomposition as the forward.  Per key tile: S^T = K Q^T,
+// dP^T = V dO^T (V rows from LDS, dO fragments in registers),
+// P = exp2(S^T*c - lse2), dS = P (dP^T - delta), dQ^T += K^T dS^T.
+__global__ __launch_bounds__(NT, 2) void k_attn_bwd_dq(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                       const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
+                                                       const float* __restrict__ lse, const float* __restrict__ delta,
+                                                       __bf16* __restrict__ dq, long long dq_rs, AttnShape sh) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int G = sh.H / sh.Hkv;
+  const int per_pair = (sh.S / QT) * G / NW;
+  const BlockMap bm = map_block(sh, per_pair);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, hi = lane >> 5, ql = lane & 31;
+  const int u = bm.bi * NW + w, qt = u / G, h = bm.kvh * G + (u % G);
+  const int q0 = qt * QT;
+  const int qt_max = (bm.bi * NW + NW - 1) / G;
+  const int ntiles = (qt_max * QT + QT + KT - 1) / KT;
+  const long long tok0 = (long long)bm.b * sh.S;
+  const __bf16* kb = k + tok0 * sh.k_rs + (long long)bm.kvh * HD;
+  const __bf16* vb = v + tok0 * sh.v_rs + (long long)bm.kvh * HD;
+  const int qrow = q0 + ql;
+
+  bf16x8 qf[8], df[8];
+  {
+    const __bf16* qr = q + (tok0 + qrow) * sh.q_rs + (long long)h * HD + 8 * hi;
+    const __bf16* dr = dout + (tok0 + qrow) * sh.o_rs + (long long)h * HD + 8 * hi;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      qf[ks] = *reinterpret_cast<const bf16x8*>(qr + 16 * ks);
+      df[ks] = *reinterpret_cast<const bf16x8*>(dr + 16 * ks);
+    }
+  }
+  const long long li = ((long long)bm.b * sh.H + h) * sh.S + qrow;
+  const float lse2 = lse[li], dlt = delta[li];
+  const float sl = sh.scale * LOG2E;
+  f32x16 acc[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) acc[db] = (f32x16){};
+
+  TileRegs tk, tv;
+  tile_load(tk, kb, sh.k_rs);
+  tile_load(tv, vb, sh.v_rs);
+  tile_store(tk, smem);
+  tile_store(tv, smem + TILE_B);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int k0 = t * KT;
+    const char* ktile = smem + (t & 1) * 2 * TILE_B;
+    const char* vtile = ktile + TILE_B;
+    if (t + 1 < ntiles) {
+      tile_load(tk, kb + (long long)(k0 + KT) * sh.k_rs, sh.k_rs);
+      tile_load(tv, vb + (long long)(k0 + KT) * sh.v_rs, sh.v_rs);
+    }
+    if (k0 <= q0 + QT - 1) {
+      f32x16 st[2], dp[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        st[kt] = (f32x16){};
+        dp[kt] = (f32x16){};
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          st[kt] = mfma(row_operand(ktile, 32 * kt, ks), qf[ks], st[kt]);
+          dp[kt] = mfma(row_operand(vtile, 32 * kt, ks), df[ks], dp[kt]);
+        }
+      }
+      const bool diag = k0 + KT - 1 > q0;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float p = __builtin_amdgcn_exp2f(st[kt][i] * sl - lse2);
+          if (diag) {
+            const int key = k0 + 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hi;
+            if (key > qrow) p = 0.f;
+          }
+          st[kt][i] = p * (dp[kt][i] - dlt);  // dS (softmax scale applied at the end)
+        }
+      bf16x8 sf[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        float tmp[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tmp[j] = st[ks >> 1][8 * (ks & 1) + j];
+        sf[ks] = acc_to_operand(tmp);
+      }
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) acc[db] = mfma(tr_operand(ktile, 16 * ks, 32 * db), sf[ks], acc[db]);
+    }
+    if (t + 1 < ntiles) {
+      char* nt = smem + ((t + 1) & 1) * 2 * TILE_B;
+      tile_store(tk, nt);
+      tile_store(tv, nt + TILE_B);
+    }
+    __syncthreads();
+  }
+  __bf16* drow = dq + (tok0 + qrow) * dq_rs + (long long)h * HD + 4 * hi;
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float c = sh.scale;
+      u32x2 pk = {pack2(acc[db][4 * g] * c, acc[db][4 * g + 1] * c), pack2(acc[db][4 * g + 2] * c, acc[db][4 * g + 3] * c)};
+      *reinterpret_cast<u32x2*>(drow + 32 * db + 8 * g) = pk;
+    }
+}
+
+// ------------------------------------------------------------ dK/dV kernel
+// Block = (batch, kv head, 128 keys); wave w owns keys kb0 + 32w .. +31.
+// Loops over the G query heads x 32-row query tiles from the diagonal on;
+// Q and dO tiles (32 x 128) + LSE/delta rows are staged in LDS per step
+// (shared by the 4 waves).  Per step and wave: S = Q K^T and dP = dO V^T
+// (key on the lane, K/V fragments in registers, accumulators initialised
+// with -lse2/c and -delta), P = exp2(c S), dS = P dP;
+// dV^T += dO^T P, dK^T += Q^T dS (transposed LDS reads of dO / Q).
+constexpr int KB = NW * 32;           // keys per block
+constexpr int QTB = 32 * 256;          // one 32 x 128 bf16 tile in bytes
+__global__ __launch_bounds__(NT, 1) void k_attn_bwd_dkdv(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                         const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
+                                                         const float* __restrict__ lse, const float* __restrict__ delta,
+                                                         __bf16* __restrict__ dk, __bf16* __restrict__ dv,
+                                                         long long dkv_rs, AttnShape sh) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [2][Q | dO] + [2][lse | delta]
+  float* rowc = reinterpret_cast<float*>(smem + 4 * QTB);       // [2][2][32]
+  const int G = sh.H / sh.Hkv;
+  const int nkb = sh.S / KB;
+  // block -> (b, kvh, key block), heaviest (earliest keys) first, XCD-grouped
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  int lin = bid;
+  if ((nblk & 7) == 0) lin = (bid & 7) * (nblk >> 3) + (bid >> 3);
+  const int pair = lin / nkb, kbi = lin % nkb;
+  const int b = pair / sh.Hkv, kvh = pair % sh.Hkv;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, hi = lane >> 5, kl = lane & 31;
+  const int kb0 = kbi * KB, key = kb0 + 32 * w + kl;
+  const long long tok0 = (long long)b * sh.S;
+
+  // K, V fragments (B operands of S = Q K^T and dP = dO V^T)
+  bf16x8 kf[8], vf[8];
+  {
+    const __bf16* kr = k + (tok0 + key) * sh.k_rs + (long long)kvh * HD + 8 * hi;
+    const __bf16* vr = v + (tok0 + key) * sh.v_rs + (long long)kvh * HD + 8 * hi;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      kf[ks] = *reinterpret_cast<const bf16x8*>(kr + 16 * ks);
+      vf[ks] = *reinterpret_cast<const bf16x8*>(vr + 16 * ks);
+    }
+  }
+  f32x16 dka[4], dva[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    dka[db] = (f32x16){};
+    dva[db] = (f32x16){};
+  }
+  const float sl = sh.scale * LOG2E;
+  const float inv_sl = 1.f / sl;
+  const int nqt = (sh.S - kb0) / QT;  // query tiles from the block's first key on
+  const int nsteps = G * nqt;
+
+  // step s -> (head g, query tile qt); Q/dO tile of 32 rows x 256 B:
+  // 2 x 512 chunks of 16 B over 256 threads
+  auto stage = [&](int s, uint4 (&r)[4], float& c) {
+    const int g = s / nqt, qt = s % nqt, h = kvh * G + g;
+    const long long tok = tok0 + kb0 + (long long)qt * QT;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int c_ = threadIdx.x + NT * p, rr = c_ >> 4, ch = c_ & 15;
+      r[p] = *reinterpret_cast<const uint4*>(q + (tok + rr) * sh.q_rs + (long long)h * HD + ch * 8);
+      r[2 + p] = *reinterpret_cast<const uint4*>(dout + (tok + rr) * sh.o_rs + (long long)h * HD + ch * 8);
+    }
+    const long long li = ((long long)b * sh.H + h) * sh.S + kb0 + (long long)qt * QT;
+    if (threadIdx.x < 32) c = lse[li + threadIdx.x];
+    else if (threadIdx.x < 64) c = delta[li + threadIdx.x - 32];
+  };
+  auto commit = [&](int buf, const uint4 (&r)[4], float c) {
+    char* qtile = smem + buf * 2 * QTB;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int c_ = threadIdx.x + NT * p, rr = c_ >> 4, ch = c_ & 15;
+      *reinterpret_cast<uint4*>(qtile + swz(rr, ch)) = r[p];
+      *reinterpret_cast<uint4*>(qtile + QTB + swz(rr, ch)) = r[2 + p];
+    }
+    if (threadIdx.x < 64) rowc[buf * 64 + threadIdx.x] = c;
+  };
+
+  uint4 regs[4];
+  float rc = 0.f;
+  stage(0, regs, rc);
+  commit(0, regs, rc);
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nsteps) stage(s + 1, regs, rc);
+    const int qt = s % nqt;
+    const int q0 = kb0 + qt * QT;  // first query row of this tile
+    if (q0 + QT - 1 >= kb0 + 32 * w) {  // wave-uniform: some query >= some key of this wave
+      const char* qtile = smem + buf * 2 * QTB;
+      const char* dtile = qtile + QTB;
+      const float* lrow = rowc + buf * 64;
+      // accumulator init with the row constants: row q = (i&3)+8(i>>2)+4hi
+      f32x16 sa, pa;
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const float4 l4 = *reinterpret_cast<const float4*>(lrow + 8 * gg + 4 * hi);
+        const float4 d4 = *reinterpret_cast<const float4*>(lrow + 32 + 8 * gg + 4 * hi);
+        sa[4 * gg] = -l4.x * inv_sl; sa[4 * gg + 1] = -l4.y * inv_sl;
+        sa[4 * gg + 2] = -l4.z * inv_sl; sa[4 * gg + 3] = -l4.w * inv_sl;
+        pa[4 * gg] = -d4.x; pa[4 * gg + 1] = -d4.y; pa[4 * gg + 2] = -d4.z; pa[4 * gg + 3] = -d4.w;
+      }
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        sa = mfma(row_operand(qtile, 0, ks), kf[ks], sa);
+        pa = mfma(row_operand(dtile, 0, ks), vf[ks], pa);
+      }
+      const bool diag = q0 < kb0 + 32 * w + 31;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float p = __builtin_amdgcn_exp2f(sa[i] * sl);
+        if (diag) {
+          const int qr = q0 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+          if (key > qr) p = 0.f;
+        }
+        sa[i] = p;
+        pa[i] = p * pa[i];  // dS
+      }
+      bf16x8 pf[2], sf[2];
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        float t0[8], t1[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          t0[j] = sa[8 * qs + j];
+          t1[j] = pa[8 * qs + j];
+        }
+        pf[qs] = acc_to_operand(t0);
+        sf[qs] = acc_to_operand(t1);
+      }
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int qs = 0; qs < 2; ++qs) {
+          dva[db] = mfma(tr_operand(dtile, 16 * qs, 32 * db), pf[qs], dva[db]);
+          dka[db] = mfma(tr_operand(qtile, 16 * qs, 32 * db), sf[qs], dka[db]);
+        }
+    }
+    if (s + 1 < nsteps) commit(buf ^ 1, regs, rc);
+    __syncthreads();
+  }
+  // dK^T / dV^T: lane = key, registers = d (32db + 8g + 4hi + 0..3)
+  __bf16* dkr = dk + (tok0 + key) * dkv_rs + (long long)kvh * HD + 4 * hi;
+  __bf16* dvr = dv + (tok0 + key) * dkv_rs + (long long)kvh * HD + 4 * hi;
+  const float c = sh.scale;
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      u32x2 pk = {pack2(dka[db][4 * g] * c, dka[db][4 * g + 1] * c), pack2(dka[db][4 * g + 2] * c, dka[db][4 * g + 3] * c)};
+      *reinterpret_cast<u32x2*>(dkr + 32 * db + 8 * g) = pk;
+      u32x2 pv = {pack2(dva[db][4 * g], dva[db][4 * g + 1]), pack2(dva[db][4 * g + 2], dva[db][4 * g + 3])};
+      *reinterpret_cast<u32x2*>(dvr + 32 * db + 8 * g) = pv;
+    }
+}
+
+}  // namespace
+
+#define PTO_API extern "C" __attribute__((visibility("default")))
+
+static bool attn_shape_ok(const AttnShape& sh) {
+  if (sh.H % sh.Hkv) return false;
+  const int G = sh.H / sh.Hkv;
+  return sh.S % KB == 0 && sh.S % KT == 0 && ((sh.S / QT) * G) % NW == 0 && sh.B > 0;
+}
+
+static AttnShape make_shape(int B, int S, int H, int Hkv, long long q_rs, long long k_rs, long long v_rs,
+                            long long o_rs, float scale) {
+  AttnShape sh{B, S, H, Hkv, q_rs, k_rs, v_rs, o_rs, scale};
+  return sh;
+}
+
+// Returns -1 for unsupported shapes (S % 128, H % Hkv, head_dim != 128 is the
+// caller's contract).
+PTO_API int pto_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H,
+                         int Hkv, long long q_rs, long long k_rs, long long v_rs, long long o_rs, float scale,
+                         hipStream_t s) {
+  const AttnShape sh = make_shape(B, S, H, Hkv, q_rs, k_rs, v_rs, o_rs, scale);
+  if (!attn_shape_ok(sh)) return -1;
+  const int G = H / Hkv;
+  const int nblk = B * Hkv * ((S / QT) * G / NW);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_attn_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE_B);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_attn_fwd, dim3(nblk), dim3(NT), 4 * TILE_B, s, (const __bf16*)q, (const __bf16*)k,
+                     (const __bf16*)v, (__bf16*)o, lse, sh);
+  return (int)hipGetLastError();
+}
+
+// delta = rowsum(dO * O); dq/dk/dv written at row stride dqkv_rs (the dQKV
+// buffer; dk/dv point at the K / V column blocks).
+PTO_API int pto_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                         const float* lse, float* delta, void* dq, void* dk, void* dv, long long dqkv_rs, int B,
+                         int S, int H, int Hkv, long long q_rs, long long k_rs, long long v_rs, long long o_rs,
+                         float scale, hipStream_t s) {
+  const AttnShape sh = make_shape(B, S, H, Hkv, q_rs, k_rs, v_rs, o_rs, scale);
+  if (!attn_shape_ok(sh)) return -1;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_attn_bwd_dq, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE_B);
+    (void)hipFuncSetAttribute((const void*)k_attn_bwd_dkdv, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        4 * QTB + 2 * 64 * 4);
+    attr = true;
+  }
+  const long long rows = (long long)B * S * H;
+  hipLaunchKernelGGL(k_attn_bwd_delta, dim3((unsigned)((rows + 7) / 8)), dim3(256), 0, s, (const __bf16*)o,
+                     (const __bf16*)dout, delta, sh);
+  const int G = H / Hkv;
+  hipLaunchKernelGGL(k_attn_bwd_dkdv, dim3(B * Hkv * (S / KB)), dim3(NT), 4 * QTB + 2 * 64 * 4, s,
+                     (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta,
+                     (__bf16*)dk, (__bf16*)dv, dqkv_rs, sh);
+  hipLaunchKernelGGL(k_attn_bwd_dq, dim3(B * Hkv * ((S / QT) * G / NW)), dim3(NT), 4 * TILE_B, s,
+                     (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta,
+                     (__bf16*)dq, dqkv_rs, sh);
+  return (int)hipGetLastError();
+}

@@ -26,11 +26,16 @@ the numerics reference (and for CPU tests).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+# impl="hip" attention: "hip" = csrc/kernels/attention.hip (head_dim 128,
+# S % 128 == 0; other shapes fall back to SDPA), "sdpa" = ROCm SDPA.
+ATTN_IMPL = os.environ.get("PTO_ATTN", "hip")
 
 
 @dataclass
@@ -114,7 +119,11 @@ class LlamaBlock(nn.Module):
             h, y = llm.add_rmsnorm(h, delta, self.attn_norm, c.norm_eps)
         qkv = F.linear(y, self.wqkv.weight)
         qkv = llm.rope_(qkv, rope[0], rope[1], S, c.n_heads + c.n_kv_heads, c.head_dim)
-        attn = F.linear(self._attend(qkv, B, S), self.wo.weight)
+        if ATTN_IMPL == "hip" and llm.flash_attention_supported(S, c.n_heads, c.n_kv_heads, c.head_dim):
+            ctx = llm.flash_attention(qkv, B, S, c.n_heads, c.n_kv_heads)  # [B*S, H*128], no transposes
+        else:
+            ctx = self._attend(qkv, B, S)
+        attn = F.linear(ctx, self.wo.weight)
         h, y = llm.add_rmsnorm(h, attn, self.ffn_norm, c.norm_eps)
         mlp = F.linear(llm.swiglu(F.linear(y, self.w13.weight)), self.w2.weight)
         return h, mlp

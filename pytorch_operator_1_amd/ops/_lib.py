@@ -29,7 +29,7 @@ ARCH = os.environ.get("PTO_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 
 HIP_SOURCES = ("kernels/mnist_kernels.hip", "kernels/common_kernels.hip", "kernels/optim_kernels.hip",
-               "kernels/llm_kernels.hip", "comm/xgmi_allreduce.hip")
+               "kernels/llm_kernels.hip", "kernels/attention.hip", "comm/xgmi_allreduce.hip")
 
 _lock = threading.Lock()
 _lib = None
@@ -107,6 +107,9 @@ _SIGS = {
     "pto_rope": [_P, _P, _P, _P, _L, _I, _I, _I, _I, _L, _I, _P],
     "pto_ce_fwd": [_P, _P, _P, _P, _L, _I, _L, _P],
     "pto_ce_bwd": [_P, _P, _P, _P, _L, _I, _L, _P],
+    # causal GQA flash attention, head_dim 128 (csrc/kernels/attention.hip)
+    "pto_attn_fwd": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _L, _L, _L, _L, _F, _P],
+    "pto_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _L, _L, _L, _L, _F, _P],
     # xGMI peer all-reduce (csrc/comm/xgmi_allreduce.hip)
     "pto_ar_ipc_handle_size": [],
     "pto_ar_flag_bytes": [_I],

@@ -195,3 +195,51 @@ class _CrossEntropy(torch.autograd.Function):
 def cross_entropy(logits, labels, ignore_index: int = -100):
     """Mean token cross-entropy over non-ignored labels on bf16 logits."""
     return _CrossEntropy.apply(logits, labels, ignore_index)
+
+
+def flash_attention_supported(S: int, H: int, Hkv: int, head_dim: int) -> bool:
+    """Shapes the HIP kernels cover: head_dim 128, S % 128 == 0, H % Hkv == 0."""
+    return head_dim == 128 and S % 128 == 0 and H % Hkv == 0 and ((S // 32) * (H // Hkv)) % 4 == 0
+
+
+class _FlashAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, B, S, H, Hkv):
+        qkv = _req(qkv, "flash_attention")
+        D = 128
+        rs = qkv.shape[-1]
+        if rs != (H + 2 * Hkv) * D or qkv.numel() != B * S * rs:
+            raise ValueError("flash_attention: qkv must be [B*S, (H + 2*Hkv)*128]")
+        o = torch.empty(B * S, H * D, device=qkv.device, dtype=qkv.dtype)
+        lse = torch.empty(B, H, S, device=qkv.device, dtype=torch.float32)
+        base = qkv.data_ptr()
+        esz = qkv.element_size()
+        _lib.check(_lib.lib().pto_attn_fwd(base, base + H * D * esz, base + (H + Hkv) * D * esz, o.data_ptr(),
+                                           lse.data_ptr(), B, S, H, Hkv, rs, rs, rs, H * D, D ** -0.5,
+                                           _lib.stream_ptr(qkv.device)), "attn_fwd")
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.shape = (B, S, H, Hkv)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        B, S, H, Hkv = ctx.shape
+        D = 128
+        rs = qkv.shape[-1]
+        do = do.contiguous()
+        dqkv = torch.empty_like(qkv)
+        delta = torch.empty(B, H, S, device=qkv.device, dtype=torch.float32)
+        base, dbase, esz = qkv.data_ptr(), dqkv.data_ptr(), qkv.element_size()
+        _lib.check(_lib.lib().pto_attn_bwd(base, base + H * D * esz, base + (H + Hkv) * D * esz, o.data_ptr(),
+                                           do.data_ptr(), lse.data_ptr(), delta.data_ptr(), dbase,
+                                           dbase + H * D * esz, dbase + (H + Hkv) * D * esz, rs, B, S, H, Hkv,
+                                           rs, rs, rs, H * D, D ** -0.5, _lib.stream_ptr(qkv.device)), "attn_bwd")
+        return dqkv, None, None, None, None
+
+
+def flash_attention(qkv, B: int, S: int, H: int, Hkv: int):
+    """Causal GQA attention straight from the fused QKV projection
+    ``[B*S, (H + 2*Hkv)*128]`` (q heads, then k, then v heads per row) to
+    ``O [B*S, H*128]`` — the layout the output projection consumes."""
+    return _FlashAttention.apply(qkv, B, S, H, Hkv)

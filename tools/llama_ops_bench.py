@@ -91,6 +91,16 @@ def main():
             res[name] = {"fwd_ms": t, "bwd_ms": tb, "fwd_tflops": attn_fl / t / 1e9, "bwd_tflops": 2.5 * attn_fl / tb / 1e9}
         except Exception as e:  # noqa: BLE001
             res[name] = {"error": repr(e)[:200]}
+    try:  # hand-written gfx950 flash attention straight from the QKV layout
+        fa_in = qkv.clone()
+        t = timed(lambda: llm.flash_attention(fa_in, B, S, H, KV))
+        a = fa_in.clone().requires_grad_()
+        o = llm.flash_attention(a, B, S, H, KV)
+        go = torch.randn_like(o)
+        tb = timed(lambda: torch.autograd.grad(o, a, go, retain_graph=True))
+        res["flash_hip"] = {"fwd_ms": t, "bwd_ms": tb, "fwd_tflops": attn_fl / t / 1e9, "bwd_tflops": 2.5 * attn_fl / tb / 1e9}
+    except Exception as e:  # noqa: BLE001
+        res["flash_hip"] = {"error": repr(e)[:200]}
     try:
         from torch.nn.attention import SDPBackend, sdpa_kernel
 
