@@ -115,7 +115,6 @@ class XgmiAllReduce:
         for c, (off, n) in enumerate(ranges):
             self.allreduce_(off, n, chan=c % 2)
         torch.cuda.synchronize(self.device)
-        self.check()
         bad = 0.0
         for off, n in ranges:
             bad = max(bad, (self.buf[off:off + n] - ref[off:off + n]).abs().max().item())
@@ -123,6 +122,19 @@ class XgmiAllReduce:
         chk = self.buf.clone()
         dist.all_reduce(chk, op=dist.ReduceOp.MAX, group=self.group)
         identical = float((chk - self.buf).abs().max().item()) == 0.0
+        scale = max(1.0, ref.abs().max().item())
+        timed_out = int(self.err.item()) != 0
+
+        def agree(flag: bool) -> bool:  # every rank takes the same branch
+            t = torch.tensor([1.0 if flag else 0.0], device=self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+            return t.item() == 1.0
+
+        result = {"use_xgmi": False, "correct": False, "max_abs_err": bad, "timed_out": timed_out}
+        if not agree(bad <= 1e-5 * scale and identical and not timed_out):
+            self.buf.copy_(saved)
+            torch.cuda.synchronize(self.device)
+            return result
 
         def timed(fn):
             torch.cuda.synchronize(self.device)
@@ -145,15 +157,12 @@ class XgmiAllReduce:
 
         run_xgmi(), run_rccl()  # warm
         tx, tr = timed(run_xgmi), timed(run_rccl)
-        self.check()
+        ok_after = agree(int(self.err.item()) == 0)
         self.buf.copy_(saved)
         torch.cuda.synchronize(self.device)
-        scale = max(1.0, max(ref.abs().max().item(), 1.0))
-        okf = torch.tensor([1.0 if (bad <= 1e-5 * scale and identical) else 0.0], device=self.device)
-        dist.all_reduce(okf, op=dist.ReduceOp.MIN, group=self.group)
-        correct = okf.item() == 1.0
-        return {"use_xgmi": bool(correct and tx < tr), "correct": correct, "xgmi_us": round(tx, 2),
-                "rccl_us": round(tr, 2), "max_abs_err": bad}
+        result.update(correct=ok_after, use_xgmi=bool(ok_after and tx < tr), xgmi_us=round(tx, 2),
+                      rccl_us=round(tr, 2), timed_out=not ok_after)
+        return result
 
     def close(self):
         L = _lib.lib()

@@ -29,6 +29,9 @@ class ResNetTrainer:
         from ..models.resnet import resnet50, synthetic_images
 
         torch.manual_seed(seed)
+        # MIOpen find: benchmark the conv solvers once per shape (warmup) and
+        # keep the fastest instead of the heuristic pick
+        torch.backends.cudnn.benchmark = True
         self.device = device
         self.batch_size = batch_size
         self.model = resnet50().to(device=device, memory_format=torch.channels_last)
