@@ -360,13 +360,10 @@ __global__ __launch_bounds__(256) void k_relu_bwd(const float* __restrict__ g, c
 // (= dlogits @ W2, masked by ReLU).  `inv_b` = 1/B for a mean loss.  All 99
 // loads of a lane (8 activations, 80 weights, 10 biases, the label) are
 // issued before the first FMA.
-__global__ __launch_bounds__(256) void k_fc2_ce(const float* __restrict__ h1, const float* __restrict__ w,
-                                                const float* __restrict__ bias, const int64_t* __restrict__ labels,
-                                                float* __restrict__ logp, float* __restrict__ loss_rows,
-                                                float* __restrict__ dlogits, float* __restrict__ dh1, int B,
-                                                float inv_b, const long long* __restrict__ bidx) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= B) return;
+PTO_DEV void fc2_ce_row(int row, int lane, const float* __restrict__ h1, const float* __restrict__ w,
+                        const float* __restrict__ bias, const int64_t* __restrict__ labels,
+                        float* __restrict__ logp, float* __restrict__ loss_rows, float* __restrict__ dlogits,
+                        float* __restrict__ dh1, int B, float inv_b, const long long* __restrict__ bidx) {
   float h[8], wv[NCLS][8], bz[NCLS];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -433,6 +430,56 @@ __global__ __launch_bounds__(256) void k_fc2_ce(const float* __restrict__ h1, co
       dh1[row * F1OUT + k] = h[j] > 0.f ? s : 0.f;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void k_fc2_ce(const float* __restrict__ h1, const float* __restrict__ w,
+                                                const float* __restrict__ bias, const int64_t* __restrict__ labels,
+                                                float* __restrict__ logp, float* __restrict__ loss_rows,
+                                                float* __restrict__ dlogits, float* __restrict__ dh1, int B,
+                                                float inv_b, const long long* __restrict__ bidx) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B) return;
+  fc2_ce_row(row, lane, h1, w, bias, labels, logp, loss_rows, dlogits, dh1, B, inv_b, bidx);
+}
+
+// F3+F4 in one launch: the fc1 tiles as k_linear_fwd_vec, then the LAST
+// block to finish a 16-row group (per-group arrival counter) runs
+// fc2 + log_softmax + NLL + dlogits + dh1 for those 16 rows.  Hand-off per
+// MI355X_MICROARCH.md "inter-workgroup visibility": producers wait for
+// their stores, barrier, one agent release + counter add; the last arriver
+// does one agent acquire, waits, barriers, then loads h1.  The last block
+// re-arms the counter, so graph replays need no reset launch.
+__global__ __launch_bounds__(512) void k_fc12_ce(const float* __restrict__ a2p, const float* __restrict__ w1,
+                                                 const float* __restrict__ b1, float* __restrict__ h1,
+                                                 const float* __restrict__ w2, const float* __restrict__ b2,
+                                                 const int64_t* __restrict__ labels, float* __restrict__ loss_rows,
+                                                 float* __restrict__ dlogits, float* __restrict__ dh1, int B,
+                                                 float inv_b, const long long* __restrict__ bidx,
+                                                 unsigned* __restrict__ counters) {
+  __shared__ float red[8 * 256];
+  __shared__ int is_last;
+  block_gemm_splitk<LAY_ROWK, LAY_ROWK, EpiBiasRelu, 8, true, true>(a2p, F1IN, w1, F1IN, B, F1OUT, F1IN, blockIdx.x,
+                                                                    red, EpiBiasRelu{b1, h1, F1OUT, true});
+  const int mtiles = (B + 15) >> 4, ntiles = (F1OUT + 15) >> 4;
+  const int mt = blockIdx.x % mtiles;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = atomicAdd(&counters[mt], 1u);
+    is_last = prev == (unsigned)(ntiles - 1);
+    if (is_last) {
+      counters[mt] = 0u;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!is_last) return;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int row = mt * 16 + w; row < min(B, mt * 16 + 16); row += 8)
+    fc2_ce_row(row, lane, h1, w2, b2, labels, nullptr, loss_rows, dlogits, dh1, B, inv_b, bidx);
 }
 
 // ---------------------------------------------------------------- B3 ----
@@ -943,6 +990,16 @@ PTO_API int pto_fc2_ce(const float* h1, const float* w, const float* b, const in
                        hipStream_t s) {
   hipLaunchKernelGGL(k_fc2_ce, dim3((B + 3) / 4), dim3(256), 0, s, h1, w, b, labels, logp, loss_rows, dlogits, dh1,
                      B, inv_b, bidx);
+  LAUNCH_CHECK();
+}
+
+// counters: >= (B+15)/16 zero-initialised uint32 (re-armed by the kernel).
+PTO_API int pto_fc12_ce(const float* a2p, const float* w1, const float* b1, float* h1, const float* w2,
+                        const float* b2, const int64_t* labels, float* loss_rows, float* dlogits, float* dh1, int B,
+                        float inv_b, const long long* bidx, unsigned* counters, hipStream_t s) {
+  const int tiles = ((B + 15) / 16) * ((F1OUT + 15) / 16);
+  hipLaunchKernelGGL(k_fc12_ce, dim3(tiles), dim3(512), 0, s, a2p, w1, b1, h1, w2, b2, labels, loss_rows, dlogits,
+                     dh1, B, inv_b, bidx, counters);
   LAUNCH_CHECK();
 }
 

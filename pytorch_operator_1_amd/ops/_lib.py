@@ -83,6 +83,7 @@ _SIGS = {
     "pto_linear_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "pto_relu_bwd": [_P, _P, _P, _I, _P],
     "pto_fc2_ce": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _P, _P],
+    "pto_fc12_ce": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _P, _P, _P],
     "pto_fc_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P],
     "pto_conv2_bwd": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P],
     "pto_conv1_bwd": [_P, _P, _P, _P, _P, _I, _P, _P],

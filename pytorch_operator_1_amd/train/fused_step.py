@@ -99,6 +99,10 @@ class FusedMnistTrainer:
         # device-side batch cursor: read by conv1 fwd/bwd and fc2_ce, advanced
         # by the optimizer launch (no per-step copy kernels, graph-safe)
         self.batch_idx = torch.zeros(1, device=device, dtype=torch.int64)
+        # fused fc1+fc2/CE launch (PTO_FUSE_FC=0: the two-launch path) and its
+        # per-16-row arrival counters (re-armed by the kernel itself)
+        self.fuse_fc = os.environ.get("PTO_FUSE_FC", "1") == "1"
+        self.fc_counters = torch.zeros(max(1, (self.B + 15) // 16), device=device, dtype=torch.int32)
 
         # SGD launch table (one "tensor" = the whole flat buffer).
         from ..ops.optim import SgdTable
@@ -168,11 +172,17 @@ class FusedMnistTrainer:
         c(L.pto_conv12_fwd(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
                            P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
                            self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi, s), "conv12_fwd")
-        c(L.pto_linear_fwd(self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
-                           self.h1.data_ptr(), B, 500, 800, 1, s), "fc1_fwd")
-        c(L.pto_fc2_ce(self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
-                       self.target.data_ptr(), None, self.loss_rows.data_ptr(), self.dlogits.data_ptr(),
-                       self.dh1.data_ptr(), B, 1.0 / B, bi, s), "fc2_ce")
+        if self.fuse_fc:  # fc1 + (last block per 16 rows) fc2/CE/dlogits/dh1 in one launch
+            c(L.pto_fc12_ce(self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
+                            self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
+                            self.target.data_ptr(), self.loss_rows.data_ptr(), self.dlogits.data_ptr(),
+                            self.dh1.data_ptr(), B, 1.0 / B, bi, self.fc_counters.data_ptr(), s), "fc12_ce")
+        else:
+            c(L.pto_linear_fwd(self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
+                               self.h1.data_ptr(), B, 500, 800, 1, s), "fc1_fwd")
+            c(L.pto_fc2_ce(self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
+                           self.target.data_ptr(), None, self.loss_rows.data_ptr(), self.dlogits.data_ptr(),
+                           self.dh1.data_ptr(), B, 1.0 / B, bi, s), "fc2_ce")
         c(L.pto_fc_bwd(self.dh1.data_ptr(), self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), self.h1.data_ptr(),
                        self.dlogits.data_ptr(), G["fc1.weight"].data_ptr(), G["fc1.bias"].data_ptr(),
                        G["fc2.weight"].data_ptr(), G["fc2.bias"].data_ptr(), self.da2p.data_ptr(), B, s), "fc_bwd")

@@ -16,3 +16,8 @@ cat gpurun_out/llama8b_b$b.json
 done
 timeout -k 10 300 python bench.py --model resnet50 --steps 20 --warmup 5 > gpurun_out/resnet.json 2> gpurun_out/resnet.err || { tail -30 gpurun_out/resnet.err; exit 1; }
 cat gpurun_out/resnet.json
+timeout -k 10 300 python -m pytest tests/test_kernels_gpu.py tests/test_graph_gpu.py -x -q > gpurun_out/pytest_mnist.log 2>&1 || { tail -40 gpurun_out/pytest_mnist.log; exit 1; }
+tail -2 gpurun_out/pytest_mnist.log
+timeout -k 10 200 python tools/kernel_bench.py --iters 200 --json gpurun_out/kbench.json | grep -E "fc|conv12|sgd"
+timeout -k 10 200 python bench.py --steps 3000 --warmup 300 > gpurun_out/fused_bench.json 2> gpurun_out/fused_bench.err || { tail -20 gpurun_out/fused_bench.err; exit 1; }
+cat gpurun_out/fused_bench.json

@@ -47,6 +47,11 @@ def main():
         "fc2_ce": lambda: L.pto_fc2_ce(tr.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
                                        tr.target.data_ptr(), None, tr.loss_rows.data_ptr(), tr.dlogits.data_ptr(),
                                        tr.dh1.data_ptr(), B, 1.0 / B, bi, s),
+        "fc12_ce(fused)": lambda: L.pto_fc12_ce(tr.a2p.data_ptr(), P["fc1.weight"].data_ptr(),
+                                                P["fc1.bias"].data_ptr(), tr.h1.data_ptr(), P["fc2.weight"].data_ptr(),
+                                                P["fc2.bias"].data_ptr(), tr.target.data_ptr(),
+                                                tr.loss_rows.data_ptr(), tr.dlogits.data_ptr(), tr.dh1.data_ptr(), B,
+                                                1.0 / B, bi, tr.fc_counters.data_ptr(), s),
         "fc_bwd": lambda: L.pto_fc_bwd(tr.dh1.data_ptr(), tr.a2p.data_ptr(), P["fc1.weight"].data_ptr(),
                                        tr.h1.data_ptr(), tr.dlogits.data_ptr(), G["fc1.weight"].data_ptr(),
                                        G["fc1.bias"].data_ptr(), G["fc2.weight"].data_ptr(), G["fc2.bias"].data_ptr(),
