@@ -10,9 +10,13 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
 import statistics
+import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch.nn.functional as F
 
 
