@@ -101,24 +101,29 @@ __device__ __forceinline__ bf16x8 row_operand(const char* tile, int r0, int ks) 
   return *reinterpret_cast<const bf16x8*>(tile + swz(r0 + (lane & 31), 2 * ks + (lane >> 5)));
 }
 
-// Cooperative tile copy global -> registers -> LDS (64 rows x 256 B).
-struct TileRegs {
-  uint4 v[4];
-};
-__device__ __forceinline__ void tile_load(TileRegs& t, const __bf16* base, long long rs) {
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int c = threadIdx.x + NT * p, r = c >> 4, ch = c & 15;
-    t.v[p] = *reinterpret_cast<const uint4*>(base + (long long)r * rs + ch * 8);
-  }
+// Cooperative tile copy global -> registers -> LDS (64 rows x 256 B):
+// four 16-byte pieces per thread.  Kept as named scalars and loaded
+// unconditionally (the last iteration re-reads its own tile): a
+// conditionally-filled struct/array is demoted to scratch by hipcc and
+// every load then waits vmcnt(0) before its scratch store.
+__device__ __forceinline__ uint4 tile_piece_load(const __bf16* base, long long rs, int p) {
+  const int c = threadIdx.x + NT * p, r = c >> 4, ch = c & 15;
+  return *reinterpret_cast<const uint4*>(base + (long long)r * rs + ch * 8);
 }
-__device__ __forceinline__ void tile_store(const TileRegs& t, char* tile) {
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int c = threadIdx.x + NT * p, r = c >> 4, ch = c & 15;
-    *reinterpret_cast<uint4*>(tile + swz(r, ch)) = t.v[p];
-  }
+__device__ __forceinline__ void tile_piece_store(char* tile, int p, uint4 v) {
+  const int c = threadIdx.x + NT * p, r = c >> 4, ch = c & 15;
+  *reinterpret_cast<uint4*>(tile + swz(r, ch)) = v;
 }
+#define TILE_LOAD(R, base, rs)              \
+  R##0 = tile_piece_load(base, rs, 0);      \
+  R##1 = tile_piece_load(base, rs, 1);      \
+  R##2 = tile_piece_load(base, rs, 2);      \
+  R##3 = tile_piece_load(base, rs, 3)
+#define TILE_STORE(R, tile)             \
+  tile_piece_store(tile, 0, R##0);      \
+  tile_piece_store(tile, 1, R##1);      \
+  tile_piece_store(tile, 2, R##2);      \
+  tile_piece_store(tile, 3, R##3)
 
 struct AttnShape {
   int B, S, H, Hkv;
@@ -177,20 +182,21 @@ __global__ __launch_bounds__(NT, 2) void k_attn_fwd(const __bf16* __restrict__ q
   const float sl = sh.scale * LOG2E;
   const int qrow = q0 + ql;
 
-  TileRegs tk, tv;
-  tile_load(tk, kb, sh.k_rs);
-  tile_load(tv, vb, sh.v_rs);
-  tile_store(tk, smem);
-  tile_store(tv, smem + TILE_B);
+  uint4 tk0, tk1, tk2, tk3, tv0, tv1, tv2, tv3;
+  TILE_LOAD(tk, kb, sh.k_rs);
+  TILE_LOAD(tv, vb, sh.v_rs);
+  TILE_STORE(tk, smem);
+  TILE_STORE(tv, smem + TILE_B);
   __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
     const int k0 = t * KT;
     const char* ktile = smem + (t & 1) * 2 * TILE_B;
     const char* vtile = ktile + TILE_B;
-    if (t + 1 < ntiles) {  // next tile in flight during this tile's math
-      tile_load(tk, kb + (long long)(k0 + KT) * sh.k_rs, sh.k_rs);
-      tile_load(tv, vb + (long long)(k0 + KT) * sh.v_rs, sh.v_rs);
+    {  // next tile in flight during this tile's math (the last iteration re-reads its own)
+      const int kn = (t + 1 < ntiles) ? k0 + KT : k0;
+      TILE_LOAD(tk, kb + (long long)kn * sh.k_rs, sh.k_rs);
+      TILE_LOAD(tv, vb + (long long)kn * sh.v_rs, sh.v_rs);
     }
     if (k0 <= q0 + QT - 1) {  // wave-uniform: this tile has unmasked keys for this wave
       // S^T (keys on registers, query on the lane)
@@ -248,8 +254,8 @@ __global__ __launch_bounds__(NT, 2) void k_attn_fwd(const __bf16* __restrict__ q
     }
     if (t + 1 < ntiles) {
       char* nt = smem + ((t + 1) & 1) * 2 * TILE_B;
-      tile_store(tk, nt);
-      tile_store(tv, nt + TILE_B);
+      TILE_STORE(tk, nt);
+      TILE_STORE(tv, nt + TILE_B);
     }
     __syncthreads();
   }
@@ -333,61 +339,61 @@ __global__ __launch_bounds__(NT, 2) void k_attn_bwd_dq(const __bf16* __restrict_
 #pragma unroll
   for (int db = 0; db < 4; ++db) acc[db] = (f32x16){};
 
-  TileRegs tk, tv;
-  tile_load(tk, kb, sh.k_rs);
-  tile_load(tv, vb, sh.v_rs);
-  tile_store(tk, smem);
-  tile_store(tv, smem + TILE_B);
+  uint4 tk0, tk1, tk2, tk3, tv0, tv1, tv2, tv3;
+  TILE_LOAD(tk, kb, sh.k_rs);
+  TILE_LOAD(tv, vb, sh.v_rs);
+  TILE_STORE(tk, smem);
+  TILE_STORE(tv, smem + TILE_B);
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
     const int k0 = t * KT;
     const char* ktile = smem + (t & 1) * 2 * TILE_B;
     const char* vtile = ktile + TILE_B;
-    if (t + 1 < ntiles) {
-      tile_load(tk, kb + (long long)(k0 + KT) * sh.k_rs, sh.k_rs);
-      tile_load(tv, vb + (long long)(k0 + KT) * sh.v_rs, sh.v_rs);
+    {
+      const int kn = (t + 1 < ntiles) ? k0 + KT : k0;
+      TILE_LOAD(tk, kb + (long long)kn * sh.k_rs, sh.k_rs);
+      TILE_LOAD(tv, vb + (long long)kn * sh.v_rs, sh.v_rs);
     }
     if (k0 <= q0 + QT - 1) {
-      f32x16 st[2], dp[2];
+      const bool diag = k0 + KT - 1 > q0;
+      // one 32-key half at a time: S^T/dP^T accumulators for 32 keys only
+      // (keeps the kernel inside 256 VGPRs, no scratch)
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
-        st[kt] = (f32x16){};
-        dp[kt] = (f32x16){};
+        f32x16 st = (f32x16){}, dp = (f32x16){};
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) {
-          st[kt] = mfma(row_operand(ktile, 32 * kt, ks), qf[ks], st[kt]);
-          dp[kt] = mfma(row_operand(vtile, 32 * kt, ks), df[ks], dp[kt]);
+          st = mfma(row_operand(ktile, 32 * kt, ks), qf[ks], st);
+          dp = mfma(row_operand(vtile, 32 * kt, ks), df[ks], dp);
         }
-      }
-      const bool diag = k0 + KT - 1 > q0;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float p = __builtin_amdgcn_exp2f(st[kt][i] * sl - lse2);
+          float p = __builtin_amdgcn_exp2f(st[i] * sl - lse2);
           if (diag) {
             const int key = k0 + 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hi;
             if (key > qrow) p = 0.f;
           }
-          st[kt][i] = p * (dp[kt][i] - dlt);  // dS (softmax scale applied at the end)
+          st[i] = p * (dp[i] - dlt);  // dS (softmax scale applied at the end)
         }
-      bf16x8 sf[4];
+        bf16x8 sf[2];
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        float tmp[8];
+        for (int hs = 0; hs < 2; ++hs) {
+          float tmp[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) tmp[j] = st[ks >> 1][8 * (ks & 1) + j];
-        sf[ks] = acc_to_operand(tmp);
+          for (int j = 0; j < 8; ++j) tmp[j] = st[8 * hs + j];
+          sf[hs] = acc_to_operand(tmp);
+        }
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+#pragma unroll
+          for (int hs = 0; hs < 2; ++hs)
+            acc[db] = mfma(tr_operand(ktile, 32 * kt + 16 * hs, 32 * db), sf[hs], acc[db]);
       }
-#pragma unroll
-      for (int db = 0; db < 4; ++db)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) acc[db] = mfma(tr_operand(ktile, 16 * ks, 32 * db), sf[ks], acc[db]);
     }
     if (t + 1 < ntiles) {
       char* nt = smem + ((t + 1) & 1) * 2 * TILE_B;
-      tile_store(tk, nt);
-      tile_store(tv, nt + TILE_B);
+      TILE_STORE(tk, nt);
+      TILE_STORE(tv, nt + TILE_B);
     }
     __syncthreads();
   }
@@ -454,39 +460,38 @@ __global__ __launch_bounds__(NT, 1) void k_attn_bwd_dkdv(const __bf16* __restric
   const int nsteps = G * nqt;
 
   // step s -> (head g, query tile qt); Q/dO tile of 32 rows x 256 B:
-  // 2 x 512 chunks of 16 B over 256 threads
-  auto stage = [&](int s, uint4 (&r)[4], float& c) {
+  // 2 x 512 chunks of 16 B over 256 threads (named scalars, see TILE_LOAD)
+  uint4 rq0, rq1, rd0, rd1;
+  float rc = 0.f;
+  auto stage = [&](int s) {
     const int g = s / nqt, qt = s % nqt, h = kvh * G + g;
     const long long tok = tok0 + kb0 + (long long)qt * QT;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int c_ = threadIdx.x + NT * p, rr = c_ >> 4, ch = c_ & 15;
-      r[p] = *reinterpret_cast<const uint4*>(q + (tok + rr) * sh.q_rs + (long long)h * HD + ch * 8);
-      r[2 + p] = *reinterpret_cast<const uint4*>(dout + (tok + rr) * sh.o_rs + (long long)h * HD + ch * 8);
-    }
+    const int c0 = threadIdx.x, c1 = threadIdx.x + NT;
+    const __bf16* qh = q + (long long)h * HD;
+    const __bf16* dh = dout + (long long)h * HD;
+    rq0 = *reinterpret_cast<const uint4*>(qh + (tok + (c0 >> 4)) * sh.q_rs + (c0 & 15) * 8);
+    rq1 = *reinterpret_cast<const uint4*>(qh + (tok + (c1 >> 4)) * sh.q_rs + (c1 & 15) * 8);
+    rd0 = *reinterpret_cast<const uint4*>(dh + (tok + (c0 >> 4)) * sh.o_rs + (c0 & 15) * 8);
+    rd1 = *reinterpret_cast<const uint4*>(dh + (tok + (c1 >> 4)) * sh.o_rs + (c1 & 15) * 8);
     const long long li = ((long long)b * sh.H + h) * sh.S + kb0 + (long long)qt * QT;
-    if (threadIdx.x < 32) c = lse[li + threadIdx.x];
-    else if (threadIdx.x < 64) c = delta[li + threadIdx.x - 32];
+    rc = threadIdx.x < 32 ? lse[li + threadIdx.x] : (threadIdx.x < 64 ? delta[li + threadIdx.x - 32] : 0.f);
   };
-  auto commit = [&](int buf, const uint4 (&r)[4], float c) {
+  auto commit = [&](int buf) {
     char* qtile = smem + buf * 2 * QTB;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int c_ = threadIdx.x + NT * p, rr = c_ >> 4, ch = c_ & 15;
-      *reinterpret_cast<uint4*>(qtile + swz(rr, ch)) = r[p];
-      *reinterpret_cast<uint4*>(qtile + QTB + swz(rr, ch)) = r[2 + p];
-    }
-    if (threadIdx.x < 64) rowc[buf * 64 + threadIdx.x] = c;
+    const int c0 = threadIdx.x, c1 = threadIdx.x + NT;
+    *reinterpret_cast<uint4*>(qtile + swz(c0 >> 4, c0 & 15)) = rq0;
+    *reinterpret_cast<uint4*>(qtile + swz(c1 >> 4, c1 & 15)) = rq1;
+    *reinterpret_cast<uint4*>(qtile + QTB + swz(c0 >> 4, c0 & 15)) = rd0;
+    *reinterpret_cast<uint4*>(qtile + QTB + swz(c1 >> 4, c1 & 15)) = rd1;
+    if (threadIdx.x < 64) rowc[buf * 64 + threadIdx.x] = rc;
   };
 
-  uint4 regs[4];
-  float rc = 0.f;
-  stage(0, regs, rc);
-  commit(0, regs, rc);
+  stage(0);
+  commit(0);
   __syncthreads();
   for (int s = 0; s < nsteps; ++s) {
     const int buf = s & 1;
-    if (s + 1 < nsteps) stage(s + 1, regs, rc);
+    stage(s + 1 < nsteps ? s + 1 : s);
     const int qt = s % nqt;
     const int q0 = kb0 + qt * QT;  // first query row of this tile
     if (q0 + QT - 1 >= kb0 + 32 * w) {  // wave-uniform: some query >= some key of this wave
@@ -539,7 +544,7 @@ __global__ __launch_bounds__(NT, 1) void k_attn_bwd_dkdv(const __bf16* __restric
           dka[db] = mfma(tr_operand(qtile, 16 * qs, 32 * db), sf[qs], dka[db]);
         }
     }
-    if (s + 1 < nsteps) commit(buf ^ 1, regs, rc);
+    if (s + 1 < nsteps) commit(buf ^ 1);
     __syncthreads();
   }
   // dK^T / dV^T: lane = key, registers = d (32db + 8g + 4hi + 0..3)
