@@ -40,7 +40,7 @@ def parse_args(argv=None):
     p.add_argument("--warmup", type=int, default=None, help="untimed steps (default 200 mnist, 3 others)")
     p.add_argument("--model", default=os.environ.get("BENCH_MODEL", "mnist"),
                    choices=["mnist", "resnet50", "llama3-8b", "llama3-1b", "llama3-tiny"])
-    p.add_argument("--batch-size", type=int, default=None, help="per-rank batch (64 mnist, 256 resnet50, 2 llama)")
+    p.add_argument("--batch-size", type=int, default=None, help="per-rank batch (64 mnist, 256 resnet50, 4 x seq-len llama: 191 GB of the 288 GB HBM)")
     p.add_argument("--seq-len", type=int, default=4096, help="llama sequence length")
     p.add_argument("--checkpoint", choices=["none", "full"], default="none", help="llama activation checkpointing")
     p.add_argument("--breakdown", action="store_true",
@@ -63,7 +63,7 @@ def main(argv=None):
     if args.warmup is None:
         args.warmup = 200 if mnist else 3
     if args.batch_size is None:
-        args.batch_size = 64 if mnist else (256 if args.model == "resnet50" else 2)
+        args.batch_size = 64 if mnist else (256 if args.model == "resnet50" else 4)
     from pytorch_operator_1_amd.utils import dist as pdist
 
     use_gpu = torch.cuda.is_available() and not args.cpu
