@@ -417,14 +417,15 @@ __global__ __launch_bounds__(NT, 2) void k_attn_bwd_dq(const __bf16* __restrict_
 // with -lse2/c and -delta), P = exp2(c S), dS = P dP;
 // dV^T += dO^T P, dK^T += Q^T dS (transposed LDS reads of dO / Q).
 constexpr int KB = NW * 32;           // keys per block
-constexpr int QTB = 32 * 256;          // one 32 x 128 bf16 tile in bytes
+constexpr int QSTG = 64;               // query rows staged per step (two 32-row MFMA tiles)
+constexpr int QTB = QSTG * 256;        // one staged 64 x 128 bf16 tile in bytes
 __global__ __launch_bounds__(NT, 1) void k_attn_bwd_dkdv(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                          const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                          const float* __restrict__ lse, const float* __restrict__ delta,
                                                          __bf16* __restrict__ dk, __bf16* __restrict__ dv,
                                                          long long dkv_rs, AttnShape sh) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [2][Q | dO] + [2][lse | delta]
-  float* rowc = reinterpret_cast<float*>(smem + 4 * QTB);       // [2][2][32]
+  float* rowc = reinterpret_cast<float*>(smem + 4 * QTB);       // [2][lse 64 | delta 64]
   const int G = sh.H / sh.Hkv;
   const int nkb = sh.S / KB;
   // block -> (b, kvh, key block), heaviest (earliest keys) first, XCD-grouped
@@ -456,34 +457,28 @@ __global__ __launch_bounds__(NT, 1) void k_attn_bwd_dkdv(const __bf16* __restric
   }
   const float sl = sh.scale * LOG2E;
   const float inv_sl = 1.f / sl;
-  const int nqt = (sh.S - kb0) / QT;  // query tiles from the block's first key on
+  const int nqt = (sh.S - kb0) / QSTG;  // staged query tiles from the block's first key on
   const int nsteps = G * nqt;
 
-  // step s -> (head g, query tile qt); Q/dO tile of 32 rows x 256 B:
-  // 2 x 512 chunks of 16 B over 256 threads (named scalars, see TILE_LOAD)
-  uint4 rq0, rq1, rd0, rd1;
+  // step s -> (head g, staged query tile qt): Q/dO tiles of 64 rows x 256 B
+  // = 1024 chunks of 16 B each, 4 per thread (named scalars, see TILE_LOAD)
+  uint4 rq0, rq1, rq2, rq3, rd0, rd1, rd2, rd3;
   float rc = 0.f;
   auto stage = [&](int s) {
     const int g = s / nqt, qt = s % nqt, h = kvh * G + g;
-    const long long tok = tok0 + kb0 + (long long)qt * QT;
-    const int c0 = threadIdx.x, c1 = threadIdx.x + NT;
-    const __bf16* qh = q + (long long)h * HD;
-    const __bf16* dh = dout + (long long)h * HD;
-    rq0 = *reinterpret_cast<const uint4*>(qh + (tok + (c0 >> 4)) * sh.q_rs + (c0 & 15) * 8);
-    rq1 = *reinterpret_cast<const uint4*>(qh + (tok + (c1 >> 4)) * sh.q_rs + (c1 & 15) * 8);
-    rd0 = *reinterpret_cast<const uint4*>(dh + (tok + (c0 >> 4)) * sh.o_rs + (c0 & 15) * 8);
-    rd1 = *reinterpret_cast<const uint4*>(dh + (tok + (c1 >> 4)) * sh.o_rs + (c1 & 15) * 8);
-    const long long li = ((long long)b * sh.H + h) * sh.S + kb0 + (long long)qt * QT;
-    rc = threadIdx.x < 32 ? lse[li + threadIdx.x] : (threadIdx.x < 64 ? delta[li + threadIdx.x - 32] : 0.f);
+    const long long tok = tok0 + kb0 + (long long)qt * QSTG;
+    const __bf16* qh = q + tok * sh.q_rs + (long long)h * HD;
+    const __bf16* dh = dout + tok * sh.o_rs + (long long)h * HD;
+    TILE_LOAD(rq, qh, sh.q_rs);
+    TILE_LOAD(rd, dh, sh.o_rs);
+    const long long li = ((long long)b * sh.H + h) * sh.S + kb0 + (long long)qt * QSTG;
+    rc = threadIdx.x < 64 ? lse[li + threadIdx.x] : (threadIdx.x < 128 ? delta[li + threadIdx.x - 64] : 0.f);
   };
   auto commit = [&](int buf) {
     char* qtile = smem + buf * 2 * QTB;
-    const int c0 = threadIdx.x, c1 = threadIdx.x + NT;
-    *reinterpret_cast<uint4*>(qtile + swz(c0 >> 4, c0 & 15)) = rq0;
-    *reinterpret_cast<uint4*>(qtile + swz(c1 >> 4, c1 & 15)) = rq1;
-    *reinterpret_cast<uint4*>(qtile + QTB + swz(c0 >> 4, c0 & 15)) = rd0;
-    *reinterpret_cast<uint4*>(qtile + QTB + swz(c1 >> 4, c1 & 15)) = rd1;
-    if (threadIdx.x < 64) rowc[buf * 64 + threadIdx.x] = rc;
+    TILE_STORE(rq, qtile);
+    TILE_STORE(rd, qtile + QTB);
+    if (threadIdx.x < 128) rowc[buf * 128 + threadIdx.x] = rc;
   };
 
   stage(0);
@@ -493,17 +488,19 @@ __global__ __launch_bounds__(NT, 1) void k_attn_bwd_dkdv(const __bf16* __restric
     const int buf = s & 1;
     stage(s + 1 < nsteps ? s + 1 : s);
     const int qt = s % nqt;
-    const int q0 = kb0 + qt * QT;  // first query row of this tile
+#pragma unroll
+    for (int sub = 0; sub < QSTG / QT; ++sub) {
+    const int q0 = kb0 + qt * QSTG + sub * QT;  // first query row of this 32-row tile
     if (q0 + QT - 1 >= kb0 + 32 * w) {  // wave-uniform: some query >= some key of this wave
-      const char* qtile = smem + buf * 2 * QTB;
+      const char* qtile = smem + buf * 2 * QTB + sub * QT * 256;
       const char* dtile = qtile + QTB;
-      const float* lrow = rowc + buf * 64;
+      const float* lrow = rowc + buf * 128 + sub * QT;
       // accumulator init with the row constants: row q = (i&3)+8(i>>2)+4hi
       f32x16 sa, pa;
 #pragma unroll
       for (int gg = 0; gg < 4; ++gg) {
         const float4 l4 = *reinterpret_cast<const float4*>(lrow + 8 * gg + 4 * hi);
-        const float4 d4 = *reinterpret_cast<const float4*>(lrow + 32 + 8 * gg + 4 * hi);
+        const float4 d4 = *reinterpret_cast<const float4*>(lrow + QSTG + 8 * gg + 4 * hi);
         sa[4 * gg] = -l4.x * inv_sl; sa[4 * gg + 1] = -l4.y * inv_sl;
         sa[4 * gg + 2] = -l4.z * inv_sl; sa[4 * gg + 3] = -l4.w * inv_sl;
         pa[4 * gg] = -d4.x; pa[4 * gg + 1] = -d4.y; pa[4 * gg + 2] = -d4.z; pa[4 * gg + 3] = -d4.w;
@@ -544,6 +541,7 @@ __global__ __launch_bounds__(NT, 1) void k_attn_bwd_dkdv(const __bf16* __restric
           dka[db] = mfma(tr_operand(qtile, 16 * qs, 32 * db), sf[qs], dka[db]);
         }
     }
+    }  // sub-tile
     if (s + 1 < nsteps) commit(buf ^ 1);
     __syncthreads();
   }
@@ -609,14 +607,14 @@ PTO_API int pto_attn_bwd(const void* q, const void* k, const void* v, const void
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)k_attn_bwd_dq, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE_B);
     (void)hipFuncSetAttribute((const void*)k_attn_bwd_dkdv, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        4 * QTB + 2 * 64 * 4);
+                        4 * QTB + 2 * 128 * 4);
     attr = true;
   }
   const long long rows = (long long)B * S * H;
   hipLaunchKernelGGL(k_attn_bwd_delta, dim3((unsigned)((rows + 7) / 8)), dim3(256), 0, s, (const __bf16*)o,
                      (const __bf16*)dout, delta, sh);
   const int G = H / Hkv;
-  hipLaunchKernelGGL(k_attn_bwd_dkdv, dim3(B * Hkv * (S / KB)), dim3(NT), 4 * QTB + 2 * 64 * 4, s,
+  hipLaunchKernelGGL(k_attn_bwd_dkdv, dim3(B * Hkv * (S / KB)), dim3(NT), 4 * QTB + 2 * 128 * 4, s,
                      (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta,
                      (__bf16*)dk, (__bf16*)dv, dqkv_rs, sh);
   hipLaunchKernelGGL(k_attn_bwd_dq, dim3(B * Hkv * ((S / QT) * G / NW)), dim3(NT), 4 * TILE_B, s,
