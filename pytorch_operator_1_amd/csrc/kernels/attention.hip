@@ -207,37 +207,45 @@ __global__ __launch_bounds__(NT, 2) void k_attn_fwd(const __bf16* __restrict__ q
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) st[kt] = mfma(row_operand(ktile, 32 * kt, ks), qf[ks], st[kt]);
       }
-      const bool diag = k0 + KT - 1 > q0;
+      // causal mask only on the diagonal tile (wave-uniform branch: the
+      // other tiles run no compare/select)
+      if (k0 + KT - 1 > q0) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = k0 + 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hi;
+            if (key > qrow) st[kt][i] = -INFINITY;
+          }
+      }
+      // raw-score max (the softmax scale is positive), then one fma per
+      // score: p = exp2(s * c - m)
       float mx = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float s = st[kt][i] * sl;
-          if (diag) {
-            const int key = k0 + 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hi;
-            if (key > qrow) s = -INFINITY;
-          }
-          st[kt][i] = s;
-          mx = fmaxf(mx, s);
-        }
+        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, st[kt][i]);
       mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float m_new = fmaxf(m_run, mx);
+      const float m_new = fmaxf(m_run, mx * sl);
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
       float rs = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(st[kt][i] - m_new);
+          const float p = __builtin_amdgcn_exp2f(fmaf(st[kt][i], sl, -m_new));
           st[kt][i] = p;
           rs += p;
         }
       rs += __shfl_xor(rs, 32);
       l_run = l_run * alpha + rs;
       m_run = m_new;
+      // rescale O only when some row's running max moved (rare after the
+      // first tiles of a causal row)
+      if (__any(alpha != 1.f)) {
 #pragma unroll
-      for (int db = 0; db < 4; ++db) acc_o[db] *= alpha;
+        for (int db = 0; db < 4; ++db) acc_o[db] *= alpha;
+      }
       bf16x8 pf[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
@@ -366,13 +374,16 @@ __global__ __launch_bounds__(NT, 2) void k_attn_bwd_dq(const __bf16* __restrict_
           st = mfma(row_operand(ktile, 32 * kt, ks), qf[ks], st);
           dp = mfma(row_operand(vtile, 32 * kt, ks), df[ks], dp);
         }
+        if (diag) {  // wave-uniform: causal mask on the diagonal tile only
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = k0 + 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hi;
+            if (key > qrow) st[i] = -INFINITY;
+          }
+        }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float p = __builtin_amdgcn_exp2f(st[i] * sl - lse2);
-          if (diag) {
-            const int key = k0 + 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * hi;
-            if (key > qrow) p = 0.f;
-          }
+          const float p = __builtin_amdgcn_exp2f(fmaf(st[i], sl, -lse2));
           st[i] = p * (dp[i] - dlt);  // dS (softmax scale applied at the end)
         }
         bf16x8 sf[2];
@@ -510,14 +521,16 @@ __global__ __launch_bounds__(NT, 1) void k_attn_bwd_dkdv(const __bf16* __restric
         sa = mfma(row_operand(qtile, 0, ks), kf[ks], sa);
         pa = mfma(row_operand(dtile, 0, ks), vf[ks], pa);
       }
-      const bool diag = q0 < kb0 + 32 * w + 31;
+      if (q0 < kb0 + 32 * w + 31) {  // wave-uniform: causal mask on diagonal tiles only
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int qr = q0 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+          if (key > qr) sa[i] = -INFINITY;
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        float p = __builtin_amdgcn_exp2f(sa[i] * sl);
-        if (diag) {
-          const int qr = q0 + (i & 3) + 8 * (i >> 2) + 4 * hi;
-          if (key > qr) p = 0.f;
-        }
+        const float p = __builtin_amdgcn_exp2f(sa[i] * sl);
         sa[i] = p;
         pa[i] = p * pa[i];  // dS
       }
