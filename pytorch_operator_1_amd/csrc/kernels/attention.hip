@@ -33,6 +33,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -189,9 +191,12 @@ __global__ __launch_bounds__(NT, 2) void k_attn_fwd(const __bf16* __restrict__ q
   TILE_STORE(tv, smem + TILE_B);
   __syncthreads();
 
-  for (int t = 0; t < ntiles; ++t) {
+  // unrolled x2 so the LDS ring slot is a compile-time constant: the
+  // lane-dependent LDS addresses stay loop-invariant (immediate offsets)
+  auto step_fn = [&](const int t, auto bufc) {
+    constexpr int SLOT = decltype(bufc)::value;
     const int k0 = t * KT;
-    const char* ktile = smem + (t & 1) * 2 * TILE_B;
+    const char* ktile = smem + SLOT * 2 * TILE_B;
     const char* vtile = ktile + TILE_B;
     {  // next tile in flight during this tile's math (the last iteration re-reads its own)
       const int kn = (t + 1 < ntiles) ? k0 + KT : k0;
@@ -261,11 +266,15 @@ __global__ __launch_bounds__(NT, 2) void k_attn_fwd(const __bf16* __restrict__ q
         for (int ks = 0; ks < 4; ++ks) acc_o[db] = mfma(tr_operand(vtile, 16 * ks, 32 * db), pf[ks], acc_o[db]);
     }
     if (t + 1 < ntiles) {
-      char* nt = smem + ((t + 1) & 1) * 2 * TILE_B;
+      char* nt = smem + (SLOT ^ 1) * 2 * TILE_B;
       TILE_STORE(tk, nt);
       TILE_STORE(tv, nt + TILE_B);
     }
     __syncthreads();
+    };
+  for (int t0 = 0; t0 < ntiles; t0 += 2) {
+    step_fn(t0, std::integral_constant<int, 0>{});
+    if (t0 + 1 < ntiles) step_fn(t0 + 1, std::integral_constant<int, 1>{});
   }
   // epilogue: O[q][d] = O^T[d][q] / l ; lane holds d = 32db + 8g + 4hi + (0..3)
   const float inv = 1.f / l_run;
@@ -353,9 +362,12 @@ __global__ __launch_bounds__(NT, 2) void k_attn_bwd_dq(const __bf16* __restrict_
   TILE_STORE(tk, smem);
   TILE_STORE(tv, smem + TILE_B);
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
+  // unrolled x2 so the LDS ring slot is a compile-time constant: the
+  // lane-dependent LDS addresses stay loop-invariant (immediate offsets)
+  auto step_fn = [&](const int t, auto bufc) {
+    constexpr int SLOT = decltype(bufc)::value;
     const int k0 = t * KT;
-    const char* ktile = smem + (t & 1) * 2 * TILE_B;
+    const char* ktile = smem + SLOT * 2 * TILE_B;
     const char* vtile = ktile + TILE_B;
     {
       const int kn = (t + 1 < ntiles) ? k0 + KT : k0;
@@ -402,11 +414,15 @@ __global__ __launch_bounds__(NT, 2) void k_attn_bwd_dq(const __bf16* __restrict_
       }
     }
     if (t + 1 < ntiles) {
-      char* nt = smem + ((t + 1) & 1) * 2 * TILE_B;
+      char* nt = smem + (SLOT ^ 1) * 2 * TILE_B;
       TILE_STORE(tk, nt);
       TILE_STORE(tv, nt + TILE_B);
     }
     __syncthreads();
+    };
+  for (int t0 = 0; t0 < ntiles; t0 += 2) {
+    step_fn(t0, std::integral_constant<int, 0>{});
+    if (t0 + 1 < ntiles) step_fn(t0 + 1, std::integral_constant<int, 1>{});
   }
   __bf16* drow = dq + (tok0 + qrow) * dq_rs + (long long)h * HD + 4 * hi;
 #pragma unroll
@@ -495,8 +511,11 @@ __global__ __launch_bounds__(NT, 1) void k_attn_bwd_dkdv(const __bf16* __restric
   stage(0);
   commit(0);
   __syncthreads();
-  for (int s = 0; s < nsteps; ++s) {
-    const int buf = s & 1;
+  // unrolled x2 so the LDS ring slot is a compile-time constant: the
+  // lane-dependent LDS addresses stay loop-invariant (immediate offsets)
+  auto step_fn = [&](const int s, auto bufc) {
+    constexpr int SLOT = decltype(bufc)::value;
+    const int buf = SLOT;
     stage(s + 1 < nsteps ? s + 1 : s);
     const int qt = s % nqt;
 #pragma unroll
@@ -557,6 +576,10 @@ __global__ __launch_bounds__(NT, 1) void k_attn_bwd_dkdv(const __bf16* __restric
     }  // sub-tile
     if (s + 1 < nsteps) commit(buf ^ 1);
     __syncthreads();
+    };
+  for (int s0 = 0; s0 < nsteps; s0 += 2) {
+    step_fn(s0, std::integral_constant<int, 0>{});
+    if (s0 + 1 < nsteps) step_fn(s0 + 1, std::integral_constant<int, 1>{});
   }
   // dK^T / dV^T: lane = key, registers = d (32db + 8g + 4hi + 0..3)
   __bf16* dkr = dk + (tok0 + key) * dkv_rs + (long long)kvh * HD + 4 * hi;
