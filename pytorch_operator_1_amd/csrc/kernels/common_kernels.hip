@@ -5,6 +5,7 @@
 //   * row-wise log_softmax forward/backward and fused cross-entropy
 //     (log_softmax + NLL, forward and dlogits in one pass) (K7).
 #include "mfma_f32.h"
+#include "sgd_f32.h"
 
 struct SgdTensor {
   float* p;
@@ -16,19 +17,6 @@ struct SgdTensor {
 namespace {
 
 constexpr int SGD_CHUNK = 256 * 4;  // elements per block (one float4 per thread: max parallelism)
-
-// buf = momentum*buf + (gscale*g + wd*p);  p -= lr * (nesterov ? d + momentum*buf : buf);  g = 0
-// Matches torch.optim.SGD with dampening = 0 (torch's first step sets
-// buf = d, identical to momentum*0 + d with a zero-initialised buffer).
-PTO_DEV void sgd_elem(float& p, float& g, float& m, float lr, float mom, float wd, float gs, int nesterov) {
-  float d = g * gs;
-  if (wd != 0.f) d = fmaf(wd, p, d);
-  if (mom != 0.f) {
-    m = fmaf(mom, m, d);
-    d = nesterov ? fmaf(mom, m, d) : m;
-  }
-  p = fmaf(-lr, d, p);
-}
 
 __global__ __launch_bounds__(256) void k_sgd_multi(const SgdTensor* __restrict__ ts,
                                                    const int* __restrict__ block_start, int ntensors,

@@ -29,6 +29,7 @@
 // index (`bidx`, advanced by the SGD launch), so a captured HIP graph walks
 // the dataset without any copy kernels.
 #include "mfma_f32.h"
+#include "sgd_f32.h"
 
 namespace {
 
@@ -50,6 +51,37 @@ PTO_DEV void relu_pool4(const float v[4], float& out, uint8_t& code) {
 PTO_DEV const float* batch_ptr(const float* base, const long long* bidx, int per_batch) {
   return bidx ? base + (size_t)(*bidx) * per_batch : base;
 }
+
+// "Fused optimizer" schedule of the single-process step (no gradient
+// all-reduce between backward and the update): the optimizer runs inside
+// launches that already exist instead of a separate SGD launch.
+//   * fc + conv2 parameters: their grads are final after B3 / B2 and no
+//     later launch of the step reads those parameters, so extra blocks of
+//     the B1 launch update them (k_conv1_bwd_sgd).
+//   * conv1 parameters: their grads are final only when B1 ends, and F1
+//     of the NEXT step is their first reader.  F1 applies the pending update
+//     on the fly while staging the weights (LazyConv1), and F4 of that step
+//     (which does not read conv1) commits it: p, m written, g zeroed
+//     (Conv1Commit).  `pending` (set by B3) says whether an update is owed;
+//     the host flushes it before anyone reads the parameters.
+//   * batch cursor: F4 snapshots it for B1, B3 advances it.
+struct LazyConv1 {
+  const float* g;       // flat conv1 grads: weights [0, 500), bias [bias_off, +20)
+  const float* m;       // flat conv1 momentum, same layout
+  const int* pending;   // nullptr: plain forward
+  SgdArgs a;
+  int bias_off;
+};
+struct Conv1Commit {
+  float* p;             // flat conv1 range [0, n) of params / grads / momentum
+  float* g;
+  float* m;
+  int n;                // multiple of 4
+  const int* pending;   // nullptr: no commit
+  SgdArgs a;
+  const long long* bidx;
+  long long* bidx_snap;
+};
 
 // ---------------------------------------------------------------- F1 ----
 // thread = (sample, 4-channel group, pooled pixel); 6x6 input patch in
@@ -192,7 +224,7 @@ __global__ __launch_bounds__(256) void k_conv12_fwd(const float* __restrict__ x,
                                                     const float* __restrict__ b2, float* __restrict__ a1p,
                                                     uint8_t* __restrict__ code1, float* __restrict__ a2p,
                                                     uint8_t* __restrict__ code2, int B,
-                                                    const long long* __restrict__ bidx) {
+                                                    const long long* __restrict__ bidx, LazyConv1 lz) {
   __shared__ float ws[16 * WS_LD];
   __shared__ __attribute__((aligned(16))) float in_s[A1P];
   __shared__ __attribute__((aligned(16))) float xs[784];
@@ -210,11 +242,29 @@ __global__ __launch_bounds__(256) void k_conv12_fwd(const float* __restrict__ x,
       wv[q] = (e < nrows * 125) ? wsrc[e] : float4{0.f, 0.f, 0.f, 0.f};
     }
     const float4 xv = tid < 196 ? reinterpret_cast<const float4*>(x + b * 784)[tid] : float4{0.f, 0.f, 0.f, 0.f};
-    float wq[3];
+    float wq[3], gq[3], mq[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       const int e = tid + 256 * q;
       wq[q] = e < C1 * 25 ? w1[e] : (e < C1 * 26 ? b1[e - C1 * 25] : 0.f);
+    }
+    // the previous step's conv1 update, loaded in the same memory round
+    int pend = 0;
+    float lr = 0.f;
+    if (lz.pending) {
+      pend = *lz.pending;
+      lr = *lz.a.lr;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int e = tid + 256 * q;
+        const int fi = e < C1 * 25 ? e : lz.bias_off + (e - C1 * 25);
+        gq[q] = e < C1 * 26 ? lz.g[fi] : 0.f;
+        mq[q] = e < C1 * 26 ? lz.m[fi] : 0.f;
+      }
+    }
+    if (pend) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) sgd_elem(wq[q], gq[q], mq[q], lr, lz.a.mom, lz.a.wd, lz.a.gscale, lz.a.nesterov);
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -436,7 +486,16 @@ __global__ __launch_bounds__(256) void k_fc2_ce(const float* __restrict__ h1, co
                                                 const float* __restrict__ bias, const int64_t* __restrict__ labels,
                                                 float* __restrict__ logp, float* __restrict__ loss_rows,
                                                 float* __restrict__ dlogits, float* __restrict__ dh1, int B,
-                                                float inv_b, const long long* __restrict__ bidx) {
+                                                float inv_b, const long long* __restrict__ bidx, Conv1Commit cm) {
+  if (blockIdx.x == (unsigned)((B + 3) >> 2)) {  // extra block: conv1 commit + cursor snapshot
+    const int t = threadIdx.x;
+    if (t == 0 && cm.bidx_snap) *cm.bidx_snap = *cm.bidx;
+    if (cm.pending && *cm.pending) {
+      const float lr = *cm.a.lr;
+      for (int i = 4 * t; i < cm.n; i += 1024) sgd_flat4(cm.p, cm.g, cm.m, i, lr, cm.a);
+    }
+    return;
+  }
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= B) return;
   fc2_ce_row(row, lane, h1, w, bias, labels, logp, loss_rows, dlogits, dh1, B, inv_b, bidx);
@@ -493,9 +552,14 @@ __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ dh1, c
                                                 const float* __restrict__ dlogits, float* __restrict__ gw1,
                                                 float* __restrict__ gb1, float* __restrict__ gw2,
                                                 float* __restrict__ gb2, float* __restrict__ da2p, int B, int nA,
-                                                int nB, int nW) {
+                                                int nB, int nW, long long* __restrict__ bidx, long long nbatches,
+                                                int* __restrict__ pending) {
   __shared__ float red[4 * 256];
   int bid = blockIdx.x;
+  if (bid == 0 && threadIdx.x == 0) {  // fused-optimizer schedule: F1/F4 of this step have read the cursor
+    if (bidx) *bidx = (*bidx + 1) % nbatches;
+    if (pending) *pending = 1;        // conv1's update (after B1) is owed to the next F1
+  }
   if (bid < nA) {
     block_gemm_4tiles<LAY_KROW, LAY_KROW>(dh1, F1OUT, a2p, F1IN, F1OUT, F1IN, B, bid, EpiStore{gw1, F1IN});
     return;
@@ -805,17 +869,16 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
 // positions in a second round; 26 register accumulators, block reduction,
 // 26 atomics per block (16 blocks per channel at B=64).
 constexpr int B1_CHUNK = 4;
-__global__ __launch_bounds__(256) void k_conv1_bwd(const float* __restrict__ g1, const uint8_t* __restrict__ code1,
-                                                   const float* __restrict__ x, float* __restrict__ gw1,
-                                                   float* __restrict__ gb1, int B,
-                                                   const long long* __restrict__ bidx) {
+PTO_DEV void conv1_bwd_block(int vb, const float* __restrict__ g1, const uint8_t* __restrict__ code1,
+                             const float* __restrict__ x, float* __restrict__ gw1, float* __restrict__ gb1, int B,
+                             const long long* __restrict__ bidx) {
   // One memory round: the chunk's 4 input images (12.5 KB, coalesced
   // float4) go to LDS together with each thread's (grad, code) pairs; the
   // 25-tap patches are then read from LDS.
   __shared__ __attribute__((aligned(16))) float xs[B1_CHUNK * 784];
   __shared__ float part[4][26];
   x = batch_ptr(x, bidx, B * 784);
-  const int oc = blockIdx.x % C1, chunk = blockIdx.x / C1;
+  const int oc = vb % C1, chunk = vb / C1;
   const int b0 = chunk * B1_CHUNK, nb = min(B, b0 + B1_CHUNK) - b0;
   const int nitems = nb * 144;
   constexpr int PER = (B1_CHUNK * 144 + 255) / 256;
@@ -878,6 +941,41 @@ __global__ __launch_bounds__(256) void k_conv1_bwd(const float* __restrict__ g1,
     if (q < 25) atomicAdd(gw1 + oc * 25 + q, s);
     else atomicAdd(gb1 + oc, s);
   }
+}
+
+__global__ __launch_bounds__(256) void k_conv1_bwd(const float* __restrict__ g1, const uint8_t* __restrict__ code1,
+                                                   const float* __restrict__ x, float* __restrict__ gw1,
+                                                   float* __restrict__ gb1, int B,
+                                                   const long long* __restrict__ bidx) {
+  conv1_bwd_block(blockIdx.x, g1, code1, x, gw1, gb1, B, bidx);
+}
+
+// B1 + the optimizer for every parameter whose gradient is final before B1
+// (fc and conv2: the flat range [0, nflat), 1024 elements per extra block).
+// The extra blocks touch no byte the conv1 blocks read or write.
+__global__ __launch_bounds__(256) void k_conv1_bwd_sgd(const float* __restrict__ g1,
+                                                       const uint8_t* __restrict__ code1,
+                                                       const float* __restrict__ x, float* __restrict__ gw1,
+                                                       float* __restrict__ gb1, int B,
+                                                       const long long* __restrict__ bidx, int nconv,
+                                                       float* __restrict__ p, float* __restrict__ g,
+                                                       float* __restrict__ m, long long nflat, SgdArgs a) {
+  if ((int)blockIdx.x < nconv) {
+    conv1_bwd_block(blockIdx.x, g1, code1, x, gw1, gb1, B, bidx);
+    return;
+  }
+  const long long i = ((long long)(blockIdx.x - nconv) * 256 + threadIdx.x) * 4;
+  if (i < nflat) sgd_flat4(p, g, m, i, *a.lr, a);
+}
+
+// Host-side flush of an owed conv1 update (before the parameters are read
+// or replaced): commit it and clear `pending`.  One block.
+__global__ __launch_bounds__(256) void k_conv1_commit(Conv1Commit cm, int* __restrict__ pending) {
+  if (!*cm.pending) return;
+  const float lr = *cm.a.lr;
+  for (int i = 4 * threadIdx.x; i < cm.n; i += 1024) sgd_flat4(cm.p, cm.g, cm.m, i, lr, cm.a);
+  __syncthreads();
+  if (threadIdx.x == 0) *pending = 0;
 }
 
 // conv1 data gradient (only needed when the input requires grad, e.g. the
@@ -951,7 +1049,32 @@ PTO_API int pto_conv2_fwd(const float* a1p, const float* w, const float* b, floa
 PTO_API int pto_conv12_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
                            float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B, const long long* bidx,
                            hipStream_t s) {
-  hipLaunchKernelGGL(k_conv12_fwd, dim3(B * 4), dim3(256), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B, bidx);
+  LazyConv1 lz{};
+  hipLaunchKernelGGL(k_conv12_fwd, dim3(B * 4), dim3(256), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B, bidx,
+                     lz);
+  LAUNCH_CHECK();
+}
+
+static SgdArgs sgd_args(const float* lr, float mom, float wd, float gscale, int nesterov) {
+  SgdArgs a;
+  a.lr = lr;
+  a.mom = mom;
+  a.wd = wd;
+  a.gscale = gscale;
+  a.nesterov = nesterov;
+  return a;
+}
+
+// F1 with conv1's owed SGD update applied on the fly (fused-optimizer
+// schedule).  g1f/m1f: flat conv1 grads/momentum (weights at 0, bias at
+// bias_off); lr: device scalar.
+PTO_API int pto_conv12_fwd_lazy(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
+                                float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B, const long long* bidx,
+                                const float* g1f, const float* m1f, int bias_off, const int* pending, const float* lr,
+                                float mom, float wd, float gscale, int nesterov, hipStream_t s) {
+  LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off};
+  hipLaunchKernelGGL(k_conv12_fwd, dim3(B * 4), dim3(256), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B, bidx,
+                     lz);
   LAUNCH_CHECK();
 }
 
@@ -988,8 +1111,31 @@ PTO_API int pto_relu_bwd(const float* g, const float* y, float* out, int n, hipS
 PTO_API int pto_fc2_ce(const float* h1, const float* w, const float* b, const int64_t* labels, float* logp,
                        float* loss_rows, float* dlogits, float* dh1, int B, float inv_b, const long long* bidx,
                        hipStream_t s) {
+  Conv1Commit cm{};
   hipLaunchKernelGGL(k_fc2_ce, dim3((B + 3) / 4), dim3(256), 0, s, h1, w, b, labels, logp, loss_rows, dlogits, dh1,
-                     B, inv_b, bidx);
+                     B, inv_b, bidx, cm);
+  LAUNCH_CHECK();
+}
+
+// F4 + one extra block: commit conv1's owed update (flat range p1/g1/m1 of
+// n1 floats, n1 % 4 == 0, 16-byte aligned) and snapshot the batch cursor
+// into bidx_snap for B1.
+PTO_API int pto_fc2_ce_commit(const float* h1, const float* w, const float* b, const int64_t* labels,
+                              float* loss_rows, float* dlogits, float* dh1, int B, float inv_b, const long long* bidx,
+                              long long* bidx_snap, float* p1, float* g1, float* m1, int n1, const int* pending,
+                              const float* lr, float mom, float wd, float gscale, int nesterov, hipStream_t s) {
+  if (n1 % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1)) & 15)) return -1;
+  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), bidx, bidx_snap};
+  hipLaunchKernelGGL(k_fc2_ce, dim3((B + 3) / 4 + 1), dim3(256), 0, s, h1, w, b, labels, nullptr, loss_rows, dlogits,
+                     dh1, B, inv_b, bidx, cm);
+  LAUNCH_CHECK();
+}
+
+PTO_API int pto_conv1_commit(float* p1, float* g1, float* m1, int n1, int* pending, const float* lr, float mom,
+                             float wd, float gscale, int nesterov, hipStream_t s) {
+  if (n1 % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1)) & 15)) return -1;
+  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), nullptr, nullptr};
+  hipLaunchKernelGGL(k_conv1_commit, dim3(1), dim3(256), 0, s, cm, pending);
   LAUNCH_CHECK();
 }
 
@@ -1010,7 +1156,21 @@ PTO_API int pto_fc_bwd(const float* dh1, const float* a2p, const float* w1, cons
   const int nW = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4;
   const int nS = 8 + 1;
   hipLaunchKernelGGL(k_fc_bwd, dim3(nA + nB + nW + nS), dim3(256), 0, s, dh1, a2p, w1, h1, dlogits, gw1, gb1, gw2,
-                     gb2, da2p, B, nA, nB, nW);
+                     gb2, da2p, B, nA, nB, nW, nullptr, 1LL, nullptr);
+  LAUNCH_CHECK();
+}
+
+// B3 of the fused-optimizer schedule: also advances the batch cursor and
+// marks conv1's update as owed.
+PTO_API int pto_fc_bwd_adv(const float* dh1, const float* a2p, const float* w1, const float* h1,
+                           const float* dlogits, float* gw1, float* gb1, float* gw2, float* gb2, float* da2p, int B,
+                           long long* bidx, long long nbatches, int* pending, hipStream_t s) {
+  const int nA = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
+  const int nB = ((B + 15) / 16) * ((F1IN + 15) / 16);
+  const int nW = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4;
+  const int nS = 8 + 1;
+  hipLaunchKernelGGL(k_fc_bwd, dim3(nA + nB + nW + nS), dim3(256), 0, s, dh1, a2p, w1, h1, dlogits, gw1, gb1, gw2,
+                     gb2, da2p, B, nA, nB, nW, bidx, nbatches, pending);
   LAUNCH_CHECK();
 }
 
@@ -1038,6 +1198,19 @@ PTO_API int pto_conv1_bwd(const float* g1, const uint8_t* code1, const float* x,
                           const long long* bidx, hipStream_t s) {
   const int nblk = C1 * ((B + B1_CHUNK - 1) / B1_CHUNK);
   hipLaunchKernelGGL(k_conv1_bwd, dim3(nblk), dim3(256), 0, s, g1, code1, x, gw1, gb1, B, bidx);
+  LAUNCH_CHECK();
+}
+
+// B1 + SGD over the flat range [0, nflat) of (p, g, m) (nflat % 4 == 0,
+// 16-byte aligned); zeroes those grads.
+PTO_API int pto_conv1_bwd_sgd(const float* g1, const uint8_t* code1, const float* x, float* gw1, float* gb1, int B,
+                              const long long* bidx, float* p, float* g, float* m, long long nflat, const float* lr,
+                              float mom, float wd, float gscale, int nesterov, hipStream_t s) {
+  if (nflat % 4 || ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m)) & 15)) return -1;
+  const int nconv = C1 * ((B + B1_CHUNK - 1) / B1_CHUNK);
+  const int nsgd = (int)((nflat / 4 + 255) / 256);
+  hipLaunchKernelGGL(k_conv1_bwd_sgd, dim3(nconv + nsgd), dim3(256), 0, s, g1, code1, x, gw1, gb1, B, bidx, nconv, p,
+                     g, m, nflat, sgd_args(lr, mom, wd, gscale, nesterov));
   LAUNCH_CHECK();
 }
 

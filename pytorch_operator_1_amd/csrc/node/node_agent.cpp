@@ -14,7 +14,14 @@
 //     GPU discovery from the KFD topology, CPU affinity per allocation;
 //   * the worker init-container gate: a TCP connect probe of
 //     MASTER_ADDR:MASTER_PORT (the DNS wait of the reference's
-//     init-pytorch container, pkg/common/config/config.go:9-20).
+//     init-pytorch container, pkg/common/config/config.go:9-20);
+//   * warm starts (--zygote PYTHON): a pre-imported interpreter
+//     (node/zygote.py) forks `python -m MODULE` / `python SCRIPT.py`
+//     containers instead of a cold fork/exec (import torch is ~1.5-2 s of
+//     the submit -> first-step path).  The agent is a child subreaper, so
+//     zygote-forked containers are re-parented to it and reaped, restarted
+//     and killed exactly like exec'ed ones; any other argv, or a zygote
+//     that is not ready/alive, takes the fork/exec path.
 //
 // Protocol: one JSON object per line on a Unix socket (--socket) or on
 // stdin/stdout (--stdio); every request gets exactly one JSON reply line.
@@ -27,7 +34,10 @@
 #include <netinet/in.h>
 #include <poll.h>
 #include <sched.h>
+#include <limits.h>
 #include <signal.h>
+#include <stdlib.h>
+#include <sys/prctl.h>
 #include <sys/signalfd.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
@@ -81,6 +91,148 @@ struct Proc {
   bool stopping = false;     // killed on purpose: no restart
   int last_exit_code = 0;
   double last_finished_at = 0;
+  std::string launcher;  // "zygote" | "exec"
+};
+
+// ---------------------------------------------------------------- zygote --
+struct Zygote {
+  std::string python, module = "pytorch_operator_1_amd.node.zygote", pypath;
+  pid_t pid = -1;
+  int fd = -1;
+  bool ready = false;
+  std::string inbuf;
+  long long spawned = 0, fallbacks = 0;
+
+  bool enabled() const { return !python.empty(); }
+
+  void start() {
+    if (python.empty()) return;
+    int sv[2];
+    if (socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, sv) != 0) return;
+    pid_t c = fork();
+    if (c == 0) {
+      close(sv[0]);
+      int fd = dup(sv[1]);  // no CLOEXEC: inherited by the interpreter
+      sigset_t none;
+      sigemptyset(&none);
+      sigprocmask(SIG_SETMASK, &none, nullptr);
+      int devnull = open("/dev/null", O_RDWR);
+      if (devnull >= 0) {
+        dup2(devnull, 0);
+        dup2(devnull, 1);
+        if (devnull > 2) close(devnull);
+      }
+      std::string pp = pypath;
+      const char* old = getenv("PYTHONPATH");
+      if (old && *old) pp = pp.empty() ? std::string(old) : pp + ":" + old;
+      if (!pp.empty()) setenv("PYTHONPATH", pp.c_str(), 1);
+      std::string fds = std::to_string(fd);
+      execlp(python.c_str(), python.c_str(), "-m", module.c_str(), "--fd", fds.c_str(), (char*)nullptr);
+      _exit(127);
+    }
+    close(sv[1]);
+    if (c < 0) {
+      close(sv[0]);
+      return;
+    }
+    pid = c;
+    fd = sv[0];
+    ready = false;
+    inbuf.clear();
+  }
+
+  void died() {
+    if (fd >= 0) close(fd);
+    fd = -1;
+    pid = -1;
+    ready = false;
+  }
+
+  // non-blocking: consume the "ready" line once the interpreter is warm
+  void poll_ready() {
+    if (fd < 0 || ready) return;
+    char buf[4096];
+    while (true) {
+      ssize_t r = recv(fd, buf, sizeof buf, MSG_DONTWAIT);
+      if (r > 0) {
+        inbuf.append(buf, r);
+        continue;
+      }
+      if (r == 0) {
+        died();
+        return;
+      }
+      break;
+    }
+    size_t nl = inbuf.find('\n');
+    if (nl == std::string::npos) return;
+    std::string line = inbuf.substr(0, nl);
+    inbuf.erase(0, nl + 1);
+    try {
+      ready = Json::parse(line)["ready"].boolean(false);
+    } catch (std::exception&) {
+      ready = false;
+    }
+  }
+
+  // python [-u] (-m MODULE | SCRIPT.py) ... of the zygote's own interpreter
+  bool eligible(const std::vector<std::string>& argv) const {
+    if (argv.size() < 2) return false;
+    char a[PATH_MAX], b[PATH_MAX];
+    if (!realpath(argv[0].c_str(), a) || !realpath(python.c_str(), b) || strcmp(a, b) != 0) return false;
+    size_t i = 1;
+    while (i < argv.size() && argv[i] == "-u") ++i;
+    if (i >= argv.size()) return false;
+    if (argv[i] == "-m") return i + 1 < argv.size();
+    const std::string& s = argv[i];
+    return s.size() > 3 && s.compare(s.size() - 3, 3, ".py") == 0 && s[0] != '-';
+  }
+
+  // one request, one reply line (a fork takes milliseconds); -1 on any
+  // failure, and the caller falls back to fork/exec
+  pid_t spawn(const Json& req) {
+    if (!ready || fd < 0) return -1;
+    std::string line = req.dump() + "\n";
+    size_t off = 0;
+    while (off < line.size()) {
+      ssize_t w = send(fd, line.data() + off, line.size() - off, MSG_NOSIGNAL);
+      if (w <= 0) {
+        died();
+        return -1;
+      }
+      off += (size_t)w;
+    }
+    const double end = mono_s() + 10.0;
+    while (true) {
+      size_t nl = inbuf.find('\n');
+      if (nl != std::string::npos) {
+        std::string l = inbuf.substr(0, nl);
+        inbuf.erase(0, nl + 1);
+        try {
+          Json r = Json::parse(l);
+          if (!r["ok"].boolean(false)) return -1;
+          return (pid_t)r["pid"].num(-1);
+        } catch (std::exception&) {
+          return -1;
+        }
+      }
+      double left = end - mono_s();
+      if (left <= 0) {  // a late reply would desynchronise the protocol: drop this zygote
+        ::kill(pid, SIGKILL);
+        died();
+        return -1;
+      }
+      pollfd pf{fd, POLLIN, 0};
+      if (poll(&pf, 1, (int)(left * 1000) + 1) <= 0) continue;
+      char buf[4096];
+      ssize_t r = recv(fd, buf, sizeof buf, 0);
+      if (r <= 0) {
+        died();
+        return -1;
+      }
+      inbuf.append(buf, r);
+    }
+  }
 };
 
 struct Agent {
@@ -93,6 +245,7 @@ struct Agent {
   std::vector<int> gpu_numa;
   double backoff_base = 0.2, backoff_max = 10.0;
   bool quit = false;
+  Zygote zygote;
 
   void discover_gpus(int forced) {
     if (forced >= 0) {
@@ -130,7 +283,37 @@ struct Agent {
   }
 
   // ------------------------------------------------------------- spawn --
+  bool start_zygote(Proc& p) {
+    if (!zygote.enabled() || !zygote.ready || !zygote.eligible(p.argv)) return false;
+    Json req = Json::object();
+    Json argv = Json::array();
+    for (auto& a : p.argv) argv.push(a);
+    req["argv"] = argv;
+    Json env = Json::object();
+    for (auto& kv : p.env) env[kv.first] = kv.second;
+    req["env"] = env;
+    req["cwd"] = p.cwd;
+    req["log"] = p.log;
+    Json cpus = Json::array();
+    for (int c : p.cpus) cpus.push(c);
+    req["cpus"] = cpus;
+    pid_t pid = zygote.spawn(req);
+    if (pid <= 0) {
+      ++zygote.fallbacks;
+      return false;
+    }
+    ++zygote.spawned;
+    p.pid = pid;
+    p.state = "running";
+    p.reason = "";
+    p.started_at = now_s();
+    p.launcher = "zygote";
+    return true;
+  }
+
   void start(Proc& p) {
+    if (start_zygote(p)) return;
+    p.launcher = "exec";
     int pipefd[2];
     if (pipe2(pipefd, O_CLOEXEC) != 0) pipefd[0] = pipefd[1] = -1;
     pid_t pid = fork();
@@ -242,6 +425,12 @@ struct Agent {
   }
 
   void on_exit(pid_t pid, int status) {
+    if (pid == zygote.pid) {
+      fprintf(stderr, "pto-node-agent: zygote %d exited (status %d); containers fall back to fork/exec\n",
+              (int)pid, status);
+      zygote.died();
+      return;
+    }
     for (auto& kv : procs) {
       Proc& p = kv.second;
       if (p.pid != pid) continue;
@@ -305,6 +494,7 @@ struct Agent {
       j["finished_at"] = p.finished_at;
       j["last_exit_code"] = p.last_exit_code;
       j["last_finished_at"] = p.last_finished_at;
+      j["launcher"] = p.launcher;
       list.push(j);
     }
     out["procs"] = list;
@@ -424,7 +614,18 @@ struct Agent {
     }
     std::string op = req["op"].str();
     Json r;
-    if (op == "ping") { r = ok(); r["gpus"] = n_gpus; r["pid"] = (long long)getpid(); }
+    if (op == "ping") {
+      r = ok();
+      r["gpus"] = n_gpus;
+      r["pid"] = (long long)getpid();
+      Json z = Json::object();
+      z["enabled"] = zygote.enabled();
+      z["ready"] = zygote.ready;
+      z["pid"] = (long long)zygote.pid;
+      z["spawned"] = zygote.spawned;
+      z["fallbacks"] = zygote.fallbacks;
+      r["zygote"] = z;
+    }
     else if (op == "spawn") r = spawn(req);
     else if (op == "kill") r = kill_(req);
     else if (op == "remove") r = remove(req);
@@ -453,7 +654,8 @@ struct Client {
 static void usage() {
   fprintf(stderr,
           "usage: pto-node-agent (--socket PATH | --stdio) [--gpus N] [--hbm-per-gpu BYTES]\n"
-          "                      [--backoff-base S] [--backoff-max S]\n");
+          "                      [--backoff-base S] [--backoff-max S]\n"
+          "                      [--zygote PYTHON [--zygote-pythonpath DIR]]\n");
 }
 
 int main(int argc, char** argv) {
@@ -473,6 +675,8 @@ int main(int argc, char** argv) {
     else if (a == "--hbm-per-gpu") ag.hbm_per_gpu = atof(next().c_str());
     else if (a == "--backoff-base") ag.backoff_base = atof(next().c_str());
     else if (a == "--backoff-max") ag.backoff_max = atof(next().c_str());
+    else if (a == "--zygote") ag.zygote.python = next();
+    else if (a == "--zygote-pythonpath") ag.zygote.pypath = next();
     else if (a == "--version") { printf("pto-node-agent 0.1.0 (gfx950 / MI355X)\n"); return 0; }
     else { usage(); return 2; }
   }
@@ -487,6 +691,10 @@ int main(int argc, char** argv) {
   sigprocmask(SIG_BLOCK, &mask, nullptr);
   int sfd = signalfd(-1, &mask, SFD_NONBLOCK | SFD_CLOEXEC);
   signal(SIGPIPE, SIG_IGN);
+  // zygote-forked containers are orphaned by their forking parent: be their
+  // reaper so waitpid() sees them like our own children
+  prctl(PR_SET_CHILD_SUBREAPER, 1);
+  ag.zygote.start();
 
   int lfd = -1;
   std::vector<Client> clients;
@@ -510,8 +718,10 @@ int main(int argc, char** argv) {
     std::vector<pollfd> pfds;
     pfds.push_back({sfd, POLLIN, 0});
     if (lfd >= 0) pfds.push_back({lfd, POLLIN, 0});
+    if (ag.zygote.fd >= 0 && !ag.zygote.ready) pfds.push_back({ag.zygote.fd, POLLIN, 0});
     for (auto& c : clients) pfds.push_back({c.fd, POLLIN, 0});
     poll(pfds.data(), pfds.size(), 50);
+    ag.zygote.poll_ready();
     // signals
     signalfd_siginfo si;
     while (read(sfd, &si, sizeof si) == (ssize_t)sizeof si) {
@@ -566,7 +776,11 @@ int main(int argc, char** argv) {
       }
     }
   }
-  // graceful: terminate children, then reap
+  // graceful: terminate children, then reap (the zygote ends on EOF)
+  if (ag.zygote.fd >= 0) {
+    close(ag.zygote.fd);
+    ag.zygote.fd = -1;
+  }
   for (auto& kv : ag.procs)
     if (kv.second.state == "running" && kv.second.pid > 0) ::kill(-kv.second.pid, SIGTERM);
   double end = mono_s() + 5;

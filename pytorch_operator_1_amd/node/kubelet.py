@@ -106,7 +106,9 @@ class Kubelet:
         self.client = client
         if gpus is None and agent is None:
             gpus = _visible_gpu_count()
-        self.agent = agent or AgentClient(gpus=gpus, hbm_per_gpu=hbm_per_gpu)
+        # warm starts (node/zygote.py) unless PTO_ZYGOTE=0
+        self.agent = agent or AgentClient(gpus=gpus, hbm_per_gpu=hbm_per_gpu,
+                                          zygote=os.environ.get("PTO_ZYGOTE", "1") == "1")
         self.node_name = node_name
         self.log_dir = log_dir or os.path.join(os.environ.get("TMPDIR", "/tmp"), "pto-pods")
         os.makedirs(self.log_dir, exist_ok=True)
@@ -223,6 +225,7 @@ class Kubelet:
                 return
             rt.stage = "init"
             rt.started_at = now_rfc3339()
+            self._clear_pod_files(pod)
             self._annotate(pod, {LOG_ANNOTATION: self._log_path(pod), GPUS_ANNOTATION:
                                  ",".join(map(str, rt.gpus))})
         if rt.stage == "init":
@@ -305,6 +308,20 @@ class Kubelet:
     def _log_path(self, pod, container=None):
         base = f"{namespace_of(pod)}_{name_of(pod)}"
         return os.path.join(self.log_dir, base + (f".{container}" if container else "") + ".log")
+
+    def _clear_pod_files(self, pod):
+        """A new pod starts with empty logs and metrics, even when an earlier
+        pod of the same name left files behind (its first-step record would
+        otherwise be read as this pod's)."""
+        names = [None, "metrics"] + [c.get("name") for c in (pod["spec"].get("containers") or []) +
+                                     (pod["spec"].get("initContainers") or [])]
+        for n in names:
+            p = self._log_path(pod, n)
+            for path in (p, p.replace(".log", ".jsonl")):
+                try:
+                    os.unlink(path)
+                except FileNotFoundError:
+                    pass
 
     def _job_port(self, pod, wanted: int) -> int:
         job = (pod["metadata"].get("labels") or {}).get(C.LABEL_JOB_NAME) or name_of(pod)

@@ -14,6 +14,7 @@ import os
 import shutil
 import socket
 import subprocess
+import sys
 import threading
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -44,7 +45,11 @@ class AgentError(RuntimeError):
 
 class AgentClient:
     def __init__(self, gpus: int | None = None, socket_path: str | None = None, hbm_per_gpu: float | None = None,
-                 backoff_base: float = 0.2, backoff_max: float = 10.0, binary: str | None = None):
+                 backoff_base: float = 0.2, backoff_max: float = 10.0, binary: str | None = None,
+                 zygote: bool = False):
+        """``zygote``: warm starts -- the agent keeps a pre-imported
+        interpreter (``node/zygote.py``) and forks ``python -m``/``python
+        x.py`` containers from it instead of fork/exec."""
         self._lock = threading.Lock()
         self._proc = None
         self._sock = None
@@ -60,6 +65,8 @@ class AgentClient:
                 cmd += ["--gpus", str(gpus)]
             if hbm_per_gpu:
                 cmd += ["--hbm-per-gpu", str(hbm_per_gpu)]
+            if zygote:
+                cmd += ["--zygote", sys.executable, "--zygote-pythonpath", os.path.dirname(PKG_DIR)]
             self._proc = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
 
     def call(self, op: str, **kw) -> dict:
@@ -109,6 +116,24 @@ class AgentClient:
 
     def free(self, owner):
         return self.call("free", owner=owner)
+
+    def ping(self) -> dict:
+        return self.ok("ping")
+
+    def wait_warm(self, timeout: float = 60.0) -> bool:
+        """Block until the agent's zygote (if enabled) has finished its
+        imports; False if it is disabled, died, or is not ready in time."""
+        import time
+
+        end = time.time() + timeout
+        while time.time() < end:
+            z = self.ping().get("zygote", {})
+            if not z.get("enabled") or (z.get("pid", -1) < 0):
+                return False
+            if z.get("ready"):
+                return True
+            time.sleep(0.05)
+        return False
 
     def probe(self, host, port, timeout=0.5) -> bool:
         return bool(self.ok("probe", host=host, port=int(port), timeout=timeout).get("open"))
