@@ -952,20 +952,23 @@ __global__ __launch_bounds__(256) void k_conv1_bwd(const float* __restrict__ g1,
 
 // B1 + the optimizer for every parameter whose gradient is final before B1
 // (fc and conv2: the flat range [0, nflat), 1024 elements per extra block).
-// The extra blocks touch no byte the conv1 blocks read or write.
+// The extra blocks touch no byte the conv1 blocks read or write.  Grads
+// below `zero_from` (fc: B3 stores every element each step) are not zeroed;
+// the atomically accumulated conv2 weight grads are.
 __global__ __launch_bounds__(256) void k_conv1_bwd_sgd(const float* __restrict__ g1,
                                                        const uint8_t* __restrict__ code1,
                                                        const float* __restrict__ x, float* __restrict__ gw1,
                                                        float* __restrict__ gb1, int B,
                                                        const long long* __restrict__ bidx, int nconv,
                                                        float* __restrict__ p, float* __restrict__ g,
-                                                       float* __restrict__ m, long long nflat, SgdArgs a) {
+                                                       float* __restrict__ m, long long nflat, long long zero_from,
+                                                       SgdArgs a) {
   if ((int)blockIdx.x < nconv) {
     conv1_bwd_block(blockIdx.x, g1, code1, x, gw1, gb1, B, bidx);
     return;
   }
   const long long i = ((long long)(blockIdx.x - nconv) * 256 + threadIdx.x) * 4;
-  if (i < nflat) sgd_flat4(p, g, m, i, *a.lr, a);
+  if (i < nflat) sgd_flat4(p, g, m, i, *a.lr, a, i >= zero_from);
 }
 
 // Host-side flush of an owed conv1 update (before the parameters are read
@@ -1202,15 +1205,16 @@ PTO_API int pto_conv1_bwd(const float* g1, const uint8_t* code1, const float* x,
 }
 
 // B1 + SGD over the flat range [0, nflat) of (p, g, m) (nflat % 4 == 0,
-// 16-byte aligned); zeroes those grads.
+// 16-byte aligned); zeroes the grads in [zero_from, nflat).
 PTO_API int pto_conv1_bwd_sgd(const float* g1, const uint8_t* code1, const float* x, float* gw1, float* gb1, int B,
-                              const long long* bidx, float* p, float* g, float* m, long long nflat, const float* lr,
-                              float mom, float wd, float gscale, int nesterov, hipStream_t s) {
-  if (nflat % 4 || ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m)) & 15)) return -1;
+                              const long long* bidx, float* p, float* g, float* m, long long nflat,
+                              long long zero_from, const float* lr, float mom, float wd, float gscale, int nesterov,
+                              hipStream_t s) {
+  if (nflat % 4 || zero_from % 4 || ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m)) & 15)) return -1;
   const int nconv = C1 * ((B + B1_CHUNK - 1) / B1_CHUNK);
   const int nsgd = (int)((nflat / 4 + 255) / 256);
   hipLaunchKernelGGL(k_conv1_bwd_sgd, dim3(nconv + nsgd), dim3(256), 0, s, g1, code1, x, gw1, gb1, B, bidx, nconv, p,
-                     g, m, nflat, sgd_args(lr, mom, wd, gscale, nesterov));
+                     g, m, nflat, zero_from, sgd_args(lr, mom, wd, gscale, nesterov));
   LAUNCH_CHECK();
 }
 

@@ -28,9 +28,10 @@ struct SgdArgs {
 };
 
 // One float4 group (4 elements at i, 16-byte aligned, i + 3 < n) of a flat
-// (p, g, m) range: update p, m in place and zero g.
+// (p, g, m) range: update p, m in place and zero g (unless the producer of g
+// overwrites it every step: zero_g = false saves the store).
 __device__ __forceinline__ void sgd_flat4(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
-                                          long long i, float lr, const SgdArgs& a) {
+                                          long long i, float lr, const SgdArgs& a, bool zero_g = true) {
   float4 pv = *reinterpret_cast<float4*>(p + i);
   const float4 gv = *reinterpret_cast<const float4*>(g + i);
   float4 mv = *reinterpret_cast<float4*>(m + i);
@@ -40,5 +41,5 @@ __device__ __forceinline__ void sgd_flat4(float* __restrict__ p, float* __restri
   sgd_elem(pv.w, gv.w, mv.w, lr, a.mom, a.wd, a.gscale, a.nesterov);
   *reinterpret_cast<float4*>(p + i) = pv;
   *reinterpret_cast<float4*>(m + i) = mv;
-  *reinterpret_cast<float4*>(g + i) = float4{0.f, 0.f, 0.f, 0.f};
+  if (zero_g) *reinterpret_cast<float4*>(g + i) = float4{0.f, 0.f, 0.f, 0.f};
 }

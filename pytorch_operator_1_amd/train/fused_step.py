@@ -15,8 +15,12 @@ MI355X design:
     xGMI one-shot kernel from :mod:`pytorch_operator_1_amd.parallel.xgmi`),
     and the optimizer is a single fused launch that also zeroes the grads
     (so atomically accumulated grads start from zero next step).
-  * every op is a kernel from ``csrc/kernels/mnist_kernels.hip`` (8 launches
-    per step + the batch fetch); activations stay resident in HBM.
+  * every op is a kernel from ``csrc/kernels/mnist_kernels.hip``; activations
+    stay resident in HBM.  Single process: 6 launches per step, the optimizer
+    running inside them (``fused_opt``: extra blocks of the conv1-backward
+    launch update fc/conv2, conv1's update is applied on the fly by the next
+    step's first launch and committed by its fc2 launch).  DDP: 7 launches +
+    the bucketed all-reduce, then one multi-tensor SGD launch.
   * the step is captured once into a HIP graph and replayed: the host cost
     per step is one ``hipGraphLaunch`` instead of ~10 launches.  The batch
     index is a device counter advanced inside the graph, so replays walk the
@@ -37,7 +41,8 @@ from ..ops import _lib
 class FusedMnistTrainer:
     def __init__(self, device, batch_size=64, lr=0.01, momentum=0.5, dataset_size=60000, seed=1, rank=0,
                  weight_decay=0.0, nesterov=False, graph: str | None = None, comm: str | None = None,
-                 data=None, target=None, unroll: int | None = None, force_ddp: bool = False):
+                 data=None, target=None, unroll: int | None = None, force_ddp: bool = False,
+                 fused_opt: bool | None = None):
         assert device.type == "cuda", "FusedMnistTrainer runs on a HIP device"
         import os
 
@@ -62,22 +67,22 @@ class FusedMnistTrainer:
         offs, total = param_offsets()
         self.numel = total
         f32 = dict(device=device, dtype=torch.float32)
-        self.params = torch.zeros(total, **f32)
+        self._params = torch.zeros(total, **f32)
         self.grads = torch.zeros(total, **f32)
         self.mom = torch.zeros(total, **f32)
-        self.p, self.g = {}, {}
+        self._p, self.g = {}, {}
         for name, (off, shape) in offs.items():
             n = math.prod(shape)
-            self.p[name] = self.params[off:off + n].view(shape)
+            self._p[name] = self._params[off:off + n].view(shape)
             self.g[name] = self.grads[off:off + n].view(shape)
         # Same init as the stock module under the same seed.
         torch.manual_seed(seed)
         ref = MnistNet()
         with torch.no_grad():
             for name, t in ref.state_dict().items():
-                self.p[name].copy_(t.to(device))
+                self._p[name].copy_(t.to(device))
         if self.world > 1:
-            dist.broadcast(self.params, 0)  # DDP's ctor broadcast (COL1)
+            dist.broadcast(self._params, 0)  # DDP's ctor broadcast (COL1)
 
         B = self.B
         self.a1p = torch.empty(B * 2880, **f32)
@@ -103,11 +108,24 @@ class FusedMnistTrainer:
         # per-16-row arrival counters (re-armed by the kernel itself)
         self.fuse_fc = os.environ.get("PTO_FUSE_FC", "0") == "1"  # measured: 1.06M vs 1.11M samples/s unfused
         self.fc_counters = torch.zeros(max(1, (self.B + 15) // 16), device=device, dtype=torch.int32)
+        # Fused-optimizer schedule (no gradient all-reduce between backward and
+        # the update, i.e. world size 1): no SGD launch; fc/conv2 are updated by
+        # extra blocks of the conv1-backward launch, conv1's update is applied
+        # on the fly by the next step's first launch and committed by its fc2
+        # launch (mnist_kernels.hip, "Fused optimizer").  PTO_FUSED_OPT=0: the
+        # separate multi-tensor SGD launch.
+        if fused_opt is None:
+            fused_opt = os.environ.get("PTO_FUSED_OPT", "1") == "1"
+        self.fused_opt = bool(fused_opt) and not self.ddp and not self.fuse_fc
+        self.pending = torch.zeros(1, device=device, dtype=torch.int32)  # conv1 update owed
+        self.batch_snap = torch.zeros(1, device=device, dtype=torch.int64)  # cursor seen by this step's B1
+        self._c1 = offs["conv1.weight"][0]
+        self._c1_bias = offs["conv1.bias"][0] - self._c1
 
         # SGD launch table (one "tensor" = the whole flat buffer).
         from ..ops.optim import SgdTable
 
-        self.sgd = SgdTable([(self.params, self.grads, self.mom)], device)
+        self.sgd = SgdTable([(self._params, self.grads, self.mom)], device)
         self.lr_dev = torch.tensor([self.lr], **f32)
         self._graphs = None
         self._graph_unrolled = None
@@ -166,9 +184,29 @@ class FusedMnistTrainer:
         """Forward + loss + fc-layer backward: after this the fc grads
         (the first 405,632 elements of the flat buffer, 94% of the bytes)
         are final and their all-reduce can start."""
-        L, s, B, P, G = self.L, self._s(), self.B, self.p, self.g
+        L, s, B, P, G = self.L, self._s(), self.B, self._p, self.g
         c = _lib.check
         bi = self.batch_idx.data_ptr()
+        if self.fused_opt:
+            o = self._opt_args()
+            c(L.pto_conv12_fwd_lazy(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
+                                    P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
+                                    self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi,
+                                    self.grads[self._c1:].data_ptr(), self.mom[self._c1:].data_ptr(), self._c1_bias,
+                                    self.pending.data_ptr(), *o, s), "conv12_fwd_lazy")
+            c(L.pto_linear_fwd(self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
+                               self.h1.data_ptr(), B, 500, 800, 1, s), "fc1_fwd")
+            c(L.pto_fc2_ce_commit(self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
+                                  self.target.data_ptr(), self.loss_rows.data_ptr(), self.dlogits.data_ptr(),
+                                  self.dh1.data_ptr(), B, 1.0 / B, bi, self.batch_snap.data_ptr(),
+                                  self._params[self._c1:].data_ptr(), self.grads[self._c1:].data_ptr(),
+                                  self.mom[self._c1:].data_ptr(), self.numel - self._c1, self.pending.data_ptr(),
+                                  *o, s), "fc2_ce_commit")
+            c(L.pto_fc_bwd_adv(self.dh1.data_ptr(), self.a2p.data_ptr(), P["fc1.weight"].data_ptr(),
+                               self.h1.data_ptr(), self.dlogits.data_ptr(), G["fc1.weight"].data_ptr(),
+                               G["fc1.bias"].data_ptr(), G["fc2.weight"].data_ptr(), G["fc2.bias"].data_ptr(),
+                               self.da2p.data_ptr(), B, bi, self.n_batches, self.pending.data_ptr(), s), "fc_bwd_adv")
+            return
         c(L.pto_conv12_fwd(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
                            P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
                            self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi, s), "conv12_fwd")
@@ -188,7 +226,7 @@ class FusedMnistTrainer:
                        G["fc2.weight"].data_ptr(), G["fc2.bias"].data_ptr(), self.da2p.data_ptr(), B, s), "fc_bwd")
 
     def conv_backward(self):
-        L, s, B, P, G = self.L, self._s(), self.B, self.p, self.g
+        L, s, B, P, G = self.L, self._s(), self.B, self._p, self.g
         c = _lib.check
         bi = self.batch_idx.data_ptr()
         # conv2 wgrad + dgrad(col2im) + bias in one launch.  (Folding conv1's
@@ -199,6 +237,13 @@ class FusedMnistTrainer:
         c(L.pto_conv2_bwd(self.da2p.data_ptr(), self.code2.data_ptr(), self.a1p.data_ptr(),
                           P["conv2.weight"].data_ptr(), G["conv2.weight"].data_ptr(), G["conv2.bias"].data_ptr(),
                           self.da1p.data_ptr(), B, 7, None, None, None, None, None, s), "conv2_bwd")
+        if self.fused_opt:  # + the fc/conv2 update (grads final since B3/B2); B1 reads the cursor snapshot
+            c(L.pto_conv1_bwd_sgd(self.da1p.data_ptr(), self.code1.data_ptr(), self.data.data_ptr(),
+                                  G["conv1.weight"].data_ptr(), G["conv1.bias"].data_ptr(), B,
+                                  self.batch_snap.data_ptr(), self._params.data_ptr(), self.grads.data_ptr(),
+                                  self.mom.data_ptr(), self._c1, self._split(), *self._opt_args(), s),
+              "conv1_bwd_sgd")
+            return
         c(L.pto_conv1_bwd(self.da1p.data_ptr(), self.code1.data_ptr(), self.data.data_ptr(),
                           G["conv1.weight"].data_ptr(), G["conv1.bias"].data_ptr(), B, bi, s), "conv1_bwd")
 
@@ -217,7 +262,36 @@ class FusedMnistTrainer:
             self._buckets = (self.grads[:split], self.grads[split:])
         return self._buckets
 
+    def _opt_args(self):
+        """(lr device ptr, momentum, weight decay, grad scale, nesterov) for
+        the fused-optimizer launchers."""
+        return (self.lr_dev.data_ptr(), self.momentum, self.weight_decay, 1.0 / self.world, int(self.nesterov))
+
+    def flush(self):
+        """Commit an owed conv1 update (fused-optimizer schedule) so the flat
+        buffers hold exactly the parameters/momentum an eager SGD step would
+        have left.  Idempotent; a no-op for the other schedules."""
+        if not self.fused_opt or self.steps_done == 0:
+            return
+        _lib.check(self.L.pto_conv1_commit(self._params[self._c1:].data_ptr(), self.grads[self._c1:].data_ptr(),
+                                           self.mom[self._c1:].data_ptr(), self.numel - self._c1,
+                                           self.pending.data_ptr(), *self._opt_args(), self._s()), "conv1_commit")
+
+    @property
+    def params(self):
+        """Flat fp32 parameter buffer (owed updates committed first)."""
+        self.flush()
+        return self._params
+
+    @property
+    def p(self):
+        """Parameter views by reference name (owed updates committed first)."""
+        self.flush()
+        return self._p
+
     def optimizer_step(self):
+        if self.fused_opt:  # done inside the step's other launches
+            return
         self.sgd.step(self.lr_dev, self.lr, self.momentum, self.weight_decay, 1.0 / self.world, self.nesterov,
                       zero_grad=True, stream=self._s(), batch_cursor=self.batch_idx, n_batches=self.n_batches)
 
@@ -262,14 +336,15 @@ class FusedMnistTrainer:
         # Warm up on a side stream (lazy library/allocator init must not
         # happen under capture), then roll the state back so capture does
         # not change the training trajectory, then capture.
-        snap = [t.clone() for t in (self.params, self.mom, self.grads, self.batch_idx)]
+        state = (self._params, self.mom, self.grads, self.batch_idx, self.pending, self.batch_snap)
+        snap = [t.clone() for t in state]
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             self._eager_step()
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
-        for dst, src in zip((self.params, self.mom, self.grads, self.batch_idx), snap):
+        for dst, src in zip(state, snap):
             dst.copy_(src)
         torch.cuda.synchronize(self.device)
         graphs = []
@@ -354,7 +429,8 @@ class FusedMnistTrainer:
         """Test pass with the same kernels (forward + fused argmax/NLL-sum
         eval head, K11).  Returns ``(mean_loss, accuracy)`` like the
         reference's ``test()`` (examples/mnist/mnist.py:51-65)."""
-        L, s, P = self.L, self._s(), self.p
+        self.flush()
+        L, s, P = self.L, self._s(), self._p
         n = data.shape[0]
         Bm = min(batch_size, n)
         f32 = dict(device=self.device, dtype=torch.float32)
@@ -384,6 +460,7 @@ class FusedMnistTrainer:
         return loss_sum / n, correct / n
 
     def set_lr(self, lr: float):
+        self.flush()  # an owed update uses the lr of the step that produced it
         self.lr = float(lr)
         self.lr_dev.fill_(self.lr)
 
@@ -391,7 +468,8 @@ class FusedMnistTrainer:
     def state_dict(self):
         """Module-style state (same keys as the reference ``Net``) plus the
         optimizer momentum in torch.optim.SGD layout."""
-        model = {k: v.detach().clone() for k, v in self.p.items()}
+        self.flush()
+        model = {k: v.detach().clone() for k, v in self._p.items()}
         offs, _ = param_offsets()
         order = [n for n, _ in PARAM_SHAPES]
         mom = {}
@@ -402,10 +480,11 @@ class FusedMnistTrainer:
                 "batch_idx": int(self.batch_idx.item()), "steps_done": self.steps_done}
 
     def load_state_dict(self, sd):
+        self.flush()  # nothing owed afterwards: the loaded state is complete
         offs, _ = param_offsets()
         with torch.no_grad():
             for name, t in sd["model"].items():
-                self.p[name].copy_(t.to(self.device))
+                self._p[name].copy_(t.to(self.device))
             for name, t in sd.get("momentum", {}).items():
                 off, shape = offs[name]
                 self.mom[off:off + math.prod(shape)].copy_(t.reshape(-1).to(self.device))

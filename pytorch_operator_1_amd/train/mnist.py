@@ -131,6 +131,11 @@ def _main(argv=None):
         print(f"Using distributed PyTorch with {dist.get_backend()} backend")
     rank, world = env.rank, env.world_size
     metrics = Metrics()
+    # TensorBoard scalars like the reference's SummaryWriter(args.dir)
+    # (examples/mnist/mnist.py:49,65,108): 'loss' per log interval, 'accuracy' per epoch
+    from ..utils.tbevents import SummaryWriter
+
+    writer = SummaryWriter(args.dir) if args.dir else None
     xtr, ytr, xte, yte = load_data(args, device, rank)
     if args.sampler and world > 1:  # DistributedSampler semantics: disjoint shards
         n = xtr.shape[0] // world
@@ -188,6 +193,8 @@ def _main(argv=None):
             print("Train Epoch: {} [{}/{} ({:.0f}%)]\tloss={:.4f}".format(
                 epoch, batch_idx * args.batch_size, n_batches * args.batch_size, 100.0 * batch_idx / n_batches, loss))
             metrics.emit(event="train", step=step, loss=loss, samples_per_sec=round(sps * world, 1), rank=rank)
+            if writer:
+                writer.add_scalar("loss", loss, epoch * n_batches + batch_idx)
         if args.checkpoint_dir and args.checkpoint_interval and step % args.checkpoint_interval == 0 and rank == 0:
             ckpt.save(args.checkpoint_dir, step, {"trainer": trainer.state_dict(), "rng": ckpt.rng_state()})
         end_of_epoch = step % n_batches == 0 or step == total_steps
@@ -197,11 +204,16 @@ def _main(argv=None):
             else:
                 test_loss, acc = evaluate_module(trainer.model, xte, yte, args.test_batch_size)
             print("\naccuracy={:.4f}\n".format(acc))
+            if writer:
+                writer.add_scalar("accuracy", acc, epoch)
+                writer.flush()
             metrics.emit(event="test", epoch=epoch, accuracy=acc, loss=test_loss, rank=rank,
                          epoch_seconds=round(time.time() - t_epoch, 3))
             t_epoch = time.time()
         sys.stdout.flush()
     trace.__exit__(None, None, None)
+    if writer:
+        writer.close()
     if args.checkpoint_dir and rank == 0:
         ckpt.save(args.checkpoint_dir, step, {"trainer": trainer.state_dict(), "rng": ckpt.rng_state()})
     if args.save_model and rank == 0:

@@ -64,3 +64,47 @@ def test_captured_rccl_allreduce_in_graph():
     p.join(60)
     assert p.exitcode == 0
     assert err < 1e-5
+
+
+@pytest.mark.parametrize("graph,unroll", [("none", 1), (None, 1), (None, 4)])
+def test_fused_optimizer_schedule_matches_sgd_launch(graph, unroll):
+    """The fused-optimizer schedule (no SGD launch; conv1's update applied on
+    the fly by the next step and committed by its fc2 launch) leaves the
+    parameters, momentum and batch cursor of the separate SGD launch at every
+    point the host can observe them (params / state_dict / evaluate),
+    including an LR change and a checkpoint reload mid-run.  (Not bitwise:
+    the conv weight grads are fp32 atomics, so two runs of either schedule
+    differ in the last bits; a missed or doubled conv1 update would be off by
+    ~lr*grad, orders of magnitude above the tolerance.)"""
+    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+
+    dev = torch.device("cuda", 0)
+    kw = dict(dataset_size=64 * 9, seed=4, graph=graph, unroll=unroll, weight_decay=1e-4)
+    a = FusedMnistTrainer(dev, fused_opt=True, **kw)
+    b = FusedMnistTrainer(dev, fused_opt=False, **kw)
+    assert a.fused_opt and not b.fused_opt
+    for t in (a, b):
+        t.run(7)
+    torch.cuda.synchronize()
+    assert rel(a.params, b.params) < 1e-5
+    assert rel(a.mom, b.mom) < 1e-4
+    for name in a.p:
+        assert rel(a.p[name], b.p[name]) < 1e-5, name
+    assert int(a.batch_idx.item()) == int(b.batch_idx.item()) == 7 % 9
+    for t in (a, b):
+        t.set_lr(0.02)
+        t.run(6)
+    sa, sb = a.state_dict(), b.state_dict()
+    for k in sa["model"]:
+        assert rel(sa["model"][k], sb["model"][k]) < 1e-5, k
+        assert rel(sa["momentum"][k], sb["momentum"][k]) < 1e-4, k
+    x = torch.randn(256, 1, 28, 28, device=dev)
+    y = torch.randint(0, 10, (256,), device=dev)
+    (la, aa), (lb, ab) = a.evaluate(x, y), b.evaluate(x, y)
+    assert abs(la - lb) < 1e-4 and abs(aa - ab) <= 2 / 256
+    # reload mid-run: both continue identically
+    a.load_state_dict(sb)
+    for t in (a, b):
+        t.run(3)
+    assert rel(a.params, b.params) < 1e-5
+    assert abs(a.last_loss() - b.last_loss()) < 1e-4
