@@ -347,6 +347,179 @@ __global__ __launch_bounds__(256) void k_conv12_fwd(const float* __restrict__ x,
   code2[oi] = cd;
 }
 
+// F1+F2, 512-thread version: the same work as k_conv12_fwd laid out for
+// two waves per SIMD.
+//  * conv1: a wave owns (4-channel group, 64 pooled pixels), so its 100
+//    weights + 4 biases are wave-uniform: read ONCE per task from LDS as
+//    broadcast ds_read_b128 into VGPRs (channel rows padded to 28 floats),
+//    instead of 100 ds_read_b32 per pooled pixel; the 6x6 input patch is 18
+//    ds_read_b64.
+//  * conv2 GEMM: K split over the two halves of the block (waves w and w+4
+//    own the same pooled row), partial tiles combined through LDS, so each
+//    SIMD interleaves two independent MFMA chains.
+constexpr int W1LD = 28;
+__global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x, const float* __restrict__ w1,
+                                                     const float* __restrict__ b1, const float* __restrict__ w2,
+                                                     const float* __restrict__ b2, float* __restrict__ a1p,
+                                                     uint8_t* __restrict__ code1, float* __restrict__ a2p,
+                                                     uint8_t* __restrict__ code2, int B,
+                                                     const long long* __restrict__ bidx, LazyConv1 lz) {
+  __shared__ float ws[16 * WS_LD];
+  __shared__ __attribute__((aligned(16))) float in_s[A1P];
+  __shared__ __attribute__((aligned(16))) float xs[784];
+  __shared__ __attribute__((aligned(16))) float w1s[C1 * W1LD + 32];
+  __shared__ __attribute__((aligned(16))) float red[4 * 256];
+  const int b = blockIdx.x >> 2, nt = blockIdx.x & 3;
+  const int tid = threadIdx.x;
+  {
+    x = batch_ptr(x, bidx, B * 784);
+    const int nrows = min(16, C2 - nt * 16);
+    const float4* wsrc = reinterpret_cast<const float4*>(w2 + nt * 16 * 500);
+    float4 wv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 512 * q;
+      wv[q] = (e < nrows * 125) ? wsrc[e] : float4{0.f, 0.f, 0.f, 0.f};
+    }
+    const float4 xv = tid < 196 ? reinterpret_cast<const float4*>(x + b * 784)[tid] : float4{0.f, 0.f, 0.f, 0.f};
+    float wq[2], gq[2], mq[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 512 * q;
+      wq[q] = e < C1 * 25 ? w1[e] : (e < C1 * 26 ? b1[e - C1 * 25] : 0.f);
+    }
+    int pend = 0;
+    float lr = 0.f;
+    if (lz.pending) {
+      pend = *lz.pending;
+      lr = *lz.a.lr;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int e = tid + 512 * q;
+        const int fi = e < C1 * 25 ? e : lz.bias_off + (e - C1 * 25);
+        gq[q] = e < C1 * 26 ? lz.g[fi] : 0.f;
+        mq[q] = e < C1 * 26 ? lz.m[fi] : 0.f;
+      }
+    }
+    if (pend) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) sgd_elem(wq[q], gq[q], mq[q], lr, lz.a.mom, lz.a.wd, lz.a.gscale, lz.a.nesterov);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 512 * q;
+      if (e < 2000) {
+        const int row = e / 125, col = (e - row * 125) * 4;
+        float* d = ws + row * WS_LD + col;
+        d[0] = wv[q].x; d[1] = wv[q].y; d[2] = wv[q].z; d[3] = wv[q].w;
+      }
+    }
+    if (tid < 196) reinterpret_cast<float4*>(xs)[tid] = xv;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int e = tid + 512 * q;
+      if (e < C1 * 25) w1s[(e / 25) * W1LD + e % 25] = wq[q];
+      else if (e < C1 * 26) w1s[C1 * W1LD + e - C1 * 25] = wq[q];
+    }
+  }
+  __syncthreads();
+  const int wid = tid >> 6, lane = tid & 63;
+  // conv1 + bias + ReLU + pool: 15 wave tasks = 5 channel groups x 3 pixel
+  // chunks (64, 64, 16 pooled pixels)
+  for (int task = wid; task < 15; task += 8) {
+    const int cg = task / 3, pix = (task - cg * 3) * 64 + lane;
+    float wr[4][W1LD], bz[4];
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+#pragma unroll
+      for (int j = 0; j < W1LD / 4; ++j) {
+        const float4 v = *reinterpret_cast<const float4*>(w1s + (cg * 4 + cc) * W1LD + 4 * j);
+        wr[cc][4 * j] = v.x; wr[cc][4 * j + 1] = v.y; wr[cc][4 * j + 2] = v.z; wr[cc][4 * j + 3] = v.w;
+      }
+      bz[cc] = w1s[C1 * W1LD + cg * 4 + cc];
+    }
+    if (pix >= 144) continue;
+    const int ph = pix / 12, pw = pix - ph * 12;
+    float p[6][6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int c = 0; c < 6; c += 2) {
+        const float2 v = *reinterpret_cast<const float2*>(xs + (2 * ph + r) * 28 + 2 * pw + c);
+        p[r][c] = v.x;
+        p[r][c + 1] = v.y;
+      }
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      const int oc = cg * 4 + cc;
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int dy = q >> 1, dx = q & 1;
+        float sacc = bz[cc];
+#pragma unroll
+        for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw) sacc = fmaf(p[dy + kh][dx + kw], wr[cc][kh * 5 + kw], sacc);
+        v[q] = sacc;
+      }
+      float o;
+      uint8_t cd;
+      relu_pool4(v, o, cd);
+      in_s[oc * 144 + pix] = o;
+      if (nt == 0) {
+        a1p[b * A1P + oc * 144 + pix] = o;
+        code1[b * A1P + oc * 144 + pix] = cd;
+      }
+    }
+  }
+  __syncthreads();
+  // conv2 implicit GEMM (k_conv2_fwd's lane maps), K split in two halves
+  const int t = wid & 3, half = wid >> 2;
+  const int i = lane & 15, g = lane >> 4;
+  const int pw = i >> 2, dy = (i >> 1) & 1, dx = i & 1;
+  const int n = nt * 16 + (lane & 15);
+  const float* wl = ws + (lane & 15) * WS_LD + 5 * g;
+  const float* il = in_s + (2 * t + dy) * 12 + 2 * pw + dx;
+  f32x4 acc0 = zero4(), acc1 = zero4();
+  auto group = [&](int G) {
+    const int R = 4 * G + g;
+    const int ic = R / 5, kh = R - ic * 5;
+    const float* arow = il + ic * 144 + kh * 12;
+    const float* brow = wl + 20 * G;
+    acc0 = mfma16x16x4(arow[0], brow[0], acc0);
+    acc1 = mfma16x16x4(arow[1], brow[1], acc1);
+    acc0 = mfma16x16x4(arow[2], brow[2], acc0);
+    acc1 = mfma16x16x4(arow[3], brow[3], acc1);
+    acc0 = mfma16x16x4(arow[4], brow[4], acc0);
+  };
+  if (half == 0) {
+#pragma unroll
+    for (int G = 0; G < 13; ++G) group(G);
+  } else {
+#pragma unroll
+    for (int G = 13; G < 25; ++G) group(G);
+  }
+  f32x4 acc = acc0 + acc1;
+  if (half == 1) {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) red[t * 256 + rr * 64 + lane] = acc[rr];
+  }
+  __syncthreads();
+  if (half == 1) return;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) acc[rr] += red[t * 256 + rr * 64 + lane];
+  if (n >= C2 || b >= B) return;
+  const float bn = b2[n];
+  float v[4] = {acc[0] + bn, acc[1] + bn, acc[2] + bn, acc[3] + bn};
+  float o;
+  uint8_t cd;
+  relu_pool4(v, o, cd);
+  const int oi = b * F1IN + n * 16 + t * 4 + (lane >> 4);
+  a2p[oi] = o;
+  code2[oi] = cd;
+}
+
 // ---------------------------------------------------------------- F3 ----
 struct EpiBiasRelu {
   const float* bias; float* out; int ld; bool relu;
@@ -1074,10 +1247,14 @@ static SgdArgs sgd_args(const float* lr, float mom, float wd, float gscale, int 
 PTO_API int pto_conv12_fwd_lazy(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
                                 float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B, const long long* bidx,
                                 const float* g1f, const float* m1f, int bias_off, const int* pending, const float* lr,
-                                float mom, float wd, float gscale, int nesterov, hipStream_t s) {
+                                float mom, float wd, float gscale, int nesterov, int version, hipStream_t s) {
   LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off};
-  hipLaunchKernelGGL(k_conv12_fwd, dim3(B * 4), dim3(256), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B, bidx,
-                     lz);
+  if (version == 2)
+    hipLaunchKernelGGL(k_conv12_fwd2, dim3(B * 4), dim3(512), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B,
+                       bidx, lz);
+  else
+    hipLaunchKernelGGL(k_conv12_fwd, dim3(B * 4), dim3(256), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B,
+                       bidx, lz);
   LAUNCH_CHECK();
 }
 

@@ -119,6 +119,7 @@ class FusedMnistTrainer:
         self.fused_opt = bool(fused_opt) and not self.ddp and not self.fuse_fc
         self.pending = torch.zeros(1, device=device, dtype=torch.int32)  # conv1 update owed
         self.batch_snap = torch.zeros(1, device=device, dtype=torch.int64)  # cursor seen by this step's B1
+        self.conv12_version = int(os.environ.get("PTO_CONV12", "2"))  # 2: 512-thread F1+F2 launch
         self._c1 = offs["conv1.weight"][0]
         self._c1_bias = offs["conv1.bias"][0] - self._c1
 
@@ -193,7 +194,7 @@ class FusedMnistTrainer:
                                     P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
                                     self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi,
                                     self.grads[self._c1:].data_ptr(), self.mom[self._c1:].data_ptr(), self._c1_bias,
-                                    self.pending.data_ptr(), *o, s), "conv12_fwd_lazy")
+                                    self.pending.data_ptr(), *o, self.conv12_version, s), "conv12_fwd_lazy")
             c(L.pto_linear_fwd(self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
                                self.h1.data_ptr(), B, 500, 800, 1, s), "fc1_fwd")
             c(L.pto_fc2_ce_commit(self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),

@@ -15,19 +15,32 @@ def rel(a, b):
     return ((a - b).abs().max() / b.abs().max()).item()
 
 
-def test_unrolled_graph_matches_single_steps():
+@pytest.mark.parametrize("B,tol", [(4, 0.0), (64, 2e-3)])
+def test_unrolled_graph_matches_single_steps(B, tol):
+    """U-step graph replays walk the same trajectory as single steps.  At
+    B=4 every fp32-atomic gradient address receives exactly one add (conv2
+    wgrad chunks are 7 samples, conv1 chunks 4), so the step is bitwise
+    deterministic and the two must agree exactly.  At B=64 the atomics'
+    arrival order varies run to run and a ReLU at the edge can flip, which
+    amplifies last-bit differences chaotically over 21 steps; there the
+    check is a loose trajectory check."""
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
 
     dev = torch.device("cuda", 0)
-    a = FusedMnistTrainer(dev, dataset_size=64 * 12, seed=2, unroll=8)
-    b = FusedMnistTrainer(dev, dataset_size=64 * 12, seed=2, unroll=1)
+    a = FusedMnistTrainer(dev, batch_size=B, dataset_size=B * 12, seed=2, unroll=8)
+    b = FusedMnistTrainer(dev, batch_size=B, dataset_size=B * 12, seed=2, unroll=1)
     a.run(21)  # 2 unrolled replays + 5 single steps
     for _ in range(21):
         b.step()
     torch.cuda.synchronize()
     assert a.steps_done == b.steps_done == 21
     assert int(a.batch_idx.item()) == int(b.batch_idx.item()) == 21 % 12
-    assert rel(a.params, b.params) < 1e-5
+    if tol == 0.0:
+        assert torch.equal(a.params, b.params)
+        assert torch.equal(a.mom, b.mom)
+    else:
+        assert rel(a.params, b.params) < tol
+        assert abs(a.last_loss() - b.last_loss()) < 1e-2
 
 
 def _captured_ddp_worker(port, q):
@@ -73,13 +86,15 @@ def test_fused_optimizer_schedule_matches_sgd_launch(graph, unroll):
     parameters, momentum and batch cursor of the separate SGD launch at every
     point the host can observe them (params / state_dict / evaluate),
     including an LR change and a checkpoint reload mid-run.  (Not bitwise:
-    the conv weight grads are fp32 atomics, so two runs of either schedule
-    differ in the last bits; a missed or doubled conv1 update would be off by
-    ~lr*grad, orders of magnitude above the tolerance.)"""
+    the schedules evaluate the same update in a different op order; a missed
+    or doubled conv1 update would be off by ~lr*grad, orders of magnitude
+    above the tolerance.)"""
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
 
     dev = torch.device("cuda", 0)
-    kw = dict(dataset_size=64 * 9, seed=4, graph=graph, unroll=unroll, weight_decay=1e-4)
+    # B=4: one fp32-atomic add per gradient address (see the unroll test),
+    # so neither schedule has run-to-run noise to amplify
+    kw = dict(batch_size=4, dataset_size=4 * 9, seed=4, graph=graph, unroll=unroll, weight_decay=1e-4)
     a = FusedMnistTrainer(dev, fused_opt=True, **kw)
     b = FusedMnistTrainer(dev, fused_opt=False, **kw)
     assert a.fused_opt and not b.fused_opt

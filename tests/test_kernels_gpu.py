@@ -68,6 +68,40 @@ def test_conv2_relu_pool(B):
     assert rel_err(gx, gxr) < 1e-4
 
 
+@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("B", [64, 3])
+def test_conv12_fused_forward(version, B):
+    """conv1+conv2 (+bias/ReLU/pool) in one launch vs torch fp32; both
+    launch layouts; deterministic run to run."""
+    from pytorch_operator_1_amd.ops import _lib
+
+    L = _lib.lib()
+    torch.manual_seed(2)
+    x = torch.randn(B, 1, 28, 28, device=DEV)
+    w1 = torch.randn(20, 1, 5, 5, device=DEV) * 0.2
+    b1 = torch.randn(20, device=DEV) * 0.1
+    w2 = torch.randn(50, 20, 5, 5, device=DEV) * 0.05
+    b2 = torch.randn(50, device=DEV) * 0.1
+    a1r = F.max_pool2d(F.relu(F.conv2d(x, w1, b1)), 2, 2)
+    a2r = F.max_pool2d(F.relu(F.conv2d(a1r, w2, b2)), 2, 2)
+    outs = []
+    for _ in range(2):
+        a1p = torch.full((B * 2880,), float("nan"), device=DEV)
+        a2p = torch.full((B * 800,), float("nan"), device=DEV)
+        c1 = torch.empty(B * 2880, dtype=torch.uint8, device=DEV)
+        c2 = torch.empty(B * 800, dtype=torch.uint8, device=DEV)
+        _lib.check(L.pto_conv12_fwd_lazy(x.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
+                                         a1p.data_ptr(), c1.data_ptr(), a2p.data_ptr(), c2.data_ptr(), B, None, None,
+                                         None, 0, None, None, 0.0, 0.0, 1.0, 0, version, _lib.stream_ptr()), "conv12")
+        torch.cuda.synchronize()
+        outs.append((a1p.clone(), a2p.clone(), c1.clone(), c2.clone()))
+    a1p, a2p, c1, c2 = outs[0]
+    assert rel_err(a1p.view(B, 20, 12, 12), a1r) < 1e-5
+    assert rel_err(a2p.view(B, 50, 4, 4), a2r) < 1e-5
+    for u, v in zip(outs[0], outs[1]):
+        assert torch.equal(u, v)
+
+
 @pytest.mark.parametrize("M,N,K,relu", [(64, 500, 800, True), (64, 10, 500, False), (33, 70, 129, True),
                                         (1, 16, 4, False)])
 def test_linear(M, N, K, relu):
