@@ -51,6 +51,9 @@ def parse_args(argv=None):
     p.add_argument("--impl", choices=["fused", "eager"], default=None)
     p.add_argument("--synthetic", action="store_true", default=True)
     p.add_argument("--data", default=None, help="optional .npz with x_train/y_train/x_test/y_test (no pickle)")
+    p.add_argument("--data-root", default=os.environ.get("PTO_DATA_ROOT", "../data"),
+                   help="IDX files in torchvision's layout (<root>/<dataset>/raw/*-ubyte[.gz]), read if present")
+    p.add_argument("--dataset", default="FashionMNIST", help="dataset directory name under --data-root")
     p.add_argument("--train-size", type=int, default=60000)
     p.add_argument("--test-size", type=int, default=10000)
     p.add_argument("--sampler", action="store_true", help="DistributedSampler: shard the data over ranks")
@@ -79,20 +82,33 @@ class Metrics:
 
 
 def load_data(args, device, rank):
+    """Real data when available (``--data`` .npz, or the reference's
+    FashionMNIST IDX files under ``--data-root``), normalised like the
+    reference (``ToTensor`` + ``Normalize((0.1307,), (0.3081,))``,
+    examples/mnist/mnist.py:119-131); synthetic HBM-resident data otherwise."""
+    mean, std = 0.1307, 0.3081
+
+    def prep(x):
+        t = torch.from_numpy(x.astype("float32"))
+        if t.max() > 1.5:
+            t = t / 255.0
+        return ((t - mean) / std).reshape(-1, 1, 28, 28).to(device)
+
     if args.data:
         import numpy as np
 
         z = np.load(args.data, allow_pickle=False)
-        mean, std = 0.1307, 0.3081
-
-        def prep(x):
-            t = torch.from_numpy(x.astype("float32"))
-            if t.max() > 1.5:
-                t = t / 255.0
-            return ((t - mean) / std).reshape(-1, 1, 28, 28).to(device)
-
         return (prep(z["x_train"]), torch.from_numpy(z["y_train"]).long().to(device),
                 prep(z["x_test"]), torch.from_numpy(z["y_test"]).long().to(device))
+    if args.data_root:
+        from ..utils import idx
+
+        d = idx.find_dataset(args.data_root, args.dataset)
+        if d is not None:
+            (xtr, ytr), (xte, yte) = idx.load_split(d, True), idx.load_split(d, False)
+            if rank == 0:
+                print(f"[pto] {args.dataset} from {d}: {len(ytr)} train / {len(yte)} test", flush=True)
+            return (prep(xtr), torch.from_numpy(ytr).to(device), prep(xte), torch.from_numpy(yte).to(device))
     # reference-equivalent: every rank uses the same seed/order (no sampler)
     xtr, ytr = synthetic_mnist(args.train_size, device, seed=args.seed)
     xte, yte = synthetic_mnist(args.test_size, device, seed=args.seed + 7)
