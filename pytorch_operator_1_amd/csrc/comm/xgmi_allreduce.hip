@@ -32,9 +32,20 @@
 // Two independent "channels" (flag sets + epochs) let two buckets be in
 // flight at once on different streams (fc bucket overlapped with the conv
 // backward, then the conv bucket).
+//
+// Optimizer epilogue (k_xgmi_allreduce<true>): stage 2 does not store the
+// reduced gradient; it applies SGD-momentum to the local parameters and
+// momentum with it (same element formula as the multi-tensor SGD launch,
+// sgd_f32.h) and zeroes the local gradient from `zero_from` on (the
+// atomically accumulated range).  The DDP step then needs no optimizer
+// launch, and the fc bucket's update runs on the side stream under the conv
+// backward (which reads no fc parameter).  Zeroing is safe in stage 2: every
+// peer read this rank's gradient in its stage 1, before barrier 2.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
+
+#include "sgd_f32.h"
 
 #define PTO_API extern "C" __attribute__((visibility("default")))
 
@@ -85,10 +96,23 @@ __device__ __forceinline__ bool block_barrier(const ArPeers& P, int chan, int ph
   return ok;
 }
 
+// Fused optimizer epilogue of the all-reduce: own parameters/momentum (same
+// flat layout as the gradient buffer), hyper-parameters, zero range, and an
+// optional batch cursor advanced once the update is done.
+struct ArSgd {
+  float* p;
+  float* m;
+  SgdArgs a;
+  long long zero_from;  // float index: own gradient zeroed from here on
+  long long* bidx;      // nullptr: no cursor
+  long long nbatches;
+};
+
 // n4 float4 elements starting at float offset `off` of every rank's buffers.
+template <bool SGD>
 __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce(const ArPeers* __restrict__ peers, long long off,
                                                                long long n4, int rank, int world, int chan,
-                                                               uint32_t* __restrict__ epochs, int* err) {
+                                                               uint32_t* __restrict__ epochs, int* err, ArSgd f) {
   __shared__ uint32_t s_epoch;
   const ArPeers P = *peers;
   if (threadIdx.x == 0) s_epoch = epochs[chan * AR_MAX_BLOCKS + blockIdx.x] + 1;
@@ -119,7 +143,8 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce(const ArPeers* __
     }
   }
   block_barrier(P, chan, 1, rank, world, e, err);
-  // stage 2: gather every chunk into my input
+  // stage 2: gather every chunk into my input (or: update my parameters)
+  const float lr = SGD ? *f.a.lr : 0.f;
   for (long long j = (long long)blockIdx.x * AR_THREADS + threadIdx.x; j < cs; j += stride) {
     float4 v[AR_MAX_RANKS];
 #pragma unroll
@@ -127,9 +152,25 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce(const ArPeers* __
       if (q < world && (long long)q * cs + j < n4) v[q] = reinterpret_cast<const float4*>(P.tmp[q] + off)[q * cs + j];
 #pragma unroll
     for (int q = 0; q < AR_MAX_RANKS; ++q)
-      if (q < world && (long long)q * cs + j < n4) reinterpret_cast<float4*>(P.in[rank] + off)[q * cs + j] = v[q];
+      if (q < world && (long long)q * cs + j < n4) {
+        if constexpr (SGD) {
+          const long long i = off + 4 * (q * cs + j);
+          float4 pv = *reinterpret_cast<float4*>(f.p + i);
+          float4 mv = *reinterpret_cast<float4*>(f.m + i);
+          sgd_elem(pv.x, v[q].x, mv.x, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+          sgd_elem(pv.y, v[q].y, mv.y, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+          sgd_elem(pv.z, v[q].z, mv.z, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+          sgd_elem(pv.w, v[q].w, mv.w, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+          *reinterpret_cast<float4*>(f.p + i) = pv;
+          *reinterpret_cast<float4*>(f.m + i) = mv;
+          if (i >= f.zero_from) *reinterpret_cast<float4*>(P.in[rank] + i) = float4{0.f, 0.f, 0.f, 0.f};
+        } else {
+          reinterpret_cast<float4*>(P.in[rank] + off)[q * cs + j] = v[q];
+        }
+      }
   }
   if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blockIdx.x] = e;
+  if (SGD && f.bidx && blockIdx.x == 0 && threadIdx.x == 0) *f.bidx = (*f.bidx + 1) % f.nbatches;
 }
 
 }  // namespace
@@ -183,8 +224,38 @@ PTO_API int pto_ar_allreduce(const void* peers, long long off, long long n, int 
       rank >= world)
     return -1;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(k_xgmi_allreduce, dim3(pto_ar_blocks(n, world)), dim3(AR_THREADS), 0, s,
+  hipLaunchKernelGGL(k_xgmi_allreduce<false>, dim3(pto_ar_blocks(n, world)), dim3(AR_THREADS), 0, s,
                      reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,
-                     reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err));
+                     reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), ArSgd{});
+  return (int)hipGetLastError();
+}
+
+// All-reduce + SGD-momentum epilogue over the same range: p/m are this rank's
+// flat parameter/momentum buffers (gradient layout, 16-byte aligned); the
+// reduced gradient is scaled by gscale (1/world: DDP's mean), consumed by
+// the update and not stored; the local gradient is zeroed from float index
+// zero_from on; bidx (optional) advances mod nbatches after the update.
+PTO_API int pto_ar_allreduce_sgd(const void* peers, long long off, long long n, int rank, int world, int chan,
+                                 void* epochs, void* err, float* p, float* m, const float* lr, float mom, float wd,
+                                 float gscale, int nesterov, long long zero_from, long long* bidx,
+                                 long long nbatches, hipStream_t s) {
+  if (n % 4 || off % 4 || world < 2 || world > AR_MAX_RANKS || chan < 0 || chan >= AR_CHANNELS || rank < 0 ||
+      rank >= world || !p || !m || !lr || ((((uintptr_t)p) | ((uintptr_t)m)) & 15) || (bidx && nbatches < 1))
+    return -1;
+  if (n == 0) return 0;
+  ArSgd f;
+  f.p = p;
+  f.m = m;
+  f.a.lr = lr;
+  f.a.mom = mom;
+  f.a.wd = wd;
+  f.a.gscale = gscale;
+  f.a.nesterov = nesterov;
+  f.zero_from = zero_from;
+  f.bidx = bidx;
+  f.nbatches = nbatches;
+  hipLaunchKernelGGL(k_xgmi_allreduce<true>, dim3(pto_ar_blocks(n, world)), dim3(AR_THREADS), 0, s,
+                     reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,
+                     reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), f);
   return (int)hipGetLastError();
 }

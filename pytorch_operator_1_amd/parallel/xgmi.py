@@ -97,6 +97,29 @@ class XgmiAllReduce:
         _lib.check(_lib.lib().pto_ar_allreduce(self.peers.data_ptr(), offset, n, self.rank, self.world, chan,
                                                self.epochs.data_ptr(), self.err.data_ptr(), s), "xgmi_allreduce")
 
+    def allreduce_sgd_(self, offset: int, n: int, params: torch.Tensor, mom: torch.Tensor, lr_dev: torch.Tensor,
+                       momentum: float, weight_decay: float, gscale: float, nesterov: bool, zero_from: int,
+                       cursor: torch.Tensor | None = None, n_batches: int = 1, chan: int = 0, stream=None):
+        """All-reduce ``buf[offset:offset+n]`` and apply SGD-momentum with
+        the (``gscale``-scaled) result to ``params``/``mom`` (flat buffers in
+        the gradient layout) inside the same launch; the local gradient is
+        zeroed from ``zero_from`` on and ``cursor`` (int64 device scalar) is
+        advanced mod ``n_batches`` after the update."""
+        if n % 4 or offset % 4:
+            raise ValueError("XgmiAllReduce: offset and length must be multiples of 4 floats")
+        if offset + n > self.buf.numel():
+            raise ValueError("XgmiAllReduce: range outside the registered buffer")
+        for t in (params, mom):
+            if t.dtype != torch.float32 or t.numel() != self.buf.numel() or t.device != self.device:
+                raise ValueError("XgmiAllReduce: params/momentum must match the gradient buffer")
+        s = (stream or torch.cuda.current_stream(self.device)).cuda_stream
+        cur = cursor.data_ptr() if cursor is not None else None
+        _lib.check(_lib.lib().pto_ar_allreduce_sgd(self.peers.data_ptr(), offset, n, self.rank, self.world, chan,
+                                                   self.epochs.data_ptr(), self.err.data_ptr(), params.data_ptr(),
+                                                   mom.data_ptr(), lr_dev.data_ptr(), momentum, weight_decay, gscale,
+                                                   int(nesterov), zero_from, cur, n_batches, s),
+                   "xgmi_allreduce_sgd")
+
     def check(self):
         e = int(self.err.item())
         if e:

@@ -120,6 +120,8 @@ class FusedMnistTrainer:
         self.pending = torch.zeros(1, device=device, dtype=torch.int32)  # conv1 update owed
         self.batch_snap = torch.zeros(1, device=device, dtype=torch.int64)  # cursor seen by this step's B1
         self.conv12_version = int(os.environ.get("PTO_CONV12", "2"))  # 2: 512-thread F1+F2 launch
+        # xGMI DDP step: SGD applied by the all-reduce kernels' epilogue
+        self.ar_fused_sgd = os.environ.get("PTO_AR_FUSED_SGD", "1") == "1"
         self._c1 = offs["conv1.weight"][0]
         self._c1_bias = offs["conv1.bias"][0] - self._c1
 
@@ -165,7 +167,8 @@ class FusedMnistTrainer:
             raise RuntimeError(f"xGMI all-reduce failed verification: {tune}")
         if self.comm == "xgmi" or tune["use_xgmi"]:
             self._xgmi = ar
-            self.comm_info = dict(tune, transport="xgmi")
+            self.comm_info = dict(tune, transport="xgmi",
+                                  optimizer="allreduce-epilogue" if self.ar_fused_sgd else "sgd-launch")
         else:
             ar.close()
             self.comm_info = dict(tune, transport="rccl")
@@ -309,11 +312,23 @@ class FusedMnistTrainer:
     def _xgmi_step(self):
         """fc bucket all-reduced by the xGMI kernel on a side stream while
         the conv backward runs, conv bucket after it; the optimizer joins
-        both.  Pure stream work: capturable into one graph."""
+        both — by default inside the two all-reduce launches (SGD epilogue,
+        ``PTO_AR_FUSED_SGD=0``: separate launch).  Pure stream work:
+        capturable into one graph."""
         split = self._split()
         cur = torch.cuda.current_stream(self.device)
         self.forward_fc_backward()
         self._side.wait_stream(cur)
+        if self.ar_fused_sgd:  # the update rides in the all-reduce launches: no optimizer launch
+            lr, mom, wd, gs, nes = self._opt_args()
+            kw = dict(params=self._params, mom=self.mom, lr_dev=self.lr_dev, momentum=mom, weight_decay=wd,
+                      gscale=gs, nesterov=bool(nes), zero_from=split)
+            self._xgmi.allreduce_sgd_(0, split, chan=0, stream=self._side, **kw)
+            self.conv_backward()
+            self._xgmi.allreduce_sgd_(split, self.numel - split, chan=1, cursor=self.batch_idx,
+                                      n_batches=self.n_batches, **kw)
+            cur.wait_stream(self._side)
+            return
         self._xgmi.allreduce_(0, split, chan=0, stream=self._side)
         self.conv_backward()
         self._xgmi.allreduce_(split, self.numel - split, chan=1)

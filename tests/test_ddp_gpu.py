@@ -27,6 +27,9 @@ def _free_port():
 
 def _worker(rank, world, port, q, comm):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    if comm == "xgmi-sgd-launch":  # all-reduce kernel without the optimizer epilogue + separate SGD launch
+        comm = "xgmi"
+        os.environ["PTO_AR_FUSED_SGD"] = "0"
     import torch.distributed as dist
 
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
@@ -39,15 +42,19 @@ def _worker(rank, world, port, q, comm):
     for _ in range(STEPS):
         tr.step()
     torch.cuda.synchronize()
+    assert int(tr.batch_idx.item()) == STEPS % (N // 64)
+    assert float(tr.grads[tr._split():].abs().max()) == 0.0  # atomically accumulated range zeroed
     q.put((rank, tr.params.cpu()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("comm", ["rccl", "xgmi"])
+@pytest.mark.parametrize("comm", ["rccl", "xgmi", "xgmi-sgd-launch"])
 def test_fused_ddp_two_ranks_matches_reference(comm):
     """comm=rccl: host collectives (gloo here) between split graphs;
-    comm=xgmi: peer-memory all-reduce kernel inside the whole-step graph."""
+    comm=xgmi: peer-memory all-reduce kernels with the SGD epilogue inside
+    the whole-step graph (no optimizer launch); xgmi-sgd-launch: plain
+    all-reduce kernels + the multi-tensor SGD launch."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -114,3 +114,97 @@ def test_xgmi_allreduce_exact(world):
     print("autotune", res[0][3])
     for p in ps:
         assert p.exitcode == 0
+
+
+def _sgd_worker(rank, world, port, q):
+    """All-reduce + SGD epilogue vs (sum of the ranks' grads, scaled) fed to
+    the same SGD formula in torch; two buckets on two streams, weight decay,
+    nesterov, device LR, zero range and batch cursor; graph replay."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch.distributed as dist
+
+        from pytorch_operator_1_amd.parallel.xgmi import XgmiAllReduce
+
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        n, split = 431_296, 405_632
+        lr, mom, wd = 0.05, 0.9, 1e-3
+        buf = torch.zeros(n, device=dev)
+        ar = XgmiAllReduce(buf)
+        g0 = torch.Generator(device=dev).manual_seed(7)
+        p = torch.randn(n, generator=g0, device=dev)  # same start on every rank
+        m = torch.zeros(n, device=dev)
+        pr, mr = p.clone(), m.clone()
+        lr_dev = torch.tensor([lr], device=dev)
+        cursor = torch.zeros(1, dtype=torch.int64, device=dev)
+        side = torch.cuda.Stream(dev)
+
+        def step():
+            kw = dict(params=p, mom=m, lr_dev=lr_dev, momentum=mom, weight_decay=wd, gscale=1.0 / world,
+                      nesterov=True, zero_from=split)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            ar.allreduce_sgd_(0, split, chan=0, stream=side, **kw)
+            ar.allreduce_sgd_(split, n - split, chan=1, cursor=cursor, n_batches=5, **kw)
+            torch.cuda.current_stream(dev).wait_stream(side)
+
+        def ref(it):
+            d = _expected(n, world, it, dev) / world + wd * pr
+            mr.mul_(mom).add_(d)
+            pr.sub_(lr * (d + mom * mr))
+
+        worst, zero_ok = 0.0, True
+        for it in range(6):
+            _fill(buf, rank, it)
+            step()
+            torch.cuda.synchronize(dev)
+            ref(it)
+            worst = max(worst, (p - pr).abs().max().item(), (m - mr).abs().max().item())
+            zero_ok &= float(buf[split:].abs().max()) == 0.0
+        # graph capture + replay
+        _fill(buf, rank, 50)
+        s = torch.cuda.Stream(dev)
+        dist.barrier()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            step()
+        torch.cuda.synchronize(dev)
+        for it in range(60, 63):
+            _fill(buf, rank, it)
+            torch.cuda.synchronize(dev)
+            g.replay()
+            torch.cuda.synchronize(dev)
+            ref(it)
+            worst = max(worst, (p - pr).abs().max().item(), (m - mr).abs().max().item())
+        ar.check()
+        allv = [None] * world
+        dist.all_gather_object(allv, p.cpu())
+        same = all(torch.equal(allv[0], v) for v in allv)
+        cur = int(cursor.item())
+        ar.close()
+        dist.destroy_process_group()
+        q.put((rank, worst, same and zero_ok, cur))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), False, None))
+        raise
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_allreduce_sgd_epilogue(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_sgd_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+    for rank, worst, ok, cur in res:
+        assert not isinstance(worst, str), worst
+        assert worst < 1e-4, (rank, worst)
+        assert ok
+        assert cur == 9 % 5  # 6 eager + 3 replayed steps (the capture itself does not run)
+    for p in ps:
+        assert p.exitcode == 0
