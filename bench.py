@@ -91,6 +91,10 @@ def main(argv=None):
     sync()
     t0 = time.perf_counter()
     run(args.steps)  # exactly K optimizer steps
+    # the fused-optimizer schedule applies conv1's update of step i inside
+    # step i+1's launches: commit the last one inside the timed region so it
+    # holds K complete updates
+    getattr(trainer, "flush", lambda: None)()
     sync()
     pdist.barrier(device)
     sync()

@@ -211,9 +211,11 @@ class FusedMnistTrainer:
                                G["fc1.bias"].data_ptr(), G["fc2.weight"].data_ptr(), G["fc2.bias"].data_ptr(),
                                self.da2p.data_ptr(), B, bi, self.n_batches, self.pending.data_ptr(), s), "fc_bwd_adv")
             return
-        c(L.pto_conv12_fwd(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
-                           P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
-                           self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi, s), "conv12_fwd")
+        # same F1+F2 launch without an owed update (pending = nullptr)
+        c(L.pto_conv12_fwd_lazy(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
+                                P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
+                                self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi, None, None,
+                                0, None, None, 0.0, 0.0, 1.0, 0, self.conv12_version, s), "conv12_fwd")
         if self.fuse_fc:  # fc1 + (last block per 16 rows) fc2/CE/dlogits/dh1 in one launch
             c(L.pto_fc12_ce(self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
                             self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
