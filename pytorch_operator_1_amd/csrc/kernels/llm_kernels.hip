@@ -366,6 +366,57 @@ inline unsigned grid_for(long long work, int per_block = NT) {
   return (unsigned)g;
 }
 
+// ---------------------------------------------------------------- transpose
+// out[c][r] = in[r][c] for a [rows x cols] bf16 matrix (row strides ld_in /
+// ld_out).  Keeps the transposed weight copies W^T of the Llama linears
+// that make every dgrad GEMM K-contiguous (dX = dY (W^T)^T, the forward's
+// operand layout).  64x64 tile per 256-thread block through LDS.  Global
+// loads AND stores are 8 lanes per 128-byte row (16 B each).  LDS image:
+// 128-B rows, 16-B chunk c of row r stored at chunk c ^ ((r >> 3) & 7), so
+// the column reads (8 consecutive rows 8k..8k+7 of one column per lane,
+// k = lane & 7) of a wave fall on 32 distinct banks.
+constexpr int TP = 64;
+__device__ __forceinline__ int tp_swz(int r, int ch) { return r * TP + 8 * (ch ^ ((r >> 3) & 7)); }
+
+__global__ __launch_bounds__(256) void k_transpose_bf16(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                        long long rows, long long cols, long long ld_in,
+                                                        long long ld_out) {
+  __shared__ __attribute__((aligned(16))) uint16_t t[TP * TP];
+  const long long r0 = (long long)blockIdx.y * TP, c0 = (long long)blockIdx.x * TP;
+  const int tid = threadIdx.x, lr = tid >> 3, ch = tid & 7;
+  const bool full = r0 + TP <= rows && c0 + TP <= cols && (ld_in & 7) == 0 && (ld_out & 7) == 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = lr + 32 * h;
+    uint4 v = {0u, 0u, 0u, 0u};
+    if (full) {
+      v = *reinterpret_cast<const uint4*>(in + (r0 + r) * ld_in + c0 + 8 * ch);
+    } else if (r0 + r < rows) {
+      uint16_t e[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e[j] = (c0 + 8 * ch + j < cols) ? in[(r0 + r) * ld_in + c0 + 8 * ch + j] : (uint16_t)0;
+      v = *reinterpret_cast<uint4*>(e);
+    }
+    *reinterpret_cast<uint4*>(t + tp_swz(r, ch)) = v;
+  }
+  __syncthreads();
+  // output row oc (= input column), chunk k = input rows 8k..8k+7
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int oc = lr + 32 * h, k = ch;
+    uint16_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = t[tp_swz(8 * k + j, oc >> 3) + (oc & 7)];
+    if (full) {
+      *reinterpret_cast<uint4*>(out + (c0 + oc) * ld_out + r0 + 8 * k) = *reinterpret_cast<uint4*>(e);
+    } else if (c0 + oc < cols) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (r0 + 8 * k + j < rows) out[(c0 + oc) * ld_out + r0 + 8 * k + j] = e[j];
+    }
+  }
+}
+
 }  // namespace
 
 #define PTO_API extern "C" __attribute__((visibility("default")))
@@ -439,5 +490,18 @@ PTO_API int pto_ce_bwd(void* logits, const long long* labels, const float* lse, 
   if (M <= 0) return 0;
   hipLaunchKernelGGL(k_ce_bwd, dim3((unsigned)M), dim3(NT), 0, s, (uint16_t*)logits, labels, lse, scale, V,
                      ignore_index);
+  return (int)hipGetLastError();
+}
+
+// out = in^T (bf16, [rows x cols] -> [cols x rows]); 16-byte aligned fast
+// path for whole 64x64 tiles, element-wise edges.
+PTO_API int pto_transpose_bf16(const void* in, void* out, long long rows, long long cols, long long ld_in,
+                               long long ld_out, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (ld_in < cols || ld_out < rows || (cols + TP - 1) / TP > 0x7fffffff || (rows + TP - 1) / TP > 65535) return -1;
+  if ((((uintptr_t)in) | ((uintptr_t)out)) & 15) return -1;
+  dim3 grid((unsigned)((cols + TP - 1) / TP), (unsigned)((rows + TP - 1) / TP));
+  hipLaunchKernelGGL(k_transpose_bf16, grid, dim3(256), 0, s, reinterpret_cast<const uint16_t*>(in),
+                     reinterpret_cast<uint16_t*>(out), rows, cols, ld_in, ld_out);
   return (int)hipGetLastError();
 }

@@ -117,15 +117,15 @@ class LlamaBlock(nn.Module):
             y = llm.rmsnorm(h, self.attn_norm, c.norm_eps)
         else:
             h, y = llm.add_rmsnorm(h, delta, self.attn_norm, c.norm_eps)
-        qkv = F.linear(y, self.wqkv.weight)
+        qkv = _lin(y, self.wqkv)
         qkv = llm.rope_(qkv, rope[0], rope[1], S, c.n_heads + c.n_kv_heads, c.head_dim)
         if ATTN_IMPL == "hip" and llm.flash_attention_supported(S, c.n_heads, c.n_kv_heads, c.head_dim):
             ctx = llm.flash_attention(qkv, B, S, c.n_heads, c.n_kv_heads)  # [B*S, H*128], no transposes
         else:
             ctx = self._attend(qkv, B, S)
-        attn = F.linear(ctx, self.wo.weight)
+        attn = _lin(ctx, self.wo)
         h, y = llm.add_rmsnorm(h, attn, self.ffn_norm, c.norm_eps)
-        mlp = F.linear(llm.swiglu(F.linear(y, self.w13.weight)), self.w2.weight)
+        mlp = _lin(llm.swiglu(_lin(y, self.w13)), self.w2)
         return h, mlp
 
     def forward_torch(self, h, delta, rope, B, S):
@@ -146,6 +146,17 @@ class LlamaBlock(nn.Module):
         g, u = F.linear(y, self.w13.weight).chunk(2, dim=-1)
         mlp = F.linear(F.silu(g) * u, self.w2.weight)
         return h, mlp
+
+
+def _lin(x, mod: nn.Linear):
+    """Bias-free linear; with a transposed weight copy attached
+    (:meth:`Llama.enable_transposed_dgrad`) the input gradient uses it."""
+    wt = getattr(mod, "weight_t", None)
+    if wt is None:
+        return F.linear(x, mod.weight)
+    from ..ops import llm
+
+    return llm.linear_tw(x, mod.weight, wt)
 
 
 def _rmsnorm_ref(x, w, eps):
@@ -192,6 +203,31 @@ class Llama(nn.Module):
             self._rope[key] = rope_tables(S, self.cfg.head_dim, self.cfg.rope_theta, device, self.cfg.rope_scaling)
         return self._rope[key]
 
+    def linear_modules(self):
+        mods = [m for blk in self.layers for m in (blk.wqkv, blk.wo, blk.w13, blk.w2)]
+        return mods + ([self.lm_head] if self.lm_head is not None else [])
+
+    @torch.no_grad()
+    def enable_transposed_dgrad(self):
+        """Keep ``W^T`` next to every linear weight (bf16, +1x weight memory:
+        16 GB for Llama-3-8B) so each dgrad GEMM reads K-contiguous operands.
+        The copies must be refreshed after every weight update
+        (:meth:`refresh_transposed`)."""
+        for m in self.linear_modules():
+            if getattr(m, "weight_t", None) is None:
+                w = m.weight
+                m.weight_t = torch.empty(w.shape[1], w.shape[0], device=w.device, dtype=w.dtype)
+        self.refresh_transposed()
+
+    @torch.no_grad()
+    def refresh_transposed(self):
+        from ..ops import llm
+
+        for m in self.linear_modules():
+            wt = getattr(m, "weight_t", None)
+            if wt is not None:
+                llm.transpose_into(m.weight, wt)
+
     def _head_weight(self):
         return self.tok_emb.weight if self.lm_head is None else self.lm_head.weight
 
@@ -213,7 +249,7 @@ class Llama(nn.Module):
             from ..ops import llm
 
             _, y = llm.add_rmsnorm(h, delta, self.norm, self.cfg.norm_eps)
-            logits = F.linear(y, self._head_weight())
+            logits = F.linear(y, self._head_weight()) if self.lm_head is None else _lin(y, self.lm_head)
             if labels is None:
                 return logits.view(B, S, -1)
             return llm.cross_entropy(logits, labels.reshape(-1))

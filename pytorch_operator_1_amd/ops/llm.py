@@ -243,3 +243,50 @@ def flash_attention(qkv, B: int, S: int, H: int, Hkv: int):
     ``[B*S, (H + 2*Hkv)*128]`` (q heads, then k, then v heads per row) to
     ``O [B*S, H*128]`` — the layout the output projection consumes."""
     return _FlashAttention.apply(qkv, B, S, H, Hkv)
+
+
+def transpose_into(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    """``dst[:] = src.t()`` for 2-D bf16 HIP matrices (LDS-tiled kernel);
+    plain copy on CPU tensors (tests)."""
+    if src.dim() != 2 or dst.shape != (src.shape[1], src.shape[0]):
+        raise ValueError(f"transpose_into: {tuple(src.shape)} -> {tuple(dst.shape)}")
+    if not src.is_cuda:
+        dst.copy_(src.t())
+        return dst
+    src, dst_c = _req(src, "transpose_into"), dst
+    if not dst.is_contiguous() or dst.dtype != torch.bfloat16:
+        raise ValueError("transpose_into: contiguous bf16 destination required")
+    _lib.check(_lib.lib().pto_transpose_bf16(src.data_ptr(), dst_c.data_ptr(), src.shape[0], src.shape[1],
+                                             src.stride(0), dst_c.stride(0), _lib.stream_ptr(src.device)),
+               "transpose_bf16")
+    return dst
+
+
+class _LinearTW(torch.autograd.Function):
+    """``y = x W^T`` whose input gradient is computed from the transposed
+    copy ``Wt = W^T`` (``dX = dY Wt^T``): both dgrad operands are then
+    K-contiguous, the layout the forward GEMM already uses.  hipBLASLt's
+    pick for the usual ``dY W`` (B operand N-contiguous) ran at ~1.0
+    PFLOP/s in the Llama-3-8B step vs ~1.5 for the K-contiguous one
+    (profiles/llama8b_step_rocprof.md)."""
+
+    @staticmethod
+    def forward(ctx, x, w, wt):
+        ctx.save_for_backward(x, wt)
+        return torch.nn.functional.linear(x, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wt = ctx.saved_tensors
+        dx = torch.nn.functional.linear(dy, wt) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            x2 = x.reshape(-1, x.shape[-1])
+            dw = dy.reshape(-1, dy.shape[-1]).t().mm(x2)
+        return dx, dw, None
+
+
+def linear_tw(x, w, wt):
+    """``F.linear(x, w)`` with the dgrad taken from ``wt`` (== ``w.t()``,
+    kept current by the caller after every weight update)."""
+    return _LinearTW.apply(x, w, wt)

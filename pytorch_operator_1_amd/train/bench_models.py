@@ -15,6 +15,8 @@ step (forward, backward, all-reduce, update) — nothing is skipped.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -85,6 +87,10 @@ class LlamaTrainer:
         self.batch_size, self.seq_len = batch_size, seq_len
         self.model = Llama(self.cfg, impl=impl, device=device, checkpoint=checkpoint)
         self.model.train()
+        # W^T copies for K-contiguous dgrad GEMMs (PTO_WT=0: plain F.linear backward)
+        self.transposed_dgrad = impl == "hip" and os.environ.get("PTO_WT", "1") == "1"
+        if self.transposed_dgrad:
+            self.model.enable_transposed_dgrad()
         self.bucketer = GradBucketer(self.model, bucket_mb=bucket_mb)
         self.opt = FusedAdamW(self.model.parameters(), lr=lr, betas=(0.9, 0.95), eps=1e-8,
                               weight_decay=weight_decay)
@@ -103,6 +109,8 @@ class LlamaTrainer:
         with t.phase("optimizer"):
             self.opt.step(grad_scale=self.bucketer.grad_scale, zero_grad=self.bucketer.optimizer_zeroes_grads)
             self.bucketer.release()
+            if self.transposed_dgrad:
+                self.model.refresh_transposed()
         self._loss = loss.detach()
 
     def run(self, n: int):
@@ -122,4 +130,5 @@ class LlamaTrainer:
         return {"model": f"{self.name} ({self.cfg.num_params() / 1e9:.2f}B params)",
                 "optimizer": "AdamW betas=(0.9,0.95) wd=0.1 (FusedAdamW HIP, fp32 master/m/v)",
                 "amp": "bf16 params/activations, fp32 optimizer state",
-                "checkpoint": self.model.checkpoint}
+                "checkpoint": self.model.checkpoint,
+                "dgrad": "W^T copies (K-contiguous dX GEMMs)" if self.transposed_dgrad else "F.linear"}

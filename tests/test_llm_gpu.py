@@ -166,6 +166,44 @@ def test_llama_hip_matches_torch_impl():
         assert relerr(pa.grad, pb.grad) < 5e-2, n
 
 
+@pytest.mark.parametrize("rows,cols", [(4096, 6144), (128, 64), (200, 72), (63, 130), (1, 1)])
+def test_transpose_bf16(rows, cols):
+    from pytorch_operator_1_amd.ops import llm
+
+    x = torch.randn(rows, cols, device=DEV).bfloat16()
+    out = torch.full((cols, rows), float("nan"), device=DEV, dtype=torch.bfloat16)
+    llm.transpose_into(x, out)
+    assert torch.equal(out, x.t().contiguous())
+
+
+def test_llama_transposed_dgrad_matches_plain():
+    """W^T-based dgrad: same loss, identical weight grads (same dW GEMM),
+    input-side grads equal up to GEMM accumulation order; and the copies
+    follow a weight update after refresh_transposed()."""
+    from pytorch_operator_1_amd.models.llama import Llama, synthetic_tokens
+
+    torch.manual_seed(6)
+    a = Llama("llama3-tiny", impl="hip", device=DEV)
+    b = Llama("llama3-tiny", impl="hip", device=DEV)
+    b.load_state_dict(a.state_dict())
+    b.enable_transposed_dgrad()
+    for m in b.linear_modules():
+        assert torch.equal(m.weight_t, m.weight.t())
+    tok, lab = synthetic_tokens(2, 128, a.cfg.vocab_size, DEV)
+    la, lb = a(tok, lab), b(tok, lab)
+    assert la.item() == lb.item()
+    la.backward()
+    lb.backward()
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        assert relerr(pb.grad, pa.grad) < 1e-2, n
+    with torch.no_grad():
+        for m in b.linear_modules():
+            m.weight.mul_(0.5)
+    b.refresh_transposed()
+    for m in b.linear_modules():
+        assert torch.equal(m.weight_t, m.weight.t())
+
+
 def test_llama_trainer_learns_and_native_lib_loaded():
     from pytorch_operator_1_amd.ops import _lib
     from pytorch_operator_1_amd.train.bench_models import LlamaTrainer
