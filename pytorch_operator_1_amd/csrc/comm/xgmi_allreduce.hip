@@ -33,6 +33,13 @@
 // flight at once on different streams (fc bucket overlapped with the conv
 // backward, then the conv bucket).
 //
+// Small buckets (<= AR_ONESHOT_MAX floats, e.g. MNIST's 100 KB conv bucket,
+// which sits on the step's critical path) use a one-shot variant instead:
+// barrier 1, every rank reads the WHOLE range from all ranks and reduces it
+// in rank order (bit-identical everywhere; one element per thread, kept in
+// registers), barrier 2 (nobody reads my input any more), then the local
+// write / optimizer epilogue.  One remote round trip instead of two, no tmp.
+//
 // Optimizer epilogue (k_xgmi_allreduce<true>): stage 2 does not store the
 // reduced gradient; it applies SGD-momentum to the local parameters and
 // momentum with it (same element formula as the multi-tensor SGD launch,
@@ -55,6 +62,7 @@ constexpr int AR_MAX_RANKS = 8;
 constexpr int AR_MAX_BLOCKS = 64;
 constexpr int AR_CHANNELS = 2;
 constexpr int AR_THREADS = 512;
+constexpr long long AR_ONESHOT_MAX = 65536;  // floats (256 KB): one-shot path
 constexpr long long AR_TIMEOUT_TICKS = 200000000LL;  // wall_clock64 runs at 100 MHz: 2 s
 
 struct ArPeers {
@@ -173,6 +181,60 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce(const ArPeers* __
   if (SGD && f.bidx && blockIdx.x == 0 && threadIdx.x == 0) *f.bidx = (*f.bidx + 1) % f.nbatches;
 }
 
+// One-shot variant: n4 <= gridDim.x * AR_THREADS (one float4 per thread).
+template <bool SGD>
+__global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_1shot(const ArPeers* __restrict__ peers,
+                                                                     long long off, long long n4, int rank,
+                                                                     int world, int chan,
+                                                                     uint32_t* __restrict__ epochs, int* err,
+                                                                     ArSgd f) {
+  __shared__ uint32_t s_epoch;
+  const ArPeers P = *peers;
+  if (threadIdx.x == 0) s_epoch = epochs[chan * AR_MAX_BLOCKS + blockIdx.x] + 1;
+  __syncthreads();
+  const uint32_t e = s_epoch;
+  const long long i = (long long)blockIdx.x * AR_THREADS + threadIdx.x;
+  const bool act = i < n4;
+  block_barrier(P, chan, 0, rank, world, e, err);
+  float4 a = {0.f, 0.f, 0.f, 0.f};
+  if (act) {
+    float4 v[AR_MAX_RANKS];
+#pragma unroll
+    for (int q = 0; q < AR_MAX_RANKS; ++q)
+      if (q < world) v[q] = reinterpret_cast<const float4*>(P.in[q] + off)[i];
+    a = v[0];
+#pragma unroll
+    for (int q = 1; q < AR_MAX_RANKS; ++q)
+      if (q < world) {
+        a.x += v[q].x;
+        a.y += v[q].y;
+        a.z += v[q].z;
+        a.w += v[q].w;
+      }
+  }
+  block_barrier(P, chan, 1, rank, world, e, err);  // every peer is done reading my input
+  if (act) {
+    if constexpr (SGD) {
+      const float lr = *f.a.lr;
+      const long long j = off + 4 * i;
+      float4 pv = *reinterpret_cast<float4*>(f.p + j);
+      float4 mv = *reinterpret_cast<float4*>(f.m + j);
+      sgd_elem(pv.x, a.x, mv.x, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+      sgd_elem(pv.y, a.y, mv.y, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+      sgd_elem(pv.z, a.z, mv.z, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+      sgd_elem(pv.w, a.w, mv.w, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+      *reinterpret_cast<float4*>(f.p + j) = pv;
+      *reinterpret_cast<float4*>(f.m + j) = mv;
+      if (j >= f.zero_from) *reinterpret_cast<float4*>(P.in[rank] + j) = float4{0.f, 0.f, 0.f, 0.f};
+    } else {
+      reinterpret_cast<float4*>(P.in[rank] + off)[i] = a;
+    }
+  }
+  if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blockIdx.x] = e;
+  if (SGD && f.bidx && blockIdx.x == 0 && threadIdx.x == 0) *f.bidx = (*f.bidx + 1) % f.nbatches;
+}
+
+
 }  // namespace
 
 // ---------------------------------------------------------------- host API
@@ -208,6 +270,7 @@ PTO_API int pto_ar_close_ipc_handle(void* ptr) { return (int)hipIpcCloseMemHandl
 
 // Workgroups used for n floats (identical on every rank: derived from n, W).
 PTO_API int pto_ar_blocks(long long n, int world) {
+  if (n <= AR_ONESHOT_MAX) return (int)((n / 4 + AR_THREADS - 1) / AR_THREADS);
   const long long cs = ((n / 4) + world - 1) / world;
   long long b = (cs + AR_THREADS - 1) / AR_THREADS;
   if (b < 1) b = 1;
@@ -224,6 +287,12 @@ PTO_API int pto_ar_allreduce(const void* peers, long long off, long long n, int 
       rank >= world)
     return -1;
   if (n == 0) return 0;
+  if (n <= AR_ONESHOT_MAX) {
+    hipLaunchKernelGGL(k_xgmi_allreduce_1shot<false>, dim3((unsigned)((n / 4 + AR_THREADS - 1) / AR_THREADS)),
+                       dim3(AR_THREADS), 0, s, reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,
+                       reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), ArSgd{});
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(k_xgmi_allreduce<false>, dim3(pto_ar_blocks(n, world)), dim3(AR_THREADS), 0, s,
                      reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,
                      reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), ArSgd{});
@@ -254,6 +323,12 @@ PTO_API int pto_ar_allreduce_sgd(const void* peers, long long off, long long n, 
   f.zero_from = zero_from;
   f.bidx = bidx;
   f.nbatches = nbatches;
+  if (n <= AR_ONESHOT_MAX) {
+    hipLaunchKernelGGL(k_xgmi_allreduce_1shot<true>, dim3((unsigned)((n / 4 + AR_THREADS - 1) / AR_THREADS)),
+                       dim3(AR_THREADS), 0, s, reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,
+                       reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), f);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(k_xgmi_allreduce<true>, dim3(pto_ar_blocks(n, world)), dim3(AR_THREADS), 0, s,
                      reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,
                      reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), f);
