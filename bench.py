@@ -67,7 +67,9 @@ def main(argv=None):
     from pytorch_operator_1_amd.utils import dist as pdist
 
     use_gpu = torch.cuda.is_available() and not args.cpu
-    env, device = pdist.init_distributed(use_gpu=use_gpu)
+    # PTO_BACKEND=gloo: rehearse the multi-rank path with several ranks on
+    # one GPU (RCCL refuses duplicate devices); default nccl (= RCCL) on GPU
+    env, device = pdist.init_distributed(os.environ.get("PTO_BACKEND"), use_gpu=use_gpu)
     if env.world_size != args.gpus and env.rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
 
