@@ -121,6 +121,12 @@ __global__ __launch_bounds__(256) void k_sum(const float* __restrict__ x, float*
   if ((threadIdx.x & 63) == 0) atomicAdd(out, s * scale);
 }
 
+// Empty kernel: measures the cost of one more launch boundary inside a
+// replayed graph (tools: PTO_PROBE_NOOPS in fused_step.py).
+__global__ void k_noop(int* p) {
+  if (p && threadIdx.x == 0 && blockIdx.x == 0) *p = 0;
+}
+
 }  // namespace
 
 #define PTO_API extern "C" __attribute__((visibility("default")))
@@ -165,5 +171,10 @@ PTO_API int pto_sum(const float* x, float* out, long long n, float scale, hipStr
   int blocks = (int)((n + 255) / 256);
   if (blocks > 1024) blocks = 1024;
   hipLaunchKernelGGL(k_sum, dim3(blocks), dim3(256), 0, s, x, out, n, scale);
+  return (int)hipGetLastError();
+}
+
+PTO_API int pto_noop(int blocks, hipStream_t s) {
+  hipLaunchKernelGGL(k_noop, dim3(blocks), dim3(64), 0, s, nullptr);
   return (int)hipGetLastError();
 }

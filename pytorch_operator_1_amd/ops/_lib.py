@@ -115,6 +115,7 @@ _SIGS = {
     "pto_ce_fwd": [_P, _P, _P, _P, _L, _I, _L, _P],
     "pto_ce_bwd": [_P, _P, _P, _P, _L, _I, _L, _P],
     "pto_transpose_bf16": [_P, _P, _L, _L, _L, _L, _P],
+    "pto_noop": [_I, _P],
     # causal GQA flash attention, head_dim 128 (csrc/kernels/attention.hip)
     "pto_attn_fwd": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _L, _L, _L, _L, _F, _P],
     "pto_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _L, _L, _L, _L, _F, _P],

@@ -119,6 +119,7 @@ class FusedMnistTrainer:
         self.fused_opt = bool(fused_opt) and not self.ddp and not self.fuse_fc
         self.pending = torch.zeros(1, device=device, dtype=torch.int32)  # conv1 update owed
         self.batch_snap = torch.zeros(1, device=device, dtype=torch.int64)  # cursor seen by this step's B1
+        self._noops = int(os.environ.get("PTO_PROBE_NOOPS", "0"))
         self.conv12_version = int(os.environ.get("PTO_CONV12", "2"))  # 2: 512-thread F1+F2 launch
         # xGMI DDP step: SGD applied by the all-reduce kernels' epilogue
         self.ar_fused_sgd = os.environ.get("PTO_AR_FUSED_SGD", "1") == "1"
@@ -189,7 +190,7 @@ class FusedMnistTrainer:
         (the first 405,632 elements of the flat buffer, 94% of the bytes)
         are final and their all-reduce can start."""
         L, s, B, P, G = self.L, self._s(), self.B, self._p, self.g
-        c = _lib.check
+        c = self._check
         bi = self.batch_idx.data_ptr()
         if self.fused_opt:
             o = self._opt_args()
@@ -233,7 +234,7 @@ class FusedMnistTrainer:
 
     def conv_backward(self):
         L, s, B, P, G = self.L, self._s(), self.B, self._p, self.g
-        c = _lib.check
+        c = self._check
         bi = self.batch_idx.data_ptr()
         # conv2 wgrad + dgrad(col2im) + bias in one launch.  (Folding conv1's
         # wgrad into the dgrad blocks is supported by the kernel — pass gw1 —
@@ -300,6 +301,20 @@ class FusedMnistTrainer:
             return
         self.sgd.step(self.lr_dev, self.lr, self.momentum, self.weight_decay, 1.0 / self.world, self.nesterov,
                       zero_grad=True, stream=self._s(), batch_cursor=self.batch_idx, n_batches=self.n_batches)
+
+    def _check(self, rc, name):
+        _lib.check(rc, name)
+        if self._noops:
+            self._probe_noops()
+
+    def _probe_noops(self):
+        """PTO_PROBE_NOOPS=k: k empty launches after every phase launch
+        (measures what one launch boundary costs inside the graph)."""
+        import os
+
+        k = int(os.environ.get("PTO_PROBE_NOOPS", "0"))
+        for _ in range(k):
+            _lib.check(self.L.pto_noop(int(os.environ.get("PTO_PROBE_BLOCKS", "1")), self._s()), "noop")
 
     def _eager_step(self):
         if self.ddp and self._xgmi is not None:
