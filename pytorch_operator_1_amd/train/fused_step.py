@@ -58,7 +58,7 @@ class FusedMnistTrainer:
         # of the collective path at world size 1
         self.ddp = self.world > 1 or force_ddp
         # steps per graph replay in run(): amortises the host launch gap
-        self.unroll = int(unroll if unroll is not None else os.environ.get("PTO_GRAPH_UNROLL", "8"))
+        self.unroll = int(unroll if unroll is not None else os.environ.get("PTO_GRAPH_UNROLL", "32"))
         # gradient all-reduce transport: "rccl", "xgmi" (peer-memory kernel,
         # parallel/xgmi.py) or "auto" (xGMI if it verifies and beats RCCL on
         # these buckets, measured at startup; same choice on every rank)
