@@ -1,0 +1,366 @@
+// Fused training-mode BatchNorm (+ residual add) (+ ReLU) for channels-last
+// bf16 activations, fp32 statistics / affine parameters (ResNet-50, BASELINE
+// config 3).
+//
+// Why: in the ResNet-50 bf16 step MIOpen's NHWC batch-norm kernels plus the
+// separate ReLU / residual-add / ReLU-backward elementwise passes were 60 %
+// of the kernel time (profiles/resnet50_window_r1.md: BN 15.7 ms + 6.6 ms
+// elementwise of 40 ms).  Here every BN layer is
+//   forward : stats (1 read) -> finalize (per channel) -> apply (1 read,
+//             + residual read, 1 write; ReLU and the add in the same pass)
+//   backward: reduce (reads dy, x [, y]; for the residual variant also writes
+//             g = dy * relu-mask, which IS the identity branch's gradient)
+//             -> finalize -> apply (dx = k1*g + k2*x + k3)
+// with the ReLU mask recomputed from x (no saved mask, no extra pass).
+//
+// Layout: x is [M = N*H*W][C] (channels_last memory), C = 8 * 2^k <= 2048,
+// so a row is C/8 threads of 16-byte bf16x8 loads and a 256-thread block
+// covers 2048/C rows per iteration: every access is a coalesced 16-byte
+// vector.  Per-block partial sums (fp32, <= a few hundred rows per thread)
+// are combined per channel in fp64 by the finalize kernels, so E[x^2] -
+// E[x]^2 keeps full precision.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int BN_T = 256;
+constexpr int BN_U = 8;     // loads in flight per thread in the reduction kernels
+constexpr int BN_FT = 1024;  // finalize block: 32 channels x 32 partial groups
+
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+struct V8 {
+  float v[8];
+};
+__device__ __forceinline__ V8 load8(const uint16_t* p) {
+  const uint4 r = *reinterpret_cast<const uint4*>(p);
+  V8 o;
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o.v[2 * j] = __uint_as_float(w[j] << 16);
+    o.v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+  }
+  return o;
+}
+__device__ __forceinline__ void store8(uint16_t* p, const V8& a) {
+  uint4 r;
+  r.x = (uint32_t)f2bf(a.v[0]) | ((uint32_t)f2bf(a.v[1]) << 16);
+  r.y = (uint32_t)f2bf(a.v[2]) | ((uint32_t)f2bf(a.v[3]) << 16);
+  r.z = (uint32_t)f2bf(a.v[4]) | ((uint32_t)f2bf(a.v[5]) << 16);
+  r.w = (uint32_t)f2bf(a.v[6]) | ((uint32_t)f2bf(a.v[7]) << 16);
+  *reinterpret_cast<uint4*>(p) = r;
+}
+__device__ __forceinline__ V8 loadf8(const float* p) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  return V8{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
+}
+
+// Block-level combine of per-thread 8-channel partials (s, q) over the
+// row groups of the block; thread layout: tid = rsub * tpr + col.
+__device__ __forceinline__ void block_combine(const float (&s)[8], const float (&q)[8], int C, float* red,
+                                              float* __restrict__ out_s, float* __restrict__ out_q) {
+  const int tpr = C >> 3, rpi = BN_T / tpr, tid = threadIdx.x, rsub = tid / tpr, c8 = (tid - rsub * tpr) * 8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[rsub * C + c8 + j] = s[j];
+    red[2048 + rsub * C + c8 + j] = q[j];
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += BN_T) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rpi; ++r) {
+      a += red[r * C + c];
+      b += red[2048 + r * C + c];
+    }
+    out_s[c] = a;
+    out_q[c] = b;
+  }
+}
+
+// Per-block sums of x and x^2 per channel -> part[blk][2][C].
+__global__ __launch_bounds__(BN_T) void k_bn_stats(const uint16_t* __restrict__ x, long long M, int C, int iters,
+                                                   float* __restrict__ part) {
+  __shared__ float red[4096];
+  const int tpr = C >> 3, rpi = BN_T / tpr, tid = threadIdx.x, rsub = tid / tpr, c8 = (tid - rsub * tpr) * 8;
+  float s[8] = {}, q[8] = {};
+  const long long r0 = (long long)blockIdx.x * iters * rpi + rsub;
+  const V8 zero{};
+  for (int it = 0; it < iters; it += BN_U) {  // BN_U independent 16-byte loads in flight
+    V8 a[BN_U];
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const long long row = r0 + (long long)(it + u) * rpi;
+      a[u] = (it + u < iters && row < M) ? load8(x + row * C + c8) : zero;
+    }
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += a[u].v[j];
+        q[j] = fmaf(a[u].v[j], a[u].v[j], q[j]);
+      }
+  }
+  block_combine(s, q, C, red, part + (long long)blockIdx.x * 2 * C, part + (long long)blockIdx.x * 2 * C + C);
+}
+
+// Sum of the per-block partials of 32 channels (both the s and the q
+// column) in fp64: thread = (column 0..63, group 0..15) sums every 16th
+// block, then the 16 groups are combined in LDS.  Returns, for threads
+// 0..31 of the block, (S, Q) of channel blockIdx.x * 32 + tid.
+__device__ __forceinline__ void combine_partials(const float* __restrict__ part, int nblk, int C, double* red,
+                                                 double& S, double& Q) {
+  const int t = threadIdx.x, col = t & 63, grp = t >> 6;
+  const int c = blockIdx.x * 32 + (col & 31);
+  double acc = 0.0;
+  if (c < C) {
+    const float* p = part + (col >> 5) * C + c;
+#pragma unroll 8
+    for (int b = grp; b < nblk; b += BN_FT / 64) acc += (double)p[(long long)b * 2 * C];
+  }
+  red[grp * 64 + col] = acc;
+  __syncthreads();
+  S = Q = 0.0;
+  if (t < 32) {
+    for (int g = 0; g < BN_FT / 64; ++g) {
+      S += red[g * 64 + t];
+      Q += red[g * 64 + 32 + t];
+    }
+  }
+}
+
+// Per channel: mean / rstd from the partials (fp64), the affine folded into
+// scale/shift, running statistics (unbiased variance) and the batch counter.
+__global__ __launch_bounds__(BN_FT) void k_bn_finalize(const float* __restrict__ part, int nblk, long long M, int C,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float eps, float momentum,
+                                                       float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                       long long* __restrict__ nbt, float* __restrict__ stat) {
+  __shared__ double red[BN_FT];
+  double s, q;
+  combine_partials(part, nblk, C, red, s, q);
+  const int c = blockIdx.x * 32 + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
+  if (threadIdx.x >= 32 || c >= C) return;
+  const double mean = s / (double)M;
+  double var = q / (double)M - mean * mean;
+  var = var > 0.0 ? var : 0.0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * rstd;
+  stat[c] = (float)mean;
+  stat[C + c] = rstd;
+  stat[2 * C + c] = sc;
+  stat[3 * C + c] = beta[c] - (float)mean * sc;
+  if (run_mean) {
+    const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+  }
+}
+
+// y = [relu](x * scale + shift [+ res])
+__global__ __launch_bounds__(BN_T) void k_bn_apply(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+                                                   uint16_t* __restrict__ y, long long n8, int C,
+                                                   const float* __restrict__ stat, int relu) {
+  const float* scale = stat + 2 * C;
+  const float* shift = stat + 3 * C;
+  const long long stride = (long long)gridDim.x * BN_T;
+  for (long long i = (long long)blockIdx.x * BN_T + threadIdx.x; i < n8; i += stride) {
+    const int c0 = (int)((i * 8) & (C - 1));  // C is a power of two
+    V8 a = load8(x + i * 8);
+    const V8 sc = loadf8(scale + c0), sh = loadf8(shift + c0);
+    V8 r{};
+    if (res) r = load8(res + i * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = fmaf(a.v[j], sc.v[j], sh.v[j]);
+      if (res) v += r.v[j];
+      a.v[j] = relu ? fmaxf(v, 0.f) : v;
+    }
+    store8(y + i * 8, a);
+  }
+}
+
+// Backward reduction: g = dy * mask; per channel sums of g and g * xhat.
+// mode 0: no ReLU; 1: ReLU, mask recomputed from x (x*scale+shift > 0);
+// 2: ReLU after a residual add, mask = (y > 0), and g is stored (it is also
+// the gradient of the residual input).
+__global__ __launch_bounds__(BN_T) void k_bn_bwd_reduce(const uint16_t* __restrict__ dy,
+                                                        const uint16_t* __restrict__ x,
+                                                        const uint16_t* __restrict__ y, long long M, int C,
+                                                        int iters, const float* __restrict__ stat, int mode,
+                                                        uint16_t* __restrict__ g_out, float* __restrict__ part) {
+  __shared__ float red[4096];
+  const int tpr = C >> 3, rpi = BN_T / tpr, tid = threadIdx.x, rsub = tid / tpr, c8 = (tid - rsub * tpr) * 8;
+  const V8 mean = loadf8(stat + c8), rstd = loadf8(stat + C + c8);
+  const V8 sc = loadf8(stat + 2 * C + c8), sh = loadf8(stat + 3 * C + c8);
+  float s[8] = {}, q[8] = {};
+  const long long r0 = (long long)blockIdx.x * iters * rpi + rsub;
+  constexpr int U = BN_U / 2;  // two (three) streams per row
+  const V8 zero{};
+  for (int it = 0; it < iters; it += U) {
+    V8 g[U], a[U], yv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long row = r0 + (long long)(it + u) * rpi;
+      const bool ok = it + u < iters && row < M;
+      const long long o = row * C + c8;
+      g[u] = ok ? load8(dy + o) : zero;
+      a[u] = ok ? load8(x + o) : zero;
+      if (mode == 2) yv[u] = ok ? load8(y + o) : zero;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (mode == 1) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (!(fmaf(a[u].v[j], sc.v[j], sh.v[j]) > 0.f)) g[u].v[j] = 0.f;
+      } else if (mode == 2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (!(yv[u].v[j] > 0.f)) g[u].v[j] = 0.f;
+        const long long row = r0 + (long long)(it + u) * rpi;
+        if (it + u < iters && row < M) store8(g_out + row * C + c8, g[u]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += g[u].v[j];
+        q[j] = fmaf(g[u].v[j], (a[u].v[j] - mean.v[j]) * rstd.v[j], q[j]);
+      }
+    }
+  }
+  block_combine(s, q, C, red, part + (long long)blockIdx.x * 2 * C, part + (long long)blockIdx.x * 2 * C + C);
+}
+
+// dbeta = sum g, dgamma = sum g*xhat; dx = k1*g + k2*x + k3 coefficients.
+__global__ __launch_bounds__(BN_FT) void k_bn_bwd_finalize(const float* __restrict__ part, int nblk, long long M,
+                                                           int C, const float* __restrict__ gamma,
+                                                           const float* __restrict__ stat,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                           float* __restrict__ coef) {
+  __shared__ double red[BN_FT];
+  double s, q;
+  combine_partials(part, nblk, C, red, s, q);
+  const int c = blockIdx.x * 32 + threadIdx.x;
+  if (threadIdx.x >= 32 || c >= C) return;
+  const float mean = stat[c], rstd = stat[C + c];
+  dbeta[c] = (float)s;
+  dgamma[c] = (float)q;
+  const double k1 = (double)gamma[c] * rstd;
+  const double k2 = -k1 * rstd * q / (double)M;
+  const double k3 = -k1 * s / (double)M - k2 * mean;
+  coef[c] = (float)k1;
+  coef[C + c] = (float)k2;
+  coef[2 * C + c] = (float)k3;
+}
+
+// dx = k1 * g + k2 * x + k3 with g = dy (mode 0), dy * relu-mask recomputed
+// from x (mode 1) or the stored g (mode 2, passed as gsrc).
+__global__ __launch_bounds__(BN_T) void k_bn_bwd_apply(const uint16_t* __restrict__ gsrc,
+                                                       const uint16_t* __restrict__ x, uint16_t* __restrict__ dx,
+                                                       long long n8, int C, const float* __restrict__ stat,
+                                                       const float* __restrict__ coef, int mode) {
+  const long long stride = (long long)gridDim.x * BN_T;
+  for (long long i = (long long)blockIdx.x * BN_T + threadIdx.x; i < n8; i += stride) {
+    const int c0 = (int)((i * 8) & (C - 1));  // C is a power of two
+    V8 g = load8(gsrc + i * 8);
+    const V8 a = load8(x + i * 8);
+    const V8 k1 = loadf8(coef + c0), k2 = loadf8(coef + C + c0), k3 = loadf8(coef + 2 * C + c0);
+    if (mode == 1) {
+      const V8 sc = loadf8(stat + 2 * C + c0), sh = loadf8(stat + 3 * C + c0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (!(fmaf(a.v[j], sc.v[j], sh.v[j]) > 0.f)) g.v[j] = 0.f;
+    }
+    V8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o.v[j] = fmaf(k1.v[j], g.v[j], fmaf(k2.v[j], a.v[j], k3.v[j]));
+    store8(dx + i * 8, o);
+  }
+}
+
+bool bn_shape_ok(long long M, int C) {
+  if (M < 1 || C < 8 || C > 2048 || (C & 7)) return false;
+  const int tpr = C >> 3;
+  return (tpr & (tpr - 1)) == 0;  // power of two <= 256
+}
+
+// Reduction grid: enough blocks to fill the chip, per-block partials
+// bounded to 256 K floats.
+void bn_grid(long long M, int C, int* nblk, int* iters) {
+  const int rpi = BN_T / (C >> 3);
+  const long long rows_iters = (M + rpi - 1) / rpi;
+  long long nb = (rows_iters + 15) / 16;  // >= 16 iterations per block
+  const long long cap = 262144 / C < 512 ? 262144 / C : 512;
+  if (nb > cap) nb = cap;
+  if (nb < 1) nb = 1;
+  *nblk = (int)nb;
+  *iters = (int)((rows_iters + nb - 1) / nb);
+}
+
+int elementwise_blocks(long long n8) {
+  long long b = (n8 + BN_T * 4 - 1) / (BN_T * 4);  // ~4 vectors per thread
+  if (b > 8192) b = 8192;
+  return (int)(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+#define PTO_API extern "C" __attribute__((visibility("default")))
+
+// Scratch floats the launchers need for (M, C): partials.
+PTO_API int pto_bn_scratch_floats(long long M, int C) {
+  if (!bn_shape_ok(M, C)) return -1;
+  int nblk, iters;
+  bn_grid(M, C, &nblk, &iters);
+  return nblk * 2 * C;  // <= 524288 (bn_grid caps nblk * C at 256 K)
+}
+
+// Forward: stat = [mean | rstd | scale | shift] (4*C floats, saved for the
+// backward); res / run_mean / run_var / nbt may be null.
+PTO_API int pto_bn_fwd(const void* x, const void* res, void* y, long long M, int C, const float* gamma,
+                       const float* beta, float eps, float momentum, float* run_mean, float* run_var, long long* nbt,
+                       float* stat, float* scratch, int relu, hipStream_t s) {
+  if (!bn_shape_ok(M, C)) return -1;
+  if ((((uintptr_t)x) | ((uintptr_t)y) | ((uintptr_t)res)) & 15) return -1;
+  int nblk, iters;
+  bn_grid(M, C, &nblk, &iters);
+  hipLaunchKernelGGL(k_bn_stats, dim3(nblk), dim3(BN_T), 0, s, reinterpret_cast<const uint16_t*>(x), M, C, iters,
+                     scratch);
+  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 31) / 32), dim3(BN_FT), 0, s, scratch, nblk, M, C, gamma, beta,
+                     eps, momentum, run_mean, run_var, nbt, stat);
+  const long long n8 = M * C / 8;
+  hipLaunchKernelGGL(k_bn_apply, dim3(elementwise_blocks(n8)), dim3(BN_T), 0, s,
+                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(res),
+                     reinterpret_cast<uint16_t*>(y), n8, C, stat, relu);
+  return (int)hipGetLastError();
+}
+
+// Backward.  mode 0/1/2 as k_bn_bwd_reduce; y needed for mode 2, where
+// g_out (= d residual) is also written.  coef: 3*C floats scratch.
+PTO_API int pto_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* g_out, long long M, int C,
+                       const float* gamma, const float* stat, float* dgamma, float* dbeta, float* coef,
+                       float* scratch, int mode, hipStream_t s) {
+  if (!bn_shape_ok(M, C) || mode < 0 || mode > 2 || (mode == 2 && (!y || !g_out))) return -1;
+  if ((((uintptr_t)dy) | ((uintptr_t)x) | ((uintptr_t)dx) | ((uintptr_t)y) | ((uintptr_t)g_out)) & 15) return -1;
+  int nblk, iters;
+  bn_grid(M, C, &nblk, &iters);
+  hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(nblk), dim3(BN_T), 0, s, reinterpret_cast<const uint16_t*>(dy),
+                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(y), M, C, iters, stat,
+                     mode, reinterpret_cast<uint16_t*>(g_out), scratch);
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 31) / 32), dim3(BN_FT), 0, s, scratch, nblk, M, C, gamma,
+                     stat, dgamma, dbeta, coef);
+  const long long n8 = M * C / 8;
+  const void* gsrc = mode == 2 ? g_out : dy;
+  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(elementwise_blocks(n8)), dim3(BN_T), 0, s,
+                     reinterpret_cast<const uint16_t*>(gsrc), reinterpret_cast<const uint16_t*>(x),
+                     reinterpret_cast<uint16_t*>(dx), n8, C, stat, coef, mode);
+  return (int)hipGetLastError();
+}

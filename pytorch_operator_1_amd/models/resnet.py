@@ -14,6 +14,8 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from ..ops.bn import BatchNormAct
+
 
 class Bottleneck(nn.Module):
     expansion = 4
@@ -22,29 +24,28 @@ class Bottleneck(nn.Module):
         super().__init__()
         cout = width * self.expansion
         self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = BatchNormAct(width)
         self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
-        self.bn2 = nn.BatchNorm2d(width)
+        self.bn2 = BatchNormAct(width)
         self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
-        self.bn3 = nn.BatchNorm2d(cout)
-        self.relu = nn.ReLU(inplace=True)
-        self.downsample = (nn.Sequential(nn.Conv2d(cin, cout, 1, stride=stride, bias=False), nn.BatchNorm2d(cout))
+        self.bn3 = BatchNormAct(cout)
+        self.downsample = (nn.Sequential(nn.Conv2d(cin, cout, 1, stride=stride, bias=False), BatchNormAct(cout))
                            if down else None)
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.relu(self.bn2(self.conv2(y)))
-        y = self.bn3(self.conv3(y))
-        return self.relu(y + idt)
+        # BN + ReLU (+ the residual add) are one fused pass each way on the
+        # GPU (ops/bn.py); state-dict keys are the stock ones
+        idt = x if self.downsample is None else self.downsample[1](self.downsample[0](x))
+        y = self.bn1(self.conv1(x), relu=True)
+        y = self.bn2(self.conv2(y), relu=True)
+        return self.bn3(self.conv3(y), residual=idt, relu=True)
 
 
 class ResNet(nn.Module):
     def __init__(self, layers=(3, 4, 6, 3), num_classes: int = 1000, zero_init_residual: bool = True):
         super().__init__()
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn1 = BatchNormAct(64)
         self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
         cin, stages = 64, []
         for i, (n, width) in enumerate(zip(layers, (64, 128, 256, 512))):
@@ -68,7 +69,7 @@ class ResNet(nn.Module):
                     nn.init.zeros_(m.bn3.weight)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(self.bn1(self.conv1(x), relu=True))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 

@@ -29,7 +29,8 @@ ARCH = os.environ.get("PTO_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 
 HIP_SOURCES = ("kernels/mnist_kernels.hip", "kernels/common_kernels.hip", "kernels/optim_kernels.hip",
-               "kernels/llm_kernels.hip", "kernels/attention.hip", "comm/xgmi_allreduce.hip")
+               "kernels/llm_kernels.hip", "kernels/attention.hip", "kernels/bn_kernels.hip",
+               "comm/xgmi_allreduce.hip")
 
 _lock = threading.Lock()
 _lib = None
@@ -116,6 +117,10 @@ _SIGS = {
     "pto_ce_bwd": [_P, _P, _P, _P, _L, _I, _L, _P],
     "pto_transpose_bf16": [_P, _P, _L, _L, _L, _L, _P],
     "pto_noop": [_I, _P],
+    # fused BatchNorm(+add)(+ReLU), channels-last bf16 (csrc/kernels/bn_kernels.hip)
+    "pto_bn_scratch_floats": [_L, _I],
+    "pto_bn_fwd": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _I, _P],
+    "pto_bn_bwd": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _I, _P],
     # causal GQA flash attention, head_dim 128 (csrc/kernels/attention.hip)
     "pto_attn_fwd": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _L, _L, _L, _L, _F, _P],
     "pto_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _L, _L, _L, _L, _F, _P],

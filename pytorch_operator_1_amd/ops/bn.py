@@ -1,0 +1,98 @@
+"""Fused training-mode BatchNorm (+ residual add) (+ ReLU) over channels-last
+bf16 activations (``csrc/kernels/bn_kernels.hip``), as used by the ResNet-50
+bottlenecks: ``relu(bn(x))``, ``relu(bn(x) + identity)`` and ``bn(x)``.
+
+:class:`BatchNormAct` is an ``nn.BatchNorm2d`` (same parameters, buffers and
+state-dict keys) whose ``forward(x, residual=None, relu=False)`` takes the
+fused HIP path in training mode on bf16 channels-last HIP tensors and the
+stock module (+ add / ReLU) everywhere else (CPU, eval, other dtypes).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+
+_CL = torch.channels_last
+
+
+def fused_supported(x: torch.Tensor) -> bool:
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
+        return False
+    C = x.shape[1]
+    tpr = C // 8
+    return C % 8 == 0 and 8 <= C <= 2048 and (tpr & (tpr - 1)) == 0 and os.environ.get("PTO_FUSED_BN", "1") == "1"
+
+
+class _BNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, residual, relu, momentum, eps):
+        L = _lib.lib()
+        x = x.contiguous(memory_format=_CL)
+        N, C, H, W = x.shape
+        M = N * H * W
+        dev = x.device
+        y = torch.empty_like(x, memory_format=_CL)
+        stat = torch.empty(4 * C, device=dev, dtype=torch.float32)
+        scratch = torch.empty(L.pto_bn_scratch_floats(M, C), device=dev, dtype=torch.float32)
+        res = None
+        if residual is not None:
+            res = residual.contiguous(memory_format=_CL)
+            if res.shape != x.shape or res.dtype != x.dtype:
+                raise ValueError("BatchNormAct: residual must match the input")
+        _lib.check(L.pto_bn_fwd(x.data_ptr(), None if res is None else res.data_ptr(), y.data_ptr(), M, C,
+                                weight.data_ptr(), bias.data_ptr(), eps, momentum,
+                                None if running_mean is None else running_mean.data_ptr(),
+                                None if running_var is None else running_var.data_ptr(),
+                                None if nbt is None else nbt.data_ptr(), stat.data_ptr(), scratch.data_ptr(),
+                                int(relu), _lib.stream_ptr(dev)), "bn_fwd")
+        ctx.mode = 2 if (residual is not None and relu) else (1 if relu else 0)
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, y if ctx.mode == 2 else None, weight, stat)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = _lib.lib()
+        x, y, weight, stat = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=_CL)
+        N, C, H, W = x.shape
+        M = N * H * W
+        dev = x.device
+        dx = torch.empty_like(x, memory_format=_CL)
+        g = torch.empty_like(x, memory_format=_CL) if ctx.mode == 2 else None
+        dgamma = torch.empty(C, device=dev, dtype=torch.float32)
+        dbeta = torch.empty(C, device=dev, dtype=torch.float32)
+        coef = torch.empty(3 * C, device=dev, dtype=torch.float32)
+        scratch = torch.empty(L.pto_bn_scratch_floats(M, C), device=dev, dtype=torch.float32)
+        _lib.check(L.pto_bn_bwd(dy.data_ptr(), x.data_ptr(), None if y is None else y.data_ptr(), dx.data_ptr(),
+                                None if g is None else g.data_ptr(), M, C, weight.data_ptr(), stat.data_ptr(),
+                                dgamma.data_ptr(), dbeta.data_ptr(), coef.data_ptr(), scratch.data_ptr(), ctx.mode,
+                                _lib.stream_ptr(dev)), "bn_bwd")
+        dres = (g if ctx.mode == 2 else dy) if ctx.has_res else None
+        return dx, dgamma.to(weight.dtype), dbeta.to(weight.dtype), None, None, None, dres, None, None, None
+
+
+def bn_act(x, weight, bias, running_mean=None, running_var=None, num_batches_tracked=None, residual=None,
+           relu=False, momentum: float = 0.1, eps: float = 1e-5):
+    """Training-mode ``[relu](batch_norm(x) [+ residual])`` on a bf16
+    channels-last HIP tensor; running statistics updated in place."""
+    return _BNAct.apply(x, weight, bias, running_mean, running_var, num_batches_tracked, residual, relu,
+                        float(momentum), float(eps))
+
+
+class BatchNormAct(nn.BatchNorm2d):
+    def forward(self, x, residual=None, relu: bool = False):  # noqa: D102
+        if self.training and self.momentum is not None and self.affine and fused_supported(x):
+            nbt = self.num_batches_tracked if self.track_running_stats else None
+            rm = self.running_mean if self.track_running_stats else None
+            rv = self.running_var if self.track_running_stats else None
+            return bn_act(x, self.weight, self.bias, rm, rv, nbt, residual, relu, self.momentum, self.eps)
+        y = super().forward(x)
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if relu else y
