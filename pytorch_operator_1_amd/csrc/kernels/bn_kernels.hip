@@ -165,26 +165,37 @@ __global__ __launch_bounds__(BN_FT) void k_bn_finalize(const float* __restrict__
   }
 }
 
-// y = [relu](x * scale + shift [+ res])
+// y = [relu](x * scale + shift [+ res]); two vectors per thread iteration
+// (independent loads in flight).
 __global__ __launch_bounds__(BN_T) void k_bn_apply(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                    uint16_t* __restrict__ y, long long n8, int C,
                                                    const float* __restrict__ stat, int relu) {
   const float* scale = stat + 2 * C;
   const float* shift = stat + 3 * C;
   const long long stride = (long long)gridDim.x * BN_T;
-  for (long long i = (long long)blockIdx.x * BN_T + threadIdx.x; i < n8; i += stride) {
-    const int c0 = (int)((i * 8) & (C - 1));  // C is a power of two
-    V8 a = load8(x + i * 8);
-    const V8 sc = loadf8(scale + c0), sh = loadf8(shift + c0);
-    V8 r{};
-    if (res) r = load8(res + i * 8);
+  for (long long i0 = (long long)blockIdx.x * BN_T + threadIdx.x; i0 < n8; i0 += 2 * stride) {
+    V8 a[2], r[2];
+    const long long ii[2] = {i0, i0 + stride};
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = fmaf(a.v[j], sc.v[j], sh.v[j]);
-      if (res) v += r.v[j];
-      a.v[j] = relu ? fmaxf(v, 0.f) : v;
+    for (int u = 0; u < 2; ++u) {
+      if (ii[u] < n8) {
+        a[u] = load8(x + ii[u] * 8);
+        if (res) r[u] = load8(res + ii[u] * 8);
+      }
     }
-    store8(y + i * 8, a);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (ii[u] >= n8) continue;
+      const int c0 = (int)((ii[u] * 8) & (C - 1));  // C is a power of two
+      const V8 sc = loadf8(scale + c0), sh = loadf8(shift + c0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = fmaf(a[u].v[j], sc.v[j], sh.v[j]);
+        if (res) v += r[u].v[j];
+        a[u].v[j] = relu ? fmaxf(v, 0.f) : v;
+      }
+      store8(y + ii[u] * 8, a[u]);
+    }
   }
 }
 
@@ -262,27 +273,39 @@ __global__ __launch_bounds__(BN_FT) void k_bn_bwd_finalize(const float* __restri
 }
 
 // dx = k1 * g + k2 * x + k3 with g = dy (mode 0), dy * relu-mask recomputed
-// from x (mode 1) or the stored g (mode 2, passed as gsrc).
+// from x (mode 1) or the stored g (mode 2, passed as gsrc); two vectors per
+// thread iteration.
 __global__ __launch_bounds__(BN_T) void k_bn_bwd_apply(const uint16_t* __restrict__ gsrc,
                                                        const uint16_t* __restrict__ x, uint16_t* __restrict__ dx,
                                                        long long n8, int C, const float* __restrict__ stat,
                                                        const float* __restrict__ coef, int mode) {
   const long long stride = (long long)gridDim.x * BN_T;
-  for (long long i = (long long)blockIdx.x * BN_T + threadIdx.x; i < n8; i += stride) {
-    const int c0 = (int)((i * 8) & (C - 1));  // C is a power of two
-    V8 g = load8(gsrc + i * 8);
-    const V8 a = load8(x + i * 8);
-    const V8 k1 = loadf8(coef + c0), k2 = loadf8(coef + C + c0), k3 = loadf8(coef + 2 * C + c0);
-    if (mode == 1) {
-      const V8 sc = loadf8(stat + 2 * C + c0), sh = loadf8(stat + 3 * C + c0);
+  for (long long i0 = (long long)blockIdx.x * BN_T + threadIdx.x; i0 < n8; i0 += 2 * stride) {
+    V8 g[2], a[2];
+    const long long ii[2] = {i0, i0 + stride};
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (!(fmaf(a.v[j], sc.v[j], sh.v[j]) > 0.f)) g.v[j] = 0.f;
+    for (int u = 0; u < 2; ++u) {
+      if (ii[u] < n8) {
+        g[u] = load8(gsrc + ii[u] * 8);
+        a[u] = load8(x + ii[u] * 8);
+      }
     }
-    V8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o.v[j] = fmaf(k1.v[j], g.v[j], fmaf(k2.v[j], a.v[j], k3.v[j]));
-    store8(dx + i * 8, o);
+    for (int u = 0; u < 2; ++u) {
+      if (ii[u] >= n8) continue;
+      const int c0 = (int)((ii[u] * 8) & (C - 1));  // C is a power of two
+      const V8 k1 = loadf8(coef + c0), k2 = loadf8(coef + C + c0), k3 = loadf8(coef + 2 * C + c0);
+      if (mode == 1) {
+        const V8 sc = loadf8(stat + 2 * C + c0), sh = loadf8(stat + 3 * C + c0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (!(fmaf(a[u].v[j], sc.v[j], sh.v[j]) > 0.f)) g[u].v[j] = 0.f;
+      }
+      V8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o.v[j] = fmaf(k1.v[j], g[u].v[j], fmaf(k2.v[j], a[u].v[j], k3.v[j]));
+      store8(dx + ii[u] * 8, o);
+    }
   }
 }
 
@@ -293,12 +316,12 @@ bool bn_shape_ok(long long M, int C) {
 }
 
 // Reduction grid: enough blocks to fill the chip, per-block partials
-// bounded to 256 K floats.
+// bounded to 512 K floats.
 void bn_grid(long long M, int C, int* nblk, int* iters) {
   const int rpi = BN_T / (C >> 3);
   const long long rows_iters = (M + rpi - 1) / rpi;
   long long nb = (rows_iters + 15) / 16;  // >= 16 iterations per block
-  const long long cap = 262144 / C < 512 ? 262144 / C : 512;
+  const long long cap = 524288 / C < 512 ? 524288 / C : 512;
   if (nb > cap) nb = cap;
   if (nb < 1) nb = 1;
   *nblk = (int)nb;
@@ -320,7 +343,7 @@ PTO_API int pto_bn_scratch_floats(long long M, int C) {
   if (!bn_shape_ok(M, C)) return -1;
   int nblk, iters;
   bn_grid(M, C, &nblk, &iters);
-  return nblk * 2 * C;  // <= 524288 (bn_grid caps nblk * C at 256 K)
+  return nblk * 2 * C;  // <= 1 M floats (bn_grid caps nblk * C at 512 K)
 }
 
 // Forward: stat = [mean | rstd | scale | shift] (4*C floats, saved for the
