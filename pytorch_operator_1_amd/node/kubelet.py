@@ -76,6 +76,26 @@ def _port_free(port: int) -> bool:
         s.close()
 
 
+_PORT_LOCK_DIR = os.path.join("/tmp", "pto-port-locks")
+
+
+def _reserve_port(port: int):
+    """Host-wide reservation of a virtual master port: an flock held by this
+    process for its lifetime, so two kubelets on one host (e.g. concurrent
+    test clusters) never hand the same port to two jobs before either
+    master has bound it.  Returns the lock fd, or None if taken."""
+    import fcntl
+
+    os.makedirs(_PORT_LOCK_DIR, exist_ok=True)
+    fd = os.open(os.path.join(_PORT_LOCK_DIR, f"{port}.lock"), os.O_CREAT | os.O_RDWR, 0o666)
+    try:
+        fcntl.flock(fd, fcntl.LOCK_EX | fcntl.LOCK_NB)
+        return fd
+    except OSError:
+        os.close(fd)
+        return None
+
+
 class PodRuntime:
     def __init__(self, pod):
         self.key = key_of(pod)
@@ -118,6 +138,7 @@ class Kubelet:
         self.extra_env = extra_env or {}
         self.pods: dict[str, PodRuntime] = {}
         self.job_ports: dict[str, int] = {}
+        self._port_locks: list[int] = []  # flock fds of the reserved ports (released at exit)
         self.pod_informer = Informer(client, "pods")
         self.svc_informer = Informer(client, "services")
         self.pod_informer.add_event_handler(on_delete=self._on_pod_delete)
@@ -330,7 +351,12 @@ class Kubelet:
             return self.job_ports[jk]
         used = set(self.job_ports.values())
         port = wanted
-        while port in used or not _port_free(port):
+        while True:
+            if port not in used and _port_free(port):
+                fd = _reserve_port(port)
+                if fd is not None:
+                    self._port_locks.append(fd)
+                    break
             port += 1
         self.job_ports[jk] = port
         return port

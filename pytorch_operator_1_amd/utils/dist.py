@@ -50,12 +50,23 @@ def read_env() -> DistEnv:
 
 
 def resolve_backend(name: str | None, use_gpu: bool) -> str:
+    """Torch backend for a reference ``--backend`` value.  ``mpi`` (reference
+    ``examples/mnist/v1/pytorch_job_mnist_mpi.yaml``, an MPI-built PyTorch
+    image) falls back to the collective backend of the device when this
+    PyTorch has no MPI support (the ROCm wheels do not): RCCL on a GPU,
+    gloo on CPU — same env:// world, same DDP semantics."""
     if not name:
         return "nccl" if use_gpu else "gloo"
     try:
-        return BACKEND_ALIASES[name.lower()]
+        be = BACKEND_ALIASES[name.lower()]
     except KeyError as e:
         raise ValueError(f"unknown backend {name!r}; choose from {sorted(BACKEND_ALIASES)}") from e
+    if be == "mpi" and not dist.is_mpi_available():
+        be = "nccl" if use_gpu else "gloo"
+        import sys
+
+        print(f"[pto] --backend mpi: this PyTorch has no MPI support, using {be}", file=sys.stderr, flush=True)
+    return be
 
 
 def init_distributed(backend: str | None = None, use_gpu: bool | None = None,
