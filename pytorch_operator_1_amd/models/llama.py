@@ -156,7 +156,7 @@ def _lin(x, mod: nn.Linear):
         return F.linear(x, mod.weight)
     from ..ops import llm
 
-    return llm.linear_tw(x, mod.weight, wt)
+    return llm.linear_tw(x, mod.weight, wt, getattr(mod, "dw_kcontig", False))
 
 
 def _rmsnorm_ref(x, w, eps):
@@ -207,6 +207,13 @@ class Llama(nn.Module):
         mods = [m for blk in self.layers for m in (blk.wqkv, blk.wo, blk.w13, blk.w2)]
         return mods + ([self.lm_head] if self.lm_head is not None else [])
 
+    def _mark_kcontig_dw(self):
+        """Weight-gradient GEMMs that run faster from transposed activations
+        (measured per shape, tools/dw_layout_bench.py): wo and w13."""
+        for blk in self.layers:
+            blk.wo.dw_kcontig = True
+            blk.w13.dw_kcontig = True
+
     @torch.no_grad()
     def enable_transposed_dgrad(self):
         """Keep ``W^T`` next to every linear weight (bf16, +1x weight memory:
@@ -217,6 +224,7 @@ class Llama(nn.Module):
             if getattr(m, "weight_t", None) is None:
                 w = m.weight
                 m.weight_t = torch.empty(w.shape[1], w.shape[0], device=w.device, dtype=w.dtype)
+        self._mark_kcontig_dw()
         self.refresh_transposed()
 
     @torch.no_grad()

@@ -271,8 +271,9 @@ class _LinearTW(torch.autograd.Function):
     (profiles/llama8b_step_rocprof.md)."""
 
     @staticmethod
-    def forward(ctx, x, w, wt):
+    def forward(ctx, x, w, wt, dw_kcontig):
         ctx.save_for_backward(x, wt)
+        ctx.dw_kcontig = dw_kcontig
         return torch.nn.functional.linear(x, w)
 
     @staticmethod
@@ -282,11 +283,24 @@ class _LinearTW(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
-            dw = dy.reshape(-1, dy.shape[-1]).t().mm(x2)
-        return dx, dw, None
+            dy2 = dy.reshape(-1, dy.shape[-1])
+            if ctx.dw_kcontig and x2.is_cuda:
+                # dW = (dY^T)(X^T)^T from transposed activations: both operands
+                # K(token)-contiguous.  Pays for w13/wo only
+                # (tools/dw_layout_bench.py: 3.21 -> 2.39 + 0.51 ms, 0.58 ->
+                # 0.38 + 0.14 ms at 4x4096 tokens)
+                xt = transpose_into(x2.contiguous(), torch.empty(x2.shape[1], x2.shape[0], device=x2.device,
+                                                                  dtype=x2.dtype))
+                dyt = transpose_into(dy2.contiguous(), torch.empty(dy2.shape[1], dy2.shape[0], device=dy2.device,
+                                                                    dtype=dy2.dtype))
+                dw = dyt.mm(xt.t())
+            else:
+                dw = dy2.t().mm(x2)
+        return dx, dw, None, None
 
 
-def linear_tw(x, w, wt):
+def linear_tw(x, w, wt, dw_kcontig: bool = False):
     """``F.linear(x, w)`` with the dgrad taken from ``wt`` (== ``w.t()``,
-    kept current by the caller after every weight update)."""
-    return _LinearTW.apply(x, w, wt)
+    kept current by the caller after every weight update); ``dw_kcontig``:
+    weight gradient from transposed activations."""
+    return _LinearTW.apply(x, w, wt, dw_kcontig)
