@@ -50,6 +50,9 @@ def parse_args(argv=None):
     p.add_argument("--momentum", type=float, default=0.5)
     p.add_argument("--impl", choices=["fused", "eager"], default=os.environ.get("BENCH_IMPL", "fused"))
     p.add_argument("--dataset-size", type=int, default=60000)
+    p.add_argument("--sampler", action="store_true",
+                   help="DistributedSampler semantics: one dataset, disjoint per-rank shards (true global "
+                        "throughput); default: every rank its own stream (reference-equivalent, no sampler)")
     p.add_argument("--cpu", action="store_true", help="run on CPU with gloo (debug only)")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args(argv)
@@ -78,9 +81,15 @@ def main(argv=None):
 
     from pytorch_operator_1_amd.train.runner import build_trainer
 
+    data_kw = {}
+    if args.sampler and env.world_size > 1:
+        from pytorch_operator_1_amd.models.mnist import synthetic_mnist
+
+        x, y = synthetic_mnist(args.dataset_size, device, seed=1)  # the same dataset on every rank
+        data_kw = dict(data=x[env.rank::env.world_size].contiguous(), target=y[env.rank::env.world_size].contiguous())
     trainer = build_trainer(args.impl, device=device, batch_size=args.batch_size, lr=args.lr,
                             momentum=args.momentum, dataset_size=args.dataset_size,
-                            seed=1 + env.rank * 0, rank=env.rank)
+                            seed=1 + env.rank * 0, rank=env.rank, **data_kw)
 
     def sync():
         if device.type == "cuda":
@@ -130,6 +139,8 @@ def main(argv=None):
                 "optimizer": f"SGD lr={args.lr} momentum={args.momentum}",
                 "parallelism": f"dp{n}",
                 "impl": args.impl,
+                "sampler": ("DistributedSampler (disjoint shards of one dataset)" if args.sampler and n > 1
+                            else "none (every rank its own batch stream, reference-equivalent)"),
                 "backend": (torch.distributed.get_backend() if n > 1 else "none"),
                 "baseline": "210 samples/s/rank (BASELINE.md, derived lower bound); vs_baseline = value/(210*n_gpus)",
                 "final_loss": round(loss, 4) if loss is not None else None,
