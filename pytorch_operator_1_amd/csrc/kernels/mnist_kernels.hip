@@ -1395,6 +1395,41 @@ PTO_API int pto_conv1_bwd_sgd(const float* g1, const uint8_t* code1, const float
   LAUNCH_CHECK();
 }
 
+// Optimizer-only launch of k_conv1_bwd_sgd (no conv1 blocks): SGD-momentum
+// over a flat (p, g, m) range of n floats, gradients zeroed from zero_from.
+PTO_API int pto_sgd_flat(float* p, float* g, float* m, long long n, long long zero_from, const float* lr, float mom,
+                         float wd, float gscale, int nesterov, hipStream_t s) {
+  if (n % 4 || zero_from % 4 || ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m)) & 15)) return -1;
+  if (n == 0) return 0;
+  const int nsgd = (int)((n / 4 + 255) / 256);
+  hipLaunchKernelGGL(k_conv1_bwd_sgd, dim3(nsgd), dim3(256), 0, s, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+                     nullptr, 0, p, g, m, n, zero_from, sgd_args(lr, mom, wd, gscale, nesterov));
+  LAUNCH_CHECK();
+}
+
+// B3 split in two launches for the two-stream backward of the fused-
+// optimizer schedule: part 1 = d(a2p) = dh1 W1 (what conv2's backward
+// needs) + the cursor advance / pending flag; part 2 = the fc weight and
+// bias gradients (only the optimizer needs them), run on a side stream
+// concurrently with part 1 and the conv backward.
+PTO_API int pto_fc_bwd_part(const float* dh1, const float* a2p, const float* w1, const float* h1,
+                            const float* dlogits, float* gw1, float* gb1, float* gw2, float* gb2, float* da2p, int B,
+                            long long* bidx, long long nbatches, int* pending, int part, hipStream_t s) {
+  const int nA = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
+  const int nB = ((B + 15) / 16) * ((F1IN + 15) / 16);
+  const int nW = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4;
+  const int nS = 8 + 1;
+  if (part == 1)
+    hipLaunchKernelGGL(k_fc_bwd, dim3(nB), dim3(256), 0, s, dh1, a2p, w1, h1, dlogits, gw1, gb1, gw2, gb2, da2p, B, 0,
+                       nB, 0, bidx, nbatches, pending);
+  else if (part == 2)
+    hipLaunchKernelGGL(k_fc_bwd, dim3(nA + nW + nS), dim3(256), 0, s, dh1, a2p, w1, h1, dlogits, gw1, gb1, gw2, gb2,
+                       da2p, B, nA, 0, nW, nullptr, 1LL, nullptr);
+  else
+    return -1;
+  LAUNCH_CHECK();
+}
+
 PTO_API int pto_conv1_bwd_data(const float* g1, const uint8_t* code1, const float* w, float* dx, int B,
                                hipStream_t s) {
   hipLaunchKernelGGL(k_conv1_bwd_data, dim3((B * 784 + 255) / 256), dim3(256), 0, s, g1, code1, w, dx, B);

@@ -120,9 +120,23 @@ class FusedMnistTrainer:
         self.pending = torch.zeros(1, device=device, dtype=torch.int32)  # conv1 update owed
         self.batch_snap = torch.zeros(1, device=device, dtype=torch.int64)  # cursor seen by this step's B1
         self._noops = int(os.environ.get("PTO_PROBE_NOOPS", "0"))
+        self._probe_fork = torch.cuda.Stream(device) if os.environ.get("PTO_PROBE_FORK") == "1" else None
         self.conv12_version = int(os.environ.get("PTO_CONV12", "2"))  # 2: 512-thread F1+F2 launch
         # xGMI DDP step: SGD applied by the all-reduce kernels' epilogue
         self.ar_fused_sgd = os.environ.get("PTO_AR_FUSED_SGD", "1") == "1"
+        # two-stream backward for the fused-optimizer schedule (PTO_SPLIT_BWD=1).
+        # Off: a fork/join inside the replayed graph costs ~19 us on MI355X
+        # (profiles/graph_fork_join_probe_r1.md), more than the overlap wins
+        # (89.8 vs 54.5 us/step measured)
+        self._bwd_side = (torch.cuda.Stream(device)
+                          if self.fused_opt and os.environ.get("PTO_SPLIT_BWD", "0") == "1" else None)
+        # multi-GPU schedule: overlap the fc bucket's all-reduce with the conv
+        # backward on a side stream (PTO_COMM_OVERLAP=1), or all-reduce the
+        # whole flat buffer once after the backward on the compute stream
+        # (=0: no fork/join in the graph, one collective).  Default "auto":
+        # both whole-step graphs are captured and timed at startup (max over
+        # ranks) and the faster is kept (_choose_schedule).
+        self.comm_overlap = {"1": True, "0": False}.get(os.environ.get("PTO_COMM_OVERLAP", "auto"))
         self._c1 = offs["conv1.weight"][0]
         self._c1_bias = offs["conv1.bias"][0] - self._c1
 
@@ -163,7 +177,8 @@ class FusedMnistTrainer:
             self.comm_info = {"transport": "rccl", "xgmi_error": str(e)}
             return
         split = self._split()
-        tune = ar.autotune([(0, split), (split, self.numel - split)])
+        ranges = [(0, split), (split, self.numel - split)] if self.comm_overlap else [(0, self.numel)]
+        tune = ar.autotune(ranges)
         if self.comm == "xgmi" and not tune["correct"]:
             raise RuntimeError(f"xGMI all-reduce failed verification: {tune}")
         if self.comm == "xgmi" or tune["use_xgmi"]:
@@ -183,7 +198,14 @@ class FusedMnistTrainer:
 
     def forward_backward(self):
         self.forward_fc_backward()
+        fork = self._probe_fork
+        if fork is not None:  # PTO_PROBE_FORK=1: cost of one fork/join pair inside the graph
+            cur = torch.cuda.current_stream(self.device)
+            fork.wait_stream(cur)
+            _lib.check(self.L.pto_noop(1, fork.cuda_stream), "noop")
         self.conv_backward()
+        if fork is not None:
+            torch.cuda.current_stream(self.device).wait_stream(fork)
 
     def forward_fc_backward(self):
         """Forward + loss + fc-layer backward: after this the fc grads
@@ -207,10 +229,23 @@ class FusedMnistTrainer:
                                   self._params[self._c1:].data_ptr(), self.grads[self._c1:].data_ptr(),
                                   self.mom[self._c1:].data_ptr(), self.numel - self._c1, self.pending.data_ptr(),
                                   *o, s), "fc2_ce_commit")
-            c(L.pto_fc_bwd_adv(self.dh1.data_ptr(), self.a2p.data_ptr(), P["fc1.weight"].data_ptr(),
-                               self.h1.data_ptr(), self.dlogits.data_ptr(), G["fc1.weight"].data_ptr(),
-                               G["fc1.bias"].data_ptr(), G["fc2.weight"].data_ptr(), G["fc2.bias"].data_ptr(),
-                               self.da2p.data_ptr(), B, bi, self.n_batches, self.pending.data_ptr(), s), "fc_bwd_adv")
+            fc_args = (self.dh1.data_ptr(), self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), self.h1.data_ptr(),
+                       self.dlogits.data_ptr(), G["fc1.weight"].data_ptr(), G["fc1.bias"].data_ptr(),
+                       G["fc2.weight"].data_ptr(), G["fc2.bias"].data_ptr(), self.da2p.data_ptr(), B)
+            if self._bwd_side is None:
+                c(L.pto_fc_bwd_adv(*fc_args, bi, self.n_batches, self.pending.data_ptr(), s), "fc_bwd_adv")
+                return
+            # two-stream backward: the fc weight gradients and the fc update
+            # run on a side stream next to d(a2p) -> conv2 bwd -> conv1 bwd
+            # (the update waits for d(a2p), the last reader of W1)
+            cur, side = torch.cuda.current_stream(self.device), self._bwd_side
+            side.wait_stream(cur)
+            c(L.pto_fc_bwd_part(*fc_args, None, 1, None, 2, side.cuda_stream), "fc_bwd_wgrad")
+            c(L.pto_fc_bwd_part(*fc_args, bi, self.n_batches, self.pending.data_ptr(), 1, s), "fc_bwd_dgrad")
+            side.wait_stream(cur)
+            split = self._split()
+            c(L.pto_sgd_flat(self._params.data_ptr(), self.grads.data_ptr(), self.mom.data_ptr(), split, split, *o,
+                             side.cuda_stream), "sgd_fc")
             return
         # same F1+F2 launch without an owed update (pending = nullptr)
         c(L.pto_conv12_fwd_lazy(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
@@ -245,11 +280,20 @@ class FusedMnistTrainer:
                           P["conv2.weight"].data_ptr(), G["conv2.weight"].data_ptr(), G["conv2.bias"].data_ptr(),
                           self.da1p.data_ptr(), B, 7, None, None, None, None, None, s), "conv2_bwd")
         if self.fused_opt:  # + the fc/conv2 update (grads final since B3/B2); B1 reads the cursor snapshot
+            if self._bwd_side is None:
+                c(L.pto_conv1_bwd_sgd(self.da1p.data_ptr(), self.code1.data_ptr(), self.data.data_ptr(),
+                                      G["conv1.weight"].data_ptr(), G["conv1.bias"].data_ptr(), B,
+                                      self.batch_snap.data_ptr(), self._params.data_ptr(), self.grads.data_ptr(),
+                                      self.mom.data_ptr(), self._c1, self._split(), *self._opt_args(), s),
+                  "conv1_bwd_sgd")
+                return
+            split, esz = self._split(), self._params.element_size()
             c(L.pto_conv1_bwd_sgd(self.da1p.data_ptr(), self.code1.data_ptr(), self.data.data_ptr(),
                                   G["conv1.weight"].data_ptr(), G["conv1.bias"].data_ptr(), B,
-                                  self.batch_snap.data_ptr(), self._params.data_ptr(), self.grads.data_ptr(),
-                                  self.mom.data_ptr(), self._c1, self._split(), *self._opt_args(), s),
-              "conv1_bwd_sgd")
+                                  self.batch_snap.data_ptr(), self._params.data_ptr() + split * esz,
+                                  self.grads.data_ptr() + split * esz, self.mom.data_ptr() + split * esz,
+                                  self._c1 - split, 0, *self._opt_args(), s), "conv1_bwd_sgd")
+            torch.cuda.current_stream(self.device).wait_stream(self._bwd_side)  # fc update joins the step
             return
         c(L.pto_conv1_bwd(self.da1p.data_ptr(), self.code1.data_ptr(), self.data.data_ptr(),
                           G["conv1.weight"].data_ptr(), G["conv1.bias"].data_ptr(), B, bi, s), "conv1_bwd")
@@ -327,12 +371,26 @@ class FusedMnistTrainer:
         self.optimizer_step()
 
     def _xgmi_step(self):
-        """fc bucket all-reduced by the xGMI kernel on a side stream while
-        the conv backward runs, conv bucket after it; the optimizer joins
-        both — by default inside the two all-reduce launches (SGD epilogue,
-        ``PTO_AR_FUSED_SGD=0``: separate launch).  Pure stream work:
-        capturable into one graph."""
+        """Default: forward + backward, then ONE xGMI all-reduce of the whole
+        flat gradient buffer with the SGD epilogue (update, conv-grad
+        zeroing, cursor advance) on the compute stream — no optimizer launch,
+        no side stream.  ``comm_overlap``: the fc bucket is all-reduced on a
+        side stream while the conv backward runs, the conv bucket after it
+        (a graph fork/join costs ~19 us, more than the overlap hides at this
+        size).  Pure stream work: capturable into one graph."""
         split = self._split()
+        if not self.comm_overlap:
+            self.forward_fc_backward()
+            self.conv_backward()
+            if self.ar_fused_sgd:
+                lr, mom, wd, gs, nes = self._opt_args()
+                self._xgmi.allreduce_sgd_(0, self.numel, params=self._params, mom=self.mom, lr_dev=self.lr_dev,
+                                          momentum=mom, weight_decay=wd, gscale=gs, nesterov=bool(nes),
+                                          zero_from=split, cursor=self.batch_idx, n_batches=self.n_batches)
+                return
+            self._xgmi.allreduce_(0, self.numel)
+            self.optimizer_step()
+            return
         cur = torch.cuda.current_stream(self.device)
         self.forward_fc_backward()
         self._side.wait_stream(cur)
@@ -353,9 +411,17 @@ class FusedMnistTrainer:
         self.optimizer_step()
 
     def _ddp_step(self):
-        """Bucket 0 (fc grads, 94% of the bytes) all-reduces on RCCL's
-        stream while the conv backward runs; bucket 1 follows; the
-        optimizer waits for both.  Valid eagerly and under graph capture."""
+        """RCCL: one all-reduce of the whole flat buffer after the backward
+        (default), or (``comm_overlap``) bucket 0 (fc grads, 94% of the
+        bytes) on RCCL's stream while the conv backward runs, then bucket 1;
+        the optimizer waits for both.  Valid eagerly and under graph
+        capture."""
+        if not self.comm_overlap:
+            self.forward_fc_backward()
+            self.conv_backward()
+            dist.all_reduce(self.grads)
+            self.optimizer_step()
+            return
         fc_b, conv_b = self._bucket_views()
         self.forward_fc_backward()
         w0 = dist.all_reduce(fc_b, async_op=True)
@@ -403,9 +469,56 @@ class FusedMnistTrainer:
             graphs = [ga, gb, gc]
         self._graphs = graphs
 
+    def _choose_schedule(self, reps: int = 8):
+        """Capture the step both ways (one whole-buffer all-reduce after the
+        backward / fc bucket overlapped on a side stream), time ``reps``
+        replays of each unrolled graph (max over ranks, same decision on
+        every rank), roll the training state back, keep the faster."""
+        import time
+
+        from ..utils import dist as pdist
+
+        state = (self._params, self.mom, self.grads, self.batch_idx, self.pending, self.batch_snap)
+        snap = [t.clone() for t in state]
+        res = {}
+        for ov in (False, True):
+            self.comm_overlap = ov
+            self._graphs, self._graph_unrolled = None, None
+            self._capture()
+            self._graph_unrolled.replay()  # warm
+            torch.cuda.synchronize(self.device)
+            pdist.barrier(self.device)
+            torch.cuda.synchronize(self.device)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                self._graph_unrolled.replay()
+            torch.cuda.synchronize(self.device)
+            t = pdist.all_reduce_max(time.perf_counter() - t0, self.device) / (reps * self.unroll)
+            res[ov] = (t, self._graphs, self._graph_unrolled)
+            for dst, src in zip(state, snap):
+                dst.copy_(src)
+            torch.cuda.synchronize(self.device)
+        best = min(res, key=lambda k: res[k][0])
+        self.comm_overlap = best
+        _, self._graphs, self._graph_unrolled = res[best]
+        self.comm_info["schedule"] = {"chosen": "overlap" if best else "sequential",
+                                      "sequential_us": round(res[False][0] * 1e6, 2),
+                                      "overlap_us": round(res[True][0] * 1e6, 2)}
+
     def _ensure_captured(self):
         if self._graphs is not None:
             return
+        if self.ddp and self.graph_mode == "full" and self.comm_overlap is None and self.unroll > 1:
+            try:
+                self._choose_schedule()
+                return
+            except Exception as e:  # noqa: BLE001 - fall back to the fixed schedule below
+                import warnings
+
+                warnings.warn(f"schedule autotune failed ({e}); using the sequential schedule")
+                torch.cuda.synchronize(self.device)
+                self.comm_overlap = False
+                self._graphs, self._graph_unrolled = None, None
         try:
             self._capture()
         except Exception as e:  # noqa: BLE001 - capture of collectives unsupported

@@ -30,6 +30,9 @@ def _worker(rank, world, port, q, comm):
     if comm == "xgmi-sgd-launch":  # all-reduce kernel without the optimizer epilogue + separate SGD launch
         comm = "xgmi"
         os.environ["PTO_AR_FUSED_SGD"] = "0"
+    if comm == "xgmi-overlap":  # fc bucket on a side stream under the conv backward, conv bucket after
+        comm = "xgmi"
+        os.environ["PTO_COMM_OVERLAP"] = "1"
     import torch.distributed as dist
 
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
@@ -49,12 +52,13 @@ def _worker(rank, world, port, q, comm):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("comm", ["rccl", "xgmi", "xgmi-sgd-launch"])
+@pytest.mark.parametrize("comm", ["rccl", "xgmi", "xgmi-sgd-launch", "xgmi-overlap"])
 def test_fused_ddp_two_ranks_matches_reference(comm):
     """comm=rccl: host collectives (gloo here) between split graphs;
-    comm=xgmi: peer-memory all-reduce kernels with the SGD epilogue inside
-    the whole-step graph (no optimizer launch); xgmi-sgd-launch: plain
-    all-reduce kernels + the multi-tensor SGD launch."""
+    comm=xgmi: one peer-memory all-reduce of the whole buffer with the SGD
+    epilogue inside the whole-step graph (no optimizer launch);
+    xgmi-sgd-launch: plain all-reduce kernel + the multi-tensor SGD launch;
+    xgmi-overlap: fc bucket on a side stream, conv bucket after."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
