@@ -32,6 +32,7 @@
 // the row constants -LSE and -delta are the accumulators' initial values.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -108,12 +109,14 @@ __device__ __forceinline__ bf16x8 row_operand(const char* tile, int r0, int ks) 
 // unconditionally (the last iteration re-reads its own tile): a
 // conditionally-filled struct/array is demoted to scratch by hipcc and
 // every load then waits vmcnt(0) before its scratch store.
+template <int NTH = NT>
 __device__ __forceinline__ uint4 tile_piece_load(const __bf16* base, long long rs, int p) {
-  const int c = threadIdx.x + NT * p, r = c >> 4, ch = c & 15;
+  const int c = threadIdx.x + NTH * p, r = c >> 4, ch = c & 15;
   return *reinterpret_cast<const uint4*>(base + (long long)r * rs + ch * 8);
 }
+template <int NTH = NT>
 __device__ __forceinline__ void tile_piece_store(char* tile, int p, uint4 v) {
-  const int c = threadIdx.x + NT * p, r = c >> 4, ch = c & 15;
+  const int c = threadIdx.x + NTH * p, r = c >> 4, ch = c & 15;
   *reinterpret_cast<uint4*>(tile + swz(r, ch)) = v;
 }
 #define TILE_LOAD(R, base, rs)              \
@@ -126,6 +129,21 @@ __device__ __forceinline__ void tile_piece_store(char* tile, int p, uint4 v) {
   tile_piece_store(tile, 1, R##1);      \
   tile_piece_store(tile, 2, R##2);      \
   tile_piece_store(tile, 3, R##3)
+// Same for a block of NTH threads (constexpr in scope): 1024 / NTH pieces.
+#define TILE_LOAD_W(R, base, rs)                                  \
+  R##0 = tile_piece_load<NTH>(base, rs, 0);                       \
+  R##1 = tile_piece_load<NTH>(base, rs, 1);                       \
+  if constexpr (NTH == 256) {                                     \
+    R##2 = tile_piece_load<NTH>(base, rs, 2);                     \
+    R##3 = tile_piece_load<NTH>(base, rs, 3);                     \
+  }
+#define TILE_STORE_W(R, tile)                                     \
+  tile_piece_store<NTH>(tile, 0, R##0);                           \
+  tile_piece_store<NTH>(tile, 1, R##1);                           \
+  if constexpr (NTH == 256) {                                     \
+    tile_piece_store<NTH>(tile, 2, R##2);                         \
+    tile_piece_store<NTH>(tile, 3, R##3);                         \
+  }
 
 struct AttnShape {
   int B, S, H, Hkv;
@@ -153,17 +171,19 @@ __device__ __forceinline__ BlockMap map_block(const AttnShape& sh, int per_pair)
 }
 
 // ------------------------------------------------------------------ forward
-__global__ __launch_bounds__(NT, 2) void k_attn_fwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+template <int NWV>
+__global__ __launch_bounds__(NWV * 64, 2) void k_attn_fwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                     const __bf16* __restrict__ v, __bf16* __restrict__ o,
                                                     float* __restrict__ lse, AttnShape sh) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [2 stages][K | V]
   const int G = sh.H / sh.Hkv;
-  const int per_pair = (sh.S / QT) * G / NW;
+  constexpr int NTH = NWV * 64;
+  const int per_pair = (sh.S / QT) * G / NWV;
   const BlockMap bm = map_block(sh, per_pair);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, hi = lane >> 5, ql = lane & 31;
-  const int u = bm.bi * NW + w, qt = u / G, h = bm.kvh * G + (u % G);
+  const int u = bm.bi * NWV + w, qt = u / G, h = bm.kvh * G + (u % G);
   const int q0 = qt * QT;
-  const int qt_max = (bm.bi * NW + NW - 1) / G;
+  const int qt_max = (bm.bi * NWV + NWV - 1) / G;
   const int ntiles = (qt_max * QT + QT + KT - 1) / KT;
   const long long tok0 = (long long)bm.b * sh.S;
 
@@ -185,10 +205,10 @@ __global__ __launch_bounds__(NT, 2) void k_attn_fwd(const __bf16* __restrict__ q
   const int qrow = q0 + ql;
 
   uint4 tk0, tk1, tk2, tk3, tv0, tv1, tv2, tv3;
-  TILE_LOAD(tk, kb, sh.k_rs);
-  TILE_LOAD(tv, vb, sh.v_rs);
-  TILE_STORE(tk, smem);
-  TILE_STORE(tv, smem + TILE_B);
+  TILE_LOAD_W(tk, kb, sh.k_rs);
+  TILE_LOAD_W(tv, vb, sh.v_rs);
+  TILE_STORE_W(tk, smem);
+  TILE_STORE_W(tv, smem + TILE_B);
   __syncthreads();
 
   // unrolled x2 so the LDS ring slot is a compile-time constant: the
@@ -200,8 +220,8 @@ __global__ __launch_bounds__(NT, 2) void k_attn_fwd(const __bf16* __restrict__ q
     const char* vtile = ktile + TILE_B;
     {  // next tile in flight during this tile's math (the last iteration re-reads its own)
       const int kn = (t + 1 < ntiles) ? k0 + KT : k0;
-      TILE_LOAD(tk, kb + (long long)kn * sh.k_rs, sh.k_rs);
-      TILE_LOAD(tv, vb + (long long)kn * sh.v_rs, sh.v_rs);
+      TILE_LOAD_W(tk, kb + (long long)kn * sh.k_rs, sh.k_rs);
+      TILE_LOAD_W(tv, vb + (long long)kn * sh.v_rs, sh.v_rs);
     }
     if (k0 <= q0 + QT - 1) {  // wave-uniform: this tile has unmasked keys for this wave
       // S^T (keys on registers, query on the lane)
@@ -267,8 +287,8 @@ __global__ __launch_bounds__(NT, 2) void k_attn_fwd(const __bf16* __restrict__ q
     }
     if (t + 1 < ntiles) {
       char* nt = smem + (SLOT ^ 1) * 2 * TILE_B;
-      TILE_STORE(tk, nt);
-      TILE_STORE(tv, nt + TILE_B);
+      TILE_STORE_W(tk, nt);
+      TILE_STORE_W(tv, nt + TILE_B);
     }
     __syncthreads();
     };
@@ -321,18 +341,20 @@ __global__ __launch_bounds__(256) void k_attn_bwd_delta(const __bf16* __restrict
 // Same decomposition as the forward.  Per key tile: S^T = K Q^T,
 // dP^T = V dO^T (V rows from LDS, dO fragments in registers),
 // P = exp2(S^T*c - lse2), dS = P (dP^T - delta), dQ^T += K^T dS^T.
-__global__ __launch_bounds__(NT, 2) void k_attn_bwd_dq(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+template <int NWV>
+__global__ __launch_bounds__(NWV * 64, 2) void k_attn_bwd_dq(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                        const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                        const float* __restrict__ lse, const float* __restrict__ delta,
                                                        __bf16* __restrict__ dq, long long dq_rs, AttnShape sh) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int G = sh.H / sh.Hkv;
-  const int per_pair = (sh.S / QT) * G / NW;
+  constexpr int NTH = NWV * 64;
+  const int per_pair = (sh.S / QT) * G / NWV;
   const BlockMap bm = map_block(sh, per_pair);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, hi = lane >> 5, ql = lane & 31;
-  const int u = bm.bi * NW + w, qt = u / G, h = bm.kvh * G + (u % G);
+  const int u = bm.bi * NWV + w, qt = u / G, h = bm.kvh * G + (u % G);
   const int q0 = qt * QT;
-  const int qt_max = (bm.bi * NW + NW - 1) / G;
+  const int qt_max = (bm.bi * NWV + NWV - 1) / G;
   const int ntiles = (qt_max * QT + QT + KT - 1) / KT;
   const long long tok0 = (long long)bm.b * sh.S;
   const __bf16* kb = k + tok0 * sh.k_rs + (long long)bm.kvh * HD;
@@ -357,10 +379,10 @@ __global__ __launch_bounds__(NT, 2) void k_attn_bwd_dq(const __bf16* __restrict_
   for (int db = 0; db < 4; ++db) acc[db] = (f32x16){};
 
   uint4 tk0, tk1, tk2, tk3, tv0, tv1, tv2, tv3;
-  TILE_LOAD(tk, kb, sh.k_rs);
-  TILE_LOAD(tv, vb, sh.v_rs);
-  TILE_STORE(tk, smem);
-  TILE_STORE(tv, smem + TILE_B);
+  TILE_LOAD_W(tk, kb, sh.k_rs);
+  TILE_LOAD_W(tv, vb, sh.v_rs);
+  TILE_STORE_W(tk, smem);
+  TILE_STORE_W(tv, smem + TILE_B);
   __syncthreads();
   // unrolled x2 so the LDS ring slot is a compile-time constant: the
   // lane-dependent LDS addresses stay loop-invariant (immediate offsets)
@@ -371,8 +393,8 @@ __global__ __launch_bounds__(NT, 2) void k_attn_bwd_dq(const __bf16* __restrict_
     const char* vtile = ktile + TILE_B;
     {
       const int kn = (t + 1 < ntiles) ? k0 + KT : k0;
-      TILE_LOAD(tk, kb + (long long)kn * sh.k_rs, sh.k_rs);
-      TILE_LOAD(tv, vb + (long long)kn * sh.v_rs, sh.v_rs);
+      TILE_LOAD_W(tk, kb + (long long)kn * sh.k_rs, sh.k_rs);
+      TILE_LOAD_W(tv, vb + (long long)kn * sh.v_rs, sh.v_rs);
     }
     if (k0 <= q0 + QT - 1) {
       const bool diag = k0 + KT - 1 > q0;
@@ -415,8 +437,8 @@ __global__ __launch_bounds__(NT, 2) void k_attn_bwd_dq(const __bf16* __restrict_
     }
     if (t + 1 < ntiles) {
       char* nt = smem + (SLOT ^ 1) * 2 * TILE_B;
-      TILE_STORE(tk, nt);
-      TILE_STORE(tv, nt + TILE_B);
+      TILE_STORE_W(tk, nt);
+      TILE_STORE_W(tv, nt + TILE_B);
     }
     __syncthreads();
     };
@@ -614,20 +636,57 @@ static AttnShape make_shape(int B, int S, int H, int Hkv, long long q_rs, long l
 
 // Returns -1 for unsupported shapes (S % 128, H % Hkv, head_dim != 128 is the
 // caller's contract).
+// Waves per forward / dQ block: 8 (two 32-row query tiles x the 4 heads of
+// a GQA group share each K/V tile: 4 waves per SIMD at the same 64 KB of
+// LDS) unless PTO_ATTN_WAVES=4 or the shape does not split into 8.
+static int attn_waves(const AttnShape& sh) {
+  static int env = -1;
+  if (env < 0) {
+    const char* e = getenv("PTO_ATTN_WAVES");
+    env = (e && atoi(e) == 4) ? 4 : 8;
+  }
+  const int G = sh.H / sh.Hkv;
+  return (env == 8 && ((sh.S / QT) * G) % 8 == 0) ? 8 : 4;
+}
+
+template <int NWV>
+static void launch_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const AttnShape& sh,
+                            hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_attn_fwd<NWV>, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE_B);
+    attr = true;
+  }
+  const int G = sh.H / sh.Hkv;
+  const int nblk = sh.B * sh.Hkv * ((sh.S / QT) * G / NWV);
+  hipLaunchKernelGGL(k_attn_fwd<NWV>, dim3(nblk), dim3(NWV * 64), 4 * TILE_B, s, (const __bf16*)q,
+                     (const __bf16*)k, (const __bf16*)v, (__bf16*)o, lse, sh);
+}
+
+template <int NWV>
+static void launch_attn_dq(const void* q, const void* k, const void* v, const void* dout, const float* lse,
+                           const float* delta, void* dq, long long dqkv_rs, const AttnShape& sh, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_attn_bwd_dq<NWV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              4 * TILE_B);
+    attr = true;
+  }
+  const int G = sh.H / sh.Hkv;
+  hipLaunchKernelGGL(k_attn_bwd_dq<NWV>, dim3(sh.B * sh.Hkv * ((sh.S / QT) * G / NWV)), dim3(NWV * 64), 4 * TILE_B,
+                     s, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta,
+                     (__bf16*)dq, dqkv_rs, sh);
+}
+
 PTO_API int pto_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H,
                          int Hkv, long long q_rs, long long k_rs, long long v_rs, long long o_rs, float scale,
                          hipStream_t s) {
   const AttnShape sh = make_shape(B, S, H, Hkv, q_rs, k_rs, v_rs, o_rs, scale);
   if (!attn_shape_ok(sh)) return -1;
-  const int G = H / Hkv;
-  const int nblk = B * Hkv * ((S / QT) * G / NW);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_attn_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE_B);
-    attr = true;
-  }
-  hipLaunchKernelGGL(k_attn_fwd, dim3(nblk), dim3(NT), 4 * TILE_B, s, (const __bf16*)q, (const __bf16*)k,
-                     (const __bf16*)v, (__bf16*)o, lse, sh);
+  if (attn_waves(sh) == 8)
+    launch_attn_fwd<8>(q, k, v, o, lse, sh, s);
+  else
+    launch_attn_fwd<4>(q, k, v, o, lse, sh, s);
   return (int)hipGetLastError();
 }
 
@@ -641,7 +700,6 @@ PTO_API int pto_attn_bwd(const void* q, const void* k, const void* v, const void
   if (!attn_shape_ok(sh)) return -1;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_attn_bwd_dq, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE_B);
     (void)hipFuncSetAttribute((const void*)k_attn_bwd_dkdv, hipFuncAttributeMaxDynamicSharedMemorySize,
                         4 * QTB + 2 * 128 * 4);
     attr = true;
@@ -649,12 +707,12 @@ PTO_API int pto_attn_bwd(const void* q, const void* k, const void* v, const void
   const long long rows = (long long)B * S * H;
   hipLaunchKernelGGL(k_attn_bwd_delta, dim3((unsigned)((rows + 7) / 8)), dim3(256), 0, s, (const __bf16*)o,
                      (const __bf16*)dout, delta, sh);
-  const int G = H / Hkv;
   hipLaunchKernelGGL(k_attn_bwd_dkdv, dim3(B * Hkv * (S / KB)), dim3(NT), 4 * QTB + 2 * 128 * 4, s,
                      (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta,
                      (__bf16*)dk, (__bf16*)dv, dqkv_rs, sh);
-  hipLaunchKernelGGL(k_attn_bwd_dq, dim3(B * Hkv * ((S / QT) * G / NW)), dim3(NT), 4 * TILE_B, s,
-                     (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta,
-                     (__bf16*)dq, dqkv_rs, sh);
+  if (attn_waves(sh) == 8)
+    launch_attn_dq<8>(q, k, v, dout, lse, delta, dq, dqkv_rs, sh, s);
+  else
+    launch_attn_dq<4>(q, k, v, dout, lse, delta, dq, dqkv_rs, sh, s);
   return (int)hipGetLastError();
 }
