@@ -533,6 +533,7 @@ struct EpiStore {
   PTO_DEV void operator()(int m, int n, float v) const { out[m * ld + n] = v; }
 };
 
+
 // y[M,N] = act(x[M,K] @ w[N,K]^T + b): generic fp32 linear (fc1 and the
 // nn.Module path).  One 16x16 output tile per block, K split over 4 waves.
 __global__ __launch_bounds__(256) void k_linear_fwd(const float* __restrict__ x, const float* __restrict__ w,
@@ -1135,13 +1136,52 @@ __global__ __launch_bounds__(256) void k_conv1_bwd_sgd(const float* __restrict__
                                                        const long long* __restrict__ bidx, int nconv,
                                                        float* __restrict__ p, float* __restrict__ g,
                                                        float* __restrict__ m, long long nflat, long long zero_from,
-                                                       SgdArgs a) {
-  if ((int)blockIdx.x < nconv) {
-    conv1_bwd_block(blockIdx.x, g1, code1, x, gw1, gb1, B, bidx);
+                                                       SgdArgs a, int ndw, const float* __restrict__ dh1,
+                                                       const float* __restrict__ a2p, long long skip_lo,
+                                                       long long skip_hi, int nsgd_lo) {
+  int bid = blockIdx.x;
+  if (bid < nconv) {
+    conv1_bwd_block(bid, g1, code1, x, gw1, gb1, B, bidx);
     return;
   }
-  const long long i = ((long long)(blockIdx.x - nconv) * 256 + threadIdx.x) * 4;
-  if (i < nflat) sgd_flat4(p, g, m, i, *a.lr, a, i >= zero_from);
+  bid -= nconv;
+  if (bid < ndw) {  // dW1 = dh1^T a2p (K = B, 4 tiles per block) consumed by SGD on fc1.weight = [skip_lo, skip_hi)
+    // one 16x16 tile per wave; the wave's p/m elements are loaded before the
+    // MMA chain so their latency overlaps the operand loads
+    constexpr int MT = (F1OUT + 15) / 16, NT = (F1IN + 15) / 16;
+    const int tile = bid * 4 + (threadIdx.x >> 6);
+    if (tile >= MT * NT) return;
+    const int mt = tile % MT, nt = tile / MT, lane = threadIdx.x & 63;
+    const int n = nt * 16 + (lane & 15);
+    float* pw = p + skip_lo;
+    float* mw = m + skip_lo;
+    float pv[4], mv[4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int r = mt * 16 + (lane >> 4) * 4 + rr;
+      const bool ok = r < F1OUT && n < F1IN;
+      pv[rr] = ok ? pw[r * F1IN + n] : 0.f;
+      mv[rr] = ok ? mw[r * F1IN + n] : 0.f;
+    }
+    const float lr = *a.lr;
+    const f32x4 acc = wave_tile_16x16<LAY_KROW, LAY_KROW, 8>(dh1, F1OUT, a2p, F1IN, F1OUT, F1IN, B, mt * 16, nt * 16,
+                                                             0, B);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int r = mt * 16 + (lane >> 4) * 4 + rr;
+      if (r < F1OUT && n < F1IN) {
+        sgd_elem(pv[rr], acc[rr], mv[rr], lr, a.mom, a.wd, a.gscale, a.nesterov);
+        pw[r * F1IN + n] = pv[rr];
+        mw[r * F1IN + n] = mv[rr];
+      }
+    }
+    return;
+  }
+  bid -= ndw;
+  // flat SGD over [0, nflat) minus [skip_lo, skip_hi): nsgd_lo blocks below, the rest above
+  const long long i = bid < nsgd_lo ? ((long long)bid * 256 + threadIdx.x) * 4
+                                    : skip_hi + ((long long)(bid - nsgd_lo) * 256 + threadIdx.x) * 4;
+  if (bid < nsgd_lo ? i < skip_lo : i < nflat) sgd_flat4(p, g, m, i, *a.lr, a, i >= zero_from);
 }
 
 // Host-side flush of an owed conv1 update (before the parameters are read
@@ -1391,7 +1431,44 @@ PTO_API int pto_conv1_bwd_sgd(const float* g1, const uint8_t* code1, const float
   const int nconv = C1 * ((B + B1_CHUNK - 1) / B1_CHUNK);
   const int nsgd = (int)((nflat / 4 + 255) / 256);
   hipLaunchKernelGGL(k_conv1_bwd_sgd, dim3(nconv + nsgd), dim3(256), 0, s, g1, code1, x, gw1, gb1, B, bidx, nconv, p,
-                     g, m, nflat, zero_from, sgd_args(lr, mom, wd, gscale, nesterov));
+                     g, m, nflat, zero_from, sgd_args(lr, mom, wd, gscale, nesterov), 0, nullptr, nullptr, nflat,
+                     nflat, nsgd);
+  LAUNCH_CHECK();
+}
+
+// B1 with fc1's weight gradient moved out of B3: extra blocks compute
+// dW1 = dh1^T a2p and apply SGD to fc1.weight (flat range [w1_off,
+// w1_off + 500*800)) straight from the MMA accumulators, so that gradient is
+// never written or re-read (and its grad slot is left untouched).  The flat
+// SGD blocks skip that range.  Single-process schedule only: with DDP the
+// gradient must exist for the all-reduce.
+PTO_API int pto_conv1_bwd_sgd_dw1(const float* g1, const uint8_t* code1, const float* x, float* gw1, float* gb1,
+                                  int B, const long long* bidx, float* p, float* g, float* m, long long nflat,
+                                  long long zero_from, const float* dh1, const float* a2p, long long w1_off,
+                                  const float* lr, float mom, float wd, float gscale, int nesterov, hipStream_t s) {
+  const long long w1_end = w1_off + (long long)F1OUT * F1IN;
+  if (nflat % 4 || zero_from % 4 || w1_off % 4 || w1_end > nflat ||
+      ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m)) & 15))
+    return -1;
+  const int nconv = C1 * ((B + B1_CHUNK - 1) / B1_CHUNK);
+  const int ndw = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
+  const int nsgd_lo = (int)((w1_off / 4 + 255) / 256);
+  const int nsgd_hi = (int)(((nflat - w1_end) / 4 + 255) / 256);
+  hipLaunchKernelGGL(k_conv1_bwd_sgd, dim3(nconv + ndw + nsgd_lo + nsgd_hi), dim3(256), 0, s, g1, code1, x, gw1, gb1,
+                     B, bidx, nconv, p, g, m, nflat, zero_from, sgd_args(lr, mom, wd, gscale, nesterov), ndw, dh1, a2p,
+                     w1_off, w1_end, nsgd_lo);
+  LAUNCH_CHECK();
+}
+
+// B3 without fc1's weight gradient (it moved into pto_conv1_bwd_sgd_dw1).
+PTO_API int pto_fc_bwd_adv_nodw1(const float* dh1, const float* a2p, const float* w1, const float* h1,
+                                 const float* dlogits, float* gb1, float* gw2, float* gb2, float* da2p, int B,
+                                 long long* bidx, long long nbatches, int* pending, hipStream_t s) {
+  const int nB = ((B + 15) / 16) * ((F1IN + 15) / 16);
+  const int nW = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4;
+  const int nS = 8 + 1;
+  hipLaunchKernelGGL(k_fc_bwd, dim3(nB + nW + nS), dim3(256), 0, s, dh1, a2p, w1, h1, dlogits, nullptr, gb1, gw2,
+                     gb2, da2p, B, 0, nB, nW, bidx, nbatches, pending);
   LAUNCH_CHECK();
 }
 
@@ -1403,7 +1480,8 @@ PTO_API int pto_sgd_flat(float* p, float* g, float* m, long long n, long long ze
   if (n == 0) return 0;
   const int nsgd = (int)((n / 4 + 255) / 256);
   hipLaunchKernelGGL(k_conv1_bwd_sgd, dim3(nsgd), dim3(256), 0, s, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
-                     nullptr, 0, p, g, m, n, zero_from, sgd_args(lr, mom, wd, gscale, nesterov));
+                     nullptr, 0, p, g, m, n, zero_from, sgd_args(lr, mom, wd, gscale, nesterov), 0, nullptr, nullptr,
+                     n, n, nsgd);
   LAUNCH_CHECK();
 }
 

@@ -95,6 +95,8 @@ _SIGS = {
     "pto_conv1_commit": [_P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _P],
     "pto_fc_bwd_adv": [_P] * 10 + [_I, _P, _L, _P, _P],
     "pto_conv1_bwd_sgd": [_P] * 5 + [_I, _P, _P, _P, _P, _L, _L, _P, _F, _F, _F, _I, _P],
+    "pto_conv1_bwd_sgd_dw1": [_P] * 5 + [_I, _P, _P, _P, _P, _L, _L, _P, _P, _L, _P, _F, _F, _F, _I, _P],
+    "pto_fc_bwd_adv_nodw1": [_P] * 9 + [_I, _P, _L, _P, _P],
     "pto_sgd_flat": [_P, _P, _P, _L, _L, _P, _F, _F, _F, _I, _P],
     "pto_fc_bwd_part": [_P] * 10 + [_I, _P, _L, _P, _I, _P],
     "pto_eval_head": [_P, _P, _P, _I, _P],

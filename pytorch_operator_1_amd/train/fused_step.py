@@ -130,6 +130,12 @@ class FusedMnistTrainer:
         # (89.8 vs 54.5 us/step measured)
         self._bwd_side = (torch.cuda.Stream(device)
                           if self.fused_opt and os.environ.get("PTO_SPLIT_BWD", "0") == "1" else None)
+        # fc1's weight gradient computed in B1 and consumed there by the SGD
+        # epilogue (never stored), instead of stored by B3 and re-read by B1's
+        # SGD blocks (PTO_DW1_SGD=0: the B3 path).  The fc1.weight slot of the
+        # gradient buffer is then not maintained.
+        self.dw1_sgd = (self.fused_opt and self._bwd_side is None
+                        and os.environ.get("PTO_DW1_SGD", "1") == "1")
         # multi-GPU schedule: overlap the fc bucket's all-reduce with the conv
         # backward on a side stream (PTO_COMM_OVERLAP=1), or all-reduce the
         # whole flat buffer once after the backward on the compute stream
@@ -232,6 +238,10 @@ class FusedMnistTrainer:
             fc_args = (self.dh1.data_ptr(), self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), self.h1.data_ptr(),
                        self.dlogits.data_ptr(), G["fc1.weight"].data_ptr(), G["fc1.bias"].data_ptr(),
                        G["fc2.weight"].data_ptr(), G["fc2.bias"].data_ptr(), self.da2p.data_ptr(), B)
+            if self.dw1_sgd:
+                c(L.pto_fc_bwd_adv_nodw1(fc_args[0], fc_args[1], fc_args[2], fc_args[3], fc_args[4], *fc_args[6:],
+                                         bi, self.n_batches, self.pending.data_ptr(), s), "fc_bwd_adv_nodw1")
+                return
             if self._bwd_side is None:
                 c(L.pto_fc_bwd_adv(*fc_args, bi, self.n_batches, self.pending.data_ptr(), s), "fc_bwd_adv")
                 return
@@ -280,6 +290,14 @@ class FusedMnistTrainer:
                           P["conv2.weight"].data_ptr(), G["conv2.weight"].data_ptr(), G["conv2.bias"].data_ptr(),
                           self.da1p.data_ptr(), B, 7, None, None, None, None, None, s), "conv2_bwd")
         if self.fused_opt:  # + the fc/conv2 update (grads final since B3/B2); B1 reads the cursor snapshot
+            if self.dw1_sgd:
+                c(L.pto_conv1_bwd_sgd_dw1(self.da1p.data_ptr(), self.code1.data_ptr(), self.data.data_ptr(),
+                                          G["conv1.weight"].data_ptr(), G["conv1.bias"].data_ptr(), B,
+                                          self.batch_snap.data_ptr(), self._params.data_ptr(), self.grads.data_ptr(),
+                                          self.mom.data_ptr(), self._c1, self._split(), self.dh1.data_ptr(),
+                                          self.a2p.data_ptr(), param_offsets()[0]["fc1.weight"][0],
+                                          *self._opt_args(), s), "conv1_bwd_sgd_dw1")
+                return
             if self._bwd_side is None:
                 c(L.pto_conv1_bwd_sgd(self.da1p.data_ptr(), self.code1.data_ptr(), self.data.data_ptr(),
                                       G["conv1.weight"].data_ptr(), G["conv1.bias"].data_ptr(), B,

@@ -123,3 +123,26 @@ def test_fused_optimizer_schedule_matches_sgd_launch(graph, unroll):
         t.run(3)
     assert rel(a.params, b.params) < 1e-5
     assert abs(a.last_loss() - b.last_loss()) < 1e-4
+
+
+@pytest.mark.gpu
+def test_dw1_sgd_epilogue_matches_b3_path(monkeypatch):
+    """fc1's weight gradient consumed by the SGD epilogue inside B1
+    (PTO_DW1_SGD=1, never stored) updates the parameters exactly like the
+    path that stores it in B3 and re-reads it in B1's SGD blocks."""
+    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+
+    dev = torch.device("cuda", 0)
+    kw = dict(batch_size=4, dataset_size=4 * 9, seed=5, graph="full", unroll=4, weight_decay=1e-4)
+    monkeypatch.setenv("PTO_DW1_SGD", "1")
+    a = FusedMnistTrainer(dev, fused_opt=True, **kw)
+    monkeypatch.setenv("PTO_DW1_SGD", "0")
+    b = FusedMnistTrainer(dev, fused_opt=True, **kw)
+    assert a.dw1_sgd and not b.dw1_sgd
+    for t in (a, b):
+        t.run(9)
+    torch.cuda.synchronize()
+    for name in a.p:
+        assert rel(a.p[name], b.p[name]) < 1e-5, name
+    assert rel(a.mom, b.mom) < 1e-4
+    assert abs(a.last_loss() - b.last_loss()) < 1e-5
