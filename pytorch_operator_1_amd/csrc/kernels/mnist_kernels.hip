@@ -71,6 +71,7 @@ struct LazyConv1 {
   const int* pending;   // nullptr: plain forward
   SgdArgs a;
   int bias_off;
+  float* xout;          // nullptr, or [B][784]: the batch's images copied out for B1 (no cursor hop there)
 };
 struct Conv1Commit {
   float* p;             // flat conv1 range [0, n) of params / grads / momentum
@@ -414,7 +415,10 @@ __global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x
         d[0] = wv[q].x; d[1] = wv[q].y; d[2] = wv[q].z; d[3] = wv[q].w;
       }
     }
-    if (tid < 196) reinterpret_cast<float4*>(xs)[tid] = xv;
+    if (tid < 196) {
+      reinterpret_cast<float4*>(xs)[tid] = xv;
+      if (lz.xout && nt == 0) reinterpret_cast<float4*>(lz.xout + b * 784)[tid] = xv;
+    }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int e = tid + 512 * q;
@@ -1288,13 +1292,27 @@ PTO_API int pto_conv12_fwd_lazy(const float* x, const float* w1, const float* b1
                                 float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B, const long long* bidx,
                                 const float* g1f, const float* m1f, int bias_off, const int* pending, const float* lr,
                                 float mom, float wd, float gscale, int nesterov, int version, hipStream_t s) {
-  LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off};
+  LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off, nullptr};
   if (version == 2)
     hipLaunchKernelGGL(k_conv12_fwd2, dim3(B * 4), dim3(512), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B,
                        bidx, lz);
   else
     hipLaunchKernelGGL(k_conv12_fwd, dim3(B * 4), dim3(256), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B,
                        bidx, lz);
+  LAUNCH_CHECK();
+}
+
+// Version-2 F1+F2 launch that also copies the batch's images to xout, so
+// the conv1 weight-gradient blocks of B1 read them without the dependent
+// batch-cursor load.
+PTO_API int pto_conv12_fwd_lazy_x(const float* x, const float* w1, const float* b1, const float* w2,
+                                  const float* b2, float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B,
+                                  const long long* bidx, const float* g1f, const float* m1f, int bias_off,
+                                  const int* pending, const float* lr, float mom, float wd, float gscale, int nesterov,
+                                  float* xout, hipStream_t s) {
+  LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off, xout};
+  hipLaunchKernelGGL(k_conv12_fwd2, dim3(B * 4), dim3(512), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B,
+                     bidx, lz);
   LAUNCH_CHECK();
 }
 

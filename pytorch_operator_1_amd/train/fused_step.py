@@ -136,6 +136,11 @@ class FusedMnistTrainer:
         # gradient buffer is then not maintained.
         self.dw1_sgd = (self.fused_opt and self._bwd_side is None
                         and os.environ.get("PTO_DW1_SGD", "1") == "1")
+        # F1 copies the batch's images out for B1 (PTO_XCUR=0: B1 re-reads
+        # them through the batch cursor)
+        self.xcur = (torch.empty(self.B * 784, device=device)
+                     if self.dw1_sgd and self.conv12_version == 2 and os.environ.get("PTO_XCUR", "1") == "1"
+                     else None)
         # multi-GPU schedule: overlap the fc bucket's all-reduce with the conv
         # backward on a side stream (PTO_COMM_OVERLAP=1), or all-reduce the
         # whole flat buffer once after the backward on the compute stream
@@ -222,11 +227,15 @@ class FusedMnistTrainer:
         bi = self.batch_idx.data_ptr()
         if self.fused_opt:
             o = self._opt_args()
-            c(L.pto_conv12_fwd_lazy(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
-                                    P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
-                                    self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi,
-                                    self.grads[self._c1:].data_ptr(), self.mom[self._c1:].data_ptr(), self._c1_bias,
-                                    self.pending.data_ptr(), *o, self.conv12_version, s), "conv12_fwd_lazy")
+            f12 = (self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
+                   P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
+                   self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi,
+                   self.grads[self._c1:].data_ptr(), self.mom[self._c1:].data_ptr(), self._c1_bias,
+                   self.pending.data_ptr(), *o)
+            if self.xcur is not None:
+                c(L.pto_conv12_fwd_lazy_x(*f12, self.xcur.data_ptr(), s), "conv12_fwd_lazy_x")
+            else:
+                c(L.pto_conv12_fwd_lazy(*f12, self.conv12_version, s), "conv12_fwd_lazy")
             c(L.pto_linear_fwd(self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
                                self.h1.data_ptr(), B, 500, 800, 1, s), "fc1_fwd")
             c(L.pto_fc2_ce_commit(self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
@@ -291,9 +300,11 @@ class FusedMnistTrainer:
                           self.da1p.data_ptr(), B, 7, None, None, None, None, None, s), "conv2_bwd")
         if self.fused_opt:  # + the fc/conv2 update (grads final since B3/B2); B1 reads the cursor snapshot
             if self.dw1_sgd:
-                c(L.pto_conv1_bwd_sgd_dw1(self.da1p.data_ptr(), self.code1.data_ptr(), self.data.data_ptr(),
+                xb = (self.xcur.data_ptr(), None) if self.xcur is not None else (self.data.data_ptr(),
+                                                                                   self.batch_snap.data_ptr())
+                c(L.pto_conv1_bwd_sgd_dw1(self.da1p.data_ptr(), self.code1.data_ptr(), xb[0],
                                           G["conv1.weight"].data_ptr(), G["conv1.bias"].data_ptr(), B,
-                                          self.batch_snap.data_ptr(), self._params.data_ptr(), self.grads.data_ptr(),
+                                          xb[1], self._params.data_ptr(), self.grads.data_ptr(),
                                           self.mom.data_ptr(), self._c1, self._split(), self.dh1.data_ptr(),
                                           self.a2p.data_ptr(), param_offsets()[0]["fc1.weight"][0],
                                           *self._opt_args(), s), "conv1_bwd_sgd_dw1")

@@ -8,8 +8,8 @@ timeout -k 10 300 python -u -m pytest tests/test_graph_gpu.py tests/test_kernels
 grep -E "passed|failed" gpurun_out/pytest_dw1.log | tail -2
 for r in 1; do
   for v in 0 1; do
-    PTO_DW1_SGD=$v timeout -k 10 120 python bench.py --steps 4000 --warmup 300 > gpurun_out/bench_dw1_$v.json 2> gpurun_out/bench_dw1_$v.err
-    python -c "import json;d=json.load(open('gpurun_out/bench_dw1_$v.json'));print('dw1=$v', d['value'], d['ms_per_step'])"
+    PTO_XCUR=$v timeout -k 10 120 python bench.py --steps 4000 --warmup 300 > gpurun_out/bench_dw1_$v.json 2> gpurun_out/bench_dw1_$v.err
+    python -c "import json;d=json.load(open('gpurun_out/bench_dw1_$v.json'));print('xcur=$v', d['value'], d['ms_per_step'])"
   done
 done
 R="$GRAFT_REPO_ROOT"

@@ -53,9 +53,12 @@ def _captured_ddp_worker(port, q):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", device_id=dev)
-    ddp = FusedMnistTrainer(dev, dataset_size=64 * 10, seed=3, force_ddp=True, unroll=4)
+    # B=4: one fp32-atomic add per gradient address, so neither trainer has
+    # run-to-run noise (at B=64 the atomics' arrival order varies and 10
+    # steps amplify last-bit differences to ~1e-5)
+    ddp = FusedMnistTrainer(dev, batch_size=4, dataset_size=4 * 10, seed=3, force_ddp=True, unroll=4)
     assert ddp.graph_mode == "full"
-    ref = FusedMnistTrainer(dev, dataset_size=64 * 10, seed=3, graph="none")
+    ref = FusedMnistTrainer(dev, batch_size=4, dataset_size=4 * 10, seed=3, graph="none")
     ddp.run(10)
     for _ in range(10):
         ref.step()
@@ -138,7 +141,7 @@ def test_dw1_sgd_epilogue_matches_b3_path(monkeypatch):
     a = FusedMnistTrainer(dev, fused_opt=True, **kw)
     monkeypatch.setenv("PTO_DW1_SGD", "0")
     b = FusedMnistTrainer(dev, fused_opt=True, **kw)
-    assert a.dw1_sgd and not b.dw1_sgd
+    assert a.dw1_sgd and not b.dw1_sgd and a.xcur is not None
     for t in (a, b):
         t.run(9)
     torch.cuda.synchronize()
