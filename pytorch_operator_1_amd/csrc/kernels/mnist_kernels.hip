@@ -591,7 +591,8 @@ __global__ __launch_bounds__(256) void k_relu_bwd(const float* __restrict__ g, c
 PTO_DEV void fc2_ce_row(int row, int lane, const float* __restrict__ h1, const float* __restrict__ w,
                         const float* __restrict__ bias, const int64_t* __restrict__ labels,
                         float* __restrict__ logp, float* __restrict__ loss_rows, float* __restrict__ dlogits,
-                        float* __restrict__ dh1, int B, float inv_b, const long long* __restrict__ bidx) {
+                        float* __restrict__ dh1, int B, float inv_b, const long long* __restrict__ bidx,
+                        float* dh1_row_lds = nullptr) {
   float h[8], wv[NCLS][8], bz[NCLS];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -647,7 +648,7 @@ PTO_DEV void fc2_ce_row(int row, int lane, const float* __restrict__ h1, const f
       if (c == y) zy = z[c];
     loss_rows[row] = lse - zy;
   }
-  if (!dh1) return;
+  if (!dh1 && !dh1_row_lds) return;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int k = lane + 64 * j;
@@ -655,7 +656,9 @@ PTO_DEV void fc2_ce_row(int row, int lane, const float* __restrict__ h1, const f
       float s = 0.f;
 #pragma unroll
       for (int c = 0; c < NCLS; ++c) s = fmaf(dl[c], wv[c][j], s);
-      dh1[row * F1OUT + k] = h[j] > 0.f ? s : 0.f;
+      const float v = h[j] > 0.f ? s : 0.f;
+      if (dh1) dh1[row * F1OUT + k] = v;
+      if (dh1_row_lds) dh1_row_lds[k] = v;
     }
   }
 }
@@ -677,6 +680,58 @@ __global__ __launch_bounds__(256) void k_fc2_ce(const float* __restrict__ h1, co
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= B) return;
   fc2_ce_row(row, lane, h1, w, bias, labels, logp, loss_rows, dlogits, dh1, B, inv_b, bidx);
+}
+
+// F4 + the critical part of B3 in one launch (single-process schedule with
+// fc1's weight gradient in B1): block (mt, nt) = 16 waves; wave w runs the
+// fc2 + log_softmax + NLL + dlogits + dh1 head of row mt*16+w into LDS (the
+// nt == 0 blocks also store loss/dlogits/dh1 for B2/B1), then the 16 waves
+// split K = 500 of the d(a2p) tile [16 rows, 16 cols] = dh1 W1.  The head is
+// recomputed per column tile (50x, ~1 us of dependent latency either way)
+// so the F4 -> B3 launch boundary disappears.  The all-row reductions of B3
+// (dW2, db1, db2) run in B2's launch.  Extra last block: conv1 commit.
+constexpr int FDX_WAVES = 16;
+__global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx(
+    const float* __restrict__ h1, const float* __restrict__ w2, const float* __restrict__ b2,
+    const int64_t* __restrict__ labels, const float* __restrict__ w1, float* __restrict__ loss_rows,
+    float* __restrict__ dlogits, float* __restrict__ dh1, float* __restrict__ da2p, int B, float inv_b,
+    const long long* __restrict__ bidx, Conv1Commit cm) {
+  __shared__ __attribute__((aligned(16))) float dh1s[16 * F1OUT];
+  __shared__ float red[FDX_WAVES * 256];
+  const int mtiles = (B + 15) >> 4, ntiles = (F1IN + 15) >> 4;
+  const int t = threadIdx.x;
+  if (blockIdx.x == (unsigned)(mtiles * ntiles)) {  // conv1 commit (F1 of this step applied it on the fly)
+    if (cm.pending && *cm.pending) {
+      const float lr = *cm.a.lr;
+      for (int i = 4 * t; i < cm.n; i += 4 * FDX_WAVES * 64) sgd_flat4(cm.p, cm.g, cm.m, i, lr, cm.a);
+    }
+    return;
+  }
+  const int mt = blockIdx.x % mtiles, nt = blockIdx.x / mtiles;
+  const int w = t >> 6, lane = t & 63;
+  const int row = mt * 16 + w;
+  float* srow = dh1s + w * F1OUT;
+  if (row < B) {
+    const bool st = nt == 0;
+    fc2_ce_row(row, lane, h1, w2, b2, labels, nullptr, st ? loss_rows : nullptr, st ? dlogits : nullptr,
+               st ? dh1 : nullptr, B, inv_b, bidx, srow);
+  } else {
+    for (int k = lane; k < F1OUT; k += 64) srow[k] = 0.f;
+  }
+  __syncthreads();
+  constexpr int KC = ((F1OUT + FDX_WAVES - 1) / FDX_WAVES + 15) & ~15;  // 32
+  const f32x4 acc = wave_tile_16x16<LAY_ROWK, LAY_KROW, KC / 16>(dh1s, F1OUT, w1, F1IN, 16, F1IN, F1OUT, 0, nt * 16,
+                                                                 w * KC, (w + 1) * KC);
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) red[w * 256 + ((lane >> 4) * 4 + rr) * 16 + (lane & 15)] = acc[rr];
+  __syncthreads();
+  if (t < 256) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < FDX_WAVES; ++q) v += red[q * 256 + t];
+    const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
+    if (m < B && n < F1IN) da2p[m * F1IN + n] = v;
+  }
 }
 
 // F3+F4 in one launch: the fc1 tiles as k_linear_fwd_vec, then the LAST
@@ -779,7 +834,10 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
                                                    float* __restrict__ da1p, int B, int nA, int nB, int nC,
                                                    const float* __restrict__ x, const long long* __restrict__ bidx,
                                                    const uint8_t* __restrict__ code1, float* __restrict__ gw1,
-                                                   float* __restrict__ gb1) {
+                                                   float* __restrict__ gb1, int nF, const float* __restrict__ fdh1,
+                                                   const float* __restrict__ fh1, const float* __restrict__ fdl,
+                                                   float* __restrict__ fgw2, float* __restrict__ fgb1,
+                                                   float* __restrict__ fgb2) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int bid = blockIdx.x;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1037,7 +1095,19 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
     }
     s = wave_sum(s);
     if (lane == 0) gb2[oc] = s;
+    return;
   }
+  bid -= nC;
+  if (bid >= nF) return;
+  // ---- part F (k_fc2_ce_dx schedule): B3's all-row reductions dW2, db1, db2
+  constexpr int NWF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4;
+  if (bid < NWF) {
+    block_gemm_4tiles<LAY_KROW, LAY_KROW>(fdl, NCLS, fh1, F1OUT, NCLS, F1OUT, B, bid, EpiStore{fgw2, F1OUT});
+    return;
+  }
+  bid -= NWF;
+  if (bid < 8) block_colsum64(fdh1, F1OUT, B, F1OUT, bid * 64, smem, fgb1);
+  else block_colsum64(fdl, NCLS, B, NCLS, 0, smem, fgb2);
 }
 
 // ---------------------------------------------------------------- B1 ----
@@ -1142,8 +1212,13 @@ __global__ __launch_bounds__(256) void k_conv1_bwd_sgd(const float* __restrict__
                                                        float* __restrict__ m, long long nflat, long long zero_from,
                                                        SgdArgs a, int ndw, const float* __restrict__ dh1,
                                                        const float* __restrict__ a2p, long long skip_lo,
-                                                       long long skip_hi, int nsgd_lo) {
+                                                       long long skip_hi, int nsgd_lo, long long* __restrict__ adv,
+                                                       long long nbatches, int* __restrict__ set_pending) {
   int bid = blockIdx.x;
+  if (bid == 0 && threadIdx.x == 0) {  // no block of this launch reads the cursor (x comes from xout)
+    if (adv) *adv = (*adv + 1) % nbatches;
+    if (set_pending) *set_pending = 1;
+  }
   if (bid < nconv) {
     conv1_bwd_block(bid, g1, code1, x, gw1, gb1, B, bidx);
     return;
@@ -1427,7 +1502,38 @@ PTO_API int pto_conv2_bwd(const float* g2, const uint8_t* code2, const float* a1
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;
   if (nA + nB + nC == 0) return 0;
   hipLaunchKernelGGL(k_conv2_bwd, dim3(nA + nB + nC), dim3(256), lds, s, g2, code2, a1p, w2, gw2, gb2, da1p, B, nA,
-                     nB, nC, x, bidx, code1, (parts & 2) ? gw1 : nullptr, gb1);
+                     nB, nC, x, bidx, code1, (parts & 2) ? gw1 : nullptr, gb1, 0, nullptr, nullptr, nullptr, nullptr,
+                     nullptr, nullptr);
+  LAUNCH_CHECK();
+}
+
+// Full conv2 backward + the fc layers' all-row reductions (dW2 = dlogits^T
+// h1, db1, db2) for the k_fc2_ce_dx schedule.
+PTO_API int pto_conv2_bwd_fc(const float* g2, const uint8_t* code2, const float* a1p, const float* w2, float* gw2,
+                             float* gb2, float* da1p, int B, const float* dh1, const float* h1, const float* dlogits,
+                             float* fgw2, float* fgb1, float* fgb2, hipStream_t s) {
+  const int nA = ((B + B2_CHUNK - 1) / B2_CHUNK) * 32;
+  const int nB = B * B2_ICG;
+  const int nC = (C2 + 3) / 4;
+  const int nF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9;
+  const size_t ldsA = B2_CHUNK * (288 + F1IN + F1IN / 4) * sizeof(float);
+  const size_t ldsB = (52 * 68 + 64 * 65 + F1IN + F1IN / 4) * sizeof(float);
+  const size_t lds = ldsA > ldsB ? ldsA : ldsB;
+  hipLaunchKernelGGL(k_conv2_bwd, dim3(nA + nB + nC + nF), dim3(256), lds, s, g2, code2, a1p, w2, gw2, gb2, da1p, B,
+                     nA, nB, nC, nullptr, nullptr, nullptr, nullptr, nullptr, nF, dh1, h1, dlogits, fgw2, fgb1, fgb2);
+  LAUNCH_CHECK();
+}
+
+// F4 + d(a2p) (k_fc2_ce_dx) + the conv1 commit block.
+PTO_API int pto_fc2_ce_dx(const float* h1, const float* w2, const float* b2, const int64_t* labels, const float* w1,
+                          float* loss_rows, float* dlogits, float* dh1, float* da2p, int B, float inv_b,
+                          const long long* bidx, float* p1, float* g1, float* m1, int n1, const int* pending,
+                          const float* lr, float mom, float wd, float gscale, int nesterov, hipStream_t s) {
+  if (n1 % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1)) & 15)) return -1;
+  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), nullptr, nullptr};
+  const int nblk = ((B + 15) / 16) * ((F1IN + 15) / 16);
+  hipLaunchKernelGGL(k_fc2_ce_dx, dim3(nblk + 1), dim3(FDX_WAVES * 64), 0, s, h1, w2, b2, labels, w1, loss_rows,
+                     dlogits, dh1, da2p, B, inv_b, bidx, cm);
   LAUNCH_CHECK();
 }
 
@@ -1450,7 +1556,7 @@ PTO_API int pto_conv1_bwd_sgd(const float* g1, const uint8_t* code1, const float
   const int nsgd = (int)((nflat / 4 + 255) / 256);
   hipLaunchKernelGGL(k_conv1_bwd_sgd, dim3(nconv + nsgd), dim3(256), 0, s, g1, code1, x, gw1, gb1, B, bidx, nconv, p,
                      g, m, nflat, zero_from, sgd_args(lr, mom, wd, gscale, nesterov), 0, nullptr, nullptr, nflat,
-                     nflat, nsgd);
+                     nflat, nsgd, nullptr, 1LL, nullptr);
   LAUNCH_CHECK();
 }
 
@@ -1463,7 +1569,9 @@ PTO_API int pto_conv1_bwd_sgd(const float* g1, const uint8_t* code1, const float
 PTO_API int pto_conv1_bwd_sgd_dw1(const float* g1, const uint8_t* code1, const float* x, float* gw1, float* gb1,
                                   int B, const long long* bidx, float* p, float* g, float* m, long long nflat,
                                   long long zero_from, const float* dh1, const float* a2p, long long w1_off,
-                                  const float* lr, float mom, float wd, float gscale, int nesterov, hipStream_t s) {
+                                  long long* adv, long long nbatches, int* set_pending, const float* lr, float mom,
+                                  float wd, float gscale, int nesterov, hipStream_t s) {
+  if (adv && bidx) return -1;  // the advance would race with the conv1 blocks' cursor reads
   const long long w1_end = w1_off + (long long)F1OUT * F1IN;
   if (nflat % 4 || zero_from % 4 || w1_off % 4 || w1_end > nflat ||
       ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m)) & 15))
@@ -1474,7 +1582,7 @@ PTO_API int pto_conv1_bwd_sgd_dw1(const float* g1, const uint8_t* code1, const f
   const int nsgd_hi = (int)(((nflat - w1_end) / 4 + 255) / 256);
   hipLaunchKernelGGL(k_conv1_bwd_sgd, dim3(nconv + ndw + nsgd_lo + nsgd_hi), dim3(256), 0, s, g1, code1, x, gw1, gb1,
                      B, bidx, nconv, p, g, m, nflat, zero_from, sgd_args(lr, mom, wd, gscale, nesterov), ndw, dh1, a2p,
-                     w1_off, w1_end, nsgd_lo);
+                     w1_off, w1_end, nsgd_lo, adv, nbatches > 0 ? nbatches : 1LL, set_pending);
   LAUNCH_CHECK();
 }
 
@@ -1499,7 +1607,7 @@ PTO_API int pto_sgd_flat(float* p, float* g, float* m, long long n, long long ze
   const int nsgd = (int)((n / 4 + 255) / 256);
   hipLaunchKernelGGL(k_conv1_bwd_sgd, dim3(nsgd), dim3(256), 0, s, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
                      nullptr, 0, p, g, m, n, zero_from, sgd_args(lr, mom, wd, gscale, nesterov), 0, nullptr, nullptr,
-                     n, n, nsgd);
+                     n, n, nsgd, nullptr, 1LL, nullptr);
   LAUNCH_CHECK();
 }
 

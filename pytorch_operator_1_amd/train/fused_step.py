@@ -141,6 +141,10 @@ class FusedMnistTrainer:
         self.xcur = (torch.empty(self.B * 784, device=device)
                      if self.dw1_sgd and self.conv12_version == 2 and os.environ.get("PTO_XCUR", "1") == "1"
                      else None)
+        # F4 and B3's d(a2p) in one launch (k_fc2_ce_dx), B3's all-row
+        # reductions in B2, the batch-cursor advance in B1: 5 launches per
+        # step (PTO_F4DX=0: the 6-launch schedule)
+        self.merge_f4 = self.xcur is not None and os.environ.get("PTO_F4DX", "1") == "1"
         # multi-GPU schedule: overlap the fc bucket's all-reduce with the conv
         # backward on a side stream (PTO_COMM_OVERLAP=1), or all-reduce the
         # whole flat buffer once after the backward on the compute stream
@@ -238,6 +242,14 @@ class FusedMnistTrainer:
                 c(L.pto_conv12_fwd_lazy(*f12, self.conv12_version, s), "conv12_fwd_lazy")
             c(L.pto_linear_fwd(self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
                                self.h1.data_ptr(), B, 500, 800, 1, s), "fc1_fwd")
+            if self.merge_f4:  # F4 + d(a2p) + conv1 commit; dW2/db -> B2, cursor advance -> B1
+                c(L.pto_fc2_ce_dx(self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
+                                  self.target.data_ptr(), P["fc1.weight"].data_ptr(), self.loss_rows.data_ptr(),
+                                  self.dlogits.data_ptr(), self.dh1.data_ptr(), self.da2p.data_ptr(), B, 1.0 / B, bi,
+                                  self._params[self._c1:].data_ptr(), self.grads[self._c1:].data_ptr(),
+                                  self.mom[self._c1:].data_ptr(), self.numel - self._c1, self.pending.data_ptr(),
+                                  *o, s), "fc2_ce_dx")
+                return
             c(L.pto_fc2_ce_commit(self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
                                   self.target.data_ptr(), self.loss_rows.data_ptr(), self.dlogits.data_ptr(),
                                   self.dh1.data_ptr(), B, 1.0 / B, bi, self.batch_snap.data_ptr(),
@@ -295,9 +307,16 @@ class FusedMnistTrainer:
         # but measured break-even: every sample-block adds into the same 520
         # addresses, 64-way atomic contention.  The separate 320-block conv1
         # launch below adds each address only 16 times.)
-        c(L.pto_conv2_bwd(self.da2p.data_ptr(), self.code2.data_ptr(), self.a1p.data_ptr(),
-                          P["conv2.weight"].data_ptr(), G["conv2.weight"].data_ptr(), G["conv2.bias"].data_ptr(),
-                          self.da1p.data_ptr(), B, 7, None, None, None, None, None, s), "conv2_bwd")
+        if self.merge_f4:  # + B3's all-row reductions (dW2, db1, db2)
+            c(L.pto_conv2_bwd_fc(self.da2p.data_ptr(), self.code2.data_ptr(), self.a1p.data_ptr(),
+                                 P["conv2.weight"].data_ptr(), G["conv2.weight"].data_ptr(),
+                                 G["conv2.bias"].data_ptr(), self.da1p.data_ptr(), B, self.dh1.data_ptr(),
+                                 self.h1.data_ptr(), self.dlogits.data_ptr(), G["fc2.weight"].data_ptr(),
+                                 G["fc1.bias"].data_ptr(), G["fc2.bias"].data_ptr(), s), "conv2_bwd_fc")
+        else:
+            c(L.pto_conv2_bwd(self.da2p.data_ptr(), self.code2.data_ptr(), self.a1p.data_ptr(),
+                              P["conv2.weight"].data_ptr(), G["conv2.weight"].data_ptr(), G["conv2.bias"].data_ptr(),
+                              self.da1p.data_ptr(), B, 7, None, None, None, None, None, s), "conv2_bwd")
         if self.fused_opt:  # + the fc/conv2 update (grads final since B3/B2); B1 reads the cursor snapshot
             if self.dw1_sgd:
                 xb = (self.xcur.data_ptr(), None) if self.xcur is not None else (self.data.data_ptr(),
@@ -307,6 +326,8 @@ class FusedMnistTrainer:
                                           xb[1], self._params.data_ptr(), self.grads.data_ptr(),
                                           self.mom.data_ptr(), self._c1, self._split(), self.dh1.data_ptr(),
                                           self.a2p.data_ptr(), param_offsets()[0]["fc1.weight"][0],
+                                          bi if self.merge_f4 else None, self.n_batches,
+                                          self.pending.data_ptr() if self.merge_f4 else None,
                                           *self._opt_args(), s), "conv1_bwd_sgd_dw1")
                 return
             if self._bwd_side is None:

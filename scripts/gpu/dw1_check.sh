@@ -4,12 +4,12 @@ set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_graph_gpu.py tests/test_kernels_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_dw1.log 2>&1 || { tail -60 gpurun_out/pytest_dw1.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_graph_gpu.py tests/test_kernels_gpu.py tests/test_e2e_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_dw1.log 2>&1 || { tail -60 gpurun_out/pytest_dw1.log; exit 1; }
 grep -E "passed|failed" gpurun_out/pytest_dw1.log | tail -2
 for r in 1; do
   for v in 0 1; do
-    PTO_XCUR=$v timeout -k 10 120 python bench.py --steps 4000 --warmup 300 > gpurun_out/bench_dw1_$v.json 2> gpurun_out/bench_dw1_$v.err
-    python -c "import json;d=json.load(open('gpurun_out/bench_dw1_$v.json'));print('xcur=$v', d['value'], d['ms_per_step'])"
+    PTO_F4DX=$v timeout -k 10 120 python bench.py --steps 4000 --warmup 300 > gpurun_out/bench_dw1_$v.json 2> gpurun_out/bench_dw1_$v.err
+    python -c "import json;d=json.load(open('gpurun_out/bench_dw1_$v.json'));print('f4dx=$v', d['value'], d['ms_per_step'])"
   done
 done
 R="$GRAFT_REPO_ROOT"
