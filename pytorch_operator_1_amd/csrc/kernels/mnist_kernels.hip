@@ -30,6 +30,7 @@
 // the dataset without any copy kernels.
 #include "mfma_f32.h"
 #include "sgd_f32.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -556,6 +557,33 @@ __global__ __launch_bounds__(512) void k_linear_fwd_vec(const float* __restrict_
   __shared__ float red[8 * 256];
   block_gemm_splitk<LAY_ROWK, LAY_ROWK, EpiBiasRelu, 8, true, true>(x, K, w, K, M, N, K, blockIdx.x, red,
                                                                     EpiBiasRelu{bias, y, N, relu != 0});
+}
+
+// 16-wave variant (1024 threads, 4 waves per SIMD): each wave owns a 64-deep
+// K slice (NG = 4 groups, all 8 loads per lane in flight at once), so the
+// serial chain per wave is one memory round trip + 16 MFMAs instead of
+// 32.  Same tile count as k_linear_fwd_vec (fc1 at B=64: 128 blocks).
+__global__ __launch_bounds__(1024) void k_linear_fwd_vec16(const float* __restrict__ x, const float* __restrict__ w,
+                                                           const float* __restrict__ bias, float* __restrict__ y,
+                                                           int M, int N, int K, int relu) {
+  __shared__ float red[16 * 256];
+  const int mtiles = (M + 15) >> 4;
+  const int mt = blockIdx.x % mtiles, nt = blockIdx.x / mtiles;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int kc = (((K + 15) / 16) + 15) & ~15;
+  const f32x4 acc = wave_tile_16x16<LAY_ROWK, LAY_ROWK, 4, true, true>(x, K, w, K, M, N, K, mt * 16, nt * 16,
+                                                                       wv * kc, (wv + 1) * kc);
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) red[wv * 256 + ((lane >> 4) * 4 + rr) * 16 + (lane & 15)] = acc[rr];
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < 256) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v += red[q * 256 + t];
+    const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
+    if (m < M && n < N) EpiBiasRelu{bias, y, N, relu != 0}(m, n, v);
+  }
 }
 
 // dx[M,K] = dy[M,N] @ w[N,K]   (B operand: w as [k=N rows][n=K cols])
@@ -1243,8 +1271,12 @@ __global__ __launch_bounds__(256) void k_conv1_bwd_sgd(const float* __restrict__
       mv[rr] = ok ? mw[r * F1IN + n] : 0.f;
     }
     const float lr = *a.lr;
-    const f32x4 acc = wave_tile_16x16<LAY_KROW, LAY_KROW, 8>(dh1, F1OUT, a2p, F1IN, F1OUT, F1IN, B, mt * 16, nt * 16,
-                                                             0, B);
+    // variant 1: 4 k-groups per memory round (K = B = 64 exactly, 32 loads
+    // per lane in flight) instead of 8 with half of them masked off
+    const f32x4 acc =
+        a.variant == 1
+            ? wave_tile_16x16<LAY_KROW, LAY_KROW, 4>(dh1, F1OUT, a2p, F1IN, F1OUT, F1IN, B, mt * 16, nt * 16, 0, B)
+            : wave_tile_16x16<LAY_KROW, LAY_KROW, 8>(dh1, F1OUT, a2p, F1IN, F1OUT, F1IN, B, mt * 16, nt * 16, 0, B);
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int r = mt * 16 + (lane >> 4) * 4 + rr;
@@ -1357,6 +1389,7 @@ static SgdArgs sgd_args(const float* lr, float mom, float wd, float gscale, int 
   a.wd = wd;
   a.gscale = gscale;
   a.nesterov = nesterov;
+  a.variant = 0;
   return a;
 }
 
@@ -1395,7 +1428,13 @@ PTO_API int pto_linear_fwd(const float* x, const float* w, const float* b, float
                            hipStream_t s) {
   const int tiles = ((M + 15) / 16) * ((N + 15) / 16);
   const bool vec = (K % 4) == 0 && ((((uintptr_t)x) | ((uintptr_t)w)) & 15) == 0;
-  if (vec)
+  static const int waves = [] {
+    const char* e = getenv("PTO_LINEAR_WAVES");  // 8 = the 512-thread kernel (A/B)
+    return e ? atoi(e) : 16;
+  }();
+  if (vec && waves == 16)
+    hipLaunchKernelGGL(k_linear_fwd_vec16, dim3(tiles), dim3(1024), 0, s, x, w, b, y, M, N, K, relu);
+  else if (vec)
     hipLaunchKernelGGL(k_linear_fwd_vec, dim3(tiles), dim3(512), 0, s, x, w, b, y, M, N, K, relu);
   else
     hipLaunchKernelGGL(k_linear_fwd, dim3(tiles), dim3(256), 0, s, x, w, b, y, M, N, K, relu);
@@ -1580,8 +1619,14 @@ PTO_API int pto_conv1_bwd_sgd_dw1(const float* g1, const uint8_t* code1, const f
   const int ndw = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
   const int nsgd_lo = (int)((w1_off / 4 + 255) / 256);
   const int nsgd_hi = (int)(((nflat - w1_end) / 4 + 255) / 256);
+  static const int dw1_ng = [] {
+    const char* e = getenv("PTO_DW1_NG");
+    return e ? atoi(e) : 8;
+  }();
+  SgdArgs sa = sgd_args(lr, mom, wd, gscale, nesterov);
+  sa.variant = dw1_ng == 4 ? 1 : 0;
   hipLaunchKernelGGL(k_conv1_bwd_sgd, dim3(nconv + ndw + nsgd_lo + nsgd_hi), dim3(256), 0, s, g1, code1, x, gw1, gb1,
-                     B, bidx, nconv, p, g, m, nflat, zero_from, sgd_args(lr, mom, wd, gscale, nesterov), ndw, dh1, a2p,
+                     B, bidx, nconv, p, g, m, nflat, zero_from, sa, ndw, dh1, a2p,
                      w1_off, w1_end, nsgd_lo, adv, nbatches > 0 ? nbatches : 1LL, set_pending);
   LAUNCH_CHECK();
 }

@@ -25,6 +25,7 @@ struct SgdArgs {
   const float* lr;
   float mom, wd, gscale;
   int nesterov;
+  int variant;  // kernel-variant selector for launches that carry SgdArgs (0 = default)
 };
 
 // One float4 group (4 elements at i, 16-byte aligned, i + 3 < n) of a flat
