@@ -739,6 +739,19 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx(
   const int w = t >> 6, lane = t & 63;
   const int row = mt * 16 + w;
   float* srow = dh1s + w * F1OUT;
+  constexpr int KC = ((F1OUT + FDX_WAVES - 1) / FDX_WAVES + 15) & ~15;  // 32
+  constexpr int NGK = KC / 16;
+  const bool pre = cm.a.variant == 1;
+  // variant 1: the wave's W1 operand slice (K-rows [w*KC, (w+1)*KC) of 16
+  // columns, 8 floats per lane) is loaded BEFORE the head, so its memory
+  // round trip overlaps the head's instead of following the barrier.
+  const int r = lane & 15, gq = lane >> 4;
+  const int kb = w * KC, kend = min((w + 1) * KC, F1OUT);
+  float bw[NGK][4];
+  if (pre) {
+#pragma unroll
+    for (int q = 0; q < NGK; ++q) load4<LAY_KROW>(w1, F1IN, nt * 16 + r, F1IN, kb + 16 * q + 4 * gq, kend, bw[q]);
+  }
   if (row < B) {
     const bool st = nt == 0;
     fc2_ce_row(row, lane, h1, w2, b2, labels, nullptr, st ? loss_rows : nullptr, st ? dlogits : nullptr,
@@ -747,9 +760,23 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx(
     for (int k = lane; k < F1OUT; k += 64) srow[k] = 0.f;
   }
   __syncthreads();
-  constexpr int KC = ((F1OUT + FDX_WAVES - 1) / FDX_WAVES + 15) & ~15;  // 32
-  const f32x4 acc = wave_tile_16x16<LAY_ROWK, LAY_KROW, KC / 16>(dh1s, F1OUT, w1, F1IN, 16, F1IN, F1OUT, 0, nt * 16,
-                                                                 w * KC, (w + 1) * KC);
+  f32x4 acc;
+  if (pre) {
+    f32x4 acc0 = zero4(), acc1 = zero4();
+#pragma unroll
+    for (int q = 0; q < NGK; ++q) {
+      float av[4];
+      load4<LAY_ROWK>(dh1s, F1OUT, r, 16, kb + 16 * q + 4 * gq, kend, av);
+      acc0 = mfma16x16x4(av[0], bw[q][0], acc0);
+      acc1 = mfma16x16x4(av[1], bw[q][1], acc1);
+      acc0 = mfma16x16x4(av[2], bw[q][2], acc0);
+      acc1 = mfma16x16x4(av[3], bw[q][3], acc1);
+    }
+    acc = acc0 + acc1;
+  } else {
+    acc = wave_tile_16x16<LAY_ROWK, LAY_KROW, NGK>(dh1s, F1OUT, w1, F1IN, 16, F1IN, F1OUT, 0, nt * 16, kb,
+                                                   (w + 1) * KC);
+  }
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) red[w * 256 + ((lane >> 4) * 4 + rr) * 16 + (lane & 15)] = acc[rr];
   __syncthreads();
@@ -1570,6 +1597,11 @@ PTO_API int pto_fc2_ce_dx(const float* h1, const float* w2, const float* b2, con
                           const float* lr, float mom, float wd, float gscale, int nesterov, hipStream_t s) {
   if (n1 % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1)) & 15)) return -1;
   Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), nullptr, nullptr};
+  static const int prefetch = [] {
+    const char* e = getenv("PTO_FDX_PREFETCH");
+    return e ? atoi(e) : 0;
+  }();
+  cm.a.variant = prefetch ? 1 : 0;  // read only by k_fc2_ce_dx's tile loop (the commit SGD ignores it)
   const int nblk = ((B + 15) / 16) * ((F1IN + 15) / 16);
   hipLaunchKernelGGL(k_fc2_ce_dx, dim3(nblk + 1), dim3(FDX_WAVES * 64), 0, s, h1, w2, b2, labels, w1, loss_rows,
                      dlogits, dh1, da2p, B, inv_b, bidx, cm);
@@ -1620,8 +1652,8 @@ PTO_API int pto_conv1_bwd_sgd_dw1(const float* g1, const uint8_t* code1, const f
   const int nsgd_lo = (int)((w1_off / 4 + 255) / 256);
   const int nsgd_hi = (int)(((nflat - w1_end) / 4 + 255) / 256);
   static const int dw1_ng = [] {
-    const char* e = getenv("PTO_DW1_NG");
-    return e ? atoi(e) : 8;
+    const char* e = getenv("PTO_DW1_NG");  // 8 = previous loop shape (A/B)
+    return e ? atoi(e) : 4;
   }();
   SgdArgs sa = sgd_args(lr, mom, wd, gscale, nesterov);
   sa.variant = dw1_ng == 4 ? 1 : 0;
