@@ -1598,8 +1598,8 @@ PTO_API int pto_fc2_ce_dx(const float* h1, const float* w2, const float* b2, con
   if (n1 % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1)) & 15)) return -1;
   Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), nullptr, nullptr};
   static const int prefetch = [] {
-    const char* e = getenv("PTO_FDX_PREFETCH");
-    return e ? atoi(e) : 0;
+    const char* e = getenv("PTO_FDX_PREFETCH");  // 0 = operand loads after the barrier (A/B)
+    return e ? atoi(e) : 1;
   }();
   cm.a.variant = prefetch ? 1 : 0;  // read only by k_fc2_ce_dx's tile loop (the commit SGD ignores it)
   const int nblk = ((B + 15) / 16) * ((F1IN + 15) / 16);
