@@ -431,8 +431,54 @@ __global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x
   const int wid = tid >> 6, lane = tid & 63;
   // conv1 + bias + ReLU + pool: 15 wave tasks = 5 channel groups x 3 pixel
   // chunks (64, 64, 16 pooled pixels)
+  // variant 1 (balanced): tasks 0-9 = 5 channel groups x the two 64-pixel
+  // chunks; tasks 10-14 = the last 16 pixels of one channel group with the
+  // group's 4 channels spread over the lanes (lane = channel*16 + pixel), a
+  // quarter of a full task's FMAs instead of a full task's lockstep cost.
+  const bool bal = lz.a.variant == 1;
   for (int task = wid; task < 15; task += 8) {
-    const int cg = task / 3, pix = (task - cg * 3) * 64 + lane;
+    if (bal && task >= 10) {
+      const int oc = (task - 10) * 4 + (lane >> 4), pix = 128 + (lane & 15);
+      float wr1[W1LD];
+#pragma unroll
+      for (int j = 0; j < W1LD / 4; ++j) {
+        const float4 v = *reinterpret_cast<const float4*>(w1s + oc * W1LD + 4 * j);
+        wr1[4 * j] = v.x; wr1[4 * j + 1] = v.y; wr1[4 * j + 2] = v.z; wr1[4 * j + 3] = v.w;
+      }
+      const float bz1 = w1s[C1 * W1LD + oc];
+      const int ph = pix / 12, pw = pix - ph * 12;
+      float p[6][6];
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = 0; c < 6; c += 2) {
+          const float2 v = *reinterpret_cast<const float2*>(xs + (2 * ph + r) * 28 + 2 * pw + c);
+          p[r][c] = v.x;
+          p[r][c + 1] = v.y;
+        }
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int dy = q >> 1, dx = q & 1;
+        float sacc = bz1;
+#pragma unroll
+        for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw) sacc = fmaf(p[dy + kh][dx + kw], wr1[kh * 5 + kw], sacc);
+        v[q] = sacc;
+      }
+      float o;
+      uint8_t cd;
+      relu_pool4(v, o, cd);
+      in_s[oc * 144 + pix] = o;
+      if (nt == 0) {
+        a1p[b * A1P + oc * 144 + pix] = o;
+        code1[b * A1P + oc * 144 + pix] = cd;
+      }
+      continue;
+    }
+    const int cg = bal ? task >> 1 : task / 3;
+    const int pix = (bal ? (task & 1) : task - cg * 3) * 64 + lane;
     float wr[4][W1LD], bz[4];
 #pragma unroll
     for (int cc = 0; cc < 4; ++cc) {
@@ -1174,7 +1220,7 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
 constexpr int B1_CHUNK = 4;
 PTO_DEV void conv1_bwd_block(int vb, const float* __restrict__ g1, const uint8_t* __restrict__ code1,
                              const float* __restrict__ x, float* __restrict__ gw1, float* __restrict__ gb1, int B,
-                             const long long* __restrict__ bidx) {
+                             const long long* __restrict__ bidx, bool halving = false) {
   // One memory round: the chunk's 4 input images (12.5 KB, coalesced
   // float4) go to LDS together with each thread's (grad, code) pairs; the
   // 25-tap patches are then read from LDS.
@@ -1226,16 +1272,54 @@ PTO_DEV void conv1_bwd_block(int vb, const float* __restrict__ g1, const uint8_t
     acc[25] += gq;
   }
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (halving) {
+    // recursive-halving wave reduction of the 26 (padded to 32) sums: at
+    // each step a lane keeps half of its live accumulators (chosen by its
+    // lane bit) and receives its partner's copy of them: 16+8+4+2+1+1 = 32
+    // shuffles instead of 6 x 26.  Lane l ends with accumulator
+    // idx(l) = bits 5..1 of l, summed over all 64 lanes.
+    float h16[16], h8[8], h4[4], h2[2], h1;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
+    for (int k = 0; k < 16; ++k) {
+      const bool up = lane & 32;
+      const float a0 = acc[k], a1 = k + 16 < 26 ? acc[k + 16] : 0.f;
+      h16[k] = (up ? a1 : a0) + __shfl_xor(up ? a0 : a1, 32, 64);
+    }
 #pragma unroll
-    for (int k = 0; k < 26; ++k) acc[k] += __shfl_xor(acc[k], o, 64);
-  if (lane < 26) {
-    float v = acc[0];
+    for (int k = 0; k < 8; ++k) {
+      const bool up = lane & 16;
+      h8[k] = (up ? h16[k + 8] : h16[k]) + __shfl_xor(up ? h16[k] : h16[k + 8], 16, 64);
+    }
 #pragma unroll
-    for (int k = 1; k < 26; ++k)
-      if (lane == k) v = acc[k];
-    part[wv][lane] = v;
+    for (int k = 0; k < 4; ++k) {
+      const bool up = lane & 8;
+      h4[k] = (up ? h8[k + 4] : h8[k]) + __shfl_xor(up ? h8[k] : h8[k + 4], 8, 64);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const bool up = lane & 4;
+      h2[k] = (up ? h4[k + 2] : h4[k]) + __shfl_xor(up ? h4[k] : h4[k + 2], 4, 64);
+    }
+    {
+      const bool up = lane & 2;
+      h1 = (up ? h2[1] : h2[0]) + __shfl_xor(up ? h2[0] : h2[1], 2, 64);
+    }
+    h1 += __shfl_xor(h1, 1, 64);
+    const int idx = ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 + ((lane >> 2) & 1) * 2 +
+                    ((lane >> 1) & 1);
+    if (!(lane & 1) && idx < 26) part[wv][idx] = h1;
+  } else {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int k = 0; k < 26; ++k) acc[k] += __shfl_xor(acc[k], o, 64);
+    if (lane < 26) {
+      float v = acc[0];
+#pragma unroll
+      for (int k = 1; k < 26; ++k)
+        if (lane == k) v = acc[k];
+      part[wv][lane] = v;
+    }
   }
   __syncthreads();
   if (threadIdx.x < 26) {
@@ -1275,7 +1359,7 @@ __global__ __launch_bounds__(256) void k_conv1_bwd_sgd(const float* __restrict__
     if (set_pending) *set_pending = 1;
   }
   if (bid < nconv) {
-    conv1_bwd_block(bid, g1, code1, x, gw1, gb1, B, bidx);
+    conv1_bwd_block(bid, g1, code1, x, gw1, gb1, B, bidx, a.variant & 2);
     return;
   }
   bid -= nconv;
@@ -1301,7 +1385,7 @@ __global__ __launch_bounds__(256) void k_conv1_bwd_sgd(const float* __restrict__
     // variant 1: 4 k-groups per memory round (K = B = 64 exactly, 32 loads
     // per lane in flight) instead of 8 with half of them masked off
     const f32x4 acc =
-        a.variant == 1
+        (a.variant & 1)
             ? wave_tile_16x16<LAY_KROW, LAY_KROW, 4>(dh1, F1OUT, a2p, F1IN, F1OUT, F1IN, B, mt * 16, nt * 16, 0, B)
             : wave_tile_16x16<LAY_KROW, LAY_KROW, 8>(dh1, F1OUT, a2p, F1IN, F1OUT, F1IN, B, mt * 16, nt * 16, 0, B);
 #pragma unroll
@@ -1446,6 +1530,11 @@ PTO_API int pto_conv12_fwd_lazy_x(const float* x, const float* w1, const float* 
                                   const int* pending, const float* lr, float mom, float wd, float gscale, int nesterov,
                                   float* xout, hipStream_t s) {
   LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off, xout};
+  static const int bal = [] {
+    const char* e = getenv("PTO_CONV1_BALANCED");  // 0 = 15 lockstep tasks (A/B)
+    return e ? atoi(e) : 1;
+  }();
+  lz.a.variant = bal ? 1 : 0;  // conv1 task layout of k_conv12_fwd2 (the lazy SGD ignores it)
   hipLaunchKernelGGL(k_conv12_fwd2, dim3(B * 4), dim3(512), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B,
                      bidx, lz);
   LAUNCH_CHECK();
@@ -1655,8 +1744,12 @@ PTO_API int pto_conv1_bwd_sgd_dw1(const float* g1, const uint8_t* code1, const f
     const char* e = getenv("PTO_DW1_NG");  // 8 = previous loop shape (A/B)
     return e ? atoi(e) : 4;
   }();
+  static const int c1_halving = [] {
+    const char* e = getenv("PTO_CONV1_HALVING");
+    return e ? atoi(e) : 0;
+  }();
   SgdArgs sa = sgd_args(lr, mom, wd, gscale, nesterov);
-  sa.variant = dw1_ng == 4 ? 1 : 0;
+  sa.variant = (dw1_ng == 4 ? 1 : 0) | (c1_halving ? 2 : 0);
   hipLaunchKernelGGL(k_conv1_bwd_sgd, dim3(nconv + ndw + nsgd_lo + nsgd_hi), dim3(256), 0, s, g1, code1, x, gw1, gb1,
                      B, bidx, nconv, p, g, m, nflat, zero_from, sa, ndw, dh1, a2p,
                      w1_off, w1_end, nsgd_lo, adv, nbatches > 0 ? nbatches : 1LL, set_pending);

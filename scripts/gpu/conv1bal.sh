@@ -1,0 +1,17 @@
+#!/bin/bash
+# k_conv12_fwd2 with the balanced conv1 task layout (PTO_CONV1_BALANCED=1): numerics then A/B bench.
+set -e
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+R="$GRAFT_REPO_ROOT"
+PTO_CONV1_BALANCED=1 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_graph_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_conv1bal.log 2>&1 || { tail -60 gpurun_out/pytest_conv1bal.log; exit 1; }
+tail -1 gpurun_out/pytest_conv1bal.log
+for rep in 1 2; do
+for ng in 0 1; do
+PTO_CONV1_BALANCED=$ng timeout -k 10 200 python bench.py --steps 4000 --warmup 400 > gpurun_out/c1b_$ng.json 2>/dev/null
+echo "ng=$ng $(python -c "import json;d=json.load(open('gpurun_out/c1b_$ng.json'));print(d['value'],d['ms_per_step']*1000)")"
+done
+done
+cd /tmp && PTO_CONV1_BALANCED=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_c1b" -o run -- python3 "$R/bench.py" --steps 200 --warmup 20 > "$R/gpurun_out/c1b_prof.log" 2>&1
+python3 "$R/tools/rocprof_summary.py" "$R/gpurun_out/prof_c1b" --top 6
