@@ -1220,7 +1220,7 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
 constexpr int B1_CHUNK = 4;
 PTO_DEV void conv1_bwd_block(int vb, const float* __restrict__ g1, const uint8_t* __restrict__ code1,
                              const float* __restrict__ x, float* __restrict__ gw1, float* __restrict__ gb1, int B,
-                             const long long* __restrict__ bidx, bool halving = false) {
+                             const long long* __restrict__ bidx, bool halving = true) {
   // One memory round: the chunk's 4 input images (12.5 KB, coalesced
   // float4) go to LDS together with each thread's (grad, code) pairs; the
   // 25-tap patches are then read from LDS.
@@ -1359,7 +1359,7 @@ __global__ __launch_bounds__(256) void k_conv1_bwd_sgd(const float* __restrict__
     if (set_pending) *set_pending = 1;
   }
   if (bid < nconv) {
-    conv1_bwd_block(bid, g1, code1, x, gw1, gb1, B, bidx, a.variant & 2);
+    conv1_bwd_block(bid, g1, code1, x, gw1, gb1, B, bidx, !(a.variant & 2));  // bit 2: legacy 6x26-shuffle reduction
     return;
   }
   bid -= nconv;
@@ -1745,11 +1745,11 @@ PTO_API int pto_conv1_bwd_sgd_dw1(const float* g1, const uint8_t* code1, const f
     return e ? atoi(e) : 4;
   }();
   static const int c1_halving = [] {
-    const char* e = getenv("PTO_CONV1_HALVING");
-    return e ? atoi(e) : 0;
+    const char* e = getenv("PTO_CONV1_HALVING");  // 0 = legacy reduction (A/B)
+    return e ? atoi(e) : 1;
   }();
   SgdArgs sa = sgd_args(lr, mom, wd, gscale, nesterov);
-  sa.variant = (dw1_ng == 4 ? 1 : 0) | (c1_halving ? 2 : 0);
+  sa.variant = (dw1_ng == 4 ? 1 : 0) | (c1_halving ? 0 : 2);
   hipLaunchKernelGGL(k_conv1_bwd_sgd, dim3(nconv + ndw + nsgd_lo + nsgd_hi), dim3(256), 0, s, g1, code1, x, gw1, gb1,
                      B, bidx, nconv, p, g, m, nflat, zero_from, sa, ndw, dh1, a2p,
                      w1_off, w1_end, nsgd_lo, adv, nbatches > 0 ? nbatches : 1LL, set_pending);
