@@ -666,7 +666,7 @@ PTO_DEV void fc2_ce_row(int row, int lane, const float* __restrict__ h1, const f
                         const float* __restrict__ bias, const int64_t* __restrict__ labels,
                         float* __restrict__ logp, float* __restrict__ loss_rows, float* __restrict__ dlogits,
                         float* __restrict__ dh1, int B, float inv_b, const long long* __restrict__ bidx,
-                        float* dh1_row_lds = nullptr) {
+                        float* dh1_row_lds = nullptr, bool halving = true) {
   float h[8], wv[NCLS][8], bz[NCLS];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -690,11 +690,46 @@ PTO_DEV void fc2_ce_row(int row, int lane, const float* __restrict__ h1, const f
     for (int j = 0; j < 8; ++j) s = fmaf(h[j], wv[c][j], s);
     z[c] = s;
   }
-  // 10 butterfly reductions interleaved (independent chains)
+  if (halving) {
+    // recursive halving (10 sums padded to 16): 8+4+2+1 shuffles leave lane l
+    // with class idx = bits 5..2 of l summed over 16 lanes, two butterflies
+    // finish it, and each class is broadcast back with one readlane:
+    // 17 shuffles + 10 readlanes instead of 60 shuffles.
+    float h8[8], h4[4], h2[2], h1;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
+    for (int k = 0; k < 8; ++k) {
+      const bool up = lane & 32;
+      const float a0 = z[k], a1 = k + 8 < NCLS ? z[k + 8] : 0.f;
+      h8[k] = (up ? a1 : a0) + __shfl_xor(up ? a0 : a1, 32, 64);
+    }
 #pragma unroll
-    for (int c = 0; c < NCLS; ++c) z[c] += __shfl_xor(z[c], o, 64);
+    for (int k = 0; k < 4; ++k) {
+      const bool up = lane & 16;
+      h4[k] = (up ? h8[k + 4] : h8[k]) + __shfl_xor(up ? h8[k] : h8[k + 4], 16, 64);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const bool up = lane & 8;
+      h2[k] = (up ? h4[k + 2] : h4[k]) + __shfl_xor(up ? h4[k] : h4[k + 2], 8, 64);
+    }
+    {
+      const bool up = lane & 4;
+      h1 = (up ? h2[1] : h2[0]) + __shfl_xor(up ? h2[0] : h2[1], 4, 64);
+    }
+    h1 += __shfl_xor(h1, 2, 64);
+    h1 += __shfl_xor(h1, 1, 64);
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) {
+      const int src = ((c >> 3) & 1) * 32 + ((c >> 2) & 1) * 16 + ((c >> 1) & 1) * 8 + (c & 1) * 4;
+      z[c] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h1), src));
+    }
+  } else {
+    // 10 butterfly reductions interleaved (independent chains)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int c = 0; c < NCLS; ++c) z[c] += __shfl_xor(z[c], o, 64);
+  }
 #pragma unroll
   for (int c = 0; c < NCLS; ++c) z[c] += bz[c];
   float mx = z[0];
@@ -787,7 +822,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx(
   float* srow = dh1s + w * F1OUT;
   constexpr int KC = ((F1OUT + FDX_WAVES - 1) / FDX_WAVES + 15) & ~15;  // 32
   constexpr int NGK = KC / 16;
-  const bool pre = cm.a.variant == 1;
+  const bool pre = (cm.a.variant & 1) != 0;
   // variant 1: the wave's W1 operand slice (K-rows [w*KC, (w+1)*KC) of 16
   // columns, 8 floats per lane) is loaded BEFORE the head, so its memory
   // round trip overlaps the head's instead of following the barrier.
@@ -801,7 +836,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx(
   if (row < B) {
     const bool st = nt == 0;
     fc2_ce_row(row, lane, h1, w2, b2, labels, nullptr, st ? loss_rows : nullptr, st ? dlogits : nullptr,
-               st ? dh1 : nullptr, B, inv_b, bidx, srow);
+               st ? dh1 : nullptr, B, inv_b, bidx, srow, !(cm.a.variant & 2));  // bit 2: legacy butterflies
   } else {
     for (int k = lane; k < F1OUT; k += 64) srow[k] = 0.f;
   }
@@ -1690,7 +1725,11 @@ PTO_API int pto_fc2_ce_dx(const float* h1, const float* w2, const float* b2, con
     const char* e = getenv("PTO_FDX_PREFETCH");  // 0 = operand loads after the barrier (A/B)
     return e ? atoi(e) : 1;
   }();
-  cm.a.variant = prefetch ? 1 : 0;  // read only by k_fc2_ce_dx's tile loop (the commit SGD ignores it)
+  static const int head_halving = [] {
+    const char* e = getenv("PTO_HEAD_HALVING");  // 0 = 6 x 10 butterfly shuffles (A/B)
+    return e ? atoi(e) : 1;
+  }();
+  cm.a.variant = (prefetch ? 1 : 0) | (head_halving ? 0 : 2);  // read only by k_fc2_ce_dx's tile loop (the commit SGD ignores it)
   const int nblk = ((B + 15) / 16) * ((F1IN + 15) / 16);
   hipLaunchKernelGGL(k_fc2_ce_dx, dim3(nblk + 1), dim3(FDX_WAVES * 64), 0, s, h1, w2, b2, labels, w1, loss_rows,
                      dlogits, dh1, da2p, B, inv_b, bidx, cm);
