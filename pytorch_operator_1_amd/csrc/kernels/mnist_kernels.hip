@@ -431,11 +431,11 @@ __global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x
   const int wid = tid >> 6, lane = tid & 63;
   // conv1 + bias + ReLU + pool: 15 wave tasks = 5 channel groups x 3 pixel
   // chunks (64, 64, 16 pooled pixels)
-  // variant 1 (balanced): tasks 0-9 = 5 channel groups x the two 64-pixel
+  // balanced layout (default): tasks 0-9 = 5 channel groups x the two 64-pixel
   // chunks; tasks 10-14 = the last 16 pixels of one channel group with the
   // group's 4 channels spread over the lanes (lane = channel*16 + pixel), a
   // quarter of a full task's FMAs instead of a full task's lockstep cost.
-  const bool bal = lz.a.variant == 1;
+  const bool bal = !(lz.a.variant & 2);  // bit 2: legacy 15-task layout
   for (int task = wid; task < 15; task += 8) {
     if (bal && task >= 10) {
       const int oc = (task - 10) * 4 + (lane >> 4), pix = 128 + (lane & 15);
@@ -973,7 +973,7 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
                                                    float* __restrict__ gb1, int nF, const float* __restrict__ fdh1,
                                                    const float* __restrict__ fh1, const float* __restrict__ fdl,
                                                    float* __restrict__ fgw2, float* __restrict__ fgb1,
-                                                   float* __restrict__ fgb2) {
+                                                   float* __restrict__ fgb2, int ktail = 1) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int bid = blockIdx.x;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1134,6 +1134,15 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
       for (int q = 0; q < 4; ++q) acc[q] = zero4();
 #pragma unroll
       for (int k0 = 0; k0 < 4; ++k0) {
+        if (k0 == 3 && ktail) {
+          // K tail (k = 48..51): one k per lane group, so 4 MFMAs instead of
+          // 16 with three quarters of their K padding
+          const int k = 48 + gg;
+          const float a = dys[(wv * 16 + r) * 52 + k];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q] = mfma16x16x4(a, ws[k * WLD + q * 16 + r], acc[q]);
+          break;
+        }
         float av[4], bv[4][4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1569,7 +1578,7 @@ PTO_API int pto_conv12_fwd_lazy_x(const float* x, const float* w1, const float* 
     const char* e = getenv("PTO_CONV1_BALANCED");  // 0 = 15 lockstep tasks (A/B)
     return e ? atoi(e) : 1;
   }();
-  lz.a.variant = bal ? 1 : 0;  // conv1 task layout of k_conv12_fwd2 (the lazy SGD ignores it)
+  lz.a.variant = bal ? 0 : 2;  // conv1 task layout of k_conv12_fwd2 (the lazy SGD ignores it)
   hipLaunchKernelGGL(k_conv12_fwd2, dim3(B * 4), dim3(512), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B,
                      bidx, lz);
   LAUNCH_CHECK();
@@ -1693,7 +1702,7 @@ PTO_API int pto_conv2_bwd(const float* g2, const uint8_t* code2, const float* a1
   if (nA + nB + nC == 0) return 0;
   hipLaunchKernelGGL(k_conv2_bwd, dim3(nA + nB + nC), dim3(256), lds, s, g2, code2, a1p, w2, gw2, gb2, da1p, B, nA,
                      nB, nC, x, bidx, code1, (parts & 2) ? gw1 : nullptr, gb1, 0, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr);
+                     nullptr, nullptr, 1);
   LAUNCH_CHECK();
 }
 
@@ -1709,8 +1718,13 @@ PTO_API int pto_conv2_bwd_fc(const float* g2, const uint8_t* code2, const float*
   const size_t ldsA = B2_CHUNK * (288 + F1IN + F1IN / 4) * sizeof(float);
   const size_t ldsB = (52 * 68 + 64 * 65 + F1IN + F1IN / 4) * sizeof(float);
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;
+  static const int ktail = [] {
+    const char* e = getenv("PTO_C2_KTAIL");  // 0 = padded 16-deep K tail (A/B)
+    return e ? atoi(e) : 1;
+  }();
   hipLaunchKernelGGL(k_conv2_bwd, dim3(nA + nB + nC + nF), dim3(256), lds, s, g2, code2, a1p, w2, gw2, gb2, da1p, B,
-                     nA, nB, nC, nullptr, nullptr, nullptr, nullptr, nullptr, nF, dh1, h1, dlogits, fgw2, fgb1, fgb2);
+                     nA, nB, nC, nullptr, nullptr, nullptr, nullptr, nullptr, nF, dh1, h1, dlogits, fgw2, fgb1, fgb2,
+                     ktail);
   LAUNCH_CHECK();
 }
 
