@@ -360,6 +360,11 @@ __global__ __launch_bounds__(256) void k_conv12_fwd(const float* __restrict__ x,
 //    own the same pooled row), partial tiles combined through LDS, so each
 //    SIMD interleaves two independent MFMA chains.
 constexpr int W1LD = 28;
+// Balanced layout's task slots per wave (waves w and w+4 share a SIMD): per
+// SIMD 3 full, 3 full, 2 full + 3 quarter, 2 full + 2 quarter tasks
+// (1200/1200/1100/1000 FMA units vs 1300/1300/1000/900 for task += 8).
+__constant__ signed char kConv1Slots[8][3] = {{0, 1, -1}, {3, 4, -1},  {6, 10, 11}, {8, 13, -1},
+                                              {2, -1, -1}, {5, -1, -1}, {7, 12, -1}, {9, 14, -1}};
 __global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x, const float* __restrict__ w1,
                                                      const float* __restrict__ b1, const float* __restrict__ w2,
                                                      const float* __restrict__ b2, float* __restrict__ a1p,
@@ -436,7 +441,16 @@ __global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x
   // group's 4 channels spread over the lanes (lane = channel*16 + pixel), a
   // quarter of a full task's FMAs instead of a full task's lockstep cost.
   const bool bal = !(lz.a.variant & 2);  // bit 2: legacy 15-task layout
-  for (int task = wid; task < 15; task += 8) {
+  const bool slots = bal && (lz.a.variant & 4);
+  for (int si = 0; si < 3; ++si) {
+    int task;
+    if (slots) {
+      task = kConv1Slots[wid][si];
+      if (task < 0) break;
+    } else {
+      task = wid + 8 * si;
+      if (task >= 15) break;
+    }
     if (bal && task >= 10) {
       const int oc = (task - 10) * 4 + (lane >> 4), pix = 128 + (lane & 15);
       float wr1[W1LD];
@@ -1134,7 +1148,7 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
       for (int q = 0; q < 4; ++q) acc[q] = zero4();
 #pragma unroll
       for (int k0 = 0; k0 < 4; ++k0) {
-        if (k0 == 3 && ktail) {
+        if (k0 == 3 && (ktail & 1)) {
           // K tail (k = 48..51): one k per lane group, so 4 MFMAs instead of
           // 16 with three quarters of their K padding
           const int k = 48 + gg;
@@ -1165,6 +1179,46 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
     }
     __syncthreads();
     float* dsum = gstage;  // free after the dY2 expansion
+    if (ktail & 2) {
+      // 288 outputs on 256 threads: one full output per thread, then the last
+      // 32 outputs split 8 ways over all threads (<= 4 taps each, 3-step
+      // shuffle sum) instead of a second full round on half a wave
+      {
+        const int o = tid, icl = o / 144, pix = o - icl * 144;
+        const int y = pix / 12, xx = pix - y * 12;
+        float sacc = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < 5; ++kh) {
+          const int sy = y - kh;
+          if (sy < 0 || sy >= 8) continue;
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw) {
+            const int sx = xx - kw;
+            if (sx < 0 || sx >= 8) continue;
+            sacc += ts[(sy * 8 + sx) * TLD + icl * 25 + kh * 5 + kw];
+          }
+        }
+        da1p[b * A1P + (icg * 2 + icl) * 144 + pix] = sacc;
+        dsum[o] = sacc;
+      }
+      {
+        const int o = 256 + (tid >> 3), part = tid & 7, pix = o - 144;  // icl = 1
+        const int y = pix / 12, xx = pix - y * 12;
+        float sacc = 0.f;
+#pragma unroll
+        for (int tt = part; tt < 25; tt += 8) {
+          const int kh = tt / 5, kw = tt - kh * 5, sy = y - kh, sx = xx - kw;
+          if (sy >= 0 && sy < 8 && sx >= 0 && sx < 8) sacc += ts[(sy * 8 + sx) * TLD + 25 + tt];
+        }
+        sacc += __shfl_xor(sacc, 4, 64);
+        sacc += __shfl_xor(sacc, 2, 64);
+        sacc += __shfl_xor(sacc, 1, 64);
+        if (part == 0) {
+          da1p[b * A1P + (icg * 2 + 1) * 144 + pix] = sacc;
+          dsum[o] = sacc;
+        }
+      }
+    } else
     for (int o = tid; o < 2 * 144; o += 256) {
       const int icl = o / 144, pix = o - icl * 144;
       const int y = pix / 12, xx = pix - y * 12;
@@ -1578,7 +1632,11 @@ PTO_API int pto_conv12_fwd_lazy_x(const float* x, const float* w1, const float* 
     const char* e = getenv("PTO_CONV1_BALANCED");  // 0 = 15 lockstep tasks (A/B)
     return e ? atoi(e) : 1;
   }();
-  lz.a.variant = bal ? 0 : 2;  // conv1 task layout of k_conv12_fwd2 (the lazy SGD ignores it)
+  static const int slots = [] {
+    const char* e = getenv("PTO_CONV1_SLOTS");
+    return e ? atoi(e) : 0;
+  }();
+  lz.a.variant = (bal ? 0 : 2) | (slots ? 4 : 0);  // conv1 task layout of k_conv12_fwd2 (the lazy SGD ignores it)
   hipLaunchKernelGGL(k_conv12_fwd2, dim3(B * 4), dim3(512), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B,
                      bidx, lz);
   LAUNCH_CHECK();
@@ -1720,7 +1778,8 @@ PTO_API int pto_conv2_bwd_fc(const float* g2, const uint8_t* code2, const float*
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;
   static const int ktail = [] {
     const char* e = getenv("PTO_C2_KTAIL");  // 0 = padded 16-deep K tail (A/B)
-    return e ? atoi(e) : 1;
+    const char* c = getenv("PTO_C2_COL2IM_SPLIT");  // 0 = two full col2im rounds (A/B)
+    return (e ? atoi(e) : 1) | ((c ? atoi(c) : 1) ? 2 : 0);
   }();
   hipLaunchKernelGGL(k_conv2_bwd, dim3(nA + nB + nC + nF), dim3(256), lds, s, g2, code2, a1p, w2, gw2, gb2, da1p, B,
                      nA, nB, nC, nullptr, nullptr, nullptr, nullptr, nullptr, nF, dh1, h1, dlogits, fgw2, fgb1, fgb2,
