@@ -365,7 +365,8 @@ constexpr int W1LD = 28;
 // (1200/1200/1100/1000 FMA units vs 1300/1300/1000/900 for task += 8).
 __constant__ signed char kConv1Slots[8][3] = {{0, 1, -1}, {3, 4, -1},  {6, 10, 11}, {8, 13, -1},
                                               {2, -1, -1}, {5, -1, -1}, {7, 12, -1}, {9, 14, -1}};
-__global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x, const float* __restrict__ w1,
+template <int NTH>
+__global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__ x, const float* __restrict__ w1,
                                                      const float* __restrict__ b1, const float* __restrict__ w2,
                                                      const float* __restrict__ b2, float* __restrict__ a1p,
                                                      uint8_t* __restrict__ code1, float* __restrict__ a2p,
@@ -375,24 +376,26 @@ __global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x
   __shared__ __attribute__((aligned(16))) float in_s[A1P];
   __shared__ __attribute__((aligned(16))) float xs[784];
   __shared__ __attribute__((aligned(16))) float w1s[C1 * W1LD + 32];
-  __shared__ __attribute__((aligned(16))) float red[4 * 256];
+  constexpr int NWV = NTH / 64, NPART = NTH / 256;  // waves; K parts of the conv2 GEMM
+  __shared__ __attribute__((aligned(16))) float red[(NPART - 1) * 1024];
   const int b = blockIdx.x >> 2, nt = blockIdx.x & 3;
   const int tid = threadIdx.x;
   {
     x = batch_ptr(x, bidx, B * 784);
     const int nrows = min(16, C2 - nt * 16);
     const float4* wsrc = reinterpret_cast<const float4*>(w2 + nt * 16 * 500);
-    float4 wv[4];
+    float4 wv[2048 / NTH];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = tid + 512 * q;
+    for (int q = 0; q < 2048 / NTH; ++q) {
+      const int e = tid + NTH * q;
       wv[q] = (e < nrows * 125) ? wsrc[e] : float4{0.f, 0.f, 0.f, 0.f};
     }
     const float4 xv = tid < 196 ? reinterpret_cast<const float4*>(x + b * 784)[tid] : float4{0.f, 0.f, 0.f, 0.f};
-    float wq[2], gq[2], mq[2];
+    constexpr int QW1 = (C1 * 26 + NTH - 1) / NTH;
+    float wq[QW1], gq[QW1], mq[QW1];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int e = tid + 512 * q;
+    for (int q = 0; q < QW1; ++q) {
+      const int e = tid + NTH * q;
       wq[q] = e < C1 * 25 ? w1[e] : (e < C1 * 26 ? b1[e - C1 * 25] : 0.f);
     }
     int pend = 0;
@@ -401,8 +404,8 @@ __global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x
       pend = *lz.pending;
       lr = *lz.a.lr;
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int e = tid + 512 * q;
+      for (int q = 0; q < QW1; ++q) {
+        const int e = tid + NTH * q;
         const int fi = e < C1 * 25 ? e : lz.bias_off + (e - C1 * 25);
         gq[q] = e < C1 * 26 ? lz.g[fi] : 0.f;
         mq[q] = e < C1 * 26 ? lz.m[fi] : 0.f;
@@ -410,11 +413,11 @@ __global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x
     }
     if (pend) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q) sgd_elem(wq[q], gq[q], mq[q], lr, lz.a.mom, lz.a.wd, lz.a.gscale, lz.a.nesterov);
+      for (int q = 0; q < QW1; ++q) sgd_elem(wq[q], gq[q], mq[q], lr, lz.a.mom, lz.a.wd, lz.a.gscale, lz.a.nesterov);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = tid + 512 * q;
+    for (int q = 0; q < 2048 / NTH; ++q) {
+      const int e = tid + NTH * q;
       if (e < 2000) {
         const int row = e / 125, col = (e - row * 125) * 4;
         float* d = ws + row * WS_LD + col;
@@ -426,8 +429,8 @@ __global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x
       if (lz.xout && nt == 0) reinterpret_cast<float4*>(lz.xout + b * 784)[tid] = xv;
     }
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int e = tid + 512 * q;
+    for (int q = 0; q < QW1; ++q) {
+      const int e = tid + NTH * q;
       if (e < C1 * 25) w1s[(e / 25) * W1LD + e % 25] = wq[q];
       else if (e < C1 * 26) w1s[C1 * W1LD + e - C1 * 25] = wq[q];
     }
@@ -440,19 +443,24 @@ __global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x
   // chunks; tasks 10-14 = the last 16 pixels of one channel group with the
   // group's 4 channels spread over the lanes (lane = channel*16 + pixel), a
   // quarter of a full task's FMAs instead of a full task's lockstep cost.
-  const bool bal = !(lz.a.variant & 2);  // bit 2: legacy 15-task layout
-  const bool slots = bal && (lz.a.variant & 4);
+  const bool bal = NTH == 1024 || !(lz.a.variant & 2);  // bit 2: legacy 15-task layout (512 threads)
+  const bool slots = NTH == 512 && bal && (lz.a.variant & 4);
+  // 1024 threads: full tasks hold 2 channels' weights (VGPR budget of 4
+  // waves/SIMD): 20 full tasks (10 channel pairs x 2 chunks) + 5 quarter
+  // tasks, 25 over 16 waves.  512 threads: 4-channel tasks, 10 + 5.
+  constexpr int CPT = NTH == 1024 ? 2 : 4;
+  constexpr int NFULL = 2 * C1 / CPT, NTASK = NTH == 1024 ? NFULL + 5 : 15;
   for (int si = 0; si < 3; ++si) {
     int task;
     if (slots) {
       task = kConv1Slots[wid][si];
       if (task < 0) break;
     } else {
-      task = wid + 8 * si;
-      if (task >= 15) break;
+      task = wid + NWV * si;
+      if (task >= NTASK) break;
     }
-    if (bal && task >= 10) {
-      const int oc = (task - 10) * 4 + (lane >> 4), pix = 128 + (lane & 15);
+    if (bal && task >= NFULL) {
+      const int oc = (task - NFULL) * 4 + (lane >> 4), pix = 128 + (lane & 15);
       float wr1[W1LD];
 #pragma unroll
       for (int j = 0; j < W1LD / 4; ++j) {
@@ -493,15 +501,15 @@ __global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x
     }
     const int cg = bal ? task >> 1 : task / 3;
     const int pix = (bal ? (task & 1) : task - cg * 3) * 64 + lane;
-    float wr[4][W1LD], bz[4];
+    float wr[CPT][W1LD], bz[CPT];
 #pragma unroll
-    for (int cc = 0; cc < 4; ++cc) {
+    for (int cc = 0; cc < CPT; ++cc) {
 #pragma unroll
       for (int j = 0; j < W1LD / 4; ++j) {
-        const float4 v = *reinterpret_cast<const float4*>(w1s + (cg * 4 + cc) * W1LD + 4 * j);
+        const float4 v = *reinterpret_cast<const float4*>(w1s + (cg * CPT + cc) * W1LD + 4 * j);
         wr[cc][4 * j] = v.x; wr[cc][4 * j + 1] = v.y; wr[cc][4 * j + 2] = v.z; wr[cc][4 * j + 3] = v.w;
       }
-      bz[cc] = w1s[C1 * W1LD + cg * 4 + cc];
+      bz[cc] = w1s[C1 * W1LD + cg * CPT + cc];
     }
     if (pix >= 144) continue;
     const int ph = pix / 12, pw = pix - ph * 12;
@@ -515,8 +523,8 @@ __global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x
         p[r][c + 1] = v.y;
       }
 #pragma unroll
-    for (int cc = 0; cc < 4; ++cc) {
-      const int oc = cg * 4 + cc;
+    for (int cc = 0; cc < CPT; ++cc) {
+      const int oc = cg * CPT + cc;
       float v[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -539,7 +547,8 @@ __global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x
     }
   }
   __syncthreads();
-  // conv2 implicit GEMM (k_conv2_fwd's lane maps), K split in two halves
+  // conv2 implicit GEMM (k_conv2_fwd's lane maps), K (25 groups of 5 MFMAs)
+  // split over NPART wave sets: 13+12 (512 threads) or 7+6+6+6 (1024)
   const int t = wid & 3, half = wid >> 2;
   const int i = lane & 15, g = lane >> 4;
   const int pw = i >> 2, dy = (i >> 1) & 1, dx = i & 1;
@@ -558,22 +567,35 @@ __global__ __launch_bounds__(512) void k_conv12_fwd2(const float* __restrict__ x
     acc1 = mfma16x16x4(arow[3], brow[3], acc1);
     acc0 = mfma16x16x4(arow[4], brow[4], acc0);
   };
-  if (half == 0) {
+  if (NPART == 2) {
+    if (half == 0) {
 #pragma unroll
-    for (int G = 0; G < 13; ++G) group(G);
+      for (int G = 0; G < 13; ++G) group(G);
+    } else {
+#pragma unroll
+      for (int G = 13; G < 25; ++G) group(G);
+    }
   } else {
+    if (half == 0) {
 #pragma unroll
-    for (int G = 13; G < 25; ++G) group(G);
+      for (int G = 0; G < 7; ++G) group(G);
+    } else {
+      const int g0 = 7 + 6 * (half - 1);
+#pragma unroll
+      for (int G = 0; G < 6; ++G) group(g0 + G);
+    }
   }
   f32x4 acc = acc0 + acc1;
-  if (half == 1) {
+  if (half != 0) {
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) red[t * 256 + rr * 64 + lane] = acc[rr];
+    for (int rr = 0; rr < 4; ++rr) red[(half - 1) * 1024 + t * 256 + rr * 64 + lane] = acc[rr];
   }
   __syncthreads();
-  if (half == 1) return;
+  if (half != 0) return;
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) acc[rr] += red[t * 256 + rr * 64 + lane];
+  for (int pp = 0; pp < NPART - 1; ++pp)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) acc[rr] += red[pp * 1024 + t * 256 + rr * 64 + lane];
   if (n >= C2 || b >= B) return;
   const float bn = b2[n];
   float v[4] = {acc[0] + bn, acc[1] + bn, acc[2] + bn, acc[3] + bn};
@@ -1605,14 +1627,27 @@ static SgdArgs sgd_args(const float* lr, float mom, float wd, float gscale, int 
 // F1 with conv1's owed SGD update applied on the fly (fused-optimizer
 // schedule).  g1f/m1f: flat conv1 grads/momentum (weights at 0, bias at
 // bias_off); lr: device scalar.
+// Block size of the fused forward: 512 (two K halves) or 1024 threads
+// (PTO_FWD_THREADS=1024: one conv1 task per wave, four K quarters).
+static int fwd_threads() {
+  static const int n = [] {
+    const char* e = getenv("PTO_FWD_THREADS");
+    return e ? atoi(e) : 512;
+  }();
+  return n;
+}
+
 PTO_API int pto_conv12_fwd_lazy(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
                                 float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B, const long long* bidx,
                                 const float* g1f, const float* m1f, int bias_off, const int* pending, const float* lr,
                                 float mom, float wd, float gscale, int nesterov, int version, hipStream_t s) {
   LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off, nullptr};
-  if (version == 2)
-    hipLaunchKernelGGL(k_conv12_fwd2, dim3(B * 4), dim3(512), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B,
-                       bidx, lz);
+  if (version == 2 && fwd_threads() == 1024)
+    hipLaunchKernelGGL(k_conv12_fwd2_t<1024>, dim3(B * 4), dim3(1024), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p,
+                       code2, B, bidx, lz);
+  else if (version == 2)
+    hipLaunchKernelGGL(k_conv12_fwd2_t<512>, dim3(B * 4), dim3(512), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2,
+                       B, bidx, lz);
   else
     hipLaunchKernelGGL(k_conv12_fwd, dim3(B * 4), dim3(256), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B,
                        bidx, lz);
@@ -1637,8 +1672,12 @@ PTO_API int pto_conv12_fwd_lazy_x(const float* x, const float* w1, const float* 
     return e ? atoi(e) : 0;
   }();
   lz.a.variant = (bal ? 0 : 2) | (slots ? 4 : 0);  // conv1 task layout of k_conv12_fwd2 (the lazy SGD ignores it)
-  hipLaunchKernelGGL(k_conv12_fwd2, dim3(B * 4), dim3(512), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B,
-                     bidx, lz);
+  if (fwd_threads() == 1024)
+    hipLaunchKernelGGL(k_conv12_fwd2_t<1024>, dim3(B * 4), dim3(1024), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p,
+                       code2, B, bidx, lz);
+  else
+    hipLaunchKernelGGL(k_conv12_fwd2_t<512>, dim3(B * 4), dim3(512), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2,
+                       B, bidx, lz);
   LAUNCH_CHECK();
 }
 
