@@ -1628,11 +1628,11 @@ static SgdArgs sgd_args(const float* lr, float mom, float wd, float gscale, int 
 // schedule).  g1f/m1f: flat conv1 grads/momentum (weights at 0, bias at
 // bias_off); lr: device scalar.
 // Block size of the fused forward: 512 (two K halves) or 1024 threads
-// (PTO_FWD_THREADS=1024: one conv1 task per wave, four K quarters).
+// threads (default: 2-channel conv1 tasks, four K parts).
 static int fwd_threads() {
   static const int n = [] {
-    const char* e = getenv("PTO_FWD_THREADS");
-    return e ? atoi(e) : 512;
+    const char* e = getenv("PTO_FWD_THREADS");  // 512 = two K halves, 4-channel conv1 tasks (A/B)
+    return e ? atoi(e) : 1024;
   }();
   return n;
 }
