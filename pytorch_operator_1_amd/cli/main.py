@@ -198,8 +198,15 @@ def cmd_node(args):
         from ..node.native import AgentClient
 
         agent = AgentClient(socket_path=args.node_agent_socket)
+    metrics = None
+    if args.monitoring_port:
+        from ..controller.metrics import OperatorMetrics, serve_metrics
+
+        metrics = OperatorMetrics()
+        serve_metrics(metrics, args.monitoring_port)
     kl = Kubelet(RestClient(_server_url(args)), agent=agent, gpus=args.gpus, log_dir=args.log_dir,
-                 node_name=args.node_name, hbm_per_gpu=_hbm(args))
+                 node_name=args.node_name, hbm_per_gpu=_hbm(args), gpu_visibility=args.gpu_visibility,
+                 metrics=metrics)
     kl.start()
     stop.wait()
     kl.stop()
@@ -213,7 +220,8 @@ def cmd_up(args):
     from ..controller.metrics import serve_metrics
 
     c = LocalCluster(gpus=args.gpus, port=args.port, wal_path=args.wal, log_dir=args.log_dir,
-                     enable_gang_scheduling=args.enable_gang_scheduling, hbm_per_gpu=_hbm(args))
+                     enable_gang_scheduling=args.enable_gang_scheduling, hbm_per_gpu=_hbm(args),
+                     gpu_visibility=args.gpu_visibility)
     c.start()
     serve_metrics(c.metrics, args.monitoring_port)
     print(f"pto: API server {c.url}  metrics :{args.monitoring_port}/metrics  "
@@ -322,6 +330,16 @@ def cmd_describe(args):
 
     print(yaml.safe_dump({"Name": j["metadata"]["name"], "Namespace": ns, "Spec": j.get("spec"),
                           "Status": j.get("status")}, sort_keys=False))
+    # what each replica process really got (the node manager resolves the
+    # master Service name to the node address and virtualises the port)
+    pods = [p for p in c.list("pods", ns)["items"]
+            if (p["metadata"].get("labels") or {}).get(C.LABEL_JOB_NAME) == args.name]
+    if pods:
+        print("Replica processes (effective env):")
+        for p in sorted(pods, key=lambda p: p["metadata"]["name"]):
+            ann = p["metadata"].get("annotations") or {}
+            eff = ann.get("pto.amd.com/effective-env")
+            print(f"  {p['metadata']['name']}: {eff or '(not started)'}")
     evs = [e for e in c.list("events", ns)["items"] if e.get("involvedObject", {}).get("name") == args.name]
     print("Events:")
     for e in evs:
@@ -389,6 +407,11 @@ def main(argv=None):
     nd.add_argument("--node-agent-socket", default=None,
                     help="attach to a running pto-node-agent on this Unix socket instead of spawning one")
     nd.add_argument("--log-dir", default=None)
+    nd.add_argument("--gpu-visibility", choices=["node", "isolated"], default=None,
+                    help="node: replicas see every GPU and pick theirs via LOCAL_RANK (peer IPC/P2P reachable); "
+                         "isolated: HIP_VISIBLE_DEVICES = the replica's own GPUs (default: $PTO_GPU_VISIBILITY or node)")
+    nd.add_argument("--monitoring-port", type=int, default=0,
+                    help="serve the pytorchjob_* training/HBM gauges on this port (0: off)")
     nd.add_argument("--node-name", default="mi355x-0")
     nd.add_argument("--master", default="")
     nd.set_defaults(fn=cmd_node)
@@ -401,6 +424,8 @@ def main(argv=None):
     up.add_argument("--log-dir", default=None)
     up.add_argument("--monitoring-port", type=int, default=8443)
     up.add_argument("--enable-gang-scheduling", action="store_true")
+    up.add_argument("--gpu-visibility", choices=["node", "isolated"], default=None,
+                    help="GPU pinning model (see pto node --help)")
     up.set_defaults(fn=cmd_up)
 
     a = sub.add_parser("apply")

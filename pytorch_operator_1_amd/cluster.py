@@ -27,7 +27,8 @@ log = logging.getLogger("pto-cluster")
 class LocalCluster:
     def __init__(self, gpus: int | None = None, port: int = 0, wal_path: str | None = None,
                  log_dir: str | None = None, enable_gang_scheduling: bool = False, serve_http: bool = True,
-                 extra_env: dict | None = None, threadiness: int = 2, hbm_per_gpu: float | None = None):
+                 extra_env: dict | None = None, threadiness: int = 2, hbm_per_gpu: float | None = None,
+                 gpu_visibility: str | None = None):
         self.store = Store(wal_path=wal_path)
         self.client = LocalClient(self.store)
         self.server = ApiServer(self.store, port=port) if serve_http else None
@@ -36,7 +37,10 @@ class LocalCluster:
             self.client, ControllerConfig(enable_gang_scheduling=enable_gang_scheduling, threadiness=threadiness,
                                           job_resync_period=5.0), metrics=self.metrics)
         kw = {"hbm_per_gpu": hbm_per_gpu} if hbm_per_gpu else {}
-        self.kubelet = Kubelet(self.client, gpus=gpus, log_dir=log_dir, extra_env=extra_env, **kw)
+        if gpu_visibility:
+            kw["gpu_visibility"] = gpu_visibility
+        self.kubelet = Kubelet(self.client, gpus=gpus, log_dir=log_dir, extra_env=extra_env, metrics=self.metrics,
+                               **kw)
 
     def start(self):
         if self.server:

@@ -26,8 +26,20 @@
 // s_waitcnt vmcnt(0) -> barrier -> release fence (system: L2 write-back) ->
 // s_waitcnt vmcnt(0) -> relaxed system flag store; consumer = relaxed poll ->
 // system acquire (L1/L2 invalidate) -> s_waitcnt -> barrier -> loads.
-// Flags live in uncached memory; every spin is bounded (2 s) and reports a
-// timeout through *err instead of hanging the device.
+// Flags live in uncached memory; every spin is bounded (pto_ar_set_timeout_ms,
+// default 500 ms) and reports a timeout through *err instead of hanging the
+// device.
+//
+// Failure semantics (a peer died or stalled): the first barrier that times
+// out sets *err; from then on every barrier of this rank -- in this launch
+// and in every later launch -- returns at once without waiting or
+// publishing, so a dead peer costs ONE timeout, not one per barrier, and
+// the peers still waiting on this rank time out too (the whole job fails
+// together and restarts from its checkpoint).  A workgroup whose barrier
+// failed skips the rest of the kernel: no partial sums from incomplete peer
+// data are written, no parameter is updated, no gradient is zeroed.  The
+// host reads *err after every run() chunk (FusedMnistTrainer.check_comm) and
+// exits with the retryable code 138.
 //
 // Two independent "channels" (flag sets + epochs) let two buckets be in
 // flight at once on different streams (fc bucket overlapped with the conv
@@ -63,7 +75,8 @@ constexpr int AR_MAX_BLOCKS = 64;
 constexpr int AR_CHANNELS = 2;
 constexpr int AR_THREADS = 512;
 constexpr long long AR_ONESHOT_MAX = 65536;  // floats (256 KB): one-shot path
-constexpr long long AR_TIMEOUT_TICKS = 200000000LL;  // wall_clock64 runs at 100 MHz: 2 s
+constexpr long long AR_TICKS_PER_MS = 100000LL;  // wall_clock64 runs at 100 MHz
+long long g_timeout_ticks = 500 * AR_TICKS_PER_MS;  // pto_ar_set_timeout_ms
 
 struct ArPeers {
   float* in[AR_MAX_RANKS];
@@ -76,32 +89,46 @@ __host__ __device__ constexpr int flag_index(int chan, int phase, int block, int
 }
 constexpr int AR_FLAG_WORDS = AR_CHANNELS * 2 * AR_MAX_BLOCKS * AR_MAX_RANKS;
 
+// Returns false (for every thread of the block) if the barrier failed: a
+// peer did not arrive within `timeout` ticks, or an earlier barrier of this
+// rank already failed (*err != 0).  s_fail is per phase, so a fast thread
+// resetting phase 1's word cannot race a slow thread still reading phase 0's.
 __device__ __forceinline__ bool block_barrier(const ArPeers& P, int chan, int phase, int rank, int world, uint32_t e,
-                                              int* err) {
+                                              long long timeout, int* err) {
+  __shared__ int s_fail[2];
   const int t = threadIdx.x, b = blockIdx.x;
+  if (t == 0) s_fail[phase] = 0;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  bool ok = true;
   if (t < world) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back this XCD's L2
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(P.flags[t] + flag_index(chan, phase, b, rank), e, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-    uint32_t* f = P.flags[rank] + flag_index(chan, phase, b, t);
-    const long long t0 = wall_clock64();
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
-      if (wall_clock64() - t0 > AR_TIMEOUT_TICKS) {
-        atomicOr(err, 1 << phase);
-        ok = false;
-        break;
+    bool dead = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (!dead) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back this XCD's L2
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(P.flags[t] + flag_index(chan, phase, b, rank), e, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      uint32_t* f = P.flags[rank] + flag_index(chan, phase, b, t);
+      const long long t0 = wall_clock64();
+      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+        if (wall_clock64() - t0 > timeout) {
+          atomicOr(err, 1 << phase);
+          dead = true;
+          break;
+        }
+        // another block (or an earlier launch) already gave up: stop now
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+          dead = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
       }
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // invalidate L1/L2 before reading peer data
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // invalidate L1/L2 before reading peer data
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (dead) s_fail[phase] = 1;
   }
   __syncthreads();
-  return ok;
+  return s_fail[phase] == 0;
 }
 
 // Fused optimizer epilogue of the all-reduce: own parameters/momentum (same
@@ -120,16 +147,18 @@ struct ArSgd {
 template <bool SGD>
 __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce(const ArPeers* __restrict__ peers, long long off,
                                                                long long n4, int rank, int world, int chan,
-                                                               uint32_t* __restrict__ epochs, int* err, ArSgd f) {
+                                                               uint32_t* __restrict__ epochs, int* err, long long timeout,
+                                                               ArSgd f) {
   __shared__ uint32_t s_epoch;
   const ArPeers P = *peers;
   if (threadIdx.x == 0) s_epoch = epochs[chan * AR_MAX_BLOCKS + blockIdx.x] + 1;
   __syncthreads();
   const uint32_t e = s_epoch;
+  if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blockIdx.x] = e;
   const long long cs = (n4 + world - 1) / world;  // chunk length (float4)
   const long long stride = (long long)gridDim.x * AR_THREADS;
 
-  block_barrier(P, chan, 0, rank, world, e, err);
+  if (!block_barrier(P, chan, 0, rank, world, e, timeout, err)) return;
   // stage 1: reduce my chunk over all ranks (rank order 0..W-1 everywhere)
   {
     const long long c0 = (long long)rank * cs, c1 = min(n4, c0 + cs);
@@ -150,7 +179,7 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce(const ArPeers* __
       reinterpret_cast<float4*>(P.tmp[rank] + off)[i] = a;
     }
   }
-  block_barrier(P, chan, 1, rank, world, e, err);
+  if (!block_barrier(P, chan, 1, rank, world, e, timeout, err)) return;
   // stage 2: gather every chunk into my input (or: update my parameters)
   const float lr = SGD ? *f.a.lr : 0.f;
   for (long long j = (long long)blockIdx.x * AR_THREADS + threadIdx.x; j < cs; j += stride) {
@@ -177,7 +206,6 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce(const ArPeers* __
         }
       }
   }
-  if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blockIdx.x] = e;
   if (SGD && f.bidx && blockIdx.x == 0 && threadIdx.x == 0) *f.bidx = (*f.bidx + 1) % f.nbatches;
 }
 
@@ -187,15 +215,16 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_1shot(const ArPee
                                                                      long long off, long long n4, int rank,
                                                                      int world, int chan,
                                                                      uint32_t* __restrict__ epochs, int* err,
-                                                                     ArSgd f) {
+                                                                     long long timeout, ArSgd f) {
   __shared__ uint32_t s_epoch;
   const ArPeers P = *peers;
   if (threadIdx.x == 0) s_epoch = epochs[chan * AR_MAX_BLOCKS + blockIdx.x] + 1;
   __syncthreads();
   const uint32_t e = s_epoch;
+  if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blockIdx.x] = e;
   const long long i = (long long)blockIdx.x * AR_THREADS + threadIdx.x;
   const bool act = i < n4;
-  block_barrier(P, chan, 0, rank, world, e, err);
+  if (!block_barrier(P, chan, 0, rank, world, e, timeout, err)) return;
   float4 a = {0.f, 0.f, 0.f, 0.f};
   if (act) {
     float4 v[AR_MAX_RANKS];
@@ -212,7 +241,8 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_1shot(const ArPee
         a.w += v[q].w;
       }
   }
-  block_barrier(P, chan, 1, rank, world, e, err);  // every peer is done reading my input
+  // every peer is done reading my input (on failure: nothing is written)
+  if (!block_barrier(P, chan, 1, rank, world, e, timeout, err)) return;
   if (act) {
     if constexpr (SGD) {
       const float lr = *f.a.lr;
@@ -230,7 +260,6 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_1shot(const ArPee
       reinterpret_cast<float4*>(P.in[rank] + off)[i] = a;
     }
   }
-  if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blockIdx.x] = e;
   if (SGD && f.bidx && blockIdx.x == 0 && threadIdx.x == 0) *f.bidx = (*f.bidx + 1) % f.nbatches;
 }
 
@@ -243,6 +272,12 @@ PTO_API int pto_ar_flag_bytes(int) { return AR_FLAG_WORDS * (int)sizeof(uint32_t
 PTO_API int pto_ar_max_ranks() { return AR_MAX_RANKS; }
 PTO_API int pto_ar_peers_bytes() { return (int)sizeof(ArPeers); }
 PTO_API int pto_ar_epoch_words() { return AR_CHANNELS * AR_MAX_BLOCKS; }
+// Barrier spin bound for launches issued (or graph-captured) from now on.
+PTO_API int pto_ar_set_timeout_ms(int ms) {
+  if (ms < 1) return -1;
+  g_timeout_ticks = (long long)ms * AR_TICKS_PER_MS;
+  return 0;
+}
 
 // Flags: uncached device memory, zeroed.
 PTO_API int pto_ar_alloc_flags(void** out) {
@@ -290,12 +325,12 @@ PTO_API int pto_ar_allreduce(const void* peers, long long off, long long n, int 
   if (n <= AR_ONESHOT_MAX) {
     hipLaunchKernelGGL(k_xgmi_allreduce_1shot<false>, dim3((unsigned)((n / 4 + AR_THREADS - 1) / AR_THREADS)),
                        dim3(AR_THREADS), 0, s, reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,
-                       reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), ArSgd{});
+                       reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), g_timeout_ticks, ArSgd{});
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(k_xgmi_allreduce<false>, dim3(pto_ar_blocks(n, world)), dim3(AR_THREADS), 0, s,
                      reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,
-                     reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), ArSgd{});
+                     reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), g_timeout_ticks, ArSgd{});
   return (int)hipGetLastError();
 }
 
@@ -326,11 +361,11 @@ PTO_API int pto_ar_allreduce_sgd(const void* peers, long long off, long long n, 
   if (n <= AR_ONESHOT_MAX) {
     hipLaunchKernelGGL(k_xgmi_allreduce_1shot<true>, dim3((unsigned)((n / 4 + AR_THREADS - 1) / AR_THREADS)),
                        dim3(AR_THREADS), 0, s, reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,
-                       reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), f);
+                       reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), g_timeout_ticks, f);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(k_xgmi_allreduce<true>, dim3(pto_ar_blocks(n, world)), dim3(AR_THREADS), 0, s,
                      reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,
-                     reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), f);
+                     reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), g_timeout_ticks, f);
   return (int)hipGetLastError();
 }

@@ -50,6 +50,15 @@ def _digest() -> str:
     return h.hexdigest()[:16]
 
 
+def is_current() -> bool:
+    """True if the in-tree library was built from the current sources."""
+    stamp = LIB_PATH + ".stamp"
+    if not (os.path.exists(LIB_PATH) and os.path.exists(stamp)):
+        return False
+    with open(stamp) as f:
+        return f.read().strip() == _digest()
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     """Compile every HIP source for gfx950 into the in-tree library."""
     os.makedirs(LIB_DIR, exist_ok=True)
@@ -138,6 +147,7 @@ _SIGS = {
     "pto_ar_max_ranks": [],
     "pto_ar_peers_bytes": [],
     "pto_ar_epoch_words": [],
+    "pto_ar_set_timeout_ms": [_I],
     "pto_ar_alloc_flags": [ctypes.POINTER(ctypes.c_void_p)],
     "pto_ar_free": [_P],
     "pto_ar_get_ipc_handle": [_P, _P, ctypes.POINTER(ctypes.c_longlong)],
@@ -162,7 +172,10 @@ def lib():
         try:
             path = build(force=os.environ.get("PTO_REBUILD") == "1")
         except (OSError, subprocess.CalledProcessError):
-            if not os.path.exists(LIB_PATH):
+            # Only a library built from exactly these sources may stand in
+            # (e.g. hipcc missing on a run host): a stale one has launchers
+            # whose argument lists no longer match _SIGS.
+            if not is_current():
                 raise
             path = LIB_PATH
         L = ctypes.CDLL(path)

@@ -16,6 +16,14 @@ per-workgroup barriers) instead of an RCCL ring.  Setup is collective:
 
 The kernel is HIP-graph capturable (all pointers fixed at setup, epochs on
 the device), so the fused MNIST step keeps its whole-step graph.
+
+Failure semantics: every barrier spin is bounded by ``PTO_XGMI_TIMEOUT_MS``
+(default 500 ms).  The first timeout sets the device error word; after it
+every barrier of this rank returns at once and the workgroups skip their
+writes (no update from an incomplete sum).  :meth:`XgmiAllReduce.check`
+raises :class:`XgmiTimeout` (message contains "timed out", which the
+trainer maps to the retryable exit 138) and is called after every
+``FusedMnistTrainer.run`` chunk.
 """
 from __future__ import annotations
 
@@ -28,8 +36,15 @@ import torch.distributed as dist
 from ..ops import _lib
 
 
+DEFAULT_TIMEOUT_MS = 500
+
+
+class XgmiTimeout(RuntimeError):
+    """A barrier of the xGMI all-reduce timed out: a peer died or stalled."""
+
+
 class XgmiAllReduce:
-    def __init__(self, buf: torch.Tensor, group=None):
+    def __init__(self, buf: torch.Tensor, group=None, timeout_ms: int | None = None):
         """``buf``: this rank's fp32 gradient buffer (same numel on every
         rank); all-reduces operate in place on ranges of it."""
         if buf.dtype != torch.float32 or not buf.is_cuda or not buf.is_contiguous():
@@ -40,6 +55,11 @@ class XgmiAllReduce:
         L = _lib.lib()
         if self.world < 2 or self.world > L.pto_ar_max_ranks():
             raise ValueError(f"XgmiAllReduce: world size {self.world} unsupported")
+        import os
+
+        self.timeout_ms = int(timeout_ms if timeout_ms is not None
+                              else os.environ.get("PTO_XGMI_TIMEOUT_MS", DEFAULT_TIMEOUT_MS))
+        _lib.check(L.pto_ar_set_timeout_ms(self.timeout_ms), "ar_set_timeout_ms")
         self.buf = buf
         self.device = buf.device
         self.tmp = torch.empty_like(buf)
@@ -120,10 +140,15 @@ class XgmiAllReduce:
                                                    int(nesterov), zero_from, cur, n_batches, s),
                    "xgmi_allreduce_sgd")
 
+    def error_word(self) -> int:
+        """Device error word (synchronises with the current stream)."""
+        return int(self.err.item())
+
     def check(self):
-        e = int(self.err.item())
+        e = self.error_word()
         if e:
-            raise RuntimeError(f"xGMI all-reduce barrier timed out (phase mask {e})")
+            raise XgmiTimeout(f"xGMI all-reduce barrier timed out after {self.timeout_ms} ms "
+                              f"(phase mask {e}): a peer rank died or stalled")
 
     def autotune(self, ranges, iters: int = 30) -> dict:
         """Verify against RCCL and time both over ``ranges`` [(offset, n)],

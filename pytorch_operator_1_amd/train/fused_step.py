@@ -5,8 +5,8 @@ Behavioural parity: one call of :meth:`FusedMnistTrainer.step` does what one
 iteration of the reference loop does (``examples/mnist/mnist.py:37-43``):
 ``zero_grad`` → forward → ``nll_loss(log_softmax)`` → ``backward`` (DDP mean
 all-reduce) → ``SGD(lr, momentum).step()`` — in fp32, with PyTorch's
-initialisation, loss, and update semantics (see tests/test_fused_step_gpu.py
-for the numerics check against the stock-PyTorch trainer).
+initialisation, loss, and update semantics (numerics checked against the
+stock-PyTorch trainer in tests/test_kernels_gpu.py and tests/test_graph_gpu.py).
 
 MI355X design:
   * parameters, gradients and momentum each live in ONE flat fp32 buffer
@@ -162,6 +162,7 @@ class FusedMnistTrainer:
         self.lr_dev = torch.tensor([self.lr], **f32)
         self._graphs = None
         self._graph_unrolled = None
+        self._graph_pow = {}
         self._static_ar = None
         self.steps_done = 0
         self._xgmi, self.comm_info = None, {"transport": "none" if self.world == 1 else "rccl"}
@@ -498,16 +499,19 @@ class FusedMnistTrainer:
         torch.cuda.synchronize(self.device)
         graphs = []
         if self.graph_mode == "full":
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._eager_step()
-            graphs = [g]
-            if self.unroll > 1:  # U consecutive steps in one graph (device batch cursor)
-                gu = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gu):
-                    for _ in range(self.unroll):
+            # k consecutive steps per graph for k = 1, 2, 4, ..., unroll (the
+            # device batch cursor walks the data inside the graph): run(n)
+            # then needs n // unroll + popcount(n % unroll) replays, so a
+            # 20-step run costs 2 replays, not 20 (profiles/graph_unroll_sweep_r1.md)
+            self._graph_pow = {}
+            for k in self._graph_sizes():
+                gk = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gk):
+                    for _ in range(k):
                         self._eager_step()
-                self._graph_unrolled = gu
+                self._graph_pow[k] = gk
+            graphs = [self._graph_pow[1]]
+            self._graph_unrolled = self._graph_pow[max(self._graph_pow)]
         else:  # split: collectives outside the graphs, overlapped with conv bwd
             ga, gb, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(ga):
@@ -518,6 +522,13 @@ class FusedMnistTrainer:
                 self.optimizer_step()
             graphs = [ga, gb, gc]
         self._graphs = graphs
+
+    def _graph_sizes(self) -> list[int]:
+        sizes, k = [], 1
+        while k < self.unroll:
+            sizes.append(k)
+            k *= 2
+        return sizes + [max(1, self.unroll)]
 
     def _choose_schedule(self, reps: int = 8):
         """Capture the step both ways (one whole-buffer all-reduce after the
@@ -544,13 +555,13 @@ class FusedMnistTrainer:
                 self._graph_unrolled.replay()
             torch.cuda.synchronize(self.device)
             t = pdist.all_reduce_max(time.perf_counter() - t0, self.device) / (reps * self.unroll)
-            res[ov] = (t, self._graphs, self._graph_unrolled)
+            res[ov] = (t, self._graphs, self._graph_unrolled, self._graph_pow)
             for dst, src in zip(state, snap):
                 dst.copy_(src)
             torch.cuda.synchronize(self.device)
         best = min(res, key=lambda k: res[k][0])
         self.comm_overlap = best
-        _, self._graphs, self._graph_unrolled = res[best]
+        _, self._graphs, self._graph_unrolled, self._graph_pow = res[best]
         self.comm_info["schedule"] = {"chosen": "overlap" if best else "sequential",
                                       "sequential_us": round(res[False][0] * 1e6, 2),
                                       "overlap_us": round(res[True][0] * 1e6, 2)}
@@ -582,16 +593,39 @@ class FusedMnistTrainer:
             self._capture()
 
     def run(self, n: int):
-        """Run exactly ``n`` training steps (replaying the U-step graph
-        n // U times, then single-step graphs for the remainder)."""
-        if self.graph_mode == "full" and self.unroll > 1:
+        """Run exactly ``n`` training steps: the largest captured multi-step
+        graphs first (n // unroll replays of the unroll-step graph, then one
+        replay per set bit of the remainder), then check the gradient
+        transport's error word (a dead or stalled xGMI peer raises
+        :class:`~pytorch_operator_1_amd.parallel.xgmi.XgmiTimeout` here, at
+        most one chunk after it happened)."""
+        if n <= 0:
+            return
+        if self.graph_mode == "full":
             self._ensure_captured()
-            for _ in range(n // self.unroll):
-                self._graph_unrolled.replay()
-            self.steps_done += (n // self.unroll) * self.unroll
-            n %= self.unroll
+            for k in sorted(self._graph_pow, reverse=True):
+                g = self._graph_pow[k]
+                while n >= k:
+                    g.replay()
+                    self.steps_done += k
+                    n -= k
         for _ in range(n):
             self.step()
+        self.check_comm()
+
+    def check_comm(self):
+        """Raise if the xGMI all-reduce reported a barrier timeout (no-op for
+        RCCL/gloo, whose failures raise from the collective itself).
+        Synchronises with the device when xGMI is in use."""
+        if self._xgmi is not None:
+            self._xgmi.check()
+
+    @property
+    def needs_host_barrier(self) -> bool:
+        """True if peers' queued collectives time out when this rank spends
+        long on host work (checkpoint, evaluation): the caller must then
+        re-align the ranks (utils.dist.host_barrier) before the next run()."""
+        return self._xgmi is not None
 
     def step(self):
         if self.graph_mode == "none":

@@ -57,6 +57,8 @@ def parse_args(argv=None):
     p.add_argument("--train-size", type=int, default=60000)
     p.add_argument("--test-size", type=int, default=10000)
     p.add_argument("--sampler", action="store_true", help="DistributedSampler: shard the data over ranks")
+    p.add_argument("--no-shuffle", action="store_true",
+                   help="keep the training order fixed (default: reshuffle every epoch like DataLoader(shuffle=True))")
     p.add_argument("--max-steps", type=int, default=0, help="stop after N optimizer steps (0 = full epochs)")
     p.add_argument("--no-test", action="store_true")
     p.add_argument("--checkpoint-dir", default=None)
@@ -120,7 +122,7 @@ def load_data(args, device, rank):
 # restartPolicy ExitCode the survivors are recreated too and every rank
 # resumes from the latest checkpoint (kill/rejoin).
 RETRYABLE_EXIT = 138
-_COMM_ERRORS = ("Connection closed by peer", "Connection reset by peer", "NCCL", "RCCL", "Broken pipe",
+_COMM_ERRORS = ("XgmiTimeout", "host barrier", "Connection closed by peer", "Connection reset by peer", "NCCL", "RCCL", "Broken pipe",
                 "timed out", "Timeout", "DistBackendError", "ProcessGroup", "Gloo", "gloo")
 
 
@@ -134,6 +136,51 @@ def main(argv=None):
                   flush=True)
             os._exit(RETRYABLE_EXIT)
         raise
+
+
+def resume_state(ckpt_dir: str | None, rank: int, world: int):
+    """Checkpoint to resume from, agreed by every rank: rank 0 picks the
+    newest complete checkpoint in ``ckpt_dir`` and broadcasts its path;
+    every rank loads THAT file (a rank that cannot read it raises, so no
+    two ranks ever resume from different steps).  Returns ``(path, state)``
+    or ``(None, None)``."""
+    if not ckpt_dir:
+        return None, None
+    choice = [ckpt.latest(ckpt_dir) if rank == 0 else None]
+    if world > 1 and dist.is_initialized():
+        dist.broadcast_object_list(choice, src=0)
+    path = choice[0]
+    if not path:
+        return None, None
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"rank {rank}: checkpoint {path} chosen by rank 0 is not visible here "
+                                f"(--checkpoint-dir must be shared by all replicas)")
+    return path, ckpt.load(path, map_location="cpu")
+
+
+class EpochShuffler:
+    """Per-epoch reshuffle of the training set, like the reference's
+    ``DataLoader(shuffle=True)`` (examples/mnist/mnist.py:118-124): epoch e
+    trains on ``orig[perm(seed, e)]``.  The permutation is a function of
+    (seed, epoch) only, so a resumed run sees the same order.  The working
+    buffer is updated in place (stream-ordered after the previous steps),
+    so the fused trainer's graph-captured data pointer stays valid."""
+
+    def __init__(self, x, y, seed: int, enabled: bool = True):
+        self.enabled = enabled
+        self.seed = seed
+        self.orig_x, self.orig_y = (x.clone(), y.clone()) if enabled else (x, y)
+        self.x, self.y = x, y
+        self.epoch = None
+
+    def set_epoch(self, epoch: int):
+        if not self.enabled or epoch == self.epoch:
+            return
+        self.epoch = epoch
+        g = torch.Generator().manual_seed(self.seed * 100003 + epoch)
+        perm = torch.randperm(self.orig_x.shape[0], generator=g).to(self.orig_x.device)
+        self.x.copy_(self.orig_x.index_select(0, perm))
+        self.y.copy_(self.orig_y.index_select(0, perm))
 
 
 def _main(argv=None):
@@ -155,7 +202,9 @@ def _main(argv=None):
     xtr, ytr, xte, yte = load_data(args, device, rank)
     if args.sampler and world > 1:  # DistributedSampler semantics: disjoint shards
         n = xtr.shape[0] // world
-        xtr, ytr = xtr[rank * n:(rank + 1) * n], ytr[rank * n:(rank + 1) * n]
+        xtr, ytr = xtr[rank * n:(rank + 1) * n].contiguous(), ytr[rank * n:(rank + 1) * n].contiguous()
+    dataset_len = xtr.shape[0]
+    shuffler = EpochShuffler(xtr, ytr, args.seed, enabled=not args.no_shuffle)
 
     impl = args.impl or ("fused" if use_cuda else "eager")
     from .runner import build_trainer
@@ -163,22 +212,36 @@ def _main(argv=None):
     extra = {"comm": args.comm} if (args.comm and impl == "fused") else {}
     trainer = build_trainer(impl, device=device, batch_size=args.batch_size, lr=args.lr, momentum=args.momentum,
                             dataset_size=xtr.shape[0], seed=args.seed, rank=rank, data=xtr, target=ytr, **extra)
-    if getattr(trainer, "comm_info", None) and world > 1:
-        print(f"[pto] gradient all-reduce: {trainer.comm_info}", flush=True)
+    comm_info = getattr(trainer, "comm_info", None)
+    if comm_info and world > 1:
+        print(f"[pto] gradient all-reduce: {comm_info}", flush=True)
+        metrics.emit(event="comm", rank=rank, **{k: v for k, v in comm_info.items() if not isinstance(v, dict)})
     start_step = 0
-    if args.checkpoint_dir:
-        path = ckpt.latest(args.checkpoint_dir)
-        if path:
-            st = ckpt.load(path, map_location="cpu")
-            trainer.load_state_dict(st["trainer"])
-            start_step = int(st["step"])
-            print(f"Resumed from {path} at step {start_step}")
-            sys.stdout.flush()
+    path, st = resume_state(args.checkpoint_dir, rank, world)
+    if st is not None:
+        trainer.load_state_dict(st["trainer"])
+        if st.get("rng"):
+            ckpt.set_rng_state(st["rng"])
+        start_step = int(st["step"])
+        print(f"Resumed from {path} at step {start_step}")
+        sys.stdout.flush()
 
     n_batches = xtr.shape[0] // args.batch_size
+    loader_len = -(-dataset_len // args.batch_size)  # len(train_loader): the partial last batch counts
     total_steps = args.epochs * n_batches
     if args.max_steps:
         total_steps = min(total_steps, args.max_steps)
+    fail_at = args.fail_at_step if (args.fail_at_step and rank == args.fail_rank and not start_step) else 0
+    align = getattr(trainer, "needs_host_barrier", False)
+    run = getattr(trainer, "run", None) or (lambda n: [trainer.step() for _ in range(n)])
+
+    def boundary(s: int) -> bool:
+        """Host work is due after completing step s (1-based count)."""
+        b = (s - 1) % n_batches
+        return (s == start_step + 1 or b % args.log_interval == 0 or s % n_batches == 0 or s >= total_steps
+                or (args.checkpoint_interval and s % args.checkpoint_interval == 0) or s == fail_at
+                or bool(args.profile))
+
     step = start_step
     t_epoch = time.time()
     samples_since = 0
@@ -187,15 +250,22 @@ def _main(argv=None):
     trace = torch_trace(args.profile, rank)
     prof_step = trace.__enter__()
     while step < total_steps:
-        epoch = step // n_batches + 1
-        batch_idx = step % n_batches
-        if args.fail_at_step and step == args.fail_at_step and rank == args.fail_rank and not start_step:
+        if fail_at and step == fail_at:
             print(f"[fault-injection] rank {rank} SIGKILL at step {step}", flush=True)
             os.kill(os.getpid(), signal.SIGKILL)
-        trainer.step()
+        epoch = step // n_batches + 1
+        shuffler.set_epoch(epoch)
+        # steps up to the next log / checkpoint / epoch / fault boundary in
+        # one call: the fused trainer replays its multi-step HIP graphs and
+        # checks the gradient transport's error word once per chunk
+        k = 1
+        while step + k < total_steps and not boundary(step + k):
+            k += 1
+        run(k)
         prof_step()
-        step += 1
-        samples_since += args.batch_size
+        step += k
+        samples_since += args.batch_size * k
+        batch_idx = (step - 1) % n_batches
         if first:
             if device.type == "cuda":
                 torch.cuda.synchronize(device)
@@ -204,14 +274,18 @@ def _main(argv=None):
         if batch_idx % args.log_interval == 0:
             loss = trainer.last_loss()
             now = time.time()
-            sps = samples_since / max(now - t_last, 1e-9)
+            dt = max(now - t_last, 1e-9)
+            sps = samples_since / dt
+            step_s = dt * args.batch_size / max(samples_since, 1)
             samples_since, t_last = 0, now
             print("Train Epoch: {} [{}/{} ({:.0f}%)]\tloss={:.4f}".format(
-                epoch, batch_idx * args.batch_size, n_batches * args.batch_size, 100.0 * batch_idx / n_batches, loss))
-            metrics.emit(event="train", step=step, loss=loss, samples_per_sec=round(sps * world, 1), rank=rank)
+                epoch, batch_idx * args.batch_size, dataset_len, 100.0 * batch_idx / loader_len, loss))
+            metrics.emit(event="train", step=step, loss=loss, samples_per_sec=round(sps * world, 1),
+                         step_seconds=step_s, rank=rank)
             if writer:
                 writer.add_scalar("loss", loss, epoch * n_batches + batch_idx)
-        if args.checkpoint_dir and args.checkpoint_interval and step % args.checkpoint_interval == 0 and rank == 0:
+        ckpt_due = bool(args.checkpoint_dir and args.checkpoint_interval and step % args.checkpoint_interval == 0)
+        if ckpt_due and rank == 0:
             ckpt.save(args.checkpoint_dir, step, {"trainer": trainer.state_dict(), "rng": ckpt.rng_state()})
         end_of_epoch = step % n_batches == 0 or step == total_steps
         if end_of_epoch and not args.no_test:
@@ -226,6 +300,10 @@ def _main(argv=None):
             metrics.emit(event="test", epoch=epoch, accuracy=acc, loss=test_loss, rank=rank,
                          epoch_seconds=round(time.time() - t_epoch, 3))
             t_epoch = time.time()
+        if align and (ckpt_due or (end_of_epoch and not args.no_test)) and step < total_steps:
+            # xGMI barriers spin with a short timeout: nobody starts the next
+            # chunk until every rank is done with its host work
+            pdist.host_barrier()
         sys.stdout.flush()
     trace.__exit__(None, None, None)
     if writer:

@@ -110,6 +110,35 @@ def barrier(device: torch.device | None = None) -> None:
             dist.barrier()
 
 
+_host_barrier_seq = 0
+
+
+def host_barrier(timeout_s: float | None = None, tag: str = "hb") -> None:
+    """Bounded barrier over the rendezvous TCPStore (no device work, no
+    collective on the GPU streams).  Used after long host-side work
+    (checkpoint, evaluation) by trainers whose device collectives have
+    short spin timeouts (the xGMI all-reduce): no rank launches its next
+    chunk of steps before every rank is back.  A rank that died makes the
+    others raise after ``timeout_s`` (``PTO_HOST_BARRIER_TIMEOUT``, default
+    60 s) instead of blocking until the process-group timeout; the caller
+    maps that to the retryable exit."""
+    global _host_barrier_seq
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("PTO_HOST_BARRIER_TIMEOUT", "60"))
+    store = dist.distributed_c10d._get_default_store()
+    _host_barrier_seq += 1
+    key = f"pto/{tag}/{_host_barrier_seq}"
+    store.set(f"{key}/{dist.get_rank()}", "1")
+    keys = [f"{key}/{r}" for r in range(dist.get_world_size())]
+    try:
+        store.wait(keys, datetime.timedelta(seconds=timeout_s))
+    except Exception as e:  # noqa: BLE001 - store errors differ by backend/version
+        raise TimeoutError(f"host barrier {key} timed out after {timeout_s} s: a peer rank died or stalled "
+                           f"({type(e).__name__}: {e})") from e
+
+
 def all_reduce_max(value: float, device: torch.device) -> float:
     """MAX of a host scalar over ranks (bench reports the slowest rank)."""
     if not (dist.is_available() and dist.is_initialized()):

@@ -32,3 +32,22 @@ def test_bench_two_ranks_cpu_json_line(sampler):
     assert d["n_gpus"] == 2 and d["steps"] == 6 and d["warmup"] == 2 and d["scaling"] == "weak"
     assert d["value"] > 0 and d["config"]["global_batch"] == 128 and d["config"]["parallelism"] == "dp2"
     assert ("DistributedSampler" in d["config"]["sampler"]) == sampler
+
+
+def test_bench_single_rank_reports_submit_to_first_step():
+    """World size 1: after the timed run, bench.py submits a 1-replica job
+    through the operator stack (fresh child agent + zygote) and reports
+    submit -> first optimizer step in the same JSON line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "2"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "1", "--cpu",
+           "--dataset-size", "1280"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [line for line in out.stdout.splitlines() if line.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    lat = d["config"]["submit_to_first_step"]
+    assert "error" not in lat, lat
+    assert lat["job_state"] == "Succeeded" and lat["zygote_warm"] is True
+    assert 0 < d["submit_to_first_step_s"] < 60

@@ -208,3 +208,120 @@ def test_xgmi_allreduce_sgd_epilogue(world):
         assert cur == 9 % 5  # 6 eager + 3 replayed steps (the capture itself does not run)
     for p in ps:
         assert p.exitcode == 0
+
+
+def _stall_worker(rank, world, port, q):
+    """Rank 1 stalls on the host for 5 timeouts before its all-reduce:
+    rank 0's first barrier times out, every later launch returns at once,
+    and NO parameter, momentum or gradient is written on either rank."""
+    try:
+        import time
+
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch.distributed as dist
+
+        from pytorch_operator_1_amd.parallel.xgmi import XgmiAllReduce, XgmiTimeout
+
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        n, split = 431_296, 405_632
+        buf = torch.zeros(n, device=dev)
+        ar = XgmiAllReduce(buf, timeout_ms=300)
+        p = torch.randn(n, device=dev)
+        m = torch.randn(n, device=dev)
+        lr_dev = torch.tensor([0.1], device=dev)
+        kw = dict(params=p, mom=m, lr_dev=lr_dev, momentum=0.5, weight_decay=0.0, gscale=0.5, nesterov=False,
+                  zero_from=split)
+        _fill(buf, rank, 1)
+        ar.allreduce_sgd_(0, n, **kw)  # one healthy step first
+        torch.cuda.synchronize(dev)
+        ar.check()
+        _fill(buf, rank, 2)
+        snap = [t.clone() for t in (p, m, buf)]
+        dist.barrier()
+        t0 = time.perf_counter()
+        if rank == 1:
+            time.sleep(1.5)
+        for _ in range(4):
+            ar.allreduce_sgd_(0, split, chan=0, **kw)
+            ar.allreduce_sgd_(split, n - split, chan=1, **kw)
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        unchanged = all(torch.equal(a, b) for a, b in zip((p, m, buf), snap))
+        try:
+            ar.check()
+            raised = False
+        except XgmiTimeout:
+            raised = True
+        # once failed, a launch returns without waiting
+        t1 = time.perf_counter()
+        ar.allreduce_sgd_(0, n, **kw)
+        torch.cuda.synchronize(dev)
+        after = time.perf_counter() - t1
+        q.put((rank, elapsed, unchanged, raised, after))
+        dist.barrier()
+        ar.close()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), False, False, None))
+        raise
+
+
+def test_xgmi_timeout_fails_fast_without_updates():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_stall_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(2))
+    for p in ps:
+        p.join(60)
+    for rank, elapsed, unchanged, raised, after in res:
+        assert not isinstance(elapsed, str), elapsed
+        assert raised, (rank, "error word not set")
+        assert unchanged, (rank, "params/momentum/grads written by a failed all-reduce")
+        assert after < 0.1, (rank, after)
+    # rank 0: one 300 ms timeout for 8 launches, not one per barrier
+    assert res[0][1] < 1.2, res[0]
+
+
+def test_trainer_exits_retryable_when_xgmi_peer_killed(tmp_path):
+    """Two fused-trainer ranks on the one GPU (gloo for rendezvous, xGMI
+    kernel for the gradients); rank 1 SIGKILLs itself at step 100.  Rank 0
+    must exit 138 (retryable) within 5 s of the kill."""
+    import subprocess
+    import sys
+    import time
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = _port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), PTO_XGMI_TIMEOUT_MS="500", PYTHONPATH=root)
+        cmd = [sys.executable, "-m", "pytorch_operator_1_amd.train.mnist", "--backend", "gloo", "--impl", "fused",
+               "--comm", "xgmi", "--max-steps", "2000", "--log-interval", "50", "--no-test", "--train-size", "8192",
+               "--fail-at-step", "100", "--fail-rank", "1", "--dir", ""]
+        procs.append(subprocess.Popen(cmd, env=env, cwd=str(tmp_path), stdout=open(tmp_path / f"r{r}.log", "w"),
+                                      stderr=subprocess.STDOUT))
+    t_kill = None
+    end = time.time() + 200
+    while time.time() < end:
+        if t_kill is None and procs[1].poll() is not None:
+            t_kill = time.time()
+        if procs[0].poll() is not None and t_kill is not None:
+            break
+        time.sleep(0.02)
+    t_exit = time.time()
+    for p in procs:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+    log0 = (tmp_path / "r0.log").read_text()
+    log1 = (tmp_path / "r1.log").read_text()
+    assert procs[1].returncode == -9, log1[-2000:]
+    assert procs[0].returncode == 138, log0[-3000:]
+    assert "timed out" in log0
+    assert t_kill is not None and t_exit - t_kill < 5.0, (t_exit - t_kill, log0[-2000:])
