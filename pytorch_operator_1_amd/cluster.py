@@ -28,7 +28,7 @@ class LocalCluster:
     def __init__(self, gpus: int | None = None, port: int = 0, wal_path: str | None = None,
                  log_dir: str | None = None, enable_gang_scheduling: bool = False, serve_http: bool = True,
                  extra_env: dict | None = None, threadiness: int = 2, hbm_per_gpu: float | None = None,
-                 gpu_visibility: str | None = None):
+                 gpu_visibility: str | None = None, gpu_share: int | None = None):
         self.store = Store(wal_path=wal_path)
         self.client = LocalClient(self.store)
         self.server = ApiServer(self.store, port=port) if serve_http else None
@@ -39,6 +39,8 @@ class LocalCluster:
         kw = {"hbm_per_gpu": hbm_per_gpu} if hbm_per_gpu else {}
         if gpu_visibility:
             kw["gpu_visibility"] = gpu_visibility
+        if gpu_share:
+            kw["gpu_share"] = gpu_share
         self.kubelet = Kubelet(self.client, gpus=gpus, log_dir=log_dir, extra_env=extra_env, metrics=self.metrics,
                                **kw)
 

@@ -148,7 +148,7 @@ class Kubelet:
                  log_dir: str | None = None, images: dict | None = None, gpus: int | None = None,
                  poll_interval: float = 0.05, grace_seconds: float = 5.0, extra_env: dict | None = None,
                  hbm_per_gpu: float = C.HBM_PER_GPU_BYTES, gpu_visibility: str | None = None, metrics=None,
-                 sysfs_root: str | None = None):
+                 sysfs_root: str | None = None, gpu_share: int | None = None):
         self.client = client
         self.gpu_visibility = gpu_visibility or os.environ.get("PTO_GPU_VISIBILITY", "node")
         if self.gpu_visibility not in GPU_VISIBILITY_MODES:
@@ -159,6 +159,13 @@ class Kubelet:
         self._hbm_next = 0.0
         if gpus is None and agent is None:
             gpus = _visible_gpu_count()
+        # TEST-ONLY rehearsal of multi-GPU jobs on a one-GPU box: every
+        # physical GPU is offered as `gpu_share` allocatable slots, so N
+        # replicas can be admitted onto the same device (they must then use
+        # gloo + same-device xGMI IPC; RCCL refuses duplicate devices).
+        self.gpu_share = max(1, int(gpu_share or os.environ.get("PTO_GPU_SHARE", "1")))
+        if gpus is not None and agent is None:
+            gpus *= self.gpu_share
         # warm starts (node/zygote.py) unless PTO_ZYGOTE=0
         self.agent = agent or AgentClient(gpus=gpus, hbm_per_gpu=hbm_per_gpu,
                                           zygote=os.environ.get("PTO_ZYGOTE", "1") == "1")
@@ -425,16 +432,17 @@ class Kubelet:
             env["MASTER_PORT"] = str(self._job_port(pod, int(env["MASTER_PORT"])))
         # GPU pinning (module doc): one process per allocated GPU
         if gpus_requested(c) > 0 or rt.gpus:
+            mine = sorted({g // self.gpu_share for g in rt.gpus})  # allocator slot -> device
             if self.gpu_visibility == "node":
-                n = int(self.agent.gpus()["count"])
+                n = int(self.agent.gpus()["count"]) // self.gpu_share
                 env["HIP_VISIBLE_DEVICES"] = _physical_ids(list(range(n)))
-                env["LOCAL_RANK"] = str(rt.gpus[0] if rt.gpus else 0)
+                env["LOCAL_RANK"] = str(mine[0] if mine else 0)
                 env["LOCAL_WORLD_SIZE"] = env.get("WORLD_SIZE", "1")  # single node: every replica is local
             else:
-                env["HIP_VISIBLE_DEVICES"] = _physical_ids(rt.gpus)
+                env["HIP_VISIBLE_DEVICES"] = _physical_ids(mine)
                 env["LOCAL_RANK"] = "0"
                 env["LOCAL_WORLD_SIZE"] = "1"
-            env["PTO_GPU_IDS"] = _physical_ids(rt.gpus)
+            env["PTO_GPU_IDS"] = _physical_ids(mine)
         else:
             env["HIP_VISIBLE_DEVICES"] = ""
             env["PTO_NO_GPU"] = "1"

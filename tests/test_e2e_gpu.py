@@ -74,3 +74,67 @@ def test_gpu_kill_rejoin_resumes_fused_trainer(cluster, tmp_path):
     assert j["status"]["conditions"][-1]["type"] == "Succeeded", (j["status"], log[-2000:])
     assert "Resumed from" in log and "at step 100" in log
     assert any(f.startswith("ckpt-") for f in os.listdir(ck))
+
+
+# ---------------------------------------------------------------------------
+# BASELINE config 2 rehearsed through the operator on the one-GPU box: the
+# node manager offers the GPU as 4 allocatable slots (test-only gpu_share),
+# so Master=1 Worker=3 with amd.com/gpu:1 each lands on one device; ranks
+# rendezvous with gloo and all-reduce gradients with the same-device xGMI
+# kernel (RCCL refuses duplicate devices).  On the 8-GPU node the same spec
+# runs with --backend rccl, one GPU per replica.
+
+_SHARED_ARGS = ["--backend", "gloo", "--impl", "fused", "--comm", "xgmi", "--log-interval", "50", "--no-test",
+                "--train-size", "16384"]
+_SHARED_ENV = {"PTO_COMM_OVERLAP": "0"}  # skip the schedule race (4 ranks time-slice one GPU)
+
+
+@pytest.fixture(scope="module")
+def shared_cluster(tmp_path_factory):
+    c = LocalCluster(gpus=None, log_dir=str(tmp_path_factory.mktemp("pods-shared")), gpu_share=4,
+                     gpu_visibility="node").start()
+    yield c
+    c.stop()
+
+
+def _replicas(job):
+    return [f"{job}-master-0"] + [f"{job}-worker-{i}" for i in range(3)]
+
+
+def test_config2_master1_worker3_through_operator(shared_cluster):
+    c = shared_cluster
+    job = new_job("mnist-w3", image="pto/pytorch-mnist:rocm", master_args=_SHARED_ARGS + ["--max-steps", "200"],
+                  workers=3, gpus=1, env=_SHARED_ENV)
+    c.submit(job)
+    j = c.wait_for_condition("mnist-w3", timeout=400)
+    logs = {n: c.pod_log("default", n) for n in _replicas("mnist-w3")}
+    assert j["status"]["conditions"][-1]["type"] == "Succeeded", (j["status"], logs["mnist-w3-master-0"][-3000:])
+    for n, log in logs.items():
+        assert "Train Epoch: 1 [6336/16384" in log, (n, log[-2000:])
+    assert "'transport': 'xgmi'" in logs["mnist-w3-master-0"]
+    assert "Using distributed PyTorch with gloo backend" in logs["mnist-w3-master-0"]
+
+
+def test_config2_exitcode_kill_rejoin_every_replica_resumes(shared_cluster, tmp_path):
+    """Worker 0 (rank 1) is SIGKILLed at step 120 (exit 137).  The
+    survivors' xGMI barriers time out and they exit 138; both codes are
+    retryable, so the ExitCode policy recreates all four pods, which agree
+    on the newest checkpoint (step 100) and finish the job."""
+    c = shared_cluster
+    ck = str(tmp_path / "ckpt")
+    args = _SHARED_ARGS + ["--max-steps", "200", "--checkpoint-dir", ck, "--checkpoint-interval", "50",
+                           "--fail-at-step", "120", "--fail-rank", "1"]
+    job = new_job("mnist-w3-kill", image="pto/pytorch-mnist:rocm", master_args=args, workers=3, gpus=1,
+                  env=_SHARED_ENV, restart_policy="ExitCode")
+    job["spec"]["backoffLimit"] = 6
+    c.submit(job)
+    j = c.wait_for_condition("mnist-w3-kill", timeout=600)
+    logs = {n: c.pod_log("default", n) for n in _replicas("mnist-w3-kill")}
+    assert j["status"]["conditions"][-1]["type"] == "Succeeded", (j["status"], logs)
+    types = [cond["type"] for cond in j["status"]["conditions"]]
+    assert "Restarting" in types, types
+    import re
+
+    for n, log in logs.items():
+        m = re.search(r"Resumed from \S+ at step (\d+)", log)
+        assert m and int(m.group(1)) >= 100, (n, log[-2000:])
