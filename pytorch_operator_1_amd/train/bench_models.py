@@ -25,7 +25,74 @@ from ..parallel.ddp import GradBucketer
 from ..utils.profiling import StepTimer
 
 
-class ResNetTrainer:
+class _TorchOpt:
+    """Stock ``torch.optim`` behind the fused optimizers' ``step(grad_scale,
+    zero_grad)`` call (CPU runs: the HIP optimizers need a GPU)."""
+
+    def __init__(self, opt):
+        self.opt = opt
+        self.state = opt.state
+        self.param_groups = opt.param_groups
+
+    @torch.no_grad()
+    def step(self, grad_scale: float = 1.0, zero_grad: bool = False):
+        for g in self.param_groups:
+            for p in g["params"]:
+                if p.grad is not None and grad_scale != 1.0:
+                    p.grad.mul_(grad_scale)
+        self.opt.step()
+        if zero_grad:
+            self.opt.zero_grad(set_to_none=False)
+
+
+class CheckpointMixin:
+    """Named tensors of the full training state (parameters, buffers,
+    optimizer state) for :class:`..train.checkpoint.ShardedCheckpointer`,
+    and the inverse.  DDP replicas hold identical copies, so the sharded
+    checkpointer writes each tensor once (its owner rank)."""
+
+    def _param_names(self):
+        return {p: n for n, p in self.model.named_parameters()}
+
+    def checkpoint_tensors(self) -> dict:
+        t = {f"model.{n}": p.data for n, p in self.model.named_parameters()}
+        t.update({f"buffer.{n}": b for n, b in self.model.named_buffers()})
+        names = self._param_names()
+        for p, st in self.opt.state.items():
+            for k, v in st.items():
+                if torch.is_tensor(v):
+                    t[f"opt.{names[p]}.{k}"] = v
+        return t
+
+    def checkpoint_meta(self) -> dict:
+        return {"steps_done": self.steps_done, "opt_step": getattr(self.opt, "_step", None)}
+
+    def create_state(self, name: str, shape, dtype):
+        """Destination for optimizer state that does not exist yet (resume
+        before the first step): same layout as the parameter."""
+        if not name.startswith("opt."):
+            raise KeyError(name)
+        pname, key = name[4:].rsplit(".", 1)
+        p = dict(self.model.named_parameters())[pname]
+        if list(p.shape) == list(shape):
+            v = torch.zeros_like(p, dtype=dtype)
+        else:
+            v = torch.zeros(shape, dtype=dtype, device=p.device if key != "step" else "cpu")
+        self.opt.state[p][key] = v
+        return v
+
+    def after_load(self, meta: dict):
+        self.steps_done = int(meta.get("steps_done", 0))
+        if meta.get("opt_step") is not None and hasattr(self.opt, "_step"):
+            self.opt._step = int(meta["opt_step"])
+        if hasattr(self.opt, "_tables"):
+            self.opt._tables = None  # launch tables point at the old state tensors
+        refresh = getattr(self.model, "refresh_transposed", None)
+        if refresh is not None and getattr(self, "transposed_dgrad", False):
+            refresh()
+
+
+class ResNetTrainer(CheckpointMixin):
     def __init__(self, device, batch_size: int = 256, image_size: int = 224, lr: float = 0.1,
                  momentum: float = 0.9, weight_decay: float = 1e-4, seed: int = 0, bucket_mb: float | None = None):
         from ..models.resnet import resnet50, synthetic_images
@@ -39,14 +106,19 @@ class ResNetTrainer:
         self.model = resnet50().to(device=device, memory_format=torch.channels_last)
         self.model.train()
         self.bucketer = GradBucketer(self.model, bucket_mb=bucket_mb)
-        self.opt = FusedSGD(self.model.parameters(), lr=lr, momentum=momentum, weight_decay=weight_decay)
+        if device.type == "cuda":
+            self.opt = FusedSGD(self.model.parameters(), lr=lr, momentum=momentum, weight_decay=weight_decay)
+        else:
+            self.opt = _TorchOpt(torch.optim.SGD(self.model.parameters(), lr=lr, momentum=momentum,
+                                                 weight_decay=weight_decay))
         self.x, self.y = synthetic_images(batch_size, device, image_size, seed=seed)
         self._loss = None
+        self.steps_done = 0
         self.timer = StepTimer(device, enabled=False)
 
     def step(self):
         t = self.timer
-        with t.phase("forward"), torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+        with t.phase("forward"), torch.autocast(device_type=self.device.type, dtype=torch.bfloat16):
             out = self.model(self.x)
         with t.phase("forward"):
             loss = F.cross_entropy(out.float(), self.y)
@@ -58,6 +130,7 @@ class ResNetTrainer:
             self.opt.step(grad_scale=self.bucketer.grad_scale, zero_grad=self.bucketer.optimizer_zeroes_grads)
             self.bucketer.release()
         self._loss = loss.detach()
+        self.steps_done += 1
 
     def run(self, n: int):
         for _ in range(n):
@@ -74,13 +147,14 @@ class ResNetTrainer:
                 "optimizer": "SGD momentum=0.9 wd=1e-4 (FusedSGD HIP)", "amp": "bf16 autocast, fp32 master"}
 
 
-class LlamaTrainer:
+class LlamaTrainer(CheckpointMixin):
     def __init__(self, device, model: str = "llama3-8b", batch_size: int = 2, seq_len: int = 4096,
                  lr: float = 3e-4, weight_decay: float = 0.1, seed: int = 0, checkpoint: str = "none",
-                 impl: str = "hip", bucket_mb: float | None = None):
+                 impl: str | None = None, bucket_mb: float | None = None):
         from ..models.llama import CONFIGS, Llama, synthetic_tokens
 
         torch.manual_seed(seed)
+        impl = impl or ("hip" if device.type == "cuda" else "torch")
         self.cfg = CONFIGS[model]
         self.name = model
         self.device = device
@@ -92,10 +166,15 @@ class LlamaTrainer:
         if self.transposed_dgrad:
             self.model.enable_transposed_dgrad()
         self.bucketer = GradBucketer(self.model, bucket_mb=bucket_mb)
-        self.opt = FusedAdamW(self.model.parameters(), lr=lr, betas=(0.9, 0.95), eps=1e-8,
-                              weight_decay=weight_decay)
+        if device.type == "cuda":
+            self.opt = FusedAdamW(self.model.parameters(), lr=lr, betas=(0.9, 0.95), eps=1e-8,
+                                  weight_decay=weight_decay)
+        else:  # CPU: stock AdamW on the bf16 params (tests of the checkpoint/resume path)
+            self.opt = _TorchOpt(torch.optim.AdamW(self.model.parameters(), lr=lr, betas=(0.9, 0.95), eps=1e-8,
+                                                   weight_decay=weight_decay))
         self.tokens, self.labels = synthetic_tokens(batch_size, seq_len, self.cfg.vocab_size, device, seed=seed)
         self._loss = None
+        self.steps_done = 0
         self.timer = StepTimer(device, enabled=False)
 
     def step(self):
@@ -112,6 +191,7 @@ class LlamaTrainer:
             if self.transposed_dgrad:
                 self.model.refresh_transposed()
         self._loss = loss.detach()
+        self.steps_done += 1
 
     def run(self, n: int):
         for _ in range(n):

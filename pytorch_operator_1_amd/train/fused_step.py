@@ -163,6 +163,9 @@ class FusedMnistTrainer:
         self._graphs = None
         self._graph_unrolled = None
         self._graph_pow = {}
+        self._graph_close = {}
+        self._close_graphs = os.environ.get("PTO_CLOSE_GRAPHS", "1") == "1"
+        self._owed = False  # host view: a conv1 update may be owed (fused_opt)
         self._static_ar = None
         self.steps_done = 0
         self._xgmi, self.comm_info = None, {"transport": "none" if self.world == 1 else "rccl"}
@@ -372,9 +375,14 @@ class FusedMnistTrainer:
     def flush(self):
         """Commit an owed conv1 update (fused-optimizer schedule) so the flat
         buffers hold exactly the parameters/momentum an eager SGD step would
-        have left.  Idempotent; a no-op for the other schedules."""
-        if not self.fused_opt or self.steps_done == 0:
+        have left.  Idempotent; a no-op for the other schedules and after a
+        run() that ended on a closing graph."""
+        if not self.fused_opt or self.steps_done == 0 or not self._owed:
             return
+        self._commit_launch()
+        self._owed = False
+
+    def _commit_launch(self):
         _lib.check(self.L.pto_conv1_commit(self._params[self._c1:].data_ptr(), self.grads[self._c1:].data_ptr(),
                                            self.mom[self._c1:].data_ptr(), self.numel - self._c1,
                                            self.pending.data_ptr(), *self._opt_args(), self._s()), "conv1_commit")
@@ -510,6 +518,19 @@ class FusedMnistTrainer:
                     for _ in range(k):
                         self._eager_step()
                 self._graph_pow[k] = gk
+            # fused-optimizer schedule: a "closing" graph per run length
+            # 1..unroll whose last node commits the owed conv1 update, so
+            # run(n) is n // unroll replays + ONE closing replay and needs
+            # no separate flush launch afterwards
+            self._graph_close = {}
+            if self.fused_opt and self._close_graphs:
+                for k in range(1, self.unroll + 1):
+                    gk = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gk):
+                        for _ in range(k):
+                            self._eager_step()
+                        self._commit_launch()
+                    self._graph_close[k] = gk
             graphs = [self._graph_pow[1]]
             self._graph_unrolled = self._graph_pow[max(self._graph_pow)]
             # replay every graph once now and roll the training state back:
@@ -519,8 +540,8 @@ class FusedMnistTrainer:
             # peers, which replay the same graphs)
             torch.cuda.synchronize(self.device)
             snap = [t.clone() for t in state]
-            for k in sorted(self._graph_pow):
-                self._graph_pow[k].replay()
+            for g in list(self._graph_pow.values()) + list(self._graph_close.values()):
+                g.replay()
             torch.cuda.synchronize(self.device)
             for dst, src in zip(state, snap):
                 dst.copy_(src)
@@ -537,6 +558,8 @@ class FusedMnistTrainer:
         self._graphs = graphs
 
     def _graph_sizes(self) -> list[int]:
+        if self.fused_opt and self._close_graphs:
+            return sorted({1, max(1, self.unroll)})  # run() ends on a closing graph
         sizes, k = [], 1
         while k < self.unroll:
             sizes.append(k)
@@ -616,11 +639,23 @@ class FusedMnistTrainer:
             return
         if self.graph_mode == "full":
             self._ensure_captured()
+            if self._graph_close:
+                U = max(self._graph_close)
+                g = self._graph_pow[U]
+                while n > U:
+                    g.replay()
+                    self.steps_done += U
+                    n -= U
+                self._graph_close[n].replay()
+                self.steps_done += n
+                self._owed = False
+                n = 0
             for k in sorted(self._graph_pow, reverse=True):
                 g = self._graph_pow[k]
                 while n >= k:
                     g.replay()
                     self.steps_done += k
+                    self._owed = self.fused_opt
                     n -= k
         for _ in range(n):
             self.step()
@@ -663,6 +698,7 @@ class FusedMnistTrainer:
                 w1.wait()
                 self._graphs[2].replay()
         self.steps_done += 1
+        self._owed = self.fused_opt
 
     def last_loss(self):
         return float(self.loss_rows.mean().item())

@@ -126,9 +126,12 @@ _COMM_ERRORS = ("XgmiTimeout", "host barrier", "Connection closed by peer", "Con
                 "timed out", "Timeout", "DistBackendError", "ProcessGroup", "Gloo", "gloo")
 
 
-def main(argv=None):
+def run_with_retryable_exit(fn, *a, **kw):
+    """Run a trainer main; a collective/transport failure (dead or stalled
+    peer) ends the process with the retryable exit code 138 instead of a
+    traceback exit 1, so the ExitCode restart policy recreates it."""
     try:
-        return _main(argv)
+        return fn(*a, **kw)
     except Exception as e:  # noqa: BLE001
         msg = f"{type(e).__name__}: {e}"
         if any(k in msg for k in _COMM_ERRORS) or isinstance(e, getattr(dist, "DistError", ())):
@@ -136,6 +139,10 @@ def main(argv=None):
                   flush=True)
             os._exit(RETRYABLE_EXIT)
         raise
+
+
+def main(argv=None):
+    return run_with_retryable_exit(_main, argv)
 
 
 def resume_state(ckpt_dir: str | None, rank: int, world: int):

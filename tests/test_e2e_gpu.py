@@ -110,7 +110,7 @@ def test_config2_master1_worker3_through_operator(shared_cluster):
     logs = {n: c.pod_log("default", n) for n in _replicas("mnist-w3")}
     assert j["status"]["conditions"][-1]["type"] == "Succeeded", (j["status"], logs["mnist-w3-master-0"][-3000:])
     for n, log in logs.items():
-        assert "Train Epoch: 1 [6336/16384" in log, (n, log[-2000:])
+        assert "Train Epoch: 1 [6400/16384" in log, (n, log[-2000:])
     assert "'transport': 'xgmi'" in logs["mnist-w3-master-0"]
     assert "Using distributed PyTorch with gloo backend" in logs["mnist-w3-master-0"]
 

@@ -29,7 +29,7 @@ def test_unrolled_graph_matches_single_steps(B, tol):
     dev = torch.device("cuda", 0)
     a = FusedMnistTrainer(dev, batch_size=B, dataset_size=B * 12, seed=2, unroll=8)
     b = FusedMnistTrainer(dev, batch_size=B, dataset_size=B * 12, seed=2, unroll=1)
-    a.run(21)  # 2 unrolled replays + 5 single steps
+    a.run(21)  # 2 unrolled replays + one closing 5-step replay
     for _ in range(21):
         b.step()
     torch.cuda.synchronize()

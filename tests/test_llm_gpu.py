@@ -1,6 +1,7 @@
 """Numerics of the bf16 transformer kernels, FusedAdamW, and the Llama /
 ResNet DDP trainers on one MI355X.  Every HIP op is compared against a
 plain PyTorch fp32 reference of the same math."""
+import os
 import pytest
 import torch
 import torch.nn.functional as F
@@ -226,3 +227,35 @@ def test_resnet_trainer_steps():
     w = tr.model.fc.weight
     # single process: gradients are autograd's own tensors, dropped after the fused step
     assert tr.bucketer.mode == "none" and w.grad is None
+
+
+@pytest.mark.parametrize("model,extra", [("llama3-tiny", ["--seq-len", "256"]),
+                                         ("resnet50", ["--image-size", "64", "--batch-size", "8"])])
+def test_lm_trainer_kill_resume_on_gpu(tmp_path, model, extra):
+    """Config 5 for the large-model trainers: SIGKILL at step 6, restart,
+    resume from the sharded checkpoint of step 4 (params, fp32 master,
+    optimizer moments, BN buffers, step counters) and finish on the loss of
+    the uninterrupted run (HIP kernels with fp32 atomics: not bitwise)."""
+    import re
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env["PYTHONPATH"] = root
+    base = [sys.executable, "-m", "pytorch_operator_1_amd.train.lm", "--model", model, "--steps", "8",
+            "--log-interval", "2"] + extra
+
+    def run(more):
+        return subprocess.run(base + more, capture_output=True, text=True, timeout=240, env=env, cwd=str(tmp_path))
+
+    ref = run([])
+    assert ref.returncode == 0, ref.stderr[-2000:]
+    ck = ["--checkpoint-dir", str(tmp_path / "ck"), "--checkpoint-interval", "4", "--fail-at-step", "6"]
+    a = run(ck)
+    assert a.returncode == -9, a.stderr[-2000:]
+    b = run(ck)
+    assert b.returncode == 0, b.stderr[-2000:]
+    assert "Resumed from" in b.stdout and "at step 4" in b.stdout
+    fl = [float(re.search(r"final_loss=([0-9.]+)", o.stdout).group(1)) for o in (ref, b)]
+    assert abs(fl[0] - fl[1]) <= 2e-2 * abs(fl[0]), fl
