@@ -443,8 +443,8 @@ struct Agent {
         p.signal = WTERMSIG(status);
         p.exit_code = 128 + p.signal;
       }
-      // best-effort: reap the rest of the process group
-      ::kill(-pid, SIGKILL);
+      // the rest of the process group was killed by reap_one() before the
+      // leader was reaped (its pid, hence the group id, was still reserved)
       bool restart = !p.stopping && (p.restart_policy == "Always" ||
                                      (p.restart_policy == "OnFailure" && p.exit_code != 0));
       if (restart) {
@@ -658,6 +658,23 @@ static void usage() {
           "                      [--zygote PYTHON [--zygote-pythonpath DIR]]\n");
 }
 
+// Reap one exited child, if any.  The child is first observed WITHOUT
+// reaping it (WNOWAIT): while it is a zombie its pid -- and so its process
+// group id (containers are session leaders) -- cannot be recycled, so
+// SIGKILLing the group here can only hit the container's own leftovers,
+// never an unrelated group that later took the same id.
+static bool reap_one(Agent& ag) {
+  siginfo_t si;
+  memset(&si, 0, sizeof si);
+  if (waitid(P_ALL, 0, &si, WEXITED | WNOHANG | WNOWAIT) != 0 || si.si_pid == 0) return false;
+  const pid_t pid = si.si_pid;
+  if (pid != ag.zygote.pid) ::kill(-pid, SIGKILL);
+  int st = 0;
+  if (waitpid(pid, &st, 0) != pid) return false;
+  ag.on_exit(pid, st);
+  return true;
+}
+
 int main(int argc, char** argv) {
   std::string sock_path;
   bool stdio = false;
@@ -728,7 +745,10 @@ int main(int argc, char** argv) {
       if (si.ssi_signo == SIGCHLD) {
         int st;
         pid_t pid;
-        while ((pid = waitpid(-1, &st, WNOHANG)) > 0) ag.on_exit(pid, st);
+        (void)st;
+        (void)pid;
+        while (reap_one(ag)) {
+        }
       } else {
         // first SIGTERM/SIGINT: graceful stop; second: exit(1) (signals.go semantics)
         if (++signals_seen >= 2) { ag.kill_all(); return 1; }
@@ -785,9 +805,7 @@ int main(int argc, char** argv) {
     if (kv.second.state == "running" && kv.second.pid > 0) ::kill(-kv.second.pid, SIGTERM);
   double end = mono_s() + 5;
   while (mono_s() < end) {
-    int st;
-    pid_t pid = waitpid(-1, &st, WNOHANG);
-    if (pid > 0) { ag.on_exit(pid, st); continue; }
+    if (reap_one(ag)) continue;
     bool any = false;
     for (auto& kv : ag.procs) any |= kv.second.pid > 0;
     if (!any) break;

@@ -10,8 +10,8 @@ timeout -k 10 200 python bench.py --steps 20 --warmup 5 > gpurun_out/r2_bench20.
 tail -1 gpurun_out/r2_bench20.log
 timeout -k 10 200 python bench.py --no-latency > gpurun_out/r2_bench2000.log 2>&1
 tail -1 gpurun_out/r2_bench2000.log
-timeout -k 10 900 python -u -m pytest tests/test_e2e_gpu.py -x -v --timeout 600 --timeout-method thread > gpurun_out/r2_e2e.log 2>&1 || { tail -60 gpurun_out/r2_e2e.log; exit 1; }
-tail -8 gpurun_out/r2_e2e.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > gpurun_out/r2_pytest_gpu.log 2>&1 || { tail -60 gpurun_out/r2_pytest_gpu.log; exit 1; }
+tail -8 gpurun_out/r2_pytest_gpu.log
 cd /tmp
 timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/r2_prof" -o run -- python3 "$R/bench.py" --steps 50 --warmup 10 --no-latency > "$R/gpurun_out/r2_prof.log" 2>&1
 i=0
