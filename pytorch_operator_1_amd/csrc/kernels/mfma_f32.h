@@ -171,6 +171,28 @@ PTO_DEV void block_colsum64(const float* __restrict__ x, int ld, int M, int N, i
   if (t < 64 && c < N) out[c] = (red[t] + red[t + 64] + red[t + 128] + red[t + 192]) * scale;
 }
 
+// Same column sums, handed to epi(0, column, sum) instead of stored.
+template <class Epi>
+PTO_DEV void block_colsum64_epi(const float* __restrict__ x, int ld, int M, int N, int col0, float* red, Epi epi) {
+  const int t = threadIdx.x, c = col0 + (t & 63), rg = t >> 6;
+  float s = 0.f;
+  if (c < N) {
+    for (int m0 = rg; m0 < M; m0 += 64) {
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = m0 + 4 * q;
+        v[q] = m < M ? x[(size_t)m * ld + c] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s += v[q];
+    }
+  }
+  red[t] = s;
+  __syncthreads();
+  if (t < 64 && c < N) epi(0, c, red[t] + red[t + 64] + red[t + 128] + red[t + 192]);
+}
+
 PTO_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

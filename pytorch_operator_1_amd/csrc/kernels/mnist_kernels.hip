@@ -73,6 +73,7 @@ struct LazyConv1 {
   SgdArgs a;
   int bias_off;
   float* xout;          // nullptr, or [B][784]: the batch's images copied out for B1 (no cursor hop there)
+  float* w2out;         // nullptr, or [50][500]: conv2.weight as read here (k_bwd_all's dgrad reads it)
 };
 struct Conv1Commit {
   float* p;             // flat conv1 range [0, n) of params / grads / momentum
@@ -427,6 +428,13 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
     if (tid < 196) {
       reinterpret_cast<float4*>(xs)[tid] = xv;
       if (lz.xout && nt == 0) reinterpret_cast<float4*>(lz.xout + b * 784)[tid] = xv;
+    }
+    if (lz.w2out && b == 0) {  // conv2.weight snapshot: rows nt*16.. (one writer per row)
+#pragma unroll
+      for (int q = 0; q < 2048 / NTH; ++q) {
+        const int e = tid + NTH * q;
+        if (e < nrows * 125) reinterpret_cast<float4*>(lz.w2out + nt * 16 * 500)[e] = wv[q];
+      }
     }
 #pragma unroll
     for (int q = 0; q < QW1; ++q) {
@@ -1000,6 +1008,320 @@ __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ dh1, c
 constexpr int B2_CHUNK = 7;  // samples per weight-grad block (7: LDS <= 40 KB -> 4 blocks/CU, all parts co-resident)
 constexpr int B2_ICG = 10;   // input-channel pairs per sample in the dgrad part
 
+// conv2 weight-gradient block (part A of the conv2 backward): one 16-column
+// K-tile x all 64 (padded) output channels x a chunk of B2_CHUNK samples,
+// fp32 atomics into gw2.
+PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, const uint8_t* __restrict__ code2,
+                            const float* __restrict__ a1p, float* __restrict__ gw2, int B) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // ---- part A: weight gradient.  ONE staging round: the block's K-tile
+  // (16 (ic,kh,kw) columns) touches at most 2 input channels, so for all 8
+  // samples of the chunk it stages 2x144 pooled conv1 values + the 800
+  // pooled grads + 800 codes (41 KB) with coalesced 16-byte loads, then
+  // runs its 128 MFMAs from LDS.
+  const int nt = bid % 32, chunk = bid / 32;
+  const int oc = wv * 16 + (lane & 15);
+  const int g = lane >> 4;
+  const int kk = nt * 16 + (lane & 15);
+  const bool kvalid = kk < 500;
+  const int ic0 = (nt * 16) / 25;
+  const int ic = kvalid ? kk / 25 : ic0, r25 = kvalid ? kk - ic * 25 : 0;
+  const int kh = r25 / 5, kw = r25 - kh * 5;
+  const bool ocvalid = oc < C2;
+  const int b0 = chunk * B2_CHUNK, nb = min(B, b0 + B2_CHUNK) - b0;
+  float* as = smem;                                   // [8][2][144]
+  float* gs = smem + B2_CHUNK * 288;                  // [8][800]
+  uint8_t* cs = reinterpret_cast<uint8_t*>(gs + B2_CHUNK * F1IN);  // [8][800] bytes
+  const int tid = threadIdx.x;
+  {
+    float4 va[3], vg[7];
+    uint32_t vc[7];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int e = tid + 256 * q;  // float4 index over [s][ch][36]
+      const int smp = e / 72, rr = e - smp * 72, ch = rr / 36, off = (rr - ch * 36) * 4;
+      const bool ok = e < nb * 72 && ic0 + ch < C1;
+      va[q] = ok ? *reinterpret_cast<const float4*>(a1p + (b0 + smp) * A1P + (ic0 + ch) * 144 + off)
+                 : float4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      const int e = tid + 256 * q;
+      const bool ok = e < nb * (F1IN / 4);
+      vg[q] = ok ? reinterpret_cast<const float4*>(g2 + b0 * F1IN)[e] : float4{0.f, 0.f, 0.f, 0.f};
+      vc[q] = ok ? reinterpret_cast<const uint32_t*>(code2 + b0 * F1IN)[e] : 0x04040404u;
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int e = tid + 256 * q;
+      if (e < B2_CHUNK * 72) reinterpret_cast<float4*>(as)[e] = va[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      const int e = tid + 256 * q;
+      if (e < B2_CHUNK * (F1IN / 4)) {
+        reinterpret_cast<float4*>(gs)[e] = vg[q];
+        reinterpret_cast<uint32_t*>(cs)[e] = vc[q];
+      }
+    }
+  }
+  __syncthreads();
+  f32x4 acc0 = zero4(), acc1 = zero4();
+  const int koff = (ic - ic0) * 144 + kh * 12 + kw;
+  const int goff = (ocvalid ? oc : 0) * 16;
+#pragma unroll 2
+  for (int smp = 0; smp < nb; ++smp) {
+    const float* ap0 = as + smp * 288 + koff;
+#pragma unroll
+    for (int G = 0; G < 4; ++G) {
+      const int pp = 4 * G + g;
+      const float gv = ocvalid ? gs[smp * F1IN + goff + pp] : 0.f;
+      const int cd = ocvalid ? (int)cs[smp * F1IN + goff + pp] : 4;
+      const float* ap = ap0 + 2 * (pp >> 2) * 12 + 2 * (pp & 3);
+      const float bv0 = kvalid ? ap[0] : 0.f, bv1 = kvalid ? ap[1] : 0.f;
+      const float bv2 = kvalid ? ap[12] : 0.f, bv3 = kvalid ? ap[13] : 0.f;
+      acc0 = mfma16x16x4(cd == 0 ? gv : 0.f, bv0, acc0);
+      acc1 = mfma16x16x4(cd == 1 ? gv : 0.f, bv1, acc1);
+      acc0 = mfma16x16x4(cd == 2 ? gv : 0.f, bv2, acc0);
+      acc1 = mfma16x16x4(cd == 3 ? gv : 0.f, bv3, acc1);
+    }
+  }
+  const f32x4 acc = acc0 + acc1;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int m = wv * 16 + (lane >> 4) * 4 + rr;
+    const int n = nt * 16 + (lane & 15);
+    if (m < C2 && n < 500) atomicAdd(gw2 + m * 500 + n, acc[rr]);
+  }
+}
+
+// conv2 data-gradient block (part B): (sample, input-channel pair) ->
+// d(a1p) by col2im (stored when da1p != nullptr) and, with gw1 != nullptr,
+// conv1's weight/bias gradient of those two channels (fp32 atomics).
+PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, const uint8_t* __restrict__ code2,
+                            const float* __restrict__ w2, float* __restrict__ da1p, int B, const float* __restrict__ x,
+                            const long long* __restrict__ bidx, const uint8_t* __restrict__ code1,
+                            float* __restrict__ gw1, float* __restrict__ gb1, int ktail) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // ---- part B: data gradient via col2im.  Block = (sample, pair of input
+  // channels): 640 blocks at B=64, so each block's serial chain (one
+  // staging round -> dY2 expansion -> 64x64x52 GEMM -> col2im) is short.
+  // Staged: the W2 slice of the two channels (50 x 50, coalesced) + the
+  // sample's pooled grads and codes.
+  const int b = bid / B2_ICG, icg = bid - b * B2_ICG;
+  constexpr int WLD = 68;   // 64 + 4: the 4 k-rows of a wave hit disjoint banks
+  constexpr int TLD = 65;
+  float* ws = smem;                      // [52][68]
+  float* dys = ws + 52 * WLD;            // [64 pos][52 oc]   } union: ts is written
+  float* ts = dys;                       // [64 pos][65]      } after the GEMM's last dys read
+  float* gstage = dys + 64 * TLD;        // [800] grads + [800 B] codes
+  float* xs = gstage + F1IN + F1IN / 4;  // [784] input image (conv1 wgrad fusion only)
+  uint8_t* c1s = reinterpret_cast<uint8_t*>(xs + 784);  // [2][144] conv1 codes
+  const bool fuse1 = gw1 != nullptr;
+  const int r = lane & 15, gg = lane >> 4;
+  const int tid = threadIdx.x;
+  if (fuse1) {
+    const float* xb = batch_ptr(x, bidx, B * 784) + b * 784;
+    if (tid < 196) reinterpret_cast<float4*>(xs)[tid] = reinterpret_cast<const float4*>(xb)[tid];
+    if (tid < 72)
+      reinterpret_cast<uint32_t*>(c1s)[tid] =
+          reinterpret_cast<const uint32_t*>(code1 + (b * C1 + icg * 2) * 144)[tid];
+  }
+  {
+    constexpr int NW = (C2 * 50 + 255) / 256;  // 10
+    float wv_[NW];
+    const float* wb = w2 + icg * 50;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const int e = tid + 256 * q, k = e / 50, n = e - k * 50;
+      wv_[q] = e < C2 * 50 ? wb[k * 500 + n] : 0.f;
+    }
+    float4 gv4 = float4{0.f, 0.f, 0.f, 0.f};
+    uint32_t cv = 0;
+    if (tid < F1IN / 4) {
+      gv4 = reinterpret_cast<const float4*>(g2 + b * F1IN)[tid];
+      cv = reinterpret_cast<const uint32_t*>(code2 + b * F1IN)[tid];
+    }
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const int e = tid + 256 * q, k = e / 50, n = e - k * 50;
+      if (e < C2 * 50) ws[k * WLD + n] = wv_[q];
+    }
+    for (int e = tid; e < 2 * WLD; e += 256) ws[50 * WLD + e] = 0.f;     // rows 50,51
+    for (int e = tid; e < 50 * 14; e += 256) ws[(e / 14) * WLD + 50 + e % 14] = 0.f;  // cols 50..63
+    if (tid < F1IN / 4) {
+      reinterpret_cast<float4*>(gstage)[tid] = gv4;
+      reinterpret_cast<uint32_t*>(gstage + F1IN)[tid] = cv;
+    }
+  }
+  __syncthreads();
+  {
+    const float* gst = gstage;
+    const uint8_t* cst = reinterpret_cast<const uint8_t*>(gstage + F1IN);
+    for (int e = tid; e < 64 * 52; e += 256) {
+      const int pos = e / 52, oc = e - pos * 52;
+      float v = 0.f;
+      if (oc < C2) {
+        const int oh = pos >> 3, ow = pos & 7;
+        const int gi = oc * 16 + (oh >> 1) * 4 + (ow >> 1);
+        v = (cst[gi] == ((oh & 1) * 2 + (ow & 1))) ? gst[gi] : 0.f;
+      }
+      dys[e] = v;
+    }
+  }
+  __syncthreads();
+  {
+    f32x4 acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = zero4();
+#pragma unroll
+    for (int k0 = 0; k0 < 4; ++k0) {
+      if (k0 == 3 && (ktail & 1)) {
+        // K tail (k = 48..51): one k per lane group, so 4 MFMAs instead of
+        // 16 with three quarters of their K padding
+        const int k = 48 + gg;
+        const float a = dys[(wv * 16 + r) * 52 + k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = mfma16x16x4(a, ws[k * WLD + q * 16 + r], acc[q]);
+        break;
+      }
+      float av[4], bv[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = 16 * k0 + 4 * gg + j;
+        av[j] = k < 52 ? dys[(wv * 16 + r) * 52 + k] : 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bv[q][j] = k < 52 ? ws[k * WLD + q * 16 + r] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[q] = mfma16x16x4(av[j], bv[q][j], acc[q]);
+    }
+    __syncthreads();  // ts aliases dys: every wave's dys reads are done
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        ts[(wv * 16 + gg * 4 + rr) * TLD + q * 16 + r] = acc[q][rr];
+  }
+  __syncthreads();
+  float* dsum = gstage;  // free after the dY2 expansion
+  if (ktail & 2) {
+    // 288 outputs on 256 threads: one full output per thread, then the last
+    // 32 outputs split 8 ways over all threads (<= 4 taps each, 3-step
+    // shuffle sum) instead of a second full round on half a wave
+    {
+      const int o = tid, icl = o / 144, pix = o - icl * 144;
+      const int y = pix / 12, xx = pix - y * 12;
+      float sacc = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh) {
+        const int sy = y - kh;
+        if (sy < 0 || sy >= 8) continue;
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) {
+          const int sx = xx - kw;
+          if (sx < 0 || sx >= 8) continue;
+          sacc += ts[(sy * 8 + sx) * TLD + icl * 25 + kh * 5 + kw];
+        }
+      }
+      if (da1p) da1p[b * A1P + (icg * 2 + icl) * 144 + pix] = sacc;
+      dsum[o] = sacc;
+    }
+    {
+      const int o = 256 + (tid >> 3), part = tid & 7, pix = o - 144;  // icl = 1
+      const int y = pix / 12, xx = pix - y * 12;
+      float sacc = 0.f;
+#pragma unroll
+      for (int tt = part; tt < 25; tt += 8) {
+        const int kh = tt / 5, kw = tt - kh * 5, sy = y - kh, sx = xx - kw;
+        if (sy >= 0 && sy < 8 && sx >= 0 && sx < 8) sacc += ts[(sy * 8 + sx) * TLD + 25 + tt];
+      }
+      sacc += __shfl_xor(sacc, 4, 64);
+      sacc += __shfl_xor(sacc, 2, 64);
+      sacc += __shfl_xor(sacc, 1, 64);
+      if (part == 0) {
+        if (da1p) da1p[b * A1P + (icg * 2 + 1) * 144 + pix] = sacc;
+        dsum[o] = sacc;
+      }
+    }
+  } else
+  for (int o = tid; o < 2 * 144; o += 256) {
+    const int icl = o / 144, pix = o - icl * 144;
+    const int y = pix / 12, xx = pix - y * 12;
+    float s = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 5; ++kh) {
+      const int sy = y - kh;
+      if (sy < 0 || sy >= 8) continue;
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) {
+        const int sx = xx - kw;
+        if (sx < 0 || sx >= 8) continue;
+        s += ts[(sy * 8 + sx) * TLD + icl * 25 + kh * 5 + kw];
+      }
+    }
+    if (da1p) da1p[b * A1P + (icg * 2 + icl) * 144 + pix] = s;
+    dsum[o] = s;
+  }
+  if (!fuse1) return;
+  // ---- conv1 weight+bias grad of this sample's 2 channels (replaces the
+  // separate conv1-backward launch): thread = (channel, tap, pixel
+  // quarter); pooled grad expanded through the conv1 argmax code.
+  __syncthreads();
+  float* red = ws;  // free after the GEMM
+  {
+    float acc = 0.f;
+    if (tid < 208) {
+      const int pair = tid >> 2, qtr = tid & 3;
+      const int icl = pair / 26, k = pair - icl * 26;
+      const int kh = k / 5, kw = k - kh * 5;
+      for (int pix = qtr * 36; pix < qtr * 36 + 36; ++pix) {
+        const int cd = c1s[icl * 144 + pix];
+        if (cd >= 4) continue;
+        const float v = dsum[icl * 144 + pix];
+        if (k == 25) {
+          acc += v;
+        } else {
+          const int oh = 2 * (pix / 12) + (cd >> 1), ow = 2 * (pix % 12) + (cd & 1);
+          acc = fmaf(v, xs[(oh + kh) * 28 + ow + kw], acc);
+        }
+      }
+    }
+    red[tid] = acc;
+  }
+  __syncthreads();
+  if (tid < 52) {
+    const float v = red[4 * tid] + red[4 * tid + 1] + red[4 * tid + 2] + red[4 * tid + 3];
+    const int icl = tid / 26, k = tid - icl * 26, oc1 = icg * 2 + icl;
+    if (k < 25) atomicAdd(gw1 + oc1 * 25 + k, v);
+    else atomicAdd(gb1 + oc1, v);
+  }
+}
+
+// db2[oc] = sum of the unmasked pooled grads of channel oc (one wave; the
+// result is in every lane).
+PTO_DEV float c2_bias_sum(int oc, const float* __restrict__ g2, const uint8_t* __restrict__ code2, int B) {
+  const int lane = threadIdx.x & 63;
+  float s = 0.f;
+  for (int i0 = 0; i0 < B * 16; i0 += 64 * 8) {
+    float gv[8];
+    int cd[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = i0 + q * 64 + lane;
+      const int idx = (i >> 4) * F1IN + oc * 16 + (i & 15);
+      const bool ok = i < B * 16;
+      gv[q] = ok ? g2[idx] : 0.f;
+      cd[q] = ok ? (int)code2[idx] : 4;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += cd[q] < 4 ? gv[q] : 0.f;
+  }
+  return wave_sum(s);
+}
+
 __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2, const uint8_t* __restrict__ code2,
                                                    const float* __restrict__ a1p, const float* __restrict__ w2,
                                                    float* __restrict__ gw2, float* __restrict__ gb2,
@@ -1014,284 +1336,12 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
   int bid = blockIdx.x;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (bid < nA) {
-    // ---- part A: weight gradient.  ONE staging round: the block's K-tile
-    // (16 (ic,kh,kw) columns) touches at most 2 input channels, so for all 8
-    // samples of the chunk it stages 2x144 pooled conv1 values + the 800
-    // pooled grads + 800 codes (41 KB) with coalesced 16-byte loads, then
-    // runs its 128 MFMAs from LDS.
-    const int nt = bid % 32, chunk = bid / 32;
-    const int oc = wv * 16 + (lane & 15);
-    const int g = lane >> 4;
-    const int kk = nt * 16 + (lane & 15);
-    const bool kvalid = kk < 500;
-    const int ic0 = (nt * 16) / 25;
-    const int ic = kvalid ? kk / 25 : ic0, r25 = kvalid ? kk - ic * 25 : 0;
-    const int kh = r25 / 5, kw = r25 - kh * 5;
-    const bool ocvalid = oc < C2;
-    const int b0 = chunk * B2_CHUNK, nb = min(B, b0 + B2_CHUNK) - b0;
-    float* as = smem;                                   // [8][2][144]
-    float* gs = smem + B2_CHUNK * 288;                  // [8][800]
-    uint8_t* cs = reinterpret_cast<uint8_t*>(gs + B2_CHUNK * F1IN);  // [8][800] bytes
-    const int tid = threadIdx.x;
-    {
-      float4 va[3], vg[7];
-      uint32_t vc[7];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int e = tid + 256 * q;  // float4 index over [s][ch][36]
-        const int smp = e / 72, rr = e - smp * 72, ch = rr / 36, off = (rr - ch * 36) * 4;
-        const bool ok = e < nb * 72 && ic0 + ch < C1;
-        va[q] = ok ? *reinterpret_cast<const float4*>(a1p + (b0 + smp) * A1P + (ic0 + ch) * 144 + off)
-                   : float4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int q = 0; q < 7; ++q) {
-        const int e = tid + 256 * q;
-        const bool ok = e < nb * (F1IN / 4);
-        vg[q] = ok ? reinterpret_cast<const float4*>(g2 + b0 * F1IN)[e] : float4{0.f, 0.f, 0.f, 0.f};
-        vc[q] = ok ? reinterpret_cast<const uint32_t*>(code2 + b0 * F1IN)[e] : 0x04040404u;
-      }
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int e = tid + 256 * q;
-        if (e < B2_CHUNK * 72) reinterpret_cast<float4*>(as)[e] = va[q];
-      }
-#pragma unroll
-      for (int q = 0; q < 7; ++q) {
-        const int e = tid + 256 * q;
-        if (e < B2_CHUNK * (F1IN / 4)) {
-          reinterpret_cast<float4*>(gs)[e] = vg[q];
-          reinterpret_cast<uint32_t*>(cs)[e] = vc[q];
-        }
-      }
-    }
-    __syncthreads();
-    f32x4 acc0 = zero4(), acc1 = zero4();
-    const int koff = (ic - ic0) * 144 + kh * 12 + kw;
-    const int goff = (ocvalid ? oc : 0) * 16;
-#pragma unroll 2
-    for (int smp = 0; smp < nb; ++smp) {
-      const float* ap0 = as + smp * 288 + koff;
-#pragma unroll
-      for (int G = 0; G < 4; ++G) {
-        const int pp = 4 * G + g;
-        const float gv = ocvalid ? gs[smp * F1IN + goff + pp] : 0.f;
-        const int cd = ocvalid ? (int)cs[smp * F1IN + goff + pp] : 4;
-        const float* ap = ap0 + 2 * (pp >> 2) * 12 + 2 * (pp & 3);
-        const float bv0 = kvalid ? ap[0] : 0.f, bv1 = kvalid ? ap[1] : 0.f;
-        const float bv2 = kvalid ? ap[12] : 0.f, bv3 = kvalid ? ap[13] : 0.f;
-        acc0 = mfma16x16x4(cd == 0 ? gv : 0.f, bv0, acc0);
-        acc1 = mfma16x16x4(cd == 1 ? gv : 0.f, bv1, acc1);
-        acc0 = mfma16x16x4(cd == 2 ? gv : 0.f, bv2, acc0);
-        acc1 = mfma16x16x4(cd == 3 ? gv : 0.f, bv3, acc1);
-      }
-    }
-    const f32x4 acc = acc0 + acc1;
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int m = wv * 16 + (lane >> 4) * 4 + rr;
-      const int n = nt * 16 + (lane & 15);
-      if (m < C2 && n < 500) atomicAdd(gw2 + m * 500 + n, acc[rr]);
-    }
+    c2_wgrad_block(bid, smem, g2, code2, a1p, gw2, B);
     return;
   }
   bid -= nA;
   if (bid < nB) {
-    // ---- part B: data gradient via col2im.  Block = (sample, pair of input
-    // channels): 640 blocks at B=64, so each block's serial chain (one
-    // staging round -> dY2 expansion -> 64x64x52 GEMM -> col2im) is short.
-    // Staged: the W2 slice of the two channels (50 x 50, coalesced) + the
-    // sample's pooled grads and codes.
-    const int b = bid / B2_ICG, icg = bid - b * B2_ICG;
-    constexpr int WLD = 68;   // 64 + 4: the 4 k-rows of a wave hit disjoint banks
-    constexpr int TLD = 65;
-    float* ws = smem;                      // [52][68]
-    float* dys = ws + 52 * WLD;            // [64 pos][52 oc]   } union: ts is written
-    float* ts = dys;                       // [64 pos][65]      } after the GEMM's last dys read
-    float* gstage = dys + 64 * TLD;        // [800] grads + [800 B] codes
-    float* xs = gstage + F1IN + F1IN / 4;  // [784] input image (conv1 wgrad fusion only)
-    uint8_t* c1s = reinterpret_cast<uint8_t*>(xs + 784);  // [2][144] conv1 codes
-    const bool fuse1 = gw1 != nullptr;
-    const int r = lane & 15, gg = lane >> 4;
-    const int tid = threadIdx.x;
-    if (fuse1) {
-      const float* xb = batch_ptr(x, bidx, B * 784) + b * 784;
-      if (tid < 196) reinterpret_cast<float4*>(xs)[tid] = reinterpret_cast<const float4*>(xb)[tid];
-      if (tid < 72)
-        reinterpret_cast<uint32_t*>(c1s)[tid] =
-            reinterpret_cast<const uint32_t*>(code1 + (b * C1 + icg * 2) * 144)[tid];
-    }
-    {
-      constexpr int NW = (C2 * 50 + 255) / 256;  // 10
-      float wv_[NW];
-      const float* wb = w2 + icg * 50;
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        const int e = tid + 256 * q, k = e / 50, n = e - k * 50;
-        wv_[q] = e < C2 * 50 ? wb[k * 500 + n] : 0.f;
-      }
-      float4 gv4 = float4{0.f, 0.f, 0.f, 0.f};
-      uint32_t cv = 0;
-      if (tid < F1IN / 4) {
-        gv4 = reinterpret_cast<const float4*>(g2 + b * F1IN)[tid];
-        cv = reinterpret_cast<const uint32_t*>(code2 + b * F1IN)[tid];
-      }
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        const int e = tid + 256 * q, k = e / 50, n = e - k * 50;
-        if (e < C2 * 50) ws[k * WLD + n] = wv_[q];
-      }
-      for (int e = tid; e < 2 * WLD; e += 256) ws[50 * WLD + e] = 0.f;     // rows 50,51
-      for (int e = tid; e < 50 * 14; e += 256) ws[(e / 14) * WLD + 50 + e % 14] = 0.f;  // cols 50..63
-      if (tid < F1IN / 4) {
-        reinterpret_cast<float4*>(gstage)[tid] = gv4;
-        reinterpret_cast<uint32_t*>(gstage + F1IN)[tid] = cv;
-      }
-    }
-    __syncthreads();
-    {
-      const float* gst = gstage;
-      const uint8_t* cst = reinterpret_cast<const uint8_t*>(gstage + F1IN);
-      for (int e = tid; e < 64 * 52; e += 256) {
-        const int pos = e / 52, oc = e - pos * 52;
-        float v = 0.f;
-        if (oc < C2) {
-          const int oh = pos >> 3, ow = pos & 7;
-          const int gi = oc * 16 + (oh >> 1) * 4 + (ow >> 1);
-          v = (cst[gi] == ((oh & 1) * 2 + (ow & 1))) ? gst[gi] : 0.f;
-        }
-        dys[e] = v;
-      }
-    }
-    __syncthreads();
-    {
-      f32x4 acc[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] = zero4();
-#pragma unroll
-      for (int k0 = 0; k0 < 4; ++k0) {
-        if (k0 == 3 && (ktail & 1)) {
-          // K tail (k = 48..51): one k per lane group, so 4 MFMAs instead of
-          // 16 with three quarters of their K padding
-          const int k = 48 + gg;
-          const float a = dys[(wv * 16 + r) * 52 + k];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) acc[q] = mfma16x16x4(a, ws[k * WLD + q * 16 + r], acc[q]);
-          break;
-        }
-        float av[4], bv[4][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int k = 16 * k0 + 4 * gg + j;
-          av[j] = k < 52 ? dys[(wv * 16 + r) * 52 + k] : 0.f;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) bv[q][j] = k < 52 ? ws[k * WLD + q * 16 + r] : 0.f;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[q] = mfma16x16x4(av[j], bv[q][j], acc[q]);
-      }
-      __syncthreads();  // ts aliases dys: every wave's dys reads are done
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-          ts[(wv * 16 + gg * 4 + rr) * TLD + q * 16 + r] = acc[q][rr];
-    }
-    __syncthreads();
-    float* dsum = gstage;  // free after the dY2 expansion
-    if (ktail & 2) {
-      // 288 outputs on 256 threads: one full output per thread, then the last
-      // 32 outputs split 8 ways over all threads (<= 4 taps each, 3-step
-      // shuffle sum) instead of a second full round on half a wave
-      {
-        const int o = tid, icl = o / 144, pix = o - icl * 144;
-        const int y = pix / 12, xx = pix - y * 12;
-        float sacc = 0.f;
-#pragma unroll
-        for (int kh = 0; kh < 5; ++kh) {
-          const int sy = y - kh;
-          if (sy < 0 || sy >= 8) continue;
-#pragma unroll
-          for (int kw = 0; kw < 5; ++kw) {
-            const int sx = xx - kw;
-            if (sx < 0 || sx >= 8) continue;
-            sacc += ts[(sy * 8 + sx) * TLD + icl * 25 + kh * 5 + kw];
-          }
-        }
-        da1p[b * A1P + (icg * 2 + icl) * 144 + pix] = sacc;
-        dsum[o] = sacc;
-      }
-      {
-        const int o = 256 + (tid >> 3), part = tid & 7, pix = o - 144;  // icl = 1
-        const int y = pix / 12, xx = pix - y * 12;
-        float sacc = 0.f;
-#pragma unroll
-        for (int tt = part; tt < 25; tt += 8) {
-          const int kh = tt / 5, kw = tt - kh * 5, sy = y - kh, sx = xx - kw;
-          if (sy >= 0 && sy < 8 && sx >= 0 && sx < 8) sacc += ts[(sy * 8 + sx) * TLD + 25 + tt];
-        }
-        sacc += __shfl_xor(sacc, 4, 64);
-        sacc += __shfl_xor(sacc, 2, 64);
-        sacc += __shfl_xor(sacc, 1, 64);
-        if (part == 0) {
-          da1p[b * A1P + (icg * 2 + 1) * 144 + pix] = sacc;
-          dsum[o] = sacc;
-        }
-      }
-    } else
-    for (int o = tid; o < 2 * 144; o += 256) {
-      const int icl = o / 144, pix = o - icl * 144;
-      const int y = pix / 12, xx = pix - y * 12;
-      float s = 0.f;
-#pragma unroll
-      for (int kh = 0; kh < 5; ++kh) {
-        const int sy = y - kh;
-        if (sy < 0 || sy >= 8) continue;
-#pragma unroll
-        for (int kw = 0; kw < 5; ++kw) {
-          const int sx = xx - kw;
-          if (sx < 0 || sx >= 8) continue;
-          s += ts[(sy * 8 + sx) * TLD + icl * 25 + kh * 5 + kw];
-        }
-      }
-      da1p[b * A1P + (icg * 2 + icl) * 144 + pix] = s;
-      dsum[o] = s;
-    }
-    if (!fuse1) return;
-    // ---- conv1 weight+bias grad of this sample's 2 channels (replaces the
-    // separate conv1-backward launch): thread = (channel, tap, pixel
-    // quarter); pooled grad expanded through the conv1 argmax code.
-    __syncthreads();
-    float* red = ws;  // free after the GEMM
-    {
-      float acc = 0.f;
-      if (tid < 208) {
-        const int pair = tid >> 2, qtr = tid & 3;
-        const int icl = pair / 26, k = pair - icl * 26;
-        const int kh = k / 5, kw = k - kh * 5;
-        for (int pix = qtr * 36; pix < qtr * 36 + 36; ++pix) {
-          const int cd = c1s[icl * 144 + pix];
-          if (cd >= 4) continue;
-          const float v = dsum[icl * 144 + pix];
-          if (k == 25) {
-            acc += v;
-          } else {
-            const int oh = 2 * (pix / 12) + (cd >> 1), ow = 2 * (pix % 12) + (cd & 1);
-            acc = fmaf(v, xs[(oh + kh) * 28 + ow + kw], acc);
-          }
-        }
-      }
-      red[tid] = acc;
-    }
-    __syncthreads();
-    if (tid < 52) {
-      const float v = red[4 * tid] + red[4 * tid + 1] + red[4 * tid + 2] + red[4 * tid + 3];
-      const int icl = tid / 26, k = tid - icl * 26, oc1 = icg * 2 + icl;
-      if (k < 25) atomicAdd(gw1 + oc1 * 25 + k, v);
-      else atomicAdd(gb1 + oc1, v);
-    }
+    c2_dgrad_block(bid, smem, g2, code2, w2, da1p, B, x, bidx, code1, gw1, gb1, ktail);
     return;
   }
   bid -= nB;
@@ -1299,22 +1349,7 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
     // ---- part C: conv2 bias grad, one wave per output channel
     const int oc = bid * 4 + wv;
     if (oc >= C2) return;
-    float s = 0.f;
-    for (int i0 = 0; i0 < B * 16; i0 += 64 * 8) {
-      float gv[8];
-      int cd[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int i = i0 + q * 64 + lane;
-        const int idx = (i >> 4) * F1IN + oc * 16 + (i & 15);
-        const bool ok = i < B * 16;
-        gv[q] = ok ? g2[idx] : 0.f;
-        cd[q] = ok ? (int)code2[idx] : 4;
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) s += cd[q] < 4 ? gv[q] : 0.f;
-    }
-    s = wave_sum(s);
+    const float s = c2_bias_sum(oc, g2, code2, B);
     if (lane == 0) gb2[oc] = s;
     return;
   }
@@ -1329,6 +1364,42 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
   bid -= NWF;
   if (bid < 8) block_colsum64(fdh1, F1OUT, B, F1OUT, bid * 64, smem, fgb1);
   else block_colsum64(fdl, NCLS, B, NCLS, 0, smem, fgb2);
+}
+
+// One wave: a 16x16 tile of dW1 = dh1^T a2p (K = B) consumed straight from
+// the MMA accumulators by SGD on fc1.weight (pw/mw: its param/momentum
+// rows); the gradient itself is never stored.  The wave's p/m elements are
+// loaded before the MMA chain so their latency overlaps the operand loads.
+PTO_DEV void dw1_sgd_tile(int tile, const float* __restrict__ dh1, const float* __restrict__ a2p,
+                          float* __restrict__ pw, float* __restrict__ mw, int B, const SgdArgs& a) {
+  constexpr int MT = (F1OUT + 15) / 16, NT = (F1IN + 15) / 16;
+  if (tile >= MT * NT) return;
+  const int mt = tile % MT, nt = tile / MT, lane = threadIdx.x & 63;
+  const int n = nt * 16 + (lane & 15);
+  float pv[4], mv[4];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int r = mt * 16 + (lane >> 4) * 4 + rr;
+    const bool ok = r < F1OUT && n < F1IN;
+    pv[rr] = ok ? pw[r * F1IN + n] : 0.f;
+    mv[rr] = ok ? mw[r * F1IN + n] : 0.f;
+  }
+  const float lr = *a.lr;
+  // variant 1: 4 k-groups per memory round (K = B = 64 exactly, 32 loads
+  // per lane in flight) instead of 8 with half of them masked off
+  const f32x4 acc =
+      (a.variant & 1)
+          ? wave_tile_16x16<LAY_KROW, LAY_KROW, 4>(dh1, F1OUT, a2p, F1IN, F1OUT, F1IN, B, mt * 16, nt * 16, 0, B)
+          : wave_tile_16x16<LAY_KROW, LAY_KROW, 8>(dh1, F1OUT, a2p, F1IN, F1OUT, F1IN, B, mt * 16, nt * 16, 0, B);
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int r = mt * 16 + (lane >> 4) * 4 + rr;
+    if (r < F1OUT && n < F1IN) {
+      sgd_elem(pv[rr], acc[rr], mv[rr], lr, a.mom, a.wd, a.gscale, a.nesterov);
+      pw[r * F1IN + n] = pv[rr];
+      mw[r * F1IN + n] = mv[rr];
+    }
+  }
 }
 
 // ---------------------------------------------------------------- B1 ----
@@ -1484,39 +1555,7 @@ __global__ __launch_bounds__(256) void k_conv1_bwd_sgd(const float* __restrict__
   }
   bid -= nconv;
   if (bid < ndw) {  // dW1 = dh1^T a2p (K = B, 4 tiles per block) consumed by SGD on fc1.weight = [skip_lo, skip_hi)
-    // one 16x16 tile per wave; the wave's p/m elements are loaded before the
-    // MMA chain so their latency overlaps the operand loads
-    constexpr int MT = (F1OUT + 15) / 16, NT = (F1IN + 15) / 16;
-    const int tile = bid * 4 + (threadIdx.x >> 6);
-    if (tile >= MT * NT) return;
-    const int mt = tile % MT, nt = tile / MT, lane = threadIdx.x & 63;
-    const int n = nt * 16 + (lane & 15);
-    float* pw = p + skip_lo;
-    float* mw = m + skip_lo;
-    float pv[4], mv[4];
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int r = mt * 16 + (lane >> 4) * 4 + rr;
-      const bool ok = r < F1OUT && n < F1IN;
-      pv[rr] = ok ? pw[r * F1IN + n] : 0.f;
-      mv[rr] = ok ? mw[r * F1IN + n] : 0.f;
-    }
-    const float lr = *a.lr;
-    // variant 1: 4 k-groups per memory round (K = B = 64 exactly, 32 loads
-    // per lane in flight) instead of 8 with half of them masked off
-    const f32x4 acc =
-        (a.variant & 1)
-            ? wave_tile_16x16<LAY_KROW, LAY_KROW, 4>(dh1, F1OUT, a2p, F1IN, F1OUT, F1IN, B, mt * 16, nt * 16, 0, B)
-            : wave_tile_16x16<LAY_KROW, LAY_KROW, 8>(dh1, F1OUT, a2p, F1IN, F1OUT, F1IN, B, mt * 16, nt * 16, 0, B);
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int r = mt * 16 + (lane >> 4) * 4 + rr;
-      if (r < F1OUT && n < F1IN) {
-        sgd_elem(pv[rr], acc[rr], mv[rr], lr, a.mom, a.wd, a.gscale, a.nesterov);
-        pw[r * F1IN + n] = pv[rr];
-        mw[r * F1IN + n] = mv[rr];
-      }
-    }
+    dw1_sgd_tile(bid * 4 + (threadIdx.x >> 6), dh1, a2p, p + skip_lo, m + skip_lo, B, a);
     return;
   }
   bid -= ndw;
@@ -1524,6 +1563,141 @@ __global__ __launch_bounds__(256) void k_conv1_bwd_sgd(const float* __restrict__
   const long long i = bid < nsgd_lo ? ((long long)bid * 256 + threadIdx.x) * 4
                                     : skip_hi + ((long long)(bid - nsgd_lo) * 256 + threadIdx.x) * 4;
   if (bid < nsgd_lo ? i < skip_lo : i < nflat) sgd_flat4(p, g, m, i, *a.lr, a, i >= zero_from);
+}
+
+// ------------------------------------------------------ B (all-in-one) ----
+// The whole backward + optimizer of the single-process step in ONE launch
+// (F12 -> F3 -> F4dx -> B: four launches per step).  Every block range
+// consumes only what F4dx / F12 produced, and every parameter is updated by
+// the block that finishes its gradient:
+//   A  conv2 wgrad (split-K over sample chunks, fp32 atomics).  Per 16-column
+//      tile an arrival counter: the chunk block that arrives LAST (after its
+//      own atomics have been performed: vmcnt(0)) consumes the finished tile
+//      with atomic exchanges (read the memory-side sum, re-zero it for the
+//      next step) and applies SGD to conv2.weight -- a stream-K style fixup,
+//      no separate optimizer pass.  Nobody else in this launch reads
+//      conv2.weight: the dgrad blocks read F12's snapshot of it (w2f).
+//   B  conv2 dgrad via col2im, with conv1's wgrad of the same sample/channel
+//      pair fused (atomics; conv1's update stays "owed": applied by the next
+//      F12, committed by the next F4dx).  d(a1p) is never stored.
+//   C  conv2 bias: one wave per channel sums and updates.
+//   D  dW1 = dh1^T a2p tiles consumed by SGD on fc1.weight.
+//   F  dW2 (fc2) tiles, db1, db2 with SGD epilogues.
+// Block 0 advances the batch cursor and marks conv1's update as owed.
+struct BwdAllArgs {
+  const float* g2;         // d(a2p) [B][800]
+  const uint8_t* code2;
+  const float* a1p;
+  const float* w2f;        // conv2.weight as F12 read it (snapshot)
+  const float* x;          // the batch's images (F12's copy)
+  const uint8_t* code1;
+  float* gw1;              // conv1 weight/bias grads (atomics, zero on entry)
+  float* gb1;
+  float* p2w; float* g2w; float* m2w;  // conv2.weight: param, grad (zero on entry, re-zeroed here), momentum
+  int* ctr;                // [32] arrival counters, zero on entry and on exit
+  float* p2b; float* m2b;  // conv2.bias
+  const float* dh1; const float* a2p; const float* h1; const float* dl;
+  float* p1w; float* m1w;  // fc1.weight
+  float* p1b; float* m1b;  // fc1.bias
+  float* pfw; float* mfw;  // fc2.weight
+  float* pfb; float* mfb;  // fc2.bias
+  SgdArgs a;
+  long long* bidx;
+  long long nbatches;
+  int* pending;
+  int B, nA, nB, nC, nD, nF, ktail;
+};
+
+struct EpiSgd {
+  float* p; float* m; int ld; float lr; const SgdArgs* a;
+  PTO_DEV void operator()(int r, int c, float g) const {
+    const int i = r * ld + c;
+    float pv = p[i], mv = m[i];
+    sgd_elem(pv, g, mv, lr, a->mom, a->wd, a->gscale, a->nesterov);
+    p[i] = pv;
+    m[i] = mv;
+  }
+};
+
+__global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int s_last;
+  int bid = blockIdx.x;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (bid == 0 && threadIdx.x == 0) {  // no block of this launch reads the cursor
+    *A.bidx = (*A.bidx + 1) % A.nbatches;
+    *A.pending = 1;
+  }
+  if (bid < A.nA) {
+    c2_wgrad_block(bid, smem, A.g2, A.code2, A.a1p, A.g2w, A.B);
+    // arrival: every lane's atomics have been performed at the memory side
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int nt = bid % 32, nchunk = A.nA / 32;
+    if (threadIdx.x == 0) {
+      const int old = __hip_atomic_fetch_add(A.ctr + nt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == nchunk - 1;
+      if (s_last) __hip_atomic_store(A.ctr + nt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    const float lr = *A.a.lr;
+    int idx[4];
+    float gv[4], pv[4], mv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // 50 rows x 16 columns = 800 elements
+      const int e = threadIdx.x + 256 * q, row = e >> 4, col = nt * 16 + (e & 15);
+      idx[q] = (e < C2 * 16 && col < 500) ? row * 500 + col : -1;
+      if (idx[q] >= 0) {
+        gv[q] = atomicExch(A.g2w + idx[q], 0.f);
+        pv[q] = A.p2w[idx[q]];
+        mv[q] = A.m2w[idx[q]];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (idx[q] >= 0) {
+        sgd_elem(pv[q], gv[q], mv[q], lr, A.a.mom, A.a.wd, A.a.gscale, A.a.nesterov);
+        A.p2w[idx[q]] = pv[q];
+        A.m2w[idx[q]] = mv[q];
+      }
+    return;
+  }
+  bid -= A.nA;
+  if (bid < A.nB) {
+    c2_dgrad_block(bid, smem, A.g2, A.code2, A.w2f, nullptr, A.B, A.x, nullptr, A.code1, A.gw1, A.gb1, A.ktail);
+    return;
+  }
+  bid -= A.nB;
+  if (bid < A.nC) {
+    const int oc = bid * 4 + wv;
+    if (oc >= C2) return;
+    const float g = c2_bias_sum(oc, A.g2, A.code2, A.B);
+    if (lane == 0) {
+      float pv = A.p2b[oc], mv = A.m2b[oc];
+      sgd_elem(pv, g, mv, *A.a.lr, A.a.mom, A.a.wd, A.a.gscale, A.a.nesterov);
+      A.p2b[oc] = pv;
+      A.m2b[oc] = mv;
+    }
+    return;
+  }
+  bid -= A.nC;
+  if (bid < A.nD) {
+    dw1_sgd_tile(bid * 4 + wv, A.dh1, A.a2p, A.p1w, A.m1w, A.B, A.a);
+    return;
+  }
+  bid -= A.nD;
+  if (bid >= A.nF) return;
+  const float lr = *A.a.lr;
+  constexpr int NWF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4;
+  if (bid < NWF) {
+    block_gemm_4tiles<LAY_KROW, LAY_KROW>(A.dl, NCLS, A.h1, F1OUT, NCLS, F1OUT, A.B, bid,
+                                          EpiSgd{A.pfw, A.mfw, F1OUT, lr, &A.a});
+    return;
+  }
+  bid -= NWF;
+  if (bid < 8) block_colsum64_epi(A.dh1, F1OUT, A.B, F1OUT, bid * 64, smem, EpiSgd{A.p1b, A.m1b, 0, lr, &A.a});
+  else block_colsum64_epi(A.dl, NCLS, A.B, NCLS, 0, smem, EpiSgd{A.pfb, A.mfb, 0, lr, &A.a});
 }
 
 // Host-side flush of an owed conv1 update (before the parameters are read
@@ -1641,7 +1815,7 @@ PTO_API int pto_conv12_fwd_lazy(const float* x, const float* w1, const float* b1
                                 float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B, const long long* bidx,
                                 const float* g1f, const float* m1f, int bias_off, const int* pending, const float* lr,
                                 float mom, float wd, float gscale, int nesterov, int version, hipStream_t s) {
-  LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off, nullptr};
+  LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off, nullptr, nullptr};
   if (version == 2 && fwd_threads() == 1024)
     hipLaunchKernelGGL(k_conv12_fwd2_t<1024>, dim3(B * 4), dim3(1024), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p,
                        code2, B, bidx, lz);
@@ -1661,8 +1835,8 @@ PTO_API int pto_conv12_fwd_lazy_x(const float* x, const float* w1, const float* 
                                   const float* b2, float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B,
                                   const long long* bidx, const float* g1f, const float* m1f, int bias_off,
                                   const int* pending, const float* lr, float mom, float wd, float gscale, int nesterov,
-                                  float* xout, hipStream_t s) {
-  LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off, xout};
+                                  float* xout, float* w2out, hipStream_t s) {
+  LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off, xout, w2out};
   static const int bal = [] {
     const char* e = getenv("PTO_CONV1_BALANCED");  // 0 = 15 lockstep tasks (A/B)
     return e ? atoi(e) : 1;
@@ -1963,5 +2137,40 @@ PTO_API int pto_conv1_bwd_data(const float* g1, const uint8_t* code1, const floa
 
 PTO_API int pto_eval_head(const float* logp, const int64_t* labels, float* stats, int B, hipStream_t s) {
   hipLaunchKernelGGL(k_eval_head, dim3((B + 255) / 256), dim3(256), 0, s, logp, labels, stats, B);
+  LAUNCH_CHECK();
+}
+
+// The all-in-one backward + optimizer launch (k_bwd_all).  Flat-buffer
+// views: p/g/m + offsets of each parameter (elements); ctr: 32 zeroed ints.
+PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p, const float* w2f, const float* x,
+                        const uint8_t* code1, const float* dh1, const float* a2p, const float* h1, const float* dl,
+                        float* p, float* g, float* m, long long off_fc2w, long long off_fc2b, long long off_fc1w,
+                        long long off_fc1b, long long off_c2w, long long off_c2b, long long off_c1w,
+                        long long off_c1b, int* ctr, long long* bidx, long long nbatches, int* pending, int B,
+                        const float* lr, float mom, float wd, float gscale, int nesterov, hipStream_t s) {
+  if (!bidx || !pending || !ctr || nbatches < 1 || B < 1) return -1;
+  BwdAllArgs A;
+  A.g2 = g2; A.code2 = code2; A.a1p = a1p; A.w2f = w2f; A.x = x; A.code1 = code1;
+  A.gw1 = g + off_c1w; A.gb1 = g + off_c1b;
+  A.p2w = p + off_c2w; A.g2w = g + off_c2w; A.m2w = m + off_c2w; A.ctr = ctr;
+  A.p2b = p + off_c2b; A.m2b = m + off_c2b;
+  A.dh1 = dh1; A.a2p = a2p; A.h1 = h1; A.dl = dl;
+  A.p1w = p + off_fc1w; A.m1w = m + off_fc1w;
+  A.p1b = p + off_fc1b; A.m1b = m + off_fc1b;
+  A.pfw = p + off_fc2w; A.mfw = m + off_fc2w;
+  A.pfb = p + off_fc2b; A.mfb = m + off_fc2b;
+  A.a = sgd_args(lr, mom, wd, gscale, nesterov);
+  A.a.variant = 1;  // dW1 tiles: 4 k-groups per memory round
+  A.bidx = bidx; A.nbatches = nbatches; A.pending = pending; A.B = B;
+  A.nA = ((B + B2_CHUNK - 1) / B2_CHUNK) * 32;
+  A.nB = B * B2_ICG;
+  A.nC = (C2 + 3) / 4;
+  A.nD = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
+  A.nF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9;
+  A.ktail = 3;
+  const size_t ldsA = B2_CHUNK * (288 + F1IN + F1IN / 4) * sizeof(float);
+  const size_t ldsB = (52 * 68 + 64 * 65 + F1IN + F1IN / 4 + 784 + 72) * sizeof(float);
+  const size_t lds = ldsA > ldsB ? ldsA : ldsB;
+  hipLaunchKernelGGL(k_bwd_all, dim3(A.nA + A.nB + A.nC + A.nD + A.nF), dim3(256), lds, s, A);
   LAUNCH_CHECK();
 }

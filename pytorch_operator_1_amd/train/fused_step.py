@@ -145,6 +145,13 @@ class FusedMnistTrainer:
         # reductions in B2, the batch-cursor advance in B1: 5 launches per
         # step (PTO_F4DX=0: the 6-launch schedule)
         self.merge_f4 = self.xcur is not None and os.environ.get("PTO_F4DX", "1") == "1"
+        # the whole backward + optimizer as ONE launch (k_bwd_all): 4 launches
+        # per step; conv2.weight is updated by the last-arriving wgrad chunk
+        # of each tile, the dgrad blocks read F12's snapshot of it
+        # (PTO_BWD_ALL=0: conv2 backward and B1 as two launches)
+        self.bwd_all = self.merge_f4 and os.environ.get("PTO_BWD_ALL", "1") == "1"
+        self.w2f = torch.empty(50 * 500, device=device) if self.bwd_all else None
+        self.c2_ctr = torch.zeros(32, device=device, dtype=torch.int32) if self.bwd_all else None
         # multi-GPU schedule: overlap the fc bucket's all-reduce with the conv
         # backward on a side stream (PTO_COMM_OVERLAP=1), or all-reduce the
         # whole flat buffer once after the backward on the compute stream
@@ -241,7 +248,7 @@ class FusedMnistTrainer:
                    self.grads[self._c1:].data_ptr(), self.mom[self._c1:].data_ptr(), self._c1_bias,
                    self.pending.data_ptr(), *o)
             if self.xcur is not None:
-                c(L.pto_conv12_fwd_lazy_x(*f12, self.xcur.data_ptr(), s), "conv12_fwd_lazy_x")
+                c(L.pto_conv12_fwd_lazy_x(*f12, self.xcur.data_ptr(), _lib.ptr(self.w2f), s), "conv12_fwd_lazy_x")
             else:
                 c(L.pto_conv12_fwd_lazy(*f12, self.conv12_version, s), "conv12_fwd_lazy")
             c(L.pto_linear_fwd(self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
@@ -311,6 +318,16 @@ class FusedMnistTrainer:
         # but measured break-even: every sample-block adds into the same 520
         # addresses, 64-way atomic contention.  The separate 320-block conv1
         # launch below adds each address only 16 times.)
+        if self.bwd_all:  # the whole backward + every parameter update in one launch
+            offs = param_offsets()[0]
+            o = [offs[n][0] for n in ("fc2.weight", "fc2.bias", "fc1.weight", "fc1.bias", "conv2.weight",
+                                      "conv2.bias", "conv1.weight", "conv1.bias")]
+            c(L.pto_bwd_all(self.da2p.data_ptr(), self.code2.data_ptr(), self.a1p.data_ptr(), self.w2f.data_ptr(),
+                            self.xcur.data_ptr(), self.code1.data_ptr(), self.dh1.data_ptr(), self.a2p.data_ptr(),
+                            self.h1.data_ptr(), self.dlogits.data_ptr(), self._params.data_ptr(),
+                            self.grads.data_ptr(), self.mom.data_ptr(), *o, self.c2_ctr.data_ptr(), bi,
+                            self.n_batches, self.pending.data_ptr(), B, *self._opt_args(), s), "bwd_all")
+            return
         if self.merge_f4:  # + B3's all-row reductions (dW2, db1, db2)
             c(L.pto_conv2_bwd_fc(self.da2p.data_ptr(), self.code2.data_ptr(), self.a1p.data_ptr(),
                                  P["conv2.weight"].data_ptr(), G["conv2.weight"].data_ptr(),

@@ -149,3 +149,35 @@ def test_dw1_sgd_epilogue_matches_b3_path(monkeypatch):
         assert rel(a.p[name], b.p[name]) < 1e-5, name
     assert rel(a.mom, b.mom) < 1e-4
     assert abs(a.last_loss() - b.last_loss()) < 1e-5
+
+
+@pytest.mark.parametrize("B", [8, 64])
+def test_bwd_all_matches_separate_launches(monkeypatch, B):
+    """The all-in-one backward launch (k_bwd_all: conv2.weight updated by the
+    last-arriving wgrad chunk of each tile, dgrad from F12's weight
+    snapshot, every other update in its producer's epilogue) walks the same
+    trajectory as the conv2-backward + B1 launches.  B=8: two wgrad chunks
+    per tile, so the arrival counters and the atomic-exchange consume run;
+    B=64: ten.  fp32 atomics: not bitwise, loose trajectory check."""
+    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+
+    dev = torch.device("cuda", 0)
+    kw = dict(batch_size=B, dataset_size=B * 9, seed=6, unroll=4, weight_decay=1e-4)
+    monkeypatch.setenv("PTO_BWD_ALL", "1")
+    a = FusedMnistTrainer(dev, **kw)
+    monkeypatch.setenv("PTO_BWD_ALL", "0")
+    b = FusedMnistTrainer(dev, **kw)
+    assert a.bwd_all and not b.bwd_all
+    for t in (a, b):
+        t.run(7)
+    torch.cuda.synchronize()
+    for name in a.p:
+        assert rel(a.p[name], b.p[name]) < 2e-4, name
+    assert rel(a.mom, b.mom) < 2e-3
+    assert abs(a.last_loss() - b.last_loss()) < 1e-3
+    assert int(a.batch_idx.item()) == int(b.batch_idx.item()) == 7 % 9
+    assert int(a.c2_ctr.abs().sum().item()) == 0  # counters re-armed
+    g = a.grads
+    offs = __import__("pytorch_operator_1_amd.models.mnist", fromlist=["param_offsets"]).param_offsets()[0]
+    c2 = offs["conv2.weight"][0]
+    assert float(g[c2:c2 + 25000].abs().max()) == 0.0  # consumed gradients re-zeroed
