@@ -74,6 +74,8 @@ struct LazyConv1 {
   int bias_off;
   float* xout;          // nullptr, or [B][784]: the batch's images copied out for B1 (no cursor hop there)
   float* w2out;         // nullptr, or [50][500]: conv2.weight as read here (k_bwd_all's dgrad reads it)
+  const float* rep;     // extra gradient replicas (k_bwd_all): g + sum_r rep[r*rep_stride + i], r < nrep-1
+  int nrep, rep_stride;
 };
 struct Conv1Commit {
   float* p;             // flat conv1 range [0, n) of params / grads / momentum
@@ -84,7 +86,34 @@ struct Conv1Commit {
   SgdArgs a;
   const long long* bidx;
   long long* bidx_snap;
+  float* rep;           // extra gradient replicas, summed into the update and re-zeroed
+  int nrep, rep_stride;
 };
+
+// Conv1Commit's update of 4 elements at i: the gradient is the sum of the
+// primary slot and the replicas; all of them are zeroed.
+PTO_DEV void commit4(const Conv1Commit& cm, int i, float lr) {
+  if (cm.nrep <= 1) {
+    sgd_flat4(cm.p, cm.g, cm.m, i, lr, cm.a);
+    return;
+  }
+  float4 gs = *reinterpret_cast<const float4*>(cm.g + i);
+  for (int r = 0; r < cm.nrep - 1; ++r) {
+    float4* q = reinterpret_cast<float4*>(cm.rep + (size_t)r * cm.rep_stride + i);
+    const float4 v = *q;
+    gs.x += v.x; gs.y += v.y; gs.z += v.z; gs.w += v.w;
+    *q = float4{0.f, 0.f, 0.f, 0.f};
+  }
+  float4 pv = *reinterpret_cast<float4*>(cm.p + i);
+  float4 mv = *reinterpret_cast<float4*>(cm.m + i);
+  sgd_elem(pv.x, gs.x, mv.x, lr, cm.a.mom, cm.a.wd, cm.a.gscale, cm.a.nesterov);
+  sgd_elem(pv.y, gs.y, mv.y, lr, cm.a.mom, cm.a.wd, cm.a.gscale, cm.a.nesterov);
+  sgd_elem(pv.z, gs.z, mv.z, lr, cm.a.mom, cm.a.wd, cm.a.gscale, cm.a.nesterov);
+  sgd_elem(pv.w, gs.w, mv.w, lr, cm.a.mom, cm.a.wd, cm.a.gscale, cm.a.nesterov);
+  *reinterpret_cast<float4*>(cm.p + i) = pv;
+  *reinterpret_cast<float4*>(cm.m + i) = mv;
+  *reinterpret_cast<float4*>(cm.g + i) = float4{0.f, 0.f, 0.f, 0.f};
+}
 
 // ---------------------------------------------------------------- F1 ----
 // thread = (sample, 4-channel group, pooled pixel); 6x6 input patch in
@@ -261,7 +290,9 @@ __global__ __launch_bounds__(256) void k_conv12_fwd(const float* __restrict__ x,
       for (int q = 0; q < 3; ++q) {
         const int e = tid + 256 * q;
         const int fi = e < C1 * 25 ? e : lz.bias_off + (e - C1 * 25);
-        gq[q] = e < C1 * 26 ? lz.g[fi] : 0.f;
+        float gsum = e < C1 * 26 ? lz.g[fi] : 0.f;
+        for (int r = 0; r < lz.nrep - 1; ++r) gsum += e < C1 * 26 ? lz.rep[r * lz.rep_stride + fi] : 0.f;
+        gq[q] = gsum;
         mq[q] = e < C1 * 26 ? lz.m[fi] : 0.f;
       }
     }
@@ -408,7 +439,9 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
       for (int q = 0; q < QW1; ++q) {
         const int e = tid + NTH * q;
         const int fi = e < C1 * 25 ? e : lz.bias_off + (e - C1 * 25);
-        gq[q] = e < C1 * 26 ? lz.g[fi] : 0.f;
+        float gsum = e < C1 * 26 ? lz.g[fi] : 0.f;
+        for (int r = 0; r < lz.nrep - 1; ++r) gsum += e < C1 * 26 ? lz.rep[r * lz.rep_stride + fi] : 0.f;
+        gq[q] = gsum;
         mq[q] = e < C1 * 26 ? lz.m[fi] : 0.f;
       }
     }
@@ -826,7 +859,7 @@ __global__ __launch_bounds__(256) void k_fc2_ce(const float* __restrict__ h1, co
     if (t == 0 && cm.bidx_snap) *cm.bidx_snap = *cm.bidx;
     if (cm.pending && *cm.pending) {
       const float lr = *cm.a.lr;
-      for (int i = 4 * t; i < cm.n; i += 1024) sgd_flat4(cm.p, cm.g, cm.m, i, lr, cm.a);
+      for (int i = 4 * t; i < cm.n; i += 1024) commit4(cm, i, lr);
     }
     return;
   }
@@ -856,7 +889,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx(
   if (blockIdx.x == (unsigned)(mtiles * ntiles)) {  // conv1 commit (F1 of this step applied it on the fly)
     if (cm.pending && *cm.pending) {
       const float lr = *cm.a.lr;
-      for (int i = 4 * t; i < cm.n; i += 4 * FDX_WAVES * 64) sgd_flat4(cm.p, cm.g, cm.m, i, lr, cm.a);
+      for (int i = 4 * t; i < cm.n; i += 4 * FDX_WAVES * 64) commit4(cm, i, lr);
     }
     return;
   }
@@ -1007,6 +1040,43 @@ __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ dh1, c
 //  part C: db2[oc] = sum of unmasked pooled grads (one wave per channel).
 constexpr int B2_CHUNK = 7;  // samples per weight-grad block (7: LDS <= 40 KB -> 4 blocks/CU, all parts co-resident)
 constexpr int B2_ICG = 10;   // input-channel pairs per sample in the dgrad part
+
+// Recursive-halving wave reduction of 26 (padded to 32) per-lane sums: at
+// each step a lane keeps half of its live accumulators (chosen by its lane
+// bit) and receives its partner's copy of them: 16+8+4+2+1+1 = 32 shuffles
+// instead of 6 x 26.  The 26 wave totals are written to out[0..25].
+PTO_DEV void wave_halving26(const float acc[26], int lane, float* out) {
+  float h16[16], h8[8], h4[4], h2[2], h1;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const bool up = lane & 32;
+    const float a0 = acc[k], a1 = k + 16 < 26 ? acc[k + 16] : 0.f;
+    h16[k] = (up ? a1 : a0) + __shfl_xor(up ? a0 : a1, 32, 64);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const bool up = lane & 16;
+    h8[k] = (up ? h16[k + 8] : h16[k]) + __shfl_xor(up ? h16[k] : h16[k + 8], 16, 64);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool up = lane & 8;
+    h4[k] = (up ? h8[k + 4] : h8[k]) + __shfl_xor(up ? h8[k] : h8[k + 4], 8, 64);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const bool up = lane & 4;
+    h2[k] = (up ? h4[k + 2] : h4[k]) + __shfl_xor(up ? h4[k] : h4[k + 2], 4, 64);
+  }
+  {
+    const bool up = lane & 2;
+    h1 = (up ? h2[1] : h2[0]) + __shfl_xor(up ? h2[0] : h2[1], 2, 64);
+  }
+  h1 += __shfl_xor(h1, 1, 64);
+  const int idx = ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 + ((lane >> 2) & 1) * 2 +
+                  ((lane >> 1) & 1);
+  if (!(lane & 1) && idx < 26) out[idx] = h1;
+}
 
 // conv2 weight-gradient block (part A of the conv2 backward): one 16-column
 // K-tile x all 64 (padded) output channels x a chunk of B2_CHUNK samples,
@@ -1270,31 +1340,40 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
   // separate conv1-backward launch): thread = (channel, tap, pixel
   // quarter); pooled grad expanded through the conv1 argmax code.
   __syncthreads();
-  float* red = ws;  // free after the GEMM
-  {
-    float acc = 0.f;
-    if (tid < 208) {
-      const int pair = tid >> 2, qtr = tid & 3;
-      const int icl = pair / 26, k = pair - icl * 26;
-      const int kh = k / 5, kw = k - kh * 5;
-      for (int pix = qtr * 36; pix < qtr * 36 + 36; ++pix) {
+  float* part = ws;  // [4][26] wave totals (free after the GEMM)
+  if (!(ktail & 256)) {
+    // pixel-major: wave w owns channel w>>1 and 72 of its 144 pooled pixels
+    // (lanes 0..63, then lanes 0..7 again); a lane expands its pixel's
+    // (grad, code) once and accumulates the 25 taps + bias in registers;
+    // the 26 sums are reduced across the wave by recursive halving
+    const int icl = wv >> 1, p0 = (wv & 1) * 72;
+    float acc[26];
+#pragma unroll
+    for (int k = 0; k < 26; ++k) acc[k] = 0.f;
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int pl = lane + 64 * it;
+      if (pl < 72) {
+        const int pix = p0 + pl;
         const int cd = c1s[icl * 144 + pix];
-        if (cd >= 4) continue;
-        const float v = dsum[icl * 144 + pix];
-        if (k == 25) {
-          acc += v;
-        } else {
-          const int oh = 2 * (pix / 12) + (cd >> 1), ow = 2 * (pix % 12) + (cd & 1);
-          acc = fmaf(v, xs[(oh + kh) * 28 + ow + kw], acc);
-        }
+        const float v = cd < 4 ? dsum[icl * 144 + pix] : 0.f;
+        const int oh = 2 * (pix / 12) + ((cd >> 1) & 1), ow = 2 * (pix % 12) + (cd & 1);
+        const float* xp = xs + oh * 28 + ow;
+#pragma unroll
+        for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw) acc[kh * 5 + kw] = fmaf(v, xp[kh * 28 + kw], acc[kh * 5 + kw]);
+        acc[25] += v;
       }
     }
-    red[tid] = acc;
+    wave_halving26(acc, lane, part + wv * 26);
+  } else if (tid < 104) {
+    part[tid] = 0.f;
   }
   __syncthreads();
-  if (tid < 52) {
-    const float v = red[4 * tid] + red[4 * tid + 1] + red[4 * tid + 2] + red[4 * tid + 3];
+  if (tid < 52 && !(ktail & 512)) {
     const int icl = tid / 26, k = tid - icl * 26, oc1 = icg * 2 + icl;
+    const float v = part[(2 * icl) * 26 + k] + part[(2 * icl + 1) * 26 + k];
     if (k < 25) atomicAdd(gw1 + oc1 * 25 + k, v);
     else atomicAdd(gb1 + oc1, v);
   }
@@ -1464,41 +1543,7 @@ PTO_DEV void conv1_bwd_block(int vb, const float* __restrict__ g1, const uint8_t
   }
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (halving) {
-    // recursive-halving wave reduction of the 26 (padded to 32) sums: at
-    // each step a lane keeps half of its live accumulators (chosen by its
-    // lane bit) and receives its partner's copy of them: 16+8+4+2+1+1 = 32
-    // shuffles instead of 6 x 26.  Lane l ends with accumulator
-    // idx(l) = bits 5..1 of l, summed over all 64 lanes.
-    float h16[16], h8[8], h4[4], h2[2], h1;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const bool up = lane & 32;
-      const float a0 = acc[k], a1 = k + 16 < 26 ? acc[k + 16] : 0.f;
-      h16[k] = (up ? a1 : a0) + __shfl_xor(up ? a0 : a1, 32, 64);
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const bool up = lane & 16;
-      h8[k] = (up ? h16[k + 8] : h16[k]) + __shfl_xor(up ? h16[k] : h16[k + 8], 16, 64);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool up = lane & 8;
-      h4[k] = (up ? h8[k + 4] : h8[k]) + __shfl_xor(up ? h8[k] : h8[k + 4], 8, 64);
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const bool up = lane & 4;
-      h2[k] = (up ? h4[k + 2] : h4[k]) + __shfl_xor(up ? h4[k] : h4[k + 2], 4, 64);
-    }
-    {
-      const bool up = lane & 2;
-      h1 = (up ? h2[1] : h2[0]) + __shfl_xor(up ? h2[0] : h2[1], 2, 64);
-    }
-    h1 += __shfl_xor(h1, 1, 64);
-    const int idx = ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 + ((lane >> 2) & 1) * 2 +
-                    ((lane >> 1) & 1);
-    if (!(lane & 1) && idx < 26) part[wv][idx] = h1;
+    wave_halving26(acc, lane, part[wv]);
   } else {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1)
@@ -1606,6 +1651,14 @@ struct BwdAllArgs {
   long long nbatches;
   int* pending;
   int B, nA, nB, nC, nD, nF, ktail;
+  int skip;  // timing probes only (PTO_BWD_ALL_SKIP): 1 = no conv1 wgrad, 4 = no conv2 tile SGD
+  // conv1 grads are accumulated into nrep replicas (sample b -> b % nrep;
+  // replica 0 = gw1/gb1, replica r >= 1 at c1rep + (r-1)*rep_stride, same
+  // layout as the flat conv1 range: weights at 0, bias at bias_off), so
+  // each address sees B/nrep atomic adds instead of B (same-address adds
+  // serialise at the memory side); readers sum the replicas
+  float* c1rep;
+  int nrep, rep_stride, bias_off;
 };
 
 struct EpiSgd {
@@ -1628,6 +1681,36 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
     *A.bidx = (*A.bidx + 1) % A.nbatches;
     *A.pending = 1;
   }
+  // block order: the short independent ranges first (they must not queue
+  // behind the LDS-heavy conv2 blocks for a CU slot), then conv2 wgrad,
+  // conv2 dgrad, dW1
+  if (bid < A.nC) {
+    const int oc = bid * 4 + wv;
+    if (oc >= C2) return;
+    const float g = c2_bias_sum(oc, A.g2, A.code2, A.B);
+    if (lane == 0) {
+      float pv = A.p2b[oc], mv = A.m2b[oc];
+      sgd_elem(pv, g, mv, *A.a.lr, A.a.mom, A.a.wd, A.a.gscale, A.a.nesterov);
+      A.p2b[oc] = pv;
+      A.m2b[oc] = mv;
+    }
+    return;
+  }
+  bid -= A.nC;
+  if (bid < A.nF) {
+    const float lr = *A.a.lr;
+    constexpr int NWF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4;
+    if (bid < NWF) {
+      block_gemm_4tiles<LAY_KROW, LAY_KROW>(A.dl, NCLS, A.h1, F1OUT, NCLS, F1OUT, A.B, bid,
+                                            EpiSgd{A.pfw, A.mfw, F1OUT, lr, &A.a});
+      return;
+    }
+    bid -= NWF;
+    if (bid < 8) block_colsum64_epi(A.dh1, F1OUT, A.B, F1OUT, bid * 64, smem, EpiSgd{A.p1b, A.m1b, 0, lr, &A.a});
+    else block_colsum64_epi(A.dl, NCLS, A.B, NCLS, 0, smem, EpiSgd{A.pfb, A.mfb, 0, lr, &A.a});
+    return;
+  }
+  bid -= A.nF;
   if (bid < A.nA) {
     c2_wgrad_block(bid, smem, A.g2, A.code2, A.a1p, A.g2w, A.B);
     // arrival: every lane's atomics have been performed at the memory side
@@ -1640,7 +1723,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
       if (s_last) __hip_atomic_store(A.ctr + nt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    if (!s_last) return;
+    if (!s_last || (A.skip & 4)) return;
     const float lr = *A.a.lr;
     int idx[4];
     float gv[4], pv[4], mv[4];
@@ -1665,39 +1748,18 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   }
   bid -= A.nA;
   if (bid < A.nB) {
-    c2_dgrad_block(bid, smem, A.g2, A.code2, A.w2f, nullptr, A.B, A.x, nullptr, A.code1, A.gw1, A.gb1, A.ktail);
+    const int r = (bid / B2_ICG) % A.nrep;
+    float* gw1 = r == 0 ? A.gw1 : A.c1rep + (r - 1) * A.rep_stride;
+    float* gb1 = r == 0 ? A.gb1 : A.c1rep + (r - 1) * A.rep_stride + A.bias_off;
+    c2_dgrad_block(bid, smem, A.g2, A.code2, A.w2f, nullptr, A.B, A.x, nullptr, A.code1,
+                   (A.skip & 1) ? nullptr : gw1, gb1, A.ktail);
     return;
   }
   bid -= A.nB;
-  if (bid < A.nC) {
-    const int oc = bid * 4 + wv;
-    if (oc >= C2) return;
-    const float g = c2_bias_sum(oc, A.g2, A.code2, A.B);
-    if (lane == 0) {
-      float pv = A.p2b[oc], mv = A.m2b[oc];
-      sgd_elem(pv, g, mv, *A.a.lr, A.a.mom, A.a.wd, A.a.gscale, A.a.nesterov);
-      A.p2b[oc] = pv;
-      A.m2b[oc] = mv;
-    }
-    return;
-  }
-  bid -= A.nC;
   if (bid < A.nD) {
     dw1_sgd_tile(bid * 4 + wv, A.dh1, A.a2p, A.p1w, A.m1w, A.B, A.a);
     return;
   }
-  bid -= A.nD;
-  if (bid >= A.nF) return;
-  const float lr = *A.a.lr;
-  constexpr int NWF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4;
-  if (bid < NWF) {
-    block_gemm_4tiles<LAY_KROW, LAY_KROW>(A.dl, NCLS, A.h1, F1OUT, NCLS, F1OUT, A.B, bid,
-                                          EpiSgd{A.pfw, A.mfw, F1OUT, lr, &A.a});
-    return;
-  }
-  bid -= NWF;
-  if (bid < 8) block_colsum64_epi(A.dh1, F1OUT, A.B, F1OUT, bid * 64, smem, EpiSgd{A.p1b, A.m1b, 0, lr, &A.a});
-  else block_colsum64_epi(A.dl, NCLS, A.B, NCLS, 0, smem, EpiSgd{A.pfb, A.mfb, 0, lr, &A.a});
 }
 
 // Host-side flush of an owed conv1 update (before the parameters are read
@@ -1705,7 +1767,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
 __global__ __launch_bounds__(256) void k_conv1_commit(Conv1Commit cm, int* __restrict__ pending) {
   if (!*cm.pending) return;
   const float lr = *cm.a.lr;
-  for (int i = 4 * threadIdx.x; i < cm.n; i += 1024) sgd_flat4(cm.p, cm.g, cm.m, i, lr, cm.a);
+  for (int i = 4 * threadIdx.x; i < cm.n; i += 1024) commit4(cm, i, lr);
   __syncthreads();
   if (threadIdx.x == 0) *pending = 0;
 }
@@ -1835,8 +1897,10 @@ PTO_API int pto_conv12_fwd_lazy_x(const float* x, const float* w1, const float* 
                                   const float* b2, float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B,
                                   const long long* bidx, const float* g1f, const float* m1f, int bias_off,
                                   const int* pending, const float* lr, float mom, float wd, float gscale, int nesterov,
-                                  float* xout, float* w2out, hipStream_t s) {
-  LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off, xout, w2out};
+                                  float* xout, float* w2out, const float* rep, int nrep, int rep_stride,
+                                  hipStream_t s) {
+  LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off, xout, w2out, rep, nrep,
+               rep_stride};
   static const int bal = [] {
     const char* e = getenv("PTO_CONV1_BALANCED");  // 0 = 15 lockstep tasks (A/B)
     return e ? atoi(e) : 1;
@@ -1915,9 +1979,12 @@ PTO_API int pto_fc2_ce_commit(const float* h1, const float* w, const float* b, c
 }
 
 PTO_API int pto_conv1_commit(float* p1, float* g1, float* m1, int n1, int* pending, const float* lr, float mom,
-                             float wd, float gscale, int nesterov, hipStream_t s) {
-  if (n1 % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1)) & 15)) return -1;
-  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), nullptr, nullptr};
+                             float wd, float gscale, int nesterov, float* rep, int nrep, int rep_stride,
+                             hipStream_t s) {
+  if (n1 % 4 || rep_stride % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1) | ((uintptr_t)rep)) & 15))
+    return -1;
+  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), nullptr, nullptr, rep, nrep,
+                 rep_stride};
   hipLaunchKernelGGL(k_conv1_commit, dim3(1), dim3(256), 0, s, cm, pending);
   LAUNCH_CHECK();
 }
@@ -2004,9 +2071,12 @@ PTO_API int pto_conv2_bwd_fc(const float* g2, const uint8_t* code2, const float*
 PTO_API int pto_fc2_ce_dx(const float* h1, const float* w2, const float* b2, const int64_t* labels, const float* w1,
                           float* loss_rows, float* dlogits, float* dh1, float* da2p, int B, float inv_b,
                           const long long* bidx, float* p1, float* g1, float* m1, int n1, const int* pending,
-                          const float* lr, float mom, float wd, float gscale, int nesterov, hipStream_t s) {
-  if (n1 % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1)) & 15)) return -1;
-  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), nullptr, nullptr};
+                          const float* lr, float mom, float wd, float gscale, int nesterov, float* rep, int nrep,
+                          int rep_stride, hipStream_t s) {
+  if (n1 % 4 || rep_stride % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1) | ((uintptr_t)rep)) & 15))
+    return -1;
+  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), nullptr, nullptr, rep, nrep,
+                 rep_stride};
   static const int prefetch = [] {
     const char* e = getenv("PTO_FDX_PREFETCH");  // 0 = operand loads after the barrier (A/B)
     return e ? atoi(e) : 1;
@@ -2147,8 +2217,9 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
                         float* p, float* g, float* m, long long off_fc2w, long long off_fc2b, long long off_fc1w,
                         long long off_fc1b, long long off_c2w, long long off_c2b, long long off_c1w,
                         long long off_c1b, int* ctr, long long* bidx, long long nbatches, int* pending, int B,
-                        const float* lr, float mom, float wd, float gscale, int nesterov, hipStream_t s) {
-  if (!bidx || !pending || !ctr || nbatches < 1 || B < 1) return -1;
+                        const float* lr, float mom, float wd, float gscale, int nesterov, float* c1rep, int nrep,
+                        int rep_stride, hipStream_t s) {
+  if (!bidx || !pending || !ctr || nbatches < 1 || B < 1 || nrep < 1 || (nrep > 1 && !c1rep)) return -1;
   BwdAllArgs A;
   A.g2 = g2; A.code2 = code2; A.a1p = a1p; A.w2f = w2f; A.x = x; A.code1 = code1;
   A.gw1 = g + off_c1w; A.gb1 = g + off_c1b;
@@ -2161,6 +2232,10 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   A.pfb = p + off_fc2b; A.mfb = m + off_fc2b;
   A.a = sgd_args(lr, mom, wd, gscale, nesterov);
   A.a.variant = 1;  // dW1 tiles: 4 k-groups per memory round
+  A.c1rep = c1rep;
+  A.nrep = nrep;
+  A.rep_stride = rep_stride;
+  A.bias_off = (int)(off_c1b - off_c1w);
   A.bidx = bidx; A.nbatches = nbatches; A.pending = pending; A.B = B;
   A.nA = ((B + B2_CHUNK - 1) / B2_CHUNK) * 32;
   A.nB = B * B2_ICG;
@@ -2168,6 +2243,16 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   A.nD = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
   A.nF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9;
   A.ktail = 3;
+  static const int skip = [] {
+    const char* e = getenv("PTO_BWD_ALL_SKIP");  // timing probes: parts left out (wrong numerics)
+    return e ? atoi(e) : 0;
+  }();
+  A.skip = skip;
+  A.ktail |= ((skip >> 6) & 3) << 8;  // 64: no conv1 loop, 128: no conv1 atomics
+  if (skip & 2) A.nD = 0;
+  if (skip & 8) A.nB = 0;
+  if (skip & 16) A.nA = 0;
+  if (skip & 32) A.nF = 0, A.nC = 0;
   const size_t ldsA = B2_CHUNK * (288 + F1IN + F1IN / 4) * sizeof(float);
   const size_t ldsB = (52 * 68 + 64 * 65 + F1IN + F1IN / 4 + 784 + 72) * sizeof(float);
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;

@@ -152,6 +152,12 @@ class FusedMnistTrainer:
         self.bwd_all = self.merge_f4 and os.environ.get("PTO_BWD_ALL", "1") == "1"
         self.w2f = torch.empty(50 * 500, device=device) if self.bwd_all else None
         self.c2_ctr = torch.zeros(32, device=device, dtype=torch.int32) if self.bwd_all else None
+        # conv1 gradient replicas of k_bwd_all (sample b adds into replica
+        # b % R: B/R same-address atomics instead of B); summed by the lazy
+        # apply and the commit
+        self.c1_nrep = max(1, int(os.environ.get("PTO_C1_REPLICAS", "8"))) if self.bwd_all else 1
+        self.c1_stride = self.numel - offs["conv1.weight"][0]
+        self.c1rep = torch.zeros(max(1, self.c1_nrep - 1) * self.c1_stride, **f32)
         # multi-GPU schedule: overlap the fc bucket's all-reduce with the conv
         # backward on a side stream (PTO_COMM_OVERLAP=1), or all-reduce the
         # whole flat buffer once after the backward on the compute stream
@@ -248,7 +254,8 @@ class FusedMnistTrainer:
                    self.grads[self._c1:].data_ptr(), self.mom[self._c1:].data_ptr(), self._c1_bias,
                    self.pending.data_ptr(), *o)
             if self.xcur is not None:
-                c(L.pto_conv12_fwd_lazy_x(*f12, self.xcur.data_ptr(), _lib.ptr(self.w2f), s), "conv12_fwd_lazy_x")
+                c(L.pto_conv12_fwd_lazy_x(*f12, self.xcur.data_ptr(), _lib.ptr(self.w2f), self.c1rep.data_ptr(),
+                                          self.c1_nrep, self.c1_stride, s), "conv12_fwd_lazy_x")
             else:
                 c(L.pto_conv12_fwd_lazy(*f12, self.conv12_version, s), "conv12_fwd_lazy")
             c(L.pto_linear_fwd(self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
@@ -259,7 +266,7 @@ class FusedMnistTrainer:
                                   self.dlogits.data_ptr(), self.dh1.data_ptr(), self.da2p.data_ptr(), B, 1.0 / B, bi,
                                   self._params[self._c1:].data_ptr(), self.grads[self._c1:].data_ptr(),
                                   self.mom[self._c1:].data_ptr(), self.numel - self._c1, self.pending.data_ptr(),
-                                  *o, s), "fc2_ce_dx")
+                                  *o, self.c1rep.data_ptr(), self.c1_nrep, self.c1_stride, s), "fc2_ce_dx")
                 return
             c(L.pto_fc2_ce_commit(self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
                                   self.target.data_ptr(), self.loss_rows.data_ptr(), self.dlogits.data_ptr(),
@@ -326,7 +333,8 @@ class FusedMnistTrainer:
                             self.xcur.data_ptr(), self.code1.data_ptr(), self.dh1.data_ptr(), self.a2p.data_ptr(),
                             self.h1.data_ptr(), self.dlogits.data_ptr(), self._params.data_ptr(),
                             self.grads.data_ptr(), self.mom.data_ptr(), *o, self.c2_ctr.data_ptr(), bi,
-                            self.n_batches, self.pending.data_ptr(), B, *self._opt_args(), s), "bwd_all")
+                            self.n_batches, self.pending.data_ptr(), B, *self._opt_args(), self.c1rep.data_ptr(),
+                            self.c1_nrep, self.c1_stride, s), "bwd_all")
             return
         if self.merge_f4:  # + B3's all-row reductions (dW2, db1, db2)
             c(L.pto_conv2_bwd_fc(self.da2p.data_ptr(), self.code2.data_ptr(), self.a1p.data_ptr(),
@@ -402,7 +410,8 @@ class FusedMnistTrainer:
     def _commit_launch(self):
         _lib.check(self.L.pto_conv1_commit(self._params[self._c1:].data_ptr(), self.grads[self._c1:].data_ptr(),
                                            self.mom[self._c1:].data_ptr(), self.numel - self._c1,
-                                           self.pending.data_ptr(), *self._opt_args(), self._s()), "conv1_commit")
+                                           self.pending.data_ptr(), *self._opt_args(), self.c1rep.data_ptr(),
+                                           self.c1_nrep, self.c1_stride, self._s()), "conv1_commit")
 
     @property
     def params(self):
@@ -511,7 +520,7 @@ class FusedMnistTrainer:
         # Warm up on a side stream (lazy library/allocator init must not
         # happen under capture), then roll the state back so capture does
         # not change the training trajectory, then capture.
-        state = (self._params, self.mom, self.grads, self.batch_idx, self.pending, self.batch_snap)
+        state = (self._params, self.mom, self.grads, self.batch_idx, self.pending, self.batch_snap, self.c1rep)
         snap = [t.clone() for t in state]
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -592,7 +601,7 @@ class FusedMnistTrainer:
 
         from ..utils import dist as pdist
 
-        state = (self._params, self.mom, self.grads, self.batch_idx, self.pending, self.batch_snap)
+        state = (self._params, self.mom, self.grads, self.batch_idx, self.pending, self.batch_snap, self.c1rep)
         snap = [t.clone() for t in state]
         res = {}
         for ov in (False, True):

@@ -15,17 +15,19 @@ def rel(a, b):
     return ((a - b).abs().max() / b.abs().max()).item()
 
 
-@pytest.mark.parametrize("B,tol", [(4, 0.0), (64, 2e-3)])
-def test_unrolled_graph_matches_single_steps(B, tol):
-    """U-step graph replays walk the same trajectory as single steps.  At
-    B=4 every fp32-atomic gradient address receives exactly one add (conv2
-    wgrad chunks are 7 samples, conv1 chunks 4), so the step is bitwise
-    deterministic and the two must agree exactly.  At B=64 the atomics'
-    arrival order varies run to run and a ReLU at the edge can flip, which
-    amplifies last-bit differences chaotically over 21 steps; there the
-    check is a loose trajectory check."""
+@pytest.mark.parametrize("B,tol,bwd_all", [(4, 0.0, "0"), (1, 0.0, "1"), (64, 2e-3, "1")])
+def test_unrolled_graph_matches_single_steps(monkeypatch, B, tol, bwd_all):
+    """U-step graph replays walk the same trajectory as single steps.  When
+    every fp32-atomic gradient address receives exactly one add the step is
+    bitwise deterministic and the two must agree exactly: B=4 with the
+    separate conv2-backward/B1 launches (conv2 wgrad chunks are 7 samples,
+    conv1 chunks 4), B=1 with the all-in-one backward (its conv1 wgrad adds
+    once per sample).  At B=64 the atomics' arrival order varies run to run
+    and a ReLU at the edge can flip, which amplifies last-bit differences
+    chaotically over 21 steps; there the check is a loose trajectory check."""
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
 
+    monkeypatch.setenv("PTO_BWD_ALL", bwd_all)
     dev = torch.device("cuda", 0)
     a = FusedMnistTrainer(dev, batch_size=B, dataset_size=B * 12, seed=2, unroll=8)
     b = FusedMnistTrainer(dev, batch_size=B, dataset_size=B * 12, seed=2, unroll=1)
