@@ -1040,6 +1040,9 @@ __global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ dh1, c
 //  part C: db2[oc] = sum of unmasked pooled grads (one wave per channel).
 constexpr int B2_CHUNK = 7;  // samples per weight-grad block (7: LDS <= 40 KB -> 4 blocks/CU, all parts co-resident)
 constexpr int B2_ICG = 10;   // input-channel pairs per sample in the dgrad part
+// LDS of a dgrad block: R1 = max(W2 slice [52][68] + stage 1000, T [64][65])
+// + R2 = dY2 [64][52] (c2_dgrad_block)
+constexpr int B2_LDS_FLOATS = ((52 * 68 + 1000) > 64 * 65 ? (52 * 68 + 1000) : 64 * 65) + 64 * 52;
 
 // Recursive-halving wave reduction of 26 (padded to 32) per-lane sums: at
 // each step a lane keeps half of its live accumulators (chosen by its lane
@@ -1081,6 +1084,7 @@ PTO_DEV void wave_halving26(const float acc[26], int lane, float* out) {
 // conv2 weight-gradient block (part A of the conv2 backward): one 16-column
 // K-tile x all 64 (padded) output channels x a chunk of B2_CHUNK samples,
 // fp32 atomics into gw2.
+template <int CH>
 PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, const uint8_t* __restrict__ code2,
                             const float* __restrict__ a1p, float* __restrict__ gw2, int B) {
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1098,16 +1102,17 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
   const int ic = kvalid ? kk / 25 : ic0, r25 = kvalid ? kk - ic * 25 : 0;
   const int kh = r25 / 5, kw = r25 - kh * 5;
   const bool ocvalid = oc < C2;
-  const int b0 = chunk * B2_CHUNK, nb = min(B, b0 + B2_CHUNK) - b0;
+  const int b0 = chunk * CH, nb = min(B, b0 + CH) - b0;
   float* as = smem;                                   // [8][2][144]
-  float* gs = smem + B2_CHUNK * 288;                  // [8][800]
-  uint8_t* cs = reinterpret_cast<uint8_t*>(gs + B2_CHUNK * F1IN);  // [8][800] bytes
+  float* gs = smem + CH * 288;                  // [8][800]
+  uint8_t* cs = reinterpret_cast<uint8_t*>(gs + CH * F1IN);  // [8][800] bytes
   const int tid = threadIdx.x;
   {
-    float4 va[3], vg[7];
-    uint32_t vc[7];
+    constexpr int NVA = (CH * 72 + 255) / 256, NVG = (CH * (F1IN / 4) + 255) / 256;
+    float4 va[NVA], vg[NVG];
+    uint32_t vc[NVG];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
+    for (int q = 0; q < NVA; ++q) {
       const int e = tid + 256 * q;  // float4 index over [s][ch][36]
       const int smp = e / 72, rr = e - smp * 72, ch = rr / 36, off = (rr - ch * 36) * 4;
       const bool ok = e < nb * 72 && ic0 + ch < C1;
@@ -1115,22 +1120,26 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
                  : float4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int q = 0; q < 7; ++q) {
+    for (int q = 0; q < NVG; ++q) {
       const int e = tid + 256 * q;
       const bool ok = e < nb * (F1IN / 4);
       vg[q] = ok ? reinterpret_cast<const float4*>(g2 + b0 * F1IN)[e] : float4{0.f, 0.f, 0.f, 0.f};
       vc[q] = ok ? reinterpret_cast<const uint32_t*>(code2 + b0 * F1IN)[e] : 0x04040404u;
     }
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
+    for (int q = 0; q < NVA; ++q) {
       const int e = tid + 256 * q;
-      if (e < B2_CHUNK * 72) reinterpret_cast<float4*>(as)[e] = va[q];
+      if (e < CH * 72) reinterpret_cast<float4*>(as)[e] = va[q];
     }
 #pragma unroll
-    for (int q = 0; q < 7; ++q) {
+    for (int q = 0; q < NVG; ++q) {
       const int e = tid + 256 * q;
-      if (e < B2_CHUNK * (F1IN / 4)) {
-        reinterpret_cast<float4*>(gs)[e] = vg[q];
+      if (e < CH * (F1IN / 4)) {
+        // XOR-swizzled float4 slots: row oc's quad G lives at G ^ ((oc >> 1) & 3),
+        // so the 16 lanes of a K-group that read the same (pp) of 16
+        // consecutive channels hit 8 bank quads instead of 2 (8-way -> 2-way)
+        const int smp = e / (F1IN / 4), r = e - smp * (F1IN / 4), oc_ = r >> 2;
+        reinterpret_cast<float4*>(gs)[smp * (F1IN / 4) + (oc_ << 2) + ((r & 3) ^ ((oc_ >> 1) & 3))] = vg[q];
         reinterpret_cast<uint32_t*>(cs)[e] = vc[q];
       }
     }
@@ -1145,7 +1154,7 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
 #pragma unroll
     for (int G = 0; G < 4; ++G) {
       const int pp = 4 * G + g;
-      const float gv = ocvalid ? gs[smp * F1IN + goff + pp] : 0.f;
+      const float gv = ocvalid ? gs[smp * F1IN + goff + ((G ^ ((oc >> 1) & 3)) << 2) + g] : 0.f;
       const int cd = ocvalid ? (int)cs[smp * F1IN + goff + pp] : 4;
       const float* ap = ap0 + 2 * (pp >> 2) * 12 + 2 * (pp & 3);
       const float bv0 = kvalid ? ap[0] : 0.f, bv1 = kvalid ? ap[1] : 0.f;
@@ -1181,21 +1190,30 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
   const int b = bid / B2_ICG, icg = bid - b * B2_ICG;
   constexpr int WLD = 68;   // 64 + 4: the 4 k-rows of a wave hit disjoint banks
   constexpr int TLD = 65;
-  float* ws = smem;                      // [52][68]
-  float* dys = ws + 52 * WLD;            // [64 pos][52 oc]   } union: ts is written
-  float* ts = dys;                       // [64 pos][65]      } after the GEMM's last dys read
-  float* gstage = dys + 64 * TLD;        // [800] grads + [800 B] codes
-  float* xs = gstage + F1IN + F1IN / 4;  // [784] input image (conv1 wgrad fusion only)
-  uint8_t* c1s = reinterpret_cast<uint8_t*>(xs + 784);  // [2][144] conv1 codes
+  // Two LDS regions, each reused once the phase that reads it is over
+  // (31.5 KB in all: 5 blocks per CU):
+  //   R1: W2 slice [52][68] + grads/codes stage  -> after the GEMM: T [64][65]
+  //       -> after col2im: the conv1 wave partials
+  //   R2: expanded dY2 [64][52]                  -> after the GEMM: input
+  //       image [784] + conv1 codes [2][144] (held in registers until then)
+  //       + d(a1p) of the two channels [288]
+  constexpr int R1 = (52 * WLD + F1IN + F1IN / 4) > 64 * TLD ? (52 * WLD + F1IN + F1IN / 4) : 64 * TLD;
+  float* ws = smem;                      // R1
+  float* gstage = ws + 52 * WLD;         // R1 tail: [800] grads + [800 B] codes
+  float* ts = smem;                      // R1 after the GEMM
+  float* dys = smem + R1;                // R2
+  float* xs = dys;                       // R2 after the GEMM
+  uint8_t* c1s = reinterpret_cast<uint8_t*>(xs + 784);
+  float* dsum = xs + 784 + 72;
   const bool fuse1 = gw1 != nullptr;
   const int r = lane & 15, gg = lane >> 4;
   const int tid = threadIdx.x;
-  if (fuse1) {
+  float4 xv = float4{0.f, 0.f, 0.f, 0.f};
+  uint32_t c1v = 0;
+  if (fuse1) {  // issued with the other loads, stored to LDS after the GEMM
     const float* xb = batch_ptr(x, bidx, B * 784) + b * 784;
-    if (tid < 196) reinterpret_cast<float4*>(xs)[tid] = reinterpret_cast<const float4*>(xb)[tid];
-    if (tid < 72)
-      reinterpret_cast<uint32_t*>(c1s)[tid] =
-          reinterpret_cast<const uint32_t*>(code1 + (b * C1 + icg * 2) * 144)[tid];
+    if (tid < 196) xv = reinterpret_cast<const float4*>(xb)[tid];
+    if (tid < 72) c1v = reinterpret_cast<const uint32_t*>(code1 + (b * C1 + icg * 2) * 144)[tid];
   }
   {
     constexpr int NW = (C2 * 50 + 255) / 256;  // 10
@@ -1268,15 +1286,18 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[q] = mfma16x16x4(av[j], bv[q][j], acc[q]);
     }
-    __syncthreads();  // ts aliases dys: every wave's dys reads are done
+    __syncthreads();  // ts aliases ws, xs aliases dys: every wave's GEMM reads are done
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
         ts[(wv * 16 + gg * 4 + rr) * TLD + q * 16 + r] = acc[q][rr];
+    if (fuse1) {
+      if (tid < 196) reinterpret_cast<float4*>(xs)[tid] = xv;
+      if (tid < 72) reinterpret_cast<uint32_t*>(c1s)[tid] = c1v;
+    }
   }
   __syncthreads();
-  float* dsum = gstage;  // free after the dY2 expansion
   if (ktail & 2) {
     // 288 outputs on 256 threads: one full output per thread, then the last
     // 32 outputs split 8 ways over all threads (<= 4 taps each, 3-step
@@ -1415,7 +1436,7 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
   int bid = blockIdx.x;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (bid < nA) {
-    c2_wgrad_block(bid, smem, g2, code2, a1p, gw2, B);
+    c2_wgrad_block<B2_CHUNK>(bid, smem, g2, code2, a1p, gw2, B);
     return;
   }
   bid -= nA;
@@ -1672,6 +1693,7 @@ struct EpiSgd {
   }
 };
 
+template <int CH>
 __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int s_last;
@@ -1712,7 +1734,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   }
   bid -= A.nF;
   if (bid < A.nA) {
-    c2_wgrad_block(bid, smem, A.g2, A.code2, A.a1p, A.g2w, A.B);
+    c2_wgrad_block<CH>(bid, smem, A.g2, A.code2, A.a1p, A.g2w, A.B);
     // arrival: every lane's atomics have been performed at the memory side
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -2035,7 +2057,7 @@ PTO_API int pto_conv2_bwd(const float* g2, const uint8_t* code2, const float* a1
   const int nB = (parts & 2) ? B * B2_ICG : 0;
   const int nC = (parts & 4) ? (C2 + 3) / 4 : 0;
   const size_t ldsA = (parts & 1) ? B2_CHUNK * (288 + F1IN + F1IN / 4) * sizeof(float) : 0;
-  const size_t ldsB = (parts & 2) ? (52 * 68 + 64 * 65 + F1IN + F1IN / 4 + (gw1 ? 784 + 72 : 0)) * sizeof(float) : 0;
+  const size_t ldsB = (parts & 2) ? B2_LDS_FLOATS * sizeof(float) : 0;
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;
   if (nA + nB + nC == 0) return 0;
   hipLaunchKernelGGL(k_conv2_bwd, dim3(nA + nB + nC), dim3(256), lds, s, g2, code2, a1p, w2, gw2, gb2, da1p, B, nA,
@@ -2054,7 +2076,7 @@ PTO_API int pto_conv2_bwd_fc(const float* g2, const uint8_t* code2, const float*
   const int nC = (C2 + 3) / 4;
   const int nF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9;
   const size_t ldsA = B2_CHUNK * (288 + F1IN + F1IN / 4) * sizeof(float);
-  const size_t ldsB = (52 * 68 + 64 * 65 + F1IN + F1IN / 4) * sizeof(float);
+  const size_t ldsB = B2_LDS_FLOATS * sizeof(float);
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;
   static const int ktail = [] {
     const char* e = getenv("PTO_C2_KTAIL");  // 0 = padded 16-deep K tail (A/B)
@@ -2237,7 +2259,14 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   A.rep_stride = rep_stride;
   A.bias_off = (int)(off_c1b - off_c1w);
   A.bidx = bidx; A.nbatches = nbatches; A.pending = pending; A.B = B;
-  A.nA = ((B + B2_CHUNK - 1) / B2_CHUNK) * 32;
+  static const int chunk = [] {
+    // samples per conv2-wgrad block, 4..8 (A/B, profiles/bwd_all_r2.md):
+    // 6 -> 30.2 KB of LDS, 5 blocks per CU with the 31.5 KB dgrad blocks
+    const char* e = getenv("PTO_BWD_CHUNK");
+    const int v = e ? atoi(e) : 6;
+    return v < 4 ? 4 : (v > 8 ? 8 : v);
+  }();
+  A.nA = ((B + chunk - 1) / chunk) * 32;
   A.nB = B * B2_ICG;
   A.nC = (C2 + 3) / 4;
   A.nD = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
@@ -2253,9 +2282,16 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   if (skip & 8) A.nB = 0;
   if (skip & 16) A.nA = 0;
   if (skip & 32) A.nF = 0, A.nC = 0;
-  const size_t ldsA = B2_CHUNK * (288 + F1IN + F1IN / 4) * sizeof(float);
-  const size_t ldsB = (52 * 68 + 64 * 65 + F1IN + F1IN / 4 + 784 + 72) * sizeof(float);
+  const size_t ldsA = chunk * (288 + F1IN + F1IN / 4) * sizeof(float);
+  const size_t ldsB = B2_LDS_FLOATS * sizeof(float);
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;
-  hipLaunchKernelGGL(k_bwd_all, dim3(A.nA + A.nB + A.nC + A.nD + A.nF), dim3(256), lds, s, A);
+  const dim3 grid(A.nA + A.nB + A.nC + A.nD + A.nF);
+  switch (chunk) {
+    case 4: hipLaunchKernelGGL(k_bwd_all<4>, grid, dim3(256), lds, s, A); break;
+    case 5: hipLaunchKernelGGL(k_bwd_all<5>, grid, dim3(256), lds, s, A); break;
+    case 6: hipLaunchKernelGGL(k_bwd_all<6>, grid, dim3(256), lds, s, A); break;
+    case 8: hipLaunchKernelGGL(k_bwd_all<8>, grid, dim3(256), lds, s, A); break;
+    default: hipLaunchKernelGGL(k_bwd_all<7>, grid, dim3(256), lds, s, A); break;
+  }
   LAUNCH_CHECK();
 }
