@@ -1680,6 +1680,12 @@ struct BwdAllArgs {
   // serialise at the memory side); readers sum the replicas
   float* c1rep;
   int nrep, rep_stride, bias_off;
+  // grads_only (multi-GPU step): every gradient is written to the flat grad
+  // buffer (g2w/gw1/gb1 accumulated atomically, the rest stored) and no
+  // parameter is touched -- the all-reduce's SGD epilogue updates them;
+  // the cursor is left alone
+  int grads_only;
+  float* g2b; float* g1w; float* g1b; float* gfw; float* gfb;  // grad slots of conv2.bias, fc1.w/b, fc2.w/b
 };
 
 struct EpiSgd {
@@ -1699,7 +1705,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   __shared__ int s_last;
   int bid = blockIdx.x;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (bid == 0 && threadIdx.x == 0) {  // no block of this launch reads the cursor
+  if (bid == 0 && threadIdx.x == 0 && !A.grads_only) {  // no block of this launch reads the cursor
     *A.bidx = (*A.bidx + 1) % A.nbatches;
     *A.pending = 1;
   }
@@ -1710,7 +1716,8 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
     const int oc = bid * 4 + wv;
     if (oc >= C2) return;
     const float g = c2_bias_sum(oc, A.g2, A.code2, A.B);
-    if (lane == 0) {
+    if (lane == 0 && A.grads_only) A.g2b[oc] = g;
+    else if (lane == 0) {
       float pv = A.p2b[oc], mv = A.m2b[oc];
       sgd_elem(pv, g, mv, *A.a.lr, A.a.mom, A.a.wd, A.a.gscale, A.a.nesterov);
       A.p2b[oc] = pv;
@@ -1722,6 +1729,16 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   if (bid < A.nF) {
     const float lr = *A.a.lr;
     constexpr int NWF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4;
+    if (A.grads_only) {
+      if (bid < NWF) {
+        block_gemm_4tiles<LAY_KROW, LAY_KROW>(A.dl, NCLS, A.h1, F1OUT, NCLS, F1OUT, A.B, bid, EpiStore{A.gfw, F1OUT});
+        return;
+      }
+      bid -= NWF;
+      if (bid < 8) block_colsum64(A.dh1, F1OUT, A.B, F1OUT, bid * 64, smem, A.g1b);
+      else block_colsum64(A.dl, NCLS, A.B, NCLS, 0, smem, A.gfb);
+      return;
+    }
     if (bid < NWF) {
       block_gemm_4tiles<LAY_KROW, LAY_KROW>(A.dl, NCLS, A.h1, F1OUT, NCLS, F1OUT, A.B, bid,
                                             EpiSgd{A.pfw, A.mfw, F1OUT, lr, &A.a});
@@ -1735,6 +1752,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   bid -= A.nF;
   if (bid < A.nA) {
     c2_wgrad_block<CH>(bid, smem, A.g2, A.code2, A.a1p, A.g2w, A.B);
+    if (A.grads_only) return;
     // arrival: every lane's atomics have been performed at the memory side
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1779,7 +1797,11 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   }
   bid -= A.nB;
   if (bid < A.nD) {
-    dw1_sgd_tile(bid * 4 + wv, A.dh1, A.a2p, A.p1w, A.m1w, A.B, A.a);
+    if (A.grads_only)
+      block_gemm_4tiles<LAY_KROW, LAY_KROW, EpiStore, 4>(A.dh1, F1OUT, A.a2p, F1IN, F1OUT, F1IN, A.B, bid,
+                                                        EpiStore{A.g1w, F1IN});
+    else
+      dw1_sgd_tile(bid * 4 + wv, A.dh1, A.a2p, A.p1w, A.m1w, A.B, A.a);
     return;
   }
 }
@@ -2240,8 +2262,9 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
                         long long off_fc1b, long long off_c2w, long long off_c2b, long long off_c1w,
                         long long off_c1b, int* ctr, long long* bidx, long long nbatches, int* pending, int B,
                         const float* lr, float mom, float wd, float gscale, int nesterov, float* c1rep, int nrep,
-                        int rep_stride, hipStream_t s) {
-  if (!bidx || !pending || !ctr || nbatches < 1 || B < 1 || nrep < 1 || (nrep > 1 && !c1rep)) return -1;
+                        int rep_stride, int grads_only, hipStream_t s) {
+  if (!grads_only && (!bidx || !pending || !ctr || nbatches < 1)) return -1;
+  if (B < 1 || nrep < 1 || (nrep > 1 && !c1rep)) return -1;
   BwdAllArgs A;
   A.g2 = g2; A.code2 = code2; A.a1p = a1p; A.w2f = w2f; A.x = x; A.code1 = code1;
   A.gw1 = g + off_c1w; A.gb1 = g + off_c1b;
@@ -2258,6 +2281,9 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   A.nrep = nrep;
   A.rep_stride = rep_stride;
   A.bias_off = (int)(off_c1b - off_c1w);
+  A.grads_only = grads_only;
+  A.g2b = g + off_c2b; A.g1w = g + off_fc1w; A.g1b = g + off_fc1b; A.gfw = g + off_fc2w; A.gfb = g + off_fc2b;
+  if (grads_only) A.w2f = p + off_c2w;  // nothing updates conv2.weight in this launch
   A.bidx = bidx; A.nbatches = nbatches; A.pending = pending; A.B = B;
   static const int chunk = [] {
     // samples per conv2-wgrad block, 4..8 (A/B, profiles/bwd_all_r2.md):

@@ -92,6 +92,7 @@ struct Proc {
   int last_exit_code = 0;
   double last_finished_at = 0;
   std::string launcher;  // "zygote" | "exec"
+  bool exec_only = false;  // spawn request "launcher": "exec" -- never fork from the zygote
 };
 
 // ---------------------------------------------------------------- zygote --
@@ -284,7 +285,7 @@ struct Agent {
 
   // ------------------------------------------------------------- spawn --
   bool start_zygote(Proc& p) {
-    if (!zygote.enabled() || !zygote.ready || !zygote.eligible(p.argv)) return false;
+    if (p.exec_only || !zygote.enabled() || !zygote.ready || !zygote.eligible(p.argv)) return false;
     Json req = Json::object();
     Json argv = Json::array();
     for (auto& a : p.argv) argv.push(a);
@@ -388,6 +389,7 @@ struct Agent {
     p.cwd = req["cwd"].str();
     p.log = req["log"].str();
     p.restart_policy = req["restart_policy"].str("Never");
+    p.exec_only = req["launcher"].str("auto") == "exec";
     for (auto& c : req["cpus"].a) p.cpus.push_back((int)c.num());
     procs[id] = p;
     start(procs[id]);

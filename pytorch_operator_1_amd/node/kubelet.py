@@ -449,6 +449,10 @@ class Kubelet:
         env.setdefault("LOCAL_RANK", "0")
         env.setdefault("LOCAL_WORLD_SIZE", "1")
         env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+        # one TCPStore implementation for every replica of a job: the
+        # zygote-forked ones must use the classic store (node/zygote.py), and
+        # a libuv server with classic clients was seen to hang the rendezvous
+        env.setdefault("USE_LIBUV", "0")
         env["PTO_POD_NAME"] = name_of(pod)
         env["PTO_NAMESPACE"] = namespace_of(pod)
         env["PTO_JOB_NAME"] = (pod["metadata"].get("labels") or {}).get(C.LABEL_JOB_NAME, "")
@@ -479,8 +483,14 @@ class Kubelet:
                  "state": {"waiting": {"reason": "ErrImagePull", "message": str(e)}}}]})
             return
         env = self._resolve_env(pod, c, rt)
+        # The rank that hosts the rendezvous TCPStore server of a multi-rank
+        # job starts as a fresh interpreter: in a zygote-forked one the
+        # store server hung in its constructor (observed on the GPU box:
+        # master stuck in _create_c10d_store while the 3 workers had
+        # connected; replicas that are only store clients were fine).
+        hosts_store = env.get("RANK") == "0" and int(env.get("WORLD_SIZE", "1") or 1) > 1
         self.agent.spawn(pid, argv, env=env, cwd=c.get("workingDir") or REPO_ROOT,
-                         log=log_path, restart_policy=restart_policy)
+                         log=log_path, restart_policy=restart_policy, launcher="exec" if hosts_store else "auto")
         rt.proc_ids.append(pid)
         if c.get("name") == C.DEFAULT_CONTAINER_NAME:
             eff = {k: env[k] for k in _EFFECTIVE_KEYS if k in env}

@@ -94,9 +94,11 @@ class AgentClient:
         return r
 
     # convenience wrappers
-    def spawn(self, id, argv, env=None, cwd=None, log=None, restart_policy="Never", cpus=None):
+    def spawn(self, id, argv, env=None, cwd=None, log=None, restart_policy="Never", cpus=None, launcher="auto"):
+        """``launcher``: "auto" (zygote when eligible) or "exec" (always
+        fork/exec a fresh interpreter)."""
         return self.ok("spawn", id=id, argv=list(argv), env=dict(env or {}), cwd=cwd or "", log=log or "",
-                       restart_policy=restart_policy, cpus=list(cpus or []))
+                       restart_policy=restart_policy, cpus=list(cpus or []), launcher=launcher)
 
     def kill(self, id, signal=15, grace=10.0, restartable=False):
         return self.call("kill", id=id, signal=signal, grace=grace, restartable=restartable)

@@ -158,6 +158,13 @@ class FusedMnistTrainer:
         self.c1_nrep = max(1, int(os.environ.get("PTO_C1_REPLICAS", "8"))) if self.bwd_all else 1
         self.c1_stride = self.numel - offs["conv1.weight"][0]
         self.c1rep = torch.zeros(max(1, self.c1_nrep - 1) * self.c1_stride, **f32)
+        # multi-GPU step: the same single backward launch in grads-only mode
+        # (every gradient into the flat buffer, no parameter touched) after
+        # F12 / fc1 / F4dx -> 4 launches + the all-reduce (whose SGD
+        # epilogue updates) instead of 6 (PTO_DDP_BWD_ALL=0: the old split)
+        self.ddp_bwd_all = self.ddp and not self.fuse_fc and os.environ.get("PTO_DDP_BWD_ALL", "1") == "1"
+        if self.ddp_bwd_all and self.xcur is None:
+            self.xcur = torch.empty(self.B * 784, device=device)
         # multi-GPU schedule: overlap the fc bucket's all-reduce with the conv
         # backward on a side stream (PTO_COMM_OVERLAP=1), or all-reduce the
         # whole flat buffer once after the backward on the compute stream
@@ -165,6 +172,8 @@ class FusedMnistTrainer:
         # both whole-step graphs are captured and timed at startup (max over
         # ranks) and the faster is kept (_choose_schedule).
         self.comm_overlap = {"1": True, "0": False}.get(os.environ.get("PTO_COMM_OVERLAP", "auto"))
+        if self.ddp and not self.fuse_fc and os.environ.get("PTO_DDP_BWD_ALL", "1") == "1":
+            self.comm_overlap = False  # the fc gradients only exist after the single backward launch
         self._c1 = offs["conv1.weight"][0]
         self._c1_bias = offs["conv1.bias"][0] - self._c1
 
@@ -296,6 +305,22 @@ class FusedMnistTrainer:
             c(L.pto_sgd_flat(self._params.data_ptr(), self.grads.data_ptr(), self.mom.data_ptr(), split, split, *o,
                              side.cuda_stream), "sgd_fc")
             return
+        if self.ddp_bwd_all:  # F12 (copies the images out for the backward), fc1, F4 + d(a2p)
+            c(L.pto_conv12_fwd_lazy_x(self.data.data_ptr(), P["conv1.weight"].data_ptr(),
+                                      P["conv1.bias"].data_ptr(), P["conv2.weight"].data_ptr(),
+                                      P["conv2.bias"].data_ptr(), self.a1p.data_ptr(), self.code1.data_ptr(),
+                                      self.a2p.data_ptr(), self.code2.data_ptr(), B, bi, None, None, 0, None, None,
+                                      0.0, 0.0, 1.0, 0, self.xcur.data_ptr(), None, None, 1, 0, s),
+              "conv12_fwd_x")
+            c(L.pto_linear_fwd(self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
+                               self.h1.data_ptr(), B, 500, 800, 1, s), "fc1_fwd")
+            c(L.pto_fc2_ce_dx(self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
+                              self.target.data_ptr(), P["fc1.weight"].data_ptr(), self.loss_rows.data_ptr(),
+                              self.dlogits.data_ptr(), self.dh1.data_ptr(), self.da2p.data_ptr(), B, 1.0 / B, bi,
+                              self._params[self._c1:].data_ptr(), self.grads[self._c1:].data_ptr(),
+                              self.mom[self._c1:].data_ptr(), self.numel - self._c1, None, *self._opt_args(),
+                              None, 1, 0, s), "fc2_ce_dx")
+            return
         # same F1+F2 launch without an owed update (pending = nullptr)
         c(L.pto_conv12_fwd_lazy(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
                                 P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
@@ -325,16 +350,18 @@ class FusedMnistTrainer:
         # but measured break-even: every sample-block adds into the same 520
         # addresses, 64-way atomic contention.  The separate 320-block conv1
         # launch below adds each address only 16 times.)
-        if self.bwd_all:  # the whole backward + every parameter update in one launch
+        if self.bwd_all or self.ddp_bwd_all:  # the whole backward (+ every update when single-GPU) in one launch
             offs = param_offsets()[0]
             o = [offs[n][0] for n in ("fc2.weight", "fc2.bias", "fc1.weight", "fc1.bias", "conv2.weight",
                                       "conv2.bias", "conv1.weight", "conv1.bias")]
-            c(L.pto_bwd_all(self.da2p.data_ptr(), self.code2.data_ptr(), self.a1p.data_ptr(), self.w2f.data_ptr(),
+            go = not self.bwd_all  # grads-only (DDP): the all-reduce's epilogue updates
+            c(L.pto_bwd_all(self.da2p.data_ptr(), self.code2.data_ptr(), self.a1p.data_ptr(), _lib.ptr(self.w2f),
                             self.xcur.data_ptr(), self.code1.data_ptr(), self.dh1.data_ptr(), self.a2p.data_ptr(),
                             self.h1.data_ptr(), self.dlogits.data_ptr(), self._params.data_ptr(),
-                            self.grads.data_ptr(), self.mom.data_ptr(), *o, self.c2_ctr.data_ptr(), bi,
-                            self.n_batches, self.pending.data_ptr(), B, *self._opt_args(), self.c1rep.data_ptr(),
-                            self.c1_nrep, self.c1_stride, s), "bwd_all")
+                            self.grads.data_ptr(), self.mom.data_ptr(), *o, _lib.ptr(self.c2_ctr),
+                            None if go else bi, self.n_batches, None if go else self.pending.data_ptr(), B,
+                            *self._opt_args(), self.c1rep.data_ptr(), 1 if go else self.c1_nrep, self.c1_stride,
+                            int(go), s), "bwd_all")
             return
         if self.merge_f4:  # + B3's all-row reductions (dW2, db1, db2)
             c(L.pto_conv2_bwd_fc(self.da2p.data_ptr(), self.code2.data_ptr(), self.a1p.data_ptr(),
@@ -717,11 +744,15 @@ class FusedMnistTrainer:
                 # graph waits for both (DDP-style overlap)
                 fc_b, conv_b = self._bucket_views()
                 self._graphs[0].replay()
-                w0 = dist.all_reduce(fc_b, async_op=True)
-                self._graphs[1].replay()
-                w1 = dist.all_reduce(conv_b, async_op=True)
-                w0.wait()
-                w1.wait()
+                if self.ddp_bwd_all:  # the fc grads are produced by the backward launch
+                    self._graphs[1].replay()
+                    dist.all_reduce(self.grads)
+                else:
+                    w0 = dist.all_reduce(fc_b, async_op=True)
+                    self._graphs[1].replay()
+                    w1 = dist.all_reduce(conv_b, async_op=True)
+                    w0.wait()
+                    w1.wait()
                 self._graphs[2].replay()
         self.steps_done += 1
         self._owed = self.fused_opt

@@ -153,10 +153,15 @@ def resume_state(ckpt_dir: str | None, rank: int, world: int):
     or ``(None, None)``."""
     if not ckpt_dir:
         return None, None
-    choice = [ckpt.latest(ckpt_dir) if rank == 0 else None]
     if world > 1 and dist.is_initialized():
-        dist.broadcast_object_list(choice, src=0)
-    path = choice[0]
+        # agreed through the rendezvous store (no device collective): rank
+        # 0 publishes its choice, the others block on the key
+        store = dist.distributed_c10d._get_default_store()
+        if rank == 0:
+            store.set("pto/resume_path", ckpt.latest(ckpt_dir) or "")
+        path = store.get("pto/resume_path").decode() or None
+    else:
+        path = ckpt.latest(ckpt_dir)
     if not path:
         return None, None
     if not os.path.exists(path):

@@ -1,6 +1,7 @@
 """Whole stack on a real MI355X: PyTorchJob -> controller -> node agent
 (GPU pinned with HIP_VISIBLE_DEVICES) -> fused HIP trainer; plus the
 submit -> first optimizer step latency that BASELINE.json asks for."""
+import os
 import time
 
 import pytest
@@ -86,7 +87,7 @@ def test_gpu_kill_rejoin_resumes_fused_trainer(cluster, tmp_path):
 
 _SHARED_ARGS = ["--backend", "gloo", "--impl", "fused", "--comm", "xgmi", "--log-interval", "50", "--no-test",
                 "--train-size", "16384"]
-_SHARED_ENV = {"PTO_COMM_OVERLAP": "0"}  # skip the schedule race (4 ranks time-slice one GPU)
+_SHARED_ENV = {"PTO_COMM_OVERLAP": "0", "PTO_FAULTHANDLER": "1"}  # no schedule race (4 ranks share one GPU)
 
 
 @pytest.fixture(scope="module")
@@ -95,6 +96,40 @@ def shared_cluster(tmp_path_factory):
                      gpu_visibility="node").start()
     yield c
     c.stop()
+
+
+def _wait_verbose(c, name, timeout, dump_after=None):
+    """wait_for_condition that prints the job state and each replica's last
+    log line every 15 s (a silent multi-minute wait reads as a hang); after
+    ``dump_after`` s the replicas are sent SIGUSR2 (stack dump)."""
+    start = time.time()
+    end = start + timeout
+    dumped = False
+    while True:
+        try:
+            return c.wait_for_condition(name, timeout=min(15.0, max(0.1, end - time.time())))
+        except TimeoutError:
+            if time.time() >= end:
+                for n in _replicas(name):  # full logs (faulthandler stacks included) for the report
+                    print(f"==== {n}\n" + "\n".join(c.pod_log("default", n).splitlines()[-80:]), flush=True)
+                raise
+            if dump_after and time.time() > start + dump_after and not dumped:
+                dumped = True  # PTO_FAULTHANDLER pods dump every thread's stack on SIGUSR2
+                for n in _replicas(name):
+                    try:
+                        c.kubelet.inject_fault("default", n, signal=12)
+                    except Exception:  # noqa: BLE001
+                        pass
+            j = c.store.get("pytorchjobs", "default", name)
+            conds = [x["type"] for x in j.get("status", {}).get("conditions") or []]
+            print(f"[wait {name}] conditions={conds}", flush=True)
+            for n in _replicas(name):
+                try:
+                    pod = c.store.get("pods", "default", n)
+                    tail = (c.pod_log("default", n).strip().splitlines() or [""])[-1][-160:]
+                    print(f"  {n} {pod.get('status', {}).get('phase')}: {tail}", flush=True)
+                except Exception as e:  # noqa: BLE001
+                    print(f"  {n}: {e}", flush=True)
 
 
 def _replicas(job):
@@ -128,7 +163,8 @@ def test_config2_exitcode_kill_rejoin_every_replica_resumes(shared_cluster, tmp_
                   env=_SHARED_ENV, restart_policy="ExitCode")
     job["spec"]["backoffLimit"] = 6
     c.submit(job)
-    j = c.wait_for_condition("mnist-w3-kill", timeout=600)
+    j = _wait_verbose(c, "mnist-w3-kill", timeout=int(os.environ.get("PTO_TEST_KILL_TIMEOUT", "600")),
+                      dump_after=float(os.environ.get("PTO_TEST_DUMP_AFTER", "0")) or None)
     logs = {n: c.pod_log("default", n) for n in _replicas("mnist-w3-kill")}
     assert j["status"]["conditions"][-1]["type"] == "Succeeded", (j["status"], logs)
     # Restarting is not in the final conditions (Running replaces it,
