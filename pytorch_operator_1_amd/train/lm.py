@@ -92,6 +92,11 @@ def _main(argv=None):
     t_last, steps_since = time.time(), 0
     for step in range(start, args.steps):
         if fail and step == fail:
+            # deterministic injection: the kill lands after the checkpoint in
+            # flight is durable (a real crash may lose it; resume then falls
+            # back to the previous committed step)
+            if saver:
+                saver.commit()
             print(f"[fault-injection] rank {rank} SIGKILL at step {step}", flush=True)
             os.kill(os.getpid(), signal.SIGKILL)
         trainer.step()
