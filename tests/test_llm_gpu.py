@@ -258,4 +258,4 @@ def test_lm_trainer_kill_resume_on_gpu(tmp_path, model, extra):
     assert b.returncode == 0, b.stderr[-2000:]
     assert "Resumed from" in b.stdout and "at step 4" in b.stdout
     fl = [float(re.search(r"final_loss=([0-9.]+)", o.stdout).group(1)) for o in (ref, b)]
-    assert abs(fl[0] - fl[1]) <= 2e-2 * abs(fl[0]), fl
+    assert abs(fl[0] - fl[1]) <= 2e-2 * abs(fl[0]) + 1e-4, fl

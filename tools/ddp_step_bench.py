@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Per-step time of the fused MNIST trainer's MULTI-GPU schedule at world
+size 1 (``force_ddp``: the RCCL all-reduce of a 1-rank group is a no-op, so
+this is the compute + optimizer part of the DDP step), for A/B of
+PTO_DDP_BWD_ALL and friends.  Prints one JSON line.
+
+Usage: python tools/ddp_step_bench.py [--steps 2000] [--warmup 200]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    a = ap.parse_args()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+
+    tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=60000, force_ddp=True)
+    tr.run(a.warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tr.run(a.steps)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    print(json.dumps({"ddp_step_us": round(dt * 1e6, 2), "ddp_bwd_all": tr.ddp_bwd_all,
+                      "graph_mode": tr.graph_mode, "loss": round(tr.last_loss(), 4)}))
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
