@@ -16,15 +16,19 @@ MI355X design:
     and the optimizer is a single fused launch that also zeroes the grads
     (so atomically accumulated grads start from zero next step).
   * every op is a kernel from ``csrc/kernels/mnist_kernels.hip``; activations
-    stay resident in HBM.  Single process: 6 launches per step, the optimizer
-    running inside them (``fused_opt``: extra blocks of the conv1-backward
-    launch update fc/conv2, conv1's update is applied on the fly by the next
-    step's first launch and committed by its fc2 launch).  DDP: 7 launches +
-    the bucketed all-reduce, then one multi-tensor SGD launch.
-  * the step is captured once into a HIP graph and replayed: the host cost
-    per step is one ``hipGraphLaunch`` instead of ~10 launches.  The batch
-    index is a device counter advanced inside the graph, so replays walk the
-    dataset like the eager loop does.
+    stay resident in HBM.  Four launches per step: F12 (conv1+conv2
+    forward), fc1, F4dx (fc2 + loss + d(a2p)) and ``k_bwd_all`` (the whole
+    backward).  Single process: every parameter update runs inside those
+    launches (``fused_opt``: ``k_bwd_all`` updates fc/conv2 -- conv2.weight
+    by the last-arriving wgrad chunk of each tile -- and conv1's update is
+    applied on the fly by the next step's F12 and committed by its F4dx).
+    DDP: ``k_bwd_all`` in grads-only mode, then one all-reduce of the flat
+    buffer whose epilogue is the SGD update (xGMI) or the all-reduce + one
+    multi-tensor SGD launch (RCCL).
+  * steps are captured into HIP graphs and replayed (``run(n)``: the
+    largest multi-step graphs first, one replay per 32 steps + one); the
+    batch index is a device counter advanced inside the graph, so replays
+    walk the dataset like the eager loop does.
 """
 from __future__ import annotations
 
