@@ -686,12 +686,19 @@ __global__ __launch_bounds__(512) void k_linear_fwd_vec(const float* __restrict_
 // K slice (NG = 4 groups, all 8 loads per lane in flight at once), so the
 // serial chain per wave is one memory round trip + 16 MFMAs instead of
 // 32.  Same tile count as k_linear_fwd_vec (fc1 at B=64: 128 blocks).
+// XCD-aware tile order: workgroup i runs on XCD i % 8, so tile index
+// (i % 8) * (T / 8) + i / 8 puts T/8 consecutive tiles -- the m-tiles that
+// share one weight tile -- on one XCD, and each weight tile is fetched into
+// one L2 instead of up to four.  Identity unless T % 8 == 0.
+PTO_DEV int xcd_tile(int i, int T, bool on) { return (on && !(T & 7)) ? (i & 7) * (T >> 3) + (i >> 3) : i; }
+
 __global__ __launch_bounds__(1024) void k_linear_fwd_vec16(const float* __restrict__ x, const float* __restrict__ w,
                                                            const float* __restrict__ bias, float* __restrict__ y,
                                                            int M, int N, int K, int relu) {
   __shared__ float red[16 * 256];
   const int mtiles = (M + 15) >> 4;
-  const int mt = blockIdx.x % mtiles, nt = blockIdx.x / mtiles;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x, relu & 2);
+  const int mt = tile % mtiles, nt = tile / mtiles;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int kc = (((K + 15) / 16) + 15) & ~15;
   const f32x4 acc = wave_tile_16x16<LAY_ROWK, LAY_ROWK, 4, true, true>(x, K, w, K, M, N, K, mt * 16, nt * 16,
@@ -705,7 +712,7 @@ __global__ __launch_bounds__(1024) void k_linear_fwd_vec16(const float* __restri
 #pragma unroll
     for (int q = 0; q < 16; ++q) v += red[q * 256 + t];
     const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
-    if (m < M && n < N) EpiBiasRelu{bias, y, N, relu != 0}(m, n, v);
+    if (m < M && n < N) EpiBiasRelu{bias, y, N, (relu & 1) != 0}(m, n, v);
   }
 }
 
@@ -937,6 +944,171 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx(
   }
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) red[w * 256 + ((lane >> 4) * 4 + rr) * 16 + (lane & 15)] = acc[rr];
+  __syncthreads();
+  if (t < 256) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < FDX_WAVES; ++q) v += red[q * 256 + t];
+    const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
+    if (m < B && n < F1IN) da2p[m * F1IN + n] = v;
+  }
+}
+
+// k_fc2_ce_dx with the head on the matrix cores.  The per-wave head above
+// reads all of W2 (80 scalar loads per lane, 16 waves per block => ~1600
+// VMEM instructions per block, most of them the same 20 KB); here the block
+// stages its 16 h1 rows and W2 into LDS with one round of float4 loads and
+// runs the head as two tiny GEMMs:
+//   Z[16 x 16]   = h1_tile[16 x 500] W2^T   (split-K over the 16 waves)
+//   dh1[16 x 500] = dL[16 x 16] W2[16 x 500] (2 column tiles per wave, K=16)
+// with the softmax between them done by 256 threads, 16 lanes per row.
+// dh1 overwrites the h1 tile in place (each element is read for its ReLU
+// mask and written by the same lane), then the d(a2p) tile is as before.
+// Requires 16-byte aligned h1 and W2 (checked by the launcher).
+__global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
+    const float* __restrict__ h1, const float* __restrict__ w2, const float* __restrict__ b2,
+    const int64_t* __restrict__ labels, const float* __restrict__ w1, float* __restrict__ loss_rows,
+    float* __restrict__ dlogits, float* __restrict__ dh1, float* __restrict__ da2p, int B, float inv_b,
+    const long long* __restrict__ bidx, Conv1Commit cm) {
+  __shared__ __attribute__((aligned(16))) float hs[16 * F1OUT];
+  __shared__ __attribute__((aligned(16))) float w2s[NCLS * F1OUT];
+  __shared__ float red[FDX_WAVES * 256];
+  __shared__ __attribute__((aligned(16))) float dls[256];
+  const int mtiles = (B + 15) >> 4, ntiles = (F1IN + 15) >> 4;
+  const int t = threadIdx.x;
+  if (blockIdx.x == (unsigned)(mtiles * ntiles)) {
+    if (cm.pending && *cm.pending) {
+      const float lr = *cm.a.lr;
+      for (int i = 4 * t; i < cm.n; i += 4 * FDX_WAVES * 64) commit4(cm, i, lr);
+    }
+    return;
+  }
+  const int tile = xcd_tile(blockIdx.x, mtiles * ntiles, cm.a.variant & 4);
+  const int mt = tile % mtiles, nt = tile / mtiles;
+  const int w = t >> 6, lane = t & 63;
+  const int r = lane & 15, gq = lane >> 4;
+  constexpr int KC = ((F1OUT + FDX_WAVES - 1) / FDX_WAVES + 15) & ~15;  // 32
+  constexpr int NGK = KC / 16;
+  constexpr int H4 = 16 * F1OUT / 4, W4 = NCLS * F1OUT / 4;  // 2000, 1250 float4
+  constexpr int NT = FDX_WAVES * 64;
+  static_assert(F1OUT % 4 == 0 && H4 <= 2 * NT && W4 <= 2 * NT, "staging assumes two float4 rounds");
+  const int kb = w * KC, kend = min((w + 1) * KC, F1OUT);
+  // ---- one round of loads: h1 tile + W2 (float4), W1 slice, label, bias
+  const int nrow = min(16, B - mt * 16);
+  const float4* hg = reinterpret_cast<const float4*>(h1 + (size_t)mt * 16 * F1OUT);
+  const float4* wg = reinterpret_cast<const float4*>(w2);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int h4n = nrow * (F1OUT / 4);
+  const float4 hv0 = t < h4n ? hg[t] : z4;
+  const float4 hv1 = (t + NT < H4 && t + NT < h4n) ? hg[t + NT] : z4;
+  const float4 wv0 = t < W4 ? wg[t] : z4;
+  const float4 wv1 = t + NT < W4 ? wg[t + NT] : z4;
+  float bw[NGK][4];
+#pragma unroll
+  for (int q = 0; q < NGK; ++q) load4<LAY_KROW>(w1, F1IN, nt * 16 + r, F1IN, kb + 16 * q + 4 * gq, kend, bw[q]);
+  const int hm = t >> 4, hn = t & 15;  // softmax thread -> (row, class), t < 256
+  const int grow = mt * 16 + hm;
+  int y = 0;
+  float bias = 0.f;
+  if (t < 256) {
+    if (grow < B && labels) y = (int)labels[(bidx ? (size_t)(*bidx) * B : 0) + grow];
+    if (hn < NCLS) bias = b2[hn];
+  }
+  float4* hs4 = reinterpret_cast<float4*>(hs);
+  float4* ws4 = reinterpret_cast<float4*>(w2s);
+  hs4[t] = hv0;
+  if (t + NT < H4) hs4[t + NT] = hv1;
+  if (t < W4) ws4[t] = wv0;
+  if (t + NT < W4) ws4[t + NT] = wv1;
+  __syncthreads();
+  // ---- Z partial: rows r of the tile x classes r (<10), K slice of wave w
+  {
+    f32x4 acc0 = zero4(), acc1 = zero4();
+#pragma unroll
+    for (int q = 0; q < NGK; ++q) {
+      const int k0 = kb + 16 * q + 4 * gq;
+      const bool ok = k0 < F1OUT;
+      const float4 a = ok ? *reinterpret_cast<const float4*>(hs + r * F1OUT + k0) : z4;
+      const float4 b = (ok && r < NCLS) ? *reinterpret_cast<const float4*>(w2s + r * F1OUT + k0) : z4;
+      acc0 = mfma16x16x4(a.x, b.x, acc0);
+      acc1 = mfma16x16x4(a.y, b.y, acc1);
+      acc0 = mfma16x16x4(a.z, b.z, acc0);
+      acc1 = mfma16x16x4(a.w, b.w, acc1);
+    }
+    const f32x4 acc = acc0 + acc1;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) red[w * 256 + (gq * 4 + rr) * 16 + r] = acc[rr];
+  }
+  __syncthreads();
+  // ---- log_softmax + NLL + dlogits: 16 lanes per row (waves 0..3)
+  if (t < 256) {
+    float z = bias;
+#pragma unroll
+    for (int q = 0; q < FDX_WAVES; ++q) z += red[q * 256 + t];
+    const bool cls = hn < NCLS;
+    float mx = cls ? z : -INFINITY;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    float se = cls ? __expf(z - mx) : 0.f;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) se += __shfl_xor(se, o, 64);
+    const float lse = mx + __logf(se);
+    const bool live = grow < B;
+    const float dl = (cls && live) ? (__expf(z - lse) - (hn == y ? 1.f : 0.f)) * inv_b : 0.f;
+    dls[t] = dl;
+    const float zy = __shfl(z, (lane & 48) | (y & 15), 64);
+    if (nt == 0 && live) {
+      if (cls) dlogits[grow * NCLS + hn] = dl;
+      if (hn == 0) loss_rows[grow] = lse - zy;
+    }
+  }
+  __syncthreads();
+  // ---- dh1 = (dL W2) * [h1 > 0], column tiles w and w + 16, in place
+  {
+    const float4 a = *reinterpret_cast<const float4*>(dls + r * 16 + 4 * gq);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int col = (w + FDX_WAVES * hh) * 16 + r;
+      const bool cok = col < F1OUT;
+      float b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = 4 * gq + j;
+        b[j] = (cok && k < NCLS) ? w2s[k * F1OUT + col] : 0.f;
+      }
+      f32x4 acc = zero4();
+      acc = mfma16x16x4(a.x, b[0], acc);
+      acc = mfma16x16x4(a.y, b[1], acc);
+      acc = mfma16x16x4(a.z, b[2], acc);
+      acc = mfma16x16x4(a.w, b[3], acc);
+      if (cok) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int row = gq * 4 + rr;
+          const float v = hs[row * F1OUT + col] > 0.f ? acc[rr] : 0.f;
+          hs[row * F1OUT + col] = v;
+          if (nt == 0 && mt * 16 + row < B) dh1[(mt * 16 + row) * F1OUT + col] = v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---- d(a2p) tile [16 rows, 16 cols] = dh1 W1, split-K over the waves
+  {
+    f32x4 acc0 = zero4(), acc1 = zero4();
+#pragma unroll
+    for (int q = 0; q < NGK; ++q) {
+      float av[4];
+      load4<LAY_ROWK>(hs, F1OUT, r, 16, kb + 16 * q + 4 * gq, kend, av);
+      acc0 = mfma16x16x4(av[0], bw[q][0], acc0);
+      acc1 = mfma16x16x4(av[1], bw[q][1], acc1);
+      acc0 = mfma16x16x4(av[2], bw[q][2], acc0);
+      acc1 = mfma16x16x4(av[3], bw[q][3], acc1);
+    }
+    const f32x4 acc = acc0 + acc1;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) red[w * 256 + (gq * 4 + rr) * 16 + r] = acc[rr];
+  }
   __syncthreads();
   if (t < 256) {
     float v = 0.f;
@@ -1971,8 +2143,13 @@ PTO_API int pto_linear_fwd(const float* x, const float* w, const float* b, float
     const char* e = getenv("PTO_LINEAR_WAVES");  // 8 = the 512-thread kernel (A/B)
     return e ? atoi(e) : 16;
   }();
+  static const int swz = [] {
+    const char* e = getenv("PTO_XCD_SWZ");  // 0 = linear tile order (A/B)
+    return e ? atoi(e) : 1;
+  }();
   if (vec && waves == 16)
-    hipLaunchKernelGGL(k_linear_fwd_vec16, dim3(tiles), dim3(1024), 0, s, x, w, b, y, M, N, K, relu);
+    hipLaunchKernelGGL(k_linear_fwd_vec16, dim3(tiles), dim3(1024), 0, s, x, w, b, y, M, N, K,
+                       (relu ? 1 : 0) | (swz ? 2 : 0));
   else if (vec)
     hipLaunchKernelGGL(k_linear_fwd_vec, dim3(tiles), dim3(512), 0, s, x, w, b, y, M, N, K, relu);
   else
@@ -2129,8 +2306,21 @@ PTO_API int pto_fc2_ce_dx(const float* h1, const float* w2, const float* b2, con
     const char* e = getenv("PTO_HEAD_HALVING");  // 0 = 6 x 10 butterfly shuffles (A/B)
     return e ? atoi(e) : 1;
   }();
-  cm.a.variant = (prefetch ? 1 : 0) | (head_halving ? 0 : 2);  // read only by k_fc2_ce_dx's tile loop (the commit SGD ignores it)
+  static const int swz = [] {
+    const char* e = getenv("PTO_XCD_SWZ");
+    return e ? atoi(e) : 1;
+  }();
+  cm.a.variant = (prefetch ? 1 : 0) | (head_halving ? 0 : 2) | (swz ? 4 : 0);  // read only by k_fc2_ce_dx's tile loop (the commit SGD ignores it)
+  static const int mf = [] {
+    const char* e = getenv("PTO_FDX_MF");  // 0 = per-wave VALU head (A/B)
+    return e ? atoi(e) : 1;
+  }();
   const int nblk = ((B + 15) / 16) * ((F1IN + 15) / 16);
+  if (mf && !((((uintptr_t)h1) | ((uintptr_t)w2)) & 15)) {
+    hipLaunchKernelGGL(k_fc2_ce_dx_mf, dim3(nblk + 1), dim3(FDX_WAVES * 64), 0, s, h1, w2, b2, labels, w1,
+                       loss_rows, dlogits, dh1, da2p, B, inv_b, bidx, cm);
+    LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(k_fc2_ce_dx, dim3(nblk + 1), dim3(FDX_WAVES * 64), 0, s, h1, w2, b2, labels, w1, loss_rows,
                      dlogits, dh1, da2p, B, inv_b, bidx, cm);
   LAUNCH_CHECK();
