@@ -127,9 +127,68 @@ __global__ void k_noop(int* p) {
   if (p && threadIdx.x == 0 && blockIdx.x == 0) *p = 0;
 }
 
+// Launch-floor probes (tools/kernel_floor_probe.py): an otherwise empty
+// block of NT threads with `lds_rounds` LDS exchange + barrier rounds and an
+// optional coalesced store of `nstore` floats.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_probe(float* out, int nstore, int lds_rounds) {
+  __shared__ float x[NT];
+  float v = (float)threadIdx.x;
+  for (int r = 0; r < lds_rounds; ++r) {
+    x[threadIdx.x] = v;
+    __syncthreads();
+    v += x[(threadIdx.x + 1) % NT];
+    __syncthreads();
+  }
+  const int i = blockIdx.x * NT + threadIdx.x;
+  if (out && i < nstore) out[i] = v;
+}
+
+// `rounds` grid-wide barriers (all blocks must be co-resident: the caller
+// keeps blocks <= #CUs).  One thread per block: agent release, counter add,
+// spin until every block of this round arrived, agent acquire.  The spin is
+// bounded by `max_spin` polls per round (a lost arrival ends the kernel
+// instead of hanging it) and records the failure in ctr[1].
+__global__ __launch_bounds__(1024) void k_gridbar(unsigned* ctr, int rounds, int max_spin) {
+  for (int r = 0; r < rounds; ++r) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      atomicAdd(ctr, 1u);
+      const unsigned target = (unsigned)(r + 1) * gridDim.x;
+      int n = 0;
+      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && n < max_spin) {
+        __builtin_amdgcn_s_sleep(1);
+        ++n;
+      }
+      if (n >= max_spin) atomicOr(ctr + 1, 1u);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 #define PTO_API extern "C" __attribute__((visibility("default")))
+
+PTO_API int pto_probe_kernel(int blocks, int threads, float* out, int nstore, int lds_rounds, hipStream_t s) {
+  if (threads == 64)
+    hipLaunchKernelGGL(k_probe<64>, dim3(blocks), dim3(64), 0, s, out, nstore, lds_rounds);
+  else if (threads == 256)
+    hipLaunchKernelGGL(k_probe<256>, dim3(blocks), dim3(256), 0, s, out, nstore, lds_rounds);
+  else if (threads == 1024)
+    hipLaunchKernelGGL(k_probe<1024>, dim3(blocks), dim3(1024), 0, s, out, nstore, lds_rounds);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+PTO_API int pto_gridbar_probe(int blocks, int threads, unsigned* ctr, int rounds, int max_spin, hipStream_t s) {
+  if (blocks < 1 || blocks > 256 || threads < 64 || threads > 1024 || (threads & 63)) return -1;
+  hipLaunchKernelGGL(k_gridbar, dim3(blocks), dim3(threads), 0, s, ctr, rounds, max_spin);
+  return (int)hipGetLastError();
+}
 
 PTO_API int pto_sgd_block_count(long long n) { return (int)((n + SGD_CHUNK - 1) / SGD_CHUNK); }
 

@@ -77,6 +77,7 @@ struct LazyConv1 {
   const float* rep;     // extra gradient replicas (k_bwd_all): g + sum_r rep[r*rep_stride + i], r < nrep-1
   int nrep, rep_stride;
 };
+constexpr int C1_MAXREP = 16;  // max conv1 gradient replicas (launchers check)
 struct Conv1Commit {
   float* p;             // flat conv1 range [0, n) of params / grads / momentum
   float* g;
@@ -98,11 +99,15 @@ PTO_DEV void commit4(const Conv1Commit& cm, int i, float lr) {
     return;
   }
   float4 gs = *reinterpret_cast<const float4*>(cm.g + i);
-  for (int r = 0; r < cm.nrep - 1; ++r) {
-    float4* q = reinterpret_cast<float4*>(cm.rep + (size_t)r * cm.rep_stride + i);
-    const float4 v = *q;
-    gs.x += v.x; gs.y += v.y; gs.z += v.z; gs.w += v.w;
-    *q = float4{0.f, 0.f, 0.f, 0.f};
+  float4 v[C1_MAXREP - 1];  // every replica load in flight before the first add
+#pragma unroll
+  for (int r = 0; r < C1_MAXREP - 1; ++r)
+    v[r] = *reinterpret_cast<const float4*>(cm.rep + (size_t)min(r, cm.nrep - 2) * cm.rep_stride + i);
+#pragma unroll
+  for (int r = 0; r < C1_MAXREP - 1; ++r) {
+    if (r >= cm.nrep - 1) break;
+    gs.x += v[r].x; gs.y += v[r].y; gs.z += v[r].z; gs.w += v[r].w;
+    *reinterpret_cast<float4*>(cm.rep + (size_t)r * cm.rep_stride + i) = float4{0.f, 0.f, 0.f, 0.f};
   }
   float4 pv = *reinterpret_cast<float4*>(cm.p + i);
   float4 mv = *reinterpret_cast<float4*>(cm.m + i);
@@ -113,6 +118,21 @@ PTO_DEV void commit4(const Conv1Commit& cm, int i, float lr) {
   *reinterpret_cast<float4*>(cm.p + i) = pv;
   *reinterpret_cast<float4*>(cm.m + i) = mv;
   *reinterpret_cast<float4*>(cm.g + i) = float4{0.f, 0.f, 0.f, 0.f};
+}
+
+// Sum of the nrep-1 extra conv1 gradient replicas at index i (0 if !live).
+// All C1_MAXREP-1 loads are issued before the first add (clamped addresses,
+// branch-free): a runtime-bound loop here compiled to one dependent memory
+// round trip per replica, ~1 us of F12's critical path at nrep = 8.
+PTO_DEV float rep_sum(const float* __restrict__ rep, int nrep, int stride, int i, bool live) {
+  if (nrep <= 1) return 0.f;
+  float v[C1_MAXREP - 1];
+#pragma unroll
+  for (int r = 0; r < C1_MAXREP - 1; ++r) v[r] = rep[(size_t)min(r, nrep - 2) * stride + i];
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < C1_MAXREP - 1; ++r) s += (live && r < nrep - 1) ? v[r] : 0.f;
+  return s;
 }
 
 // ---------------------------------------------------------------- F1 ----
@@ -291,7 +311,7 @@ __global__ __launch_bounds__(256) void k_conv12_fwd(const float* __restrict__ x,
         const int e = tid + 256 * q;
         const int fi = e < C1 * 25 ? e : lz.bias_off + (e - C1 * 25);
         float gsum = e < C1 * 26 ? lz.g[fi] : 0.f;
-        for (int r = 0; r < lz.nrep - 1; ++r) gsum += e < C1 * 26 ? lz.rep[r * lz.rep_stride + fi] : 0.f;
+        gsum += rep_sum(lz.rep, lz.nrep, lz.rep_stride, e < C1 * 26 ? fi : 0, e < C1 * 26);
         gq[q] = gsum;
         mq[q] = e < C1 * 26 ? lz.m[fi] : 0.f;
       }
@@ -440,7 +460,7 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
         const int e = tid + NTH * q;
         const int fi = e < C1 * 25 ? e : lz.bias_off + (e - C1 * 25);
         float gsum = e < C1 * 26 ? lz.g[fi] : 0.f;
-        for (int r = 0; r < lz.nrep - 1; ++r) gsum += e < C1 * 26 ? lz.rep[r * lz.rep_stride + fi] : 0.f;
+        gsum += rep_sum(lz.rep, lz.nrep, lz.rep_stride, e < C1 * 26 ? fi : 0, e < C1 * 26);
         gq[q] = gsum;
         mq[q] = e < C1 * 26 ? lz.m[fi] : 0.f;
       }
@@ -563,6 +583,7 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
         p[r][c] = v.x;
         p[r][c + 1] = v.y;
       }
+    const bool skip1 = lz.a.variant & 8;  // timing probe (PTO_F12_PROBE): no conv1 FMAs
 #pragma unroll
     for (int cc = 0; cc < CPT; ++cc) {
       const int oc = cg * CPT + cc;
@@ -571,10 +592,12 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
       for (int q = 0; q < 4; ++q) {
         const int dy = q >> 1, dx = q & 1;
         float sacc = bz[cc];
+        if (!skip1) {
 #pragma unroll
-        for (int kh = 0; kh < 5; ++kh)
+          for (int kh = 0; kh < 5; ++kh)
 #pragma unroll
-          for (int kw = 0; kw < 5; ++kw) sacc = fmaf(p[dy + kh][dx + kw], wr[cc][kh * 5 + kw], sacc);
+            for (int kw = 0; kw < 5; ++kw) sacc = fmaf(p[dy + kh][dx + kw], wr[cc][kh * 5 + kw], sacc);
+        }
         v[q] = sacc;
       }
       float o;
@@ -608,7 +631,8 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
     acc1 = mfma16x16x4(arow[3], brow[3], acc1);
     acc0 = mfma16x16x4(arow[4], brow[4], acc0);
   };
-  if (NPART == 2) {
+  if (lz.a.variant & 16) {  // timing probe: no conv2 MFMAs
+  } else if (NPART == 2) {
     if (half == 0) {
 #pragma unroll
       for (int G = 0; G < 13; ++G) group(G);
@@ -701,8 +725,10 @@ __global__ __launch_bounds__(1024) void k_linear_fwd_vec16(const float* __restri
   const int mt = tile % mtiles, nt = tile / mtiles;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int kc = (((K + 15) / 16) + 15) & ~15;
-  const f32x4 acc = wave_tile_16x16<LAY_ROWK, LAY_ROWK, 4, true, true>(x, K, w, K, M, N, K, mt * 16, nt * 16,
-                                                                       wv * kc, (wv + 1) * kc);
+  f32x4 acc = zero4();
+  if (!(relu & 4))  // bit 4: timing probe (PTO_FC1_PROBE), no loads / MFMAs
+    acc = wave_tile_16x16<LAY_ROWK, LAY_ROWK, 4, true, true>(x, K, w, K, M, N, K, mt * 16, nt * 16, wv * kc,
+                                                             (wv + 1) * kc);
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) red[wv * 256 + ((lane >> 4) * 4 + rr) * 16 + (lane & 15)] = acc[rr];
   __syncthreads();
@@ -2125,7 +2151,11 @@ PTO_API int pto_conv12_fwd_lazy_x(const float* x, const float* w1, const float* 
     const char* e = getenv("PTO_CONV1_SLOTS");
     return e ? atoi(e) : 0;
   }();
-  lz.a.variant = (bal ? 0 : 2) | (slots ? 4 : 0);  // conv1 task layout of k_conv12_fwd2 (the lazy SGD ignores it)
+  static const int probe = [] {
+    const char* e = getenv("PTO_F12_PROBE");  // timing probes, numerics wrong: 8 no conv1 FMAs, 16 no conv2 MFMAs
+    return e ? atoi(e) : 0;
+  }();
+  lz.a.variant = (bal ? 0 : 2) | (slots ? 4 : 0) | (probe & 24);  // conv1 task layout (the lazy SGD ignores it)
   if (fwd_threads() == 1024)
     hipLaunchKernelGGL(k_conv12_fwd2_t<1024>, dim3(B * 4), dim3(1024), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p,
                        code2, B, bidx, lz);
@@ -2147,9 +2177,13 @@ PTO_API int pto_linear_fwd(const float* x, const float* w, const float* b, float
     const char* e = getenv("PTO_XCD_SWZ");  // 0 = linear tile order (A/B)
     return e ? atoi(e) : 1;
   }();
+  static const int probe = [] {
+    const char* e = getenv("PTO_FC1_PROBE");
+    return e ? atoi(e) : 0;
+  }();
   if (vec && waves == 16)
     hipLaunchKernelGGL(k_linear_fwd_vec16, dim3(tiles), dim3(1024), 0, s, x, w, b, y, M, N, K,
-                       (relu ? 1 : 0) | (swz ? 2 : 0));
+                       (relu ? 1 : 0) | (swz ? 2 : 0) | (probe & 4));
   else if (vec)
     hipLaunchKernelGGL(k_linear_fwd_vec, dim3(tiles), dim3(512), 0, s, x, w, b, y, M, N, K, relu);
   else
@@ -2454,7 +2488,7 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
                         const float* lr, float mom, float wd, float gscale, int nesterov, float* c1rep, int nrep,
                         int rep_stride, int grads_only, hipStream_t s) {
   if (!grads_only && (!bidx || !pending || !ctr || nbatches < 1)) return -1;
-  if (B < 1 || nrep < 1 || (nrep > 1 && !c1rep)) return -1;
+  if (B < 1 || nrep < 1 || nrep > C1_MAXREP || (nrep > 1 && !c1rep)) return -1;
   BwdAllArgs A;
   A.g2 = g2; A.code2 = code2; A.a1p = a1p; A.w2f = w2f; A.x = x; A.code1 = code1;
   A.gw1 = g + off_c1w; A.gb1 = g + off_c1b;

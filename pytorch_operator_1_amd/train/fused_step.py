@@ -159,7 +159,7 @@ class FusedMnistTrainer:
         # conv1 gradient replicas of k_bwd_all (sample b adds into replica
         # b % R: B/R same-address atomics instead of B); summed by the lazy
         # apply and the commit
-        self.c1_nrep = max(1, int(os.environ.get("PTO_C1_REPLICAS", "8"))) if self.bwd_all else 1
+        self.c1_nrep = min(16, max(1, int(os.environ.get("PTO_C1_REPLICAS", "8")))) if self.bwd_all else 1
         self.c1_stride = self.numel - offs["conv1.weight"][0]
         self.c1rep = torch.zeros(max(1, self.c1_nrep - 1) * self.c1_stride, **f32)
         # multi-GPU step: the same single backward launch in grads-only mode
