@@ -74,6 +74,7 @@ constexpr int AR_MAX_RANKS = 8;
 constexpr int AR_MAX_BLOCKS = 64;
 constexpr int AR_CHANNELS = 2;
 constexpr int AR_THREADS = 512;
+constexpr int AR_MAX_REP = 16;  // gradient replicas folded before barrier 1
 constexpr long long AR_ONESHOT_MAX = 65536;  // floats (256 KB): one-shot path
 constexpr long long AR_TICKS_PER_MS = 100000LL;  // wall_clock64 runs at 100 MHz
 long long g_timeout_ticks = 500 * AR_TICKS_PER_MS;  // pto_ar_set_timeout_ms
@@ -141,7 +142,35 @@ struct ArSgd {
   long long zero_from;  // float index: own gradient zeroed from here on
   long long* bidx;      // nullptr: no cursor
   long long nbatches;
+  // optional gradient replicas of the float range [rep_from, rep_from +
+  // rep_stride) (k_bwd_all's conv1 replicas, multi-GPU step): replica r >= 1
+  // at rep + (r-1)*rep_stride.  Folded into the local gradient (and zeroed)
+  // by the workgroup that owns the element, BEFORE barrier 1, so every peer
+  // reads folded values.
+  float* rep;
+  int nrep, rep_stride;
+  long long rep_from;
 };
+
+// Fold the local replicas into float4 element (float offset fi) of the local
+// gradient g, if fi lies in the replicated range.  Every replica load is
+// issued before the first add.
+__device__ __forceinline__ void fold_rep(const ArSgd& f, float* g, long long fi) {
+  if (!f.rep || f.nrep <= 1 || fi < f.rep_from || fi >= f.rep_from + f.rep_stride) return;
+  const long long k = fi - f.rep_from;
+  float4 v[AR_MAX_REP - 1];
+#pragma unroll
+  for (int r = 0; r < AR_MAX_REP - 1; ++r)
+    v[r] = *reinterpret_cast<const float4*>(f.rep + (long long)min(r, f.nrep - 2) * f.rep_stride + k);
+  float4 a = *reinterpret_cast<const float4*>(g + fi);
+#pragma unroll
+  for (int r = 0; r < AR_MAX_REP - 1; ++r) {
+    if (r >= f.nrep - 1) break;
+    a.x += v[r].x; a.y += v[r].y; a.z += v[r].z; a.w += v[r].w;
+    *reinterpret_cast<float4*>(f.rep + (long long)r * f.rep_stride + k) = float4{0.f, 0.f, 0.f, 0.f};
+  }
+  *reinterpret_cast<float4*>(g + fi) = a;
+}
 
 // n4 float4 elements starting at float offset `off` of every rank's buffers.
 template <bool SGD>
@@ -157,6 +186,12 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce(const ArPeers* __
   if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blockIdx.x] = e;
   const long long cs = (n4 + world - 1) / world;  // chunk length (float4)
   const long long stride = (long long)gridDim.x * AR_THREADS;
+  if (f.rep && f.nrep > 1 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+    // the elements this workgroup's peers will read: the same sub-range of every chunk
+    for (int q = 0; q < world; ++q)
+      for (long long j = (long long)blockIdx.x * AR_THREADS + threadIdx.x; j < cs && q * cs + j < n4; j += stride)
+        fold_rep(f, P.in[rank], off + 4 * (q * cs + j));
+  }
 
   if (!block_barrier(P, chan, 0, rank, world, e, timeout, err)) return;
   // stage 1: reduce my chunk over all ranks (rank order 0..W-1 everywhere)
@@ -224,6 +259,8 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_1shot(const ArPee
   if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blockIdx.x] = e;
   const long long i = (long long)blockIdx.x * AR_THREADS + threadIdx.x;
   const bool act = i < n4;
+  if (act && f.rep && f.nrep > 1 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+    fold_rep(f, P.in[rank], off + 4 * i);
   if (!block_barrier(P, chan, 0, rank, world, e, timeout, err)) return;
   float4 a = {0.f, 0.f, 0.f, 0.f};
   if (act) {
@@ -342,9 +379,12 @@ PTO_API int pto_ar_allreduce(const void* peers, long long off, long long n, int 
 PTO_API int pto_ar_allreduce_sgd(const void* peers, long long off, long long n, int rank, int world, int chan,
                                  void* epochs, void* err, float* p, float* m, const float* lr, float mom, float wd,
                                  float gscale, int nesterov, long long zero_from, long long* bidx,
-                                 long long nbatches, hipStream_t s) {
+                                 long long nbatches, float* rep, int nrep, int rep_stride, long long rep_from,
+                                 hipStream_t s) {
   if (n % 4 || off % 4 || world < 2 || world > AR_MAX_RANKS || chan < 0 || chan >= AR_CHANNELS || rank < 0 ||
       rank >= world || !p || !m || !lr || ((((uintptr_t)p) | ((uintptr_t)m)) & 15) || (bidx && nbatches < 1))
+    return -1;
+  if (rep && (nrep < 1 || nrep > AR_MAX_REP || rep_stride % 4 || rep_from % 4 || (((uintptr_t)rep) & 15)))
     return -1;
   if (n == 0) return 0;
   ArSgd f;
@@ -358,6 +398,10 @@ PTO_API int pto_ar_allreduce_sgd(const void* peers, long long off, long long n, 
   f.zero_from = zero_from;
   f.bidx = bidx;
   f.nbatches = nbatches;
+  f.rep = rep;
+  f.nrep = rep ? nrep : 1;
+  f.rep_stride = rep_stride;
+  f.rep_from = rep_from;
   if (n <= AR_ONESHOT_MAX) {
     hipLaunchKernelGGL(k_xgmi_allreduce_1shot<true>, dim3((unsigned)((n / 4 + AR_THREADS - 1) / AR_THREADS)),
                        dim3(AR_THREADS), 0, s, reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,

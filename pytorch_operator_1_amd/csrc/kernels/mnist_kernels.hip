@@ -2156,6 +2156,7 @@ PTO_API int pto_conv12_fwd_lazy_x(const float* x, const float* w1, const float* 
     return e ? atoi(e) : 0;
   }();
   lz.a.variant = (bal ? 0 : 2) | (slots ? 4 : 0) | (probe & 24);  // conv1 task layout (the lazy SGD ignores it)
+  if (probe & 32) bidx = nullptr;  // timing probe: no batch-cursor hop before the image load
   if (fwd_threads() == 1024)
     hipLaunchKernelGGL(k_conv12_fwd2_t<1024>, dim3(B * 4), dim3(1024), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p,
                        code2, B, bidx, lz);

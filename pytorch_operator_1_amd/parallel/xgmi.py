@@ -119,12 +119,16 @@ class XgmiAllReduce:
 
     def allreduce_sgd_(self, offset: int, n: int, params: torch.Tensor, mom: torch.Tensor, lr_dev: torch.Tensor,
                        momentum: float, weight_decay: float, gscale: float, nesterov: bool, zero_from: int,
-                       cursor: torch.Tensor | None = None, n_batches: int = 1, chan: int = 0, stream=None):
+                       cursor: torch.Tensor | None = None, n_batches: int = 1, chan: int = 0, stream=None,
+                       replicas: torch.Tensor | None = None, n_replicas: int = 1, rep_from: int = 0):
         """All-reduce ``buf[offset:offset+n]`` and apply SGD-momentum with
         the (``gscale``-scaled) result to ``params``/``mom`` (flat buffers in
         the gradient layout) inside the same launch; the local gradient is
         zeroed from ``zero_from`` on and ``cursor`` (int64 device scalar) is
-        advanced mod ``n_batches`` after the update."""
+        advanced mod ``n_batches`` after the update.  ``replicas``: extra
+        local copies of the gradient range ``[rep_from, numel)`` (replica r
+        >= 1 at ``replicas[(r-1)*(numel-rep_from):]``), folded into the
+        gradient and zeroed before the exchange."""
         if n % 4 or offset % 4:
             raise ValueError("XgmiAllReduce: offset and length must be multiples of 4 floats")
         if offset + n > self.buf.numel():
@@ -134,10 +138,17 @@ class XgmiAllReduce:
                 raise ValueError("XgmiAllReduce: params/momentum must match the gradient buffer")
         s = (stream or torch.cuda.current_stream(self.device)).cuda_stream
         cur = cursor.data_ptr() if cursor is not None else None
+        rep_stride = self.buf.numel() - rep_from
+        rep = None
+        if replicas is not None and n_replicas > 1:
+            if replicas.numel() < (n_replicas - 1) * rep_stride or replicas.device != self.device:
+                raise ValueError("XgmiAllReduce: replica buffer too small for n_replicas")
+            rep = replicas.data_ptr()
         _lib.check(_lib.lib().pto_ar_allreduce_sgd(self.peers.data_ptr(), offset, n, self.rank, self.world, chan,
                                                    self.epochs.data_ptr(), self.err.data_ptr(), params.data_ptr(),
                                                    mom.data_ptr(), lr_dev.data_ptr(), momentum, weight_decay, gscale,
-                                                   int(nesterov), zero_from, cur, n_batches, s),
+                                                   int(nesterov), zero_from, cur, n_batches, rep,
+                                                   n_replicas if rep else 1, rep_stride, rep_from, s),
                    "xgmi_allreduce_sgd")
 
     def error_word(self) -> int:

@@ -156,17 +156,20 @@ class FusedMnistTrainer:
         self.bwd_all = self.merge_f4 and os.environ.get("PTO_BWD_ALL", "1") == "1"
         self.w2f = torch.empty(50 * 500, device=device) if self.bwd_all else None
         self.c2_ctr = torch.zeros(32, device=device, dtype=torch.int32) if self.bwd_all else None
-        # conv1 gradient replicas of k_bwd_all (sample b adds into replica
-        # b % R: B/R same-address atomics instead of B); summed by the lazy
-        # apply and the commit
-        self.c1_nrep = min(16, max(1, int(os.environ.get("PTO_C1_REPLICAS", "8")))) if self.bwd_all else 1
-        self.c1_stride = self.numel - offs["conv1.weight"][0]
-        self.c1rep = torch.zeros(max(1, self.c1_nrep - 1) * self.c1_stride, **f32)
         # multi-GPU step: the same single backward launch in grads-only mode
         # (every gradient into the flat buffer, no parameter touched) after
         # F12 / fc1 / F4dx -> 4 launches + the all-reduce (whose SGD
         # epilogue updates) instead of 6 (PTO_DDP_BWD_ALL=0: the old split)
         self.ddp_bwd_all = self.ddp and not self.fuse_fc and os.environ.get("PTO_DDP_BWD_ALL", "1") == "1"
+        # conv1 gradient replicas of k_bwd_all (sample b adds into replica
+        # b % R: B/R same-address atomics instead of B); summed by the lazy
+        # apply and the commit (single GPU) or folded by the xGMI all-reduce
+        # before its exchange (multi-GPU; RCCL: 1 replica, see ddp_nrep)
+        self.c1_nrep = (min(16, max(1, int(os.environ.get("PTO_C1_REPLICAS", "8"))))
+                        if (self.bwd_all or self.ddp_bwd_all) else 1)
+        self.c1_stride = self.numel - offs["conv1.weight"][0]
+        self.c1rep = torch.zeros(max(1, self.c1_nrep - 1) * self.c1_stride, **f32)
+        self.ddp_nrep = 1
         if self.ddp_bwd_all and self.xcur is None:
             self.xcur = torch.empty(self.B * 784, device=device)
         # multi-GPU schedule: overlap the fc bucket's all-reduce with the conv
@@ -198,6 +201,8 @@ class FusedMnistTrainer:
         if self.world > 1 and self.comm in ("xgmi", "auto"):
             self._setup_xgmi()
         self._side = torch.cuda.Stream(device) if self._xgmi is not None else None
+        if self.ddp_bwd_all and self._xgmi is not None and self.ar_fused_sgd:
+            self.ddp_nrep = self.c1_nrep  # the all-reduce's SGD launch folds them
         # graph modes: "full" = the whole step (collectives included) is one
         # HIP graph; "split" = collectives issued eagerly between graphs;
         # "none" = eager launches.  The xGMI kernel and RCCL all-reduces are
@@ -364,7 +369,7 @@ class FusedMnistTrainer:
                             self.h1.data_ptr(), self.dlogits.data_ptr(), self._params.data_ptr(),
                             self.grads.data_ptr(), self.mom.data_ptr(), *o, _lib.ptr(self.c2_ctr),
                             None if go else bi, self.n_batches, None if go else self.pending.data_ptr(), B,
-                            *self._opt_args(), self.c1rep.data_ptr(), 1 if go else self.c1_nrep, self.c1_stride,
+                            *self._opt_args(), self.c1rep.data_ptr(), self.ddp_nrep if go else self.c1_nrep, self.c1_stride,
                             int(go), s), "bwd_all")
             return
         if self.merge_f4:  # + B3's all-row reductions (dW2, db1, db2)
@@ -502,7 +507,8 @@ class FusedMnistTrainer:
                 lr, mom, wd, gs, nes = self._opt_args()
                 self._xgmi.allreduce_sgd_(0, self.numel, params=self._params, mom=self.mom, lr_dev=self.lr_dev,
                                           momentum=mom, weight_decay=wd, gscale=gs, nesterov=bool(nes),
-                                          zero_from=split, cursor=self.batch_idx, n_batches=self.n_batches)
+                                          zero_from=split, cursor=self.batch_idx, n_batches=self.n_batches,
+                                          replicas=self.c1rep, n_replicas=self.ddp_nrep, rep_from=self._c1)
                 return
             self._xgmi.allreduce_(0, self.numel)
             self.optimizer_step()

@@ -47,6 +47,10 @@ def _worker(rank, world, port, q, comm):
     torch.cuda.synchronize()
     assert int(tr.batch_idx.item()) == STEPS % (N // 64)
     assert float(tr.grads[tr._split():].abs().max()) == 0.0  # atomically accumulated range zeroed
+    if comm == "xgmi" and os.environ.get("PTO_AR_FUSED_SGD", "1") == "1" and os.environ.get("PTO_COMM_OVERLAP") != "1":
+        # conv1 gradient replicas: folded by the all-reduce before the exchange, then zeroed
+        assert tr.ddp_nrep == tr.c1_nrep > 1
+        assert float(tr.c1rep.abs().max()) == 0.0
     q.put((rank, tr.params.cpu()))
     dist.barrier()
     dist.destroy_process_group()
