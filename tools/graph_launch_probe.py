@@ -35,7 +35,28 @@ def main():
         ts.sort()
         return round(ts[len(ts) // 2] * 1e6, 2)
 
+    ev = torch.cuda.Event()
+
+    def spin_timed(fn, reps=60):
+        # host waits by polling an event (no blocking wait), then synchronizes
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            ev.record()
+            while not ev.query():
+                pass
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        return round(ts[len(ts) // 2] * 1e6, 2)
+
     out = {}
+    out["C20_spin"] = spin_timed(C[20].replay)
+    out["C1_spin"] = spin_timed(C[1].replay)
+    out["sync_only"] = timed(lambda: None)
+    out["spin_only"] = spin_timed(lambda: None)
     for n in (1, 2, 4, 8, 16, 20, 32):
         out[f"C{n}"] = timed(C[n].replay)
     out["G1+C19"] = timed(lambda: (G[1].replay(), C[19].replay()))
