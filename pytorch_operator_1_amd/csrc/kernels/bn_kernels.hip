@@ -21,6 +21,7 @@
 // E[x]^2 keeps full precision.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace {
 
@@ -122,8 +123,16 @@ __device__ __forceinline__ void combine_partials(const float* __restrict__ part,
   double acc = 0.0;
   if (c < C) {
     const float* p = part + (col >> 5) * C + c;
-#pragma unroll 8
-    for (int b = grp; b < nblk; b += BN_FT / 64) acc += (double)p[(long long)b * 2 * C];
+    // up to 2048 partial rows: 32 loads in flight per thread, then the adds
+    int b = grp;
+    for (; b + 31 * (BN_FT / 64) < nblk; b += 32 * (BN_FT / 64)) {
+      float v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v[u] = p[(long long)(b + u * (BN_FT / 64)) * 2 * C];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) acc += (double)v[u];
+    }
+    for (; b < nblk; b += BN_FT / 64) acc += (double)p[(long long)b * 2 * C];
   }
   red[grp * 64 + col] = acc;
   __syncthreads();
@@ -315,13 +324,23 @@ bool bn_shape_ok(long long M, int C) {
   return (tpr & (tpr - 1)) == 0;  // power of two <= 256
 }
 
-// Reduction grid: enough blocks to fill the chip, per-block partials
-// bounded to 512 K floats.
+// Reduction grid.  These passes stream HBM, so what matters is bytes in
+// flight: BN_U 16-byte loads per thread x resident threads.  Round 1 capped
+// the grid at 512 blocks (256 at C = 2048: one 4-wave block per CU) and ran
+// at ~40 % of HBM bandwidth; the default now allows 1024 blocks (4 per CU)
+// with >= 8 row iterations each, partials bounded to 4 M floats (16 MB).
+// PTO_BN_MAXBLK / PTO_BN_MINITERS override (A/B).
+int bn_env(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
 void bn_grid(long long M, int C, int* nblk, int* iters) {
+  static const int maxblk = bn_env("PTO_BN_MAXBLK", 1024);
+  static const int minit = bn_env("PTO_BN_MINITERS", 8);
   const int rpi = BN_T / (C >> 3);
   const long long rows_iters = (M + rpi - 1) / rpi;
-  long long nb = (rows_iters + 15) / 16;  // >= 16 iterations per block
-  const long long cap = 524288 / C < 512 ? 524288 / C : 512;
+  long long nb = (rows_iters + minit - 1) / minit;
+  const long long cap = 4194304 / C < maxblk ? 4194304 / C : maxblk;
   if (nb > cap) nb = cap;
   if (nb < 1) nb = 1;
   *nblk = (int)nb;
@@ -343,7 +362,7 @@ PTO_API int pto_bn_scratch_floats(long long M, int C) {
   if (!bn_shape_ok(M, C)) return -1;
   int nblk, iters;
   bn_grid(M, C, &nblk, &iters);
-  return nblk * 2 * C;  // <= 1 M floats (bn_grid caps nblk * C at 512 K)
+  return nblk * 2 * C;  // <= 8 M floats (bn_grid caps nblk * C at 4 M)
 }
 
 // Forward: stat = [mean | rstd | scale | shift] (4*C floats, saved for the
