@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void k_conv1_fwd(const float* __restrict__ x, 
 // Both operands are staged in LDS with coalesced float4 loads: the weight
 // tile (16 x 500, row stride 501 -> conflict-free column reads) and the
 // whole pooled conv1 map of the sample (20 x 12 x 12).
-constexpr int WS_LD = 501;
+constexpr int WS_LD = 502;  // n*502 mod 32 are the 16 even banks: B reads (n, 5g) conflict-free
 __global__ __launch_bounds__(256) void k_conv2_fwd(const float* __restrict__ a1p, const float* __restrict__ w2,
                                                    const float* __restrict__ b2, float* __restrict__ a2p,
                                                    uint8_t* __restrict__ code2, int B) {
@@ -996,8 +996,13 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     const int64_t* __restrict__ labels, const float* __restrict__ w1, float* __restrict__ loss_rows,
     float* __restrict__ dlogits, float* __restrict__ dh1, float* __restrict__ da2p, int B, float inv_b,
     const long long* __restrict__ bidx, Conv1Commit cm) {
-  __shared__ __attribute__((aligned(16))) float hs[16 * F1OUT];
-  __shared__ __attribute__((aligned(16))) float w2s[NCLS * F1OUT];
+  // LDS row stride.  500 keeps the dh1 phase's scalar accesses (rows r and
+  // r + 4 in one 32-lane group, 4*500 = 16 mod 32 banks apart) conflict-free;
+  // 504 would make the float4 operand reads conflict-free instead but the
+  // dh1 phase 2-way (measured: more conflict cycles, same time)
+  constexpr int HLD = F1OUT;
+  __shared__ __attribute__((aligned(16))) float hs[16 * HLD];
+  __shared__ __attribute__((aligned(16))) float w2s[NCLS * HLD];
   __shared__ float red[FDX_WAVES * 256];
   __shared__ __attribute__((aligned(16))) float dls[256];
   const int mtiles = (B + 15) >> 4, ntiles = (F1IN + 15) >> 4;
@@ -1042,10 +1047,12 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
   }
   float4* hs4 = reinterpret_cast<float4*>(hs);
   float4* ws4 = reinterpret_cast<float4*>(w2s);
-  hs4[t] = hv0;
-  if (t + NT < H4) hs4[t + NT] = hv1;
-  if (t < W4) ws4[t] = wv0;
-  if (t + NT < W4) ws4[t + NT] = wv1;
+  constexpr int R4 = F1OUT / 4;  // float4 per row
+  auto pad4 = [](int e) { return (e / R4) * (HLD / 4) + e % R4; };
+  hs4[pad4(t)] = hv0;
+  if (t + NT < H4) hs4[pad4(t + NT)] = hv1;
+  if (t < W4) ws4[pad4(t)] = wv0;
+  if (t + NT < W4) ws4[pad4(t + NT)] = wv1;
   __syncthreads();
   // ---- Z partial: rows r of the tile x classes r (<10), K slice of wave w
   {
@@ -1054,8 +1061,8 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     for (int q = 0; q < NGK; ++q) {
       const int k0 = kb + 16 * q + 4 * gq;
       const bool ok = k0 < F1OUT;
-      const float4 a = ok ? *reinterpret_cast<const float4*>(hs + r * F1OUT + k0) : z4;
-      const float4 b = (ok && r < NCLS) ? *reinterpret_cast<const float4*>(w2s + r * F1OUT + k0) : z4;
+      const float4 a = ok ? *reinterpret_cast<const float4*>(hs + r * HLD + k0) : z4;
+      const float4 b = (ok && r < NCLS) ? *reinterpret_cast<const float4*>(w2s + r * HLD + k0) : z4;
       acc0 = mfma16x16x4(a.x, b.x, acc0);
       acc1 = mfma16x16x4(a.y, b.y, acc1);
       acc0 = mfma16x16x4(a.z, b.z, acc0);
@@ -1100,7 +1107,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int k = 4 * gq + j;
-        b[j] = (cok && k < NCLS) ? w2s[k * F1OUT + col] : 0.f;
+        b[j] = (cok && k < NCLS) ? w2s[k * HLD + col] : 0.f;
       }
       f32x4 acc = zero4();
       acc = mfma16x16x4(a.x, b[0], acc);
@@ -1111,8 +1118,8 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const int row = gq * 4 + rr;
-          const float v = hs[row * F1OUT + col] > 0.f ? acc[rr] : 0.f;
-          hs[row * F1OUT + col] = v;
+          const float v = hs[row * HLD + col] > 0.f ? acc[rr] : 0.f;
+          hs[row * HLD + col] = v;
           if (nt == 0 && mt * 16 + row < B) dh1[(mt * 16 + row) * F1OUT + col] = v;
         }
       }
@@ -1125,7 +1132,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
 #pragma unroll
     for (int q = 0; q < NGK; ++q) {
       float av[4];
-      load4<LAY_ROWK>(hs, F1OUT, r, 16, kb + 16 * q + 4 * gq, kend, av);
+      load4<LAY_ROWK>(hs, HLD, r, 16, kb + 16 * q + 4 * gq, kend, av);
       acc0 = mfma16x16x4(av[0], bw[q][0], acc0);
       acc1 = mfma16x16x4(av[1], bw[q][1], acc1);
       acc0 = mfma16x16x4(av[2], bw[q][2], acc0);
@@ -1240,7 +1247,8 @@ constexpr int B2_CHUNK = 7;  // samples per weight-grad block (7: LDS <= 40 KB -
 constexpr int B2_ICG = 10;   // input-channel pairs per sample in the dgrad part
 // LDS of a dgrad block: R1 = max(W2 slice [52][68] + stage 1000, T [64][65])
 // + R2 = dY2 [64][52] (c2_dgrad_block)
-constexpr int B2_LDS_FLOATS = ((52 * 68 + 1000) > 64 * 65 ? (52 * 68 + 1000) : 64 * 65) + 64 * 52;
+constexpr int B2_DLD = 68;  // dY^T row stride (64 positions + 4): conflict-free writes and GEMM reads
+constexpr int B2_LDS_FLOATS = ((52 * 68 + 1000) > 64 * 65 ? (52 * 68 + 1000) : 64 * 65) + C2 * B2_DLD;
 
 // Recursive-halving wave reduction of 26 (padded to 32) per-lane sums: at
 // each step a lane keeps half of its live accumulators (chosen by its lane
@@ -1392,7 +1400,7 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
   // (31.5 KB in all: 5 blocks per CU):
   //   R1: W2 slice [52][68] + grads/codes stage  -> after the GEMM: T [64][65]
   //       -> after col2im: the conv1 wave partials
-  //   R2: expanded dY2 [64][52]                  -> after the GEMM: input
+  //   R2: expanded dY2^T [50][68]               -> after the GEMM: input
   //       image [784] + conv1 codes [2][144] (held in registers until then)
   //       + d(a1p) of the two channels [288]
   constexpr int R1 = (52 * WLD + F1IN + F1IN / 4) > 64 * TLD ? (52 * WLD + F1IN + F1IN / 4) : 64 * TLD;
@@ -1444,15 +1452,15 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
   {
     const float* gst = gstage;
     const uint8_t* cst = reinterpret_cast<const uint8_t*>(gstage + F1IN);
-    for (int e = tid; e < 64 * 52; e += 256) {
-      const int pos = e / 52, oc = e - pos * 52;
-      float v = 0.f;
-      if (oc < C2) {
-        const int oh = pos >> 3, ow = pos & 7;
-        const int gi = oc * 16 + (oh >> 1) * 4 + (ow >> 1);
-        v = (cst[gi] == ((oh & 1) * 2 + (ow & 1))) ? gst[gi] : 0.f;
-      }
-      dys[e] = v;
+    // dY^T [oc][pos]: lanes run over positions, so the 32 lanes of a
+    // ds_read group read 8 distinct (grad, code) words (broadcast) and write
+    // consecutive floats (the [pos][oc] order read gst at a 16-float stride:
+    // 16-way bank conflicts)
+    for (int e = tid; e < C2 * 64; e += 256) {
+      const int oc = e >> 6, pos = e & 63;
+      const int oh = pos >> 3, ow = pos & 7;
+      const int gi = oc * 16 + (oh >> 1) * 4 + (ow >> 1);
+      dys[oc * B2_DLD + pos] = (cst[gi] == ((oh & 1) * 2 + (ow & 1))) ? gst[gi] : 0.f;
     }
   }
   __syncthreads();
@@ -1466,7 +1474,7 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
         // K tail (k = 48..51): one k per lane group, so 4 MFMAs instead of
         // 16 with three quarters of their K padding
         const int k = 48 + gg;
-        const float a = dys[(wv * 16 + r) * 52 + k];
+        const float a = k < C2 ? dys[k * B2_DLD + wv * 16 + r] : 0.f;
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[q] = mfma16x16x4(a, ws[k * WLD + q * 16 + r], acc[q]);
         break;
@@ -1475,7 +1483,7 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int k = 16 * k0 + 4 * gg + j;
-        av[j] = k < 52 ? dys[(wv * 16 + r) * 52 + k] : 0.f;
+        av[j] = k < C2 ? dys[k * B2_DLD + wv * 16 + r] : 0.f;
 #pragma unroll
         for (int q = 0; q < 4; ++q) bv[q][j] = k < 52 ? ws[k * WLD + q * 16 + r] : 0.f;
       }
