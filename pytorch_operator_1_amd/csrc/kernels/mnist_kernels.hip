@@ -1341,12 +1341,16 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
     for (int q = 0; q < NVG; ++q) {
       const int e = tid + 256 * q;
       if (e < CH * (F1IN / 4)) {
-        // XOR-swizzled float4 slots: row oc's quad G lives at G ^ ((oc >> 1) & 3),
-        // so the 16 lanes of a K-group that read the same (pp) of 16
-        // consecutive channels hit 8 bank quads instead of 2 (8-way -> 2-way)
+        // XOR-swizzled slots.  Grads: row oc's quad G lives at G ^ ((oc >> 1) & 3)
+        // and, for oc bit 3 set, its two halves are swapped, so the 32 lanes
+        // of a read group (16 channels x 2 k-slots) hit 32 distinct banks.
+        // Codes: the dword of (oc, G) lives at G ^ ((oc >> 3) & 1), so
+        // channels oc and oc + 8 land in different banks.
         const int smp = e / (F1IN / 4), r = e - smp * (F1IN / 4), oc_ = r >> 2;
-        reinterpret_cast<float4*>(gs)[smp * (F1IN / 4) + (oc_ << 2) + ((r & 3) ^ ((oc_ >> 1) & 3))] = vg[q];
-        reinterpret_cast<uint32_t*>(cs)[e] = vc[q];
+        const float4 v = vg[q];
+        reinterpret_cast<float4*>(gs)[smp * (F1IN / 4) + (oc_ << 2) + ((r & 3) ^ ((oc_ >> 1) & 3))] =
+            ((oc_ >> 3) & 1) ? float4{v.z, v.w, v.x, v.y} : v;
+        reinterpret_cast<uint32_t*>(cs)[smp * (F1IN / 4) + (oc_ << 2) + ((r & 3) ^ ((oc_ >> 3) & 1))] = vc[q];
       }
     }
   }
@@ -1360,8 +1364,9 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
 #pragma unroll
     for (int G = 0; G < 4; ++G) {
       const int pp = 4 * G + g;
-      const float gv = ocvalid ? gs[smp * F1IN + goff + ((G ^ ((oc >> 1) & 3)) << 2) + g] : 0.f;
-      const int cd = ocvalid ? (int)cs[smp * F1IN + goff + pp] : 4;
+      const float gv = ocvalid ? gs[smp * F1IN + goff + ((G ^ ((oc >> 1) & 3)) << 2) + (g ^ (((oc >> 3) & 1) << 1))]
+                               : 0.f;
+      const int cd = ocvalid ? (int)cs[smp * F1IN + goff + ((G ^ ((oc >> 3) & 1)) << 2) + g] : 4;
       const float* ap = ap0 + 2 * (pp >> 2) * 12 + 2 * (pp & 3);
       const float bv0 = kvalid ? ap[0] : 0.f, bv1 = kvalid ? ap[1] : 0.f;
       const float bv2 = kvalid ? ap[12] : 0.f, bv3 = kvalid ? ap[13] : 0.f;
@@ -1879,6 +1884,7 @@ struct BwdAllArgs {
   int* pending;
   int B, nA, nB, nC, nD, nF, ktail;
   int skip;  // timing probes only (PTO_BWD_ALL_SKIP): 1 = no conv1 wgrad, 4 = no conv2 tile SGD
+  int order;  // block-range order (PTO_BWD_ORDER): 0 wgrad,dgrad,dW1; 1 dgrad,wgrad,dW1; 2 wgrad,dW1,dgrad
   // conv1 grads are accumulated into nrep replicas (sample b -> b % nrep;
   // replica 0 = gw1/gb1, replica r >= 1 at c1rep + (r-1)*rep_stride, same
   // layout as the flat conv1 range: weights at 0, bias at bias_off), so
@@ -1956,9 +1962,16 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
     return;
   }
   bid -= A.nF;
+  if (A.order == 1) {  // dgrad range dispatched before the wgrad range
+    if (bid < A.nB) bid += A.nA;
+    else if (bid < A.nB + A.nA) bid -= A.nB;
+  } else if (A.order == 2) {  // wgrad, dW1, dgrad
+    if (bid >= A.nA && bid < A.nA + A.nD) bid += A.nB;
+    else if (bid >= A.nA + A.nD && bid < A.nA + A.nD + A.nB) bid -= A.nD;
+  }
   if (bid < A.nA) {
     c2_wgrad_block<CH>(bid, smem, A.g2, A.code2, A.a1p, A.g2w, A.B);
-    if (A.grads_only) return;
+    if (A.grads_only || (A.skip & 1024)) return;  // 1024: timing probe, no arrival / tile SGD
     // arrival: every lane's atomics have been performed at the memory side
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -2536,6 +2549,11 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
     return e ? atoi(e) : 0;
   }();
   A.skip = skip;
+  static const int order = [] {
+    const char* e = getenv("PTO_BWD_ORDER");
+    return e ? atoi(e) : 0;
+  }();
+  A.order = order;
   A.ktail |= ((skip >> 6) & 3) << 8;  // 64: no conv1 loop, 128: no conv1 atomics
   if (skip & 2) A.nD = 0;
   if (skip & 8) A.nB = 0;
