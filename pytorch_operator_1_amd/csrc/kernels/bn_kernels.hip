@@ -93,20 +93,22 @@ __global__ __launch_bounds__(BN_T) void k_bn_stats(const uint16_t* __restrict__ 
   const int tpr = C >> 3, rpi = BN_T / tpr, tid = threadIdx.x, rsub = tid / tpr, c8 = (tid - rsub * tpr) * 8;
   float s[8] = {}, q[8] = {};
   const long long r0 = (long long)blockIdx.x * iters * rpi + rsub;
-  const V8 zero{};
   for (int it = 0; it < iters; it += BN_U) {  // BN_U independent 16-byte loads in flight
     V8 a[BN_U];
+    bool ok[BN_U];
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
+    for (int u = 0; u < BN_U; ++u) {  // unconditional loads (row 0 when out of range), masked below
       const long long row = r0 + (long long)(it + u) * rpi;
-      a[u] = (it + u < iters && row < M) ? load8(x + row * C + c8) : zero;
+      ok[u] = it + u < iters && row < M;
+      a[u] = load8(x + (ok[u] ? row : 0) * C + c8);
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        s[j] += a[u].v[j];
-        q[j] = fmaf(a[u].v[j], a[u].v[j], q[j]);
+        const float v = ok[u] ? a[u].v[j] : 0.f;
+        s[j] += v;
+        q[j] = fmaf(v, v, q[j]);
       }
   }
   block_combine(s, q, C, red, part + (long long)blockIdx.x * 2 * C, part + (long long)blockIdx.x * 2 * C + C);
@@ -174,34 +176,37 @@ __global__ __launch_bounds__(BN_FT) void k_bn_finalize(const float* __restrict__
   }
 }
 
-// y = [relu](x * scale + shift [+ res]); two vectors per thread iteration
-// (independent loads in flight).
+// y = [relu](x * scale + shift [+ res]); EW_U vectors per thread iteration,
+// all loads issued before the first use (RES/RELU are template parameters,
+// out-of-range slots load vector 0 and are not stored).
+constexpr int EW_U = 4;
+template <bool RES, bool RELU>
 __global__ __launch_bounds__(BN_T) void k_bn_apply(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                    uint16_t* __restrict__ y, long long n8, int C,
-                                                   const float* __restrict__ stat, int relu) {
+                                                   const float* __restrict__ stat) {
   const float* scale = stat + 2 * C;
   const float* shift = stat + 3 * C;
   const long long stride = (long long)gridDim.x * BN_T;
-  for (long long i0 = (long long)blockIdx.x * BN_T + threadIdx.x; i0 < n8; i0 += 2 * stride) {
-    V8 a[2], r[2];
-    const long long ii[2] = {i0, i0 + stride};
+  for (long long i0 = (long long)blockIdx.x * BN_T + threadIdx.x; i0 < n8; i0 += EW_U * stride) {
+    V8 a[EW_U], r[EW_U];
+    long long ii[EW_U];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (ii[u] < n8) {
-        a[u] = load8(x + ii[u] * 8);
-        if (res) r[u] = load8(res + ii[u] * 8);
-      }
+    for (int u = 0; u < EW_U; ++u) {
+      ii[u] = i0 + u * stride;
+      const long long k = ii[u] < n8 ? ii[u] : 0;
+      a[u] = load8(x + k * 8);
+      if (RES) r[u] = load8(res + k * 8);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < EW_U; ++u) {
       if (ii[u] >= n8) continue;
       const int c0 = (int)((ii[u] * 8) & (C - 1));  // C is a power of two
       const V8 sc = loadf8(scale + c0), sh = loadf8(shift + c0);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float v = fmaf(a[u].v[j], sc.v[j], sh.v[j]);
-        if (res) v += r[u].v[j];
-        a[u].v[j] = relu ? fmaxf(v, 0.f) : v;
+        if (RES) v += r[u].v[j];
+        a[u].v[j] = RELU ? fmaxf(v, 0.f) : v;
       }
       store8(y + ii[u] * 8, a[u]);
     }
@@ -212,10 +217,14 @@ __global__ __launch_bounds__(BN_T) void k_bn_apply(const uint16_t* __restrict__ 
 // mode 0: no ReLU; 1: ReLU, mask recomputed from x (x*scale+shift > 0);
 // 2: ReLU after a residual add, mask = (y > 0), and g is stored (it is also
 // the gradient of the residual input).
+// MODE is a template parameter so every load of an unrolled group is
+// issued before the first use (a runtime mode branch between them split the
+// group); the row bound is clamped instead of predicated for the same reason.
+template <int MODE>
 __global__ __launch_bounds__(BN_T) void k_bn_bwd_reduce(const uint16_t* __restrict__ dy,
                                                         const uint16_t* __restrict__ x,
                                                         const uint16_t* __restrict__ y, long long M, int C,
-                                                        int iters, const float* __restrict__ stat, int mode,
+                                                        int iters, const float* __restrict__ stat,
                                                         uint16_t* __restrict__ g_out, float* __restrict__ part) {
   __shared__ float red[4096];
   const int tpr = C >> 3, rpi = BN_T / tpr, tid = threadIdx.x, rsub = tid / tpr, c8 = (tid - rsub * tpr) * 8;
@@ -223,31 +232,35 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_reduce(const uint16_t* __restri
   const V8 sc = loadf8(stat + 2 * C + c8), sh = loadf8(stat + 3 * C + c8);
   float s[8] = {}, q[8] = {};
   const long long r0 = (long long)blockIdx.x * iters * rpi + rsub;
-  constexpr int U = BN_U / 2;  // two (three) streams per row
-  const V8 zero{};
+  constexpr int U = MODE == 2 ? BN_U / 2 : BN_U;  // 16-byte loads in flight: 2-3 streams x U rows
   for (int it = 0; it < iters; it += U) {
     V8 g[U], a[U], yv[U];
+    bool ok[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long row = r0 + (long long)(it + u) * rpi;
-      const bool ok = it + u < iters && row < M;
-      const long long o = row * C + c8;
-      g[u] = ok ? load8(dy + o) : zero;
-      a[u] = ok ? load8(x + o) : zero;
-      if (mode == 2) yv[u] = ok ? load8(y + o) : zero;
+      ok[u] = it + u < iters && row < M;
+      const long long o = (ok[u] ? row : 0) * C + c8;  // row 0 when out of range: in bounds, masked below
+      g[u] = load8(dy + o);
+      a[u] = load8(x + o);
+      if (MODE == 2) yv[u] = load8(y + o);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (mode == 1) {
+      if (!ok[u]) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[u].v[j] = 0.f, a[u].v[j] = 0.f;
+      }
+      if (MODE == 1) {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (!(fmaf(a[u].v[j], sc.v[j], sh.v[j]) > 0.f)) g[u].v[j] = 0.f;
-      } else if (mode == 2) {
+      } else if (MODE == 2) {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (!(yv[u].v[j] > 0.f)) g[u].v[j] = 0.f;
         const long long row = r0 + (long long)(it + u) * rpi;
-        if (it + u < iters && row < M) store8(g_out + row * C + c8, g[u]);
+        if (ok[u]) store8(g_out + row * C + c8, g[u]);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -282,29 +295,30 @@ __global__ __launch_bounds__(BN_FT) void k_bn_bwd_finalize(const float* __restri
 }
 
 // dx = k1 * g + k2 * x + k3 with g = dy (mode 0), dy * relu-mask recomputed
-// from x (mode 1) or the stored g (mode 2, passed as gsrc); two vectors per
-// thread iteration.
+// from x (mode 1) or the stored g (mode 2, passed as gsrc); EW_U vectors per
+// thread iteration, loads first.
+template <int MODE>
 __global__ __launch_bounds__(BN_T) void k_bn_bwd_apply(const uint16_t* __restrict__ gsrc,
                                                        const uint16_t* __restrict__ x, uint16_t* __restrict__ dx,
                                                        long long n8, int C, const float* __restrict__ stat,
-                                                       const float* __restrict__ coef, int mode) {
+                                                       const float* __restrict__ coef) {
   const long long stride = (long long)gridDim.x * BN_T;
-  for (long long i0 = (long long)blockIdx.x * BN_T + threadIdx.x; i0 < n8; i0 += 2 * stride) {
-    V8 g[2], a[2];
-    const long long ii[2] = {i0, i0 + stride};
+  for (long long i0 = (long long)blockIdx.x * BN_T + threadIdx.x; i0 < n8; i0 += EW_U * stride) {
+    V8 g[EW_U], a[EW_U];
+    long long ii[EW_U];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (ii[u] < n8) {
-        g[u] = load8(gsrc + ii[u] * 8);
-        a[u] = load8(x + ii[u] * 8);
-      }
+    for (int u = 0; u < EW_U; ++u) {
+      ii[u] = i0 + u * stride;
+      const long long k = ii[u] < n8 ? ii[u] : 0;
+      g[u] = load8(gsrc + k * 8);
+      a[u] = load8(x + k * 8);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < EW_U; ++u) {
       if (ii[u] >= n8) continue;
       const int c0 = (int)((ii[u] * 8) & (C - 1));  // C is a power of two
       const V8 k1 = loadf8(coef + c0), k2 = loadf8(coef + C + c0), k3 = loadf8(coef + 2 * C + c0);
-      if (mode == 1) {
+      if (MODE == 1) {
         const V8 sc = loadf8(stat + 2 * C + c0), sh = loadf8(stat + 3 * C + c0);
 #pragma unroll
         for (int j = 0; j < 8; ++j)
@@ -348,7 +362,7 @@ void bn_grid(long long M, int C, int* nblk, int* iters) {
 }
 
 int elementwise_blocks(long long n8) {
-  long long b = (n8 + BN_T * 4 - 1) / (BN_T * 4);  // ~4 vectors per thread
+  long long b = (n8 + BN_T * EW_U - 1) / (BN_T * EW_U);  // ~EW_U vectors per thread
   if (b > 8192) b = 8192;
   return (int)(b < 1 ? 1 : b);
 }
@@ -379,9 +393,10 @@ PTO_API int pto_bn_fwd(const void* x, const void* res, void* y, long long M, int
   hipLaunchKernelGGL(k_bn_finalize, dim3((C + 31) / 32), dim3(BN_FT), 0, s, scratch, nblk, M, C, gamma, beta,
                      eps, momentum, run_mean, run_var, nbt, stat);
   const long long n8 = M * C / 8;
-  hipLaunchKernelGGL(k_bn_apply, dim3(elementwise_blocks(n8)), dim3(BN_T), 0, s,
-                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(res),
-                     reinterpret_cast<uint16_t*>(y), n8, C, stat, relu);
+  auto* ka = res ? (relu ? k_bn_apply<true, true> : k_bn_apply<true, false>)
+                 : (relu ? k_bn_apply<false, true> : k_bn_apply<false, false>);
+  hipLaunchKernelGGL(ka, dim3(elementwise_blocks(n8)), dim3(BN_T), 0, s, reinterpret_cast<const uint16_t*>(x),
+                     reinterpret_cast<const uint16_t*>(res), reinterpret_cast<uint16_t*>(y), n8, C, stat);
   return (int)hipGetLastError();
 }
 
@@ -394,15 +409,16 @@ PTO_API int pto_bn_bwd(const void* dy, const void* x, const void* y, void* dx, v
   if ((((uintptr_t)dy) | ((uintptr_t)x) | ((uintptr_t)dx) | ((uintptr_t)y) | ((uintptr_t)g_out)) & 15) return -1;
   int nblk, iters;
   bn_grid(M, C, &nblk, &iters);
-  hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(nblk), dim3(BN_T), 0, s, reinterpret_cast<const uint16_t*>(dy),
+  auto* kr = mode == 0 ? k_bn_bwd_reduce<0> : (mode == 1 ? k_bn_bwd_reduce<1> : k_bn_bwd_reduce<2>);
+  hipLaunchKernelGGL(kr, dim3(nblk), dim3(BN_T), 0, s, reinterpret_cast<const uint16_t*>(dy),
                      reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(y), M, C, iters, stat,
-                     mode, reinterpret_cast<uint16_t*>(g_out), scratch);
+                     reinterpret_cast<uint16_t*>(g_out), scratch);
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 31) / 32), dim3(BN_FT), 0, s, scratch, nblk, M, C, gamma,
                      stat, dgamma, dbeta, coef);
   const long long n8 = M * C / 8;
   const void* gsrc = mode == 2 ? g_out : dy;
-  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(elementwise_blocks(n8)), dim3(BN_T), 0, s,
-                     reinterpret_cast<const uint16_t*>(gsrc), reinterpret_cast<const uint16_t*>(x),
-                     reinterpret_cast<uint16_t*>(dx), n8, C, stat, coef, mode);
+  auto* kb = mode == 1 ? k_bn_bwd_apply<1> : k_bn_bwd_apply<0>;  // mode 2 applies like 0 (g stored)
+  hipLaunchKernelGGL(kb, dim3(elementwise_blocks(n8)), dim3(BN_T), 0, s, reinterpret_cast<const uint16_t*>(gsrc),
+                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<uint16_t*>(dx), n8, C, stat, coef);
   return (int)hipGetLastError();
 }
