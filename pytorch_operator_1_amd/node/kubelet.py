@@ -453,6 +453,12 @@ class Kubelet:
         # zygote-forked ones must use the classic store (node/zygote.py), and
         # a libuv server with classic clients was seen to hang the rendezvous
         env.setdefault("USE_LIBUV", "0")
+        # every replica runs on this node and the rendezvous address is
+        # 127.0.0.1: gloo's transport binds to the loopback device directly
+        # instead of resolving the machine's hostname (on a box whose
+        # resolver times out, every rank of a 4-replica job was seen stuck in
+        # the ProcessGroupGloo constructor for minutes)
+        env.setdefault("GLOO_SOCKET_IFNAME", "lo")
         env["PTO_POD_NAME"] = name_of(pod)
         env["PTO_NAMESPACE"] = namespace_of(pod)
         env["PTO_JOB_NAME"] = (pod["metadata"].get("labels") or {}).get(C.LABEL_JOB_NAME, "")

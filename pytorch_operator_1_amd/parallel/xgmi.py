@@ -155,6 +155,31 @@ class XgmiAllReduce:
         """Device error word (synchronises with the current stream)."""
         return int(self.err.item())
 
+    def poll(self):
+        """Non-blocking check: raise :class:`XgmiTimeout` for the error word
+        captured by the PREVIOUS poll (by now long complete on the device),
+        then enqueue a copy of the current one into pinned host memory.  A
+        failure therefore surfaces one call later than with :meth:`check`,
+        but the host never waits for the device here."""
+        if not hasattr(self, "_poll_buf"):
+            self._poll_buf = torch.zeros(2, dtype=self.err.dtype, pin_memory=True)
+            self._poll_ev = [None, None]
+            self._poll_i = 0
+        prev = self._poll_i ^ 1
+        if self._poll_ev[prev] is not None:
+            self._poll_ev[prev].synchronize()
+            self._poll_ev[prev] = None
+            e = int(self._poll_buf[prev])
+            if e:
+                raise XgmiTimeout(f"xGMI all-reduce barrier timed out after {self.timeout_ms} ms "
+                                  f"(phase mask {e}): a peer rank died or stalled")
+        i = self._poll_i
+        self._poll_buf[i:i + 1].copy_(self.err.view(-1)[:1], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._poll_ev[i] = ev
+        self._poll_i = prev
+
     def check(self):
         e = self.error_word()
         if e:

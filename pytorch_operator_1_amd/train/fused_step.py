@@ -691,13 +691,16 @@ class FusedMnistTrainer:
             self.graph_mode = "split"
             self._capture()
 
-    def run(self, n: int):
+    def run(self, n: int, blocking_check: bool = True):
         """Run exactly ``n`` training steps: the largest captured multi-step
         graphs first (n // unroll replays of the unroll-step graph, then one
         replay per set bit of the remainder), then check the gradient
         transport's error word (a dead or stalled xGMI peer raises
         :class:`~pytorch_operator_1_amd.parallel.xgmi.XgmiTimeout` here, at
-        most one chunk after it happened)."""
+        most one chunk after it happened).  ``blocking_check=False``: the
+        check does not wait for this chunk (it reads the word captured after
+        the previous chunk), so a training loop keeps the device busy while
+        it logs."""
         if n <= 0:
             return
         if self.graph_mode == "full":
@@ -722,14 +725,32 @@ class FusedMnistTrainer:
                     n -= k
         for _ in range(n):
             self.step()
-        self.check_comm()
+        self.check_comm(blocking_check)
 
-    def check_comm(self):
+    def check_comm(self, blocking: bool = True):
         """Raise if the xGMI all-reduce reported a barrier timeout (no-op for
         RCCL/gloo, whose failures raise from the collective itself).
-        Synchronises with the device when xGMI is in use."""
+        Synchronises with the device when xGMI is in use, unless
+        ``blocking=False`` (then the word of the previous call is checked)."""
         if self._xgmi is not None:
-            self._xgmi.check()
+            if blocking:
+                self._xgmi.check()
+            else:
+                self._xgmi.poll()
+
+    def loss_async(self):
+        """Mean loss of the last step, copied into pinned host memory without
+        waiting: returns ``(host_tensor, event)``; read the tensor after
+        ``event.synchronize()``."""
+        if getattr(self, "_loss_host", None) is None:
+            self._loss_host = torch.zeros(2, dtype=torch.float32, pin_memory=True)
+            self._loss_i = 0
+        buf = self._loss_host[self._loss_i:self._loss_i + 1]
+        self._loss_i ^= 1
+        buf.copy_(self.loss_rows.mean().view(1), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        return buf, ev
 
     @property
     def needs_host_barrier(self) -> bool:

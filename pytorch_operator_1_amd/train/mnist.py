@@ -142,6 +142,10 @@ def run_with_retryable_exit(fn, *a, **kw):
 
 
 def main(argv=None):
+    if os.environ.get("PTO_FAULTHANDLER"):  # debugging: SIGUSR2 dumps every thread's stack (exec'd replicas too)
+        import faulthandler
+
+        faulthandler.register(signal.SIGUSR2, all_threads=True)
     return run_with_retryable_exit(_main, argv)
 
 
@@ -261,41 +265,75 @@ def _main(argv=None):
     first = True
     trace = torch_trace(args.profile, rank)
     prof_step = trace.__enter__()
+    # Log lines are pipelined on the fused trainer: the loss of a log chunk
+    # is copied to pinned memory without waiting, the next chunk is
+    # enqueued, and only then is the line printed (its copy is done by then
+    # and the device is already running the next chunk), so logging every
+    # 10 steps costs no device idle time.  samples/s is measured between
+    # consecutive resolved log points.
+    loss_async = getattr(trainer, "loss_async", None) if device.type == "cuda" else None
+    pending = []
+
+    def resolve():
+        nonlocal samples_since, t_last
+        for rec in pending:
+            ep, bi, st, n_samples, lv = rec
+            if isinstance(lv, tuple):
+                lv[1].synchronize()
+                lv = float(lv[0])
+            now = time.time()
+            samples_since += n_samples
+            dt = max(now - t_last, 1e-9)
+            sps = samples_since / dt
+            step_s = dt * args.batch_size / max(samples_since, 1)
+            samples_since, t_last = 0, now
+            print("Train Epoch: {} [{}/{} ({:.0f}%)]\tloss={:.4f}".format(
+                ep, bi * args.batch_size, dataset_len, 100.0 * bi / loader_len, lv))
+            metrics.emit(event="train", step=st, loss=lv, samples_per_sec=round(sps * world, 1),
+                         step_seconds=step_s, rank=rank)
+            if writer:
+                writer.add_scalar("loss", lv, ep * n_batches + bi)
+        pending.clear()
+
+    unlogged = 0  # samples run since the last queued log record
     while step < total_steps:
         if fail_at and step == fail_at:
+            resolve()
             print(f"[fault-injection] rank {rank} SIGKILL at step {step}", flush=True)
             os.kill(os.getpid(), signal.SIGKILL)
         epoch = step // n_batches + 1
         shuffler.set_epoch(epoch)
         # steps up to the next log / checkpoint / epoch / fault boundary in
         # one call: the fused trainer replays its multi-step HIP graphs and
-        # checks the gradient transport's error word once per chunk
+        # checks the gradient transport's error word once per chunk (without
+        # waiting for the chunk when a log line is all that follows it)
         k = 1
         while step + k < total_steps and not boundary(step + k):
             k += 1
-        run(k)
+        s_next = step + k
+        hard = (s_next >= total_steps or s_next % n_batches == 0 or s_next == fail_at or bool(args.profile)
+                or bool(args.checkpoint_dir and args.checkpoint_interval and s_next % args.checkpoint_interval == 0))
+        if loss_async is not None and not first and not hard:
+            run(k, blocking_check=False)
+        else:
+            run(k)
+        resolve()  # the previous chunk's log line: its loss copy finished before this chunk started
         prof_step()
         step += k
-        samples_since += args.batch_size * k
+        unlogged += args.batch_size * k
         batch_idx = (step - 1) % n_batches
         if first:
             if device.type == "cuda":
                 torch.cuda.synchronize(device)
             metrics.emit(event="first_step", t=time.time(), rank=rank)
             first = False
+            t_last = time.time()
         if batch_idx % args.log_interval == 0:
-            loss = trainer.last_loss()
-            now = time.time()
-            dt = max(now - t_last, 1e-9)
-            sps = samples_since / dt
-            step_s = dt * args.batch_size / max(samples_since, 1)
-            samples_since, t_last = 0, now
-            print("Train Epoch: {} [{}/{} ({:.0f}%)]\tloss={:.4f}".format(
-                epoch, batch_idx * args.batch_size, dataset_len, 100.0 * batch_idx / loader_len, loss))
-            metrics.emit(event="train", step=step, loss=loss, samples_per_sec=round(sps * world, 1),
-                         step_seconds=step_s, rank=rank)
-            if writer:
-                writer.add_scalar("loss", loss, epoch * n_batches + batch_idx)
+            lv = loss_async() if loss_async is not None else trainer.last_loss()
+            pending.append((epoch, batch_idx, step, unlogged, lv))
+            unlogged = 0
+            if hard or loss_async is None:
+                resolve()
         ckpt_due = bool(args.checkpoint_dir and args.checkpoint_interval and step % args.checkpoint_interval == 0)
         if ckpt_due and rank == 0:
             ckpt.save(args.checkpoint_dir, step, {"trainer": trainer.state_dict(), "rng": ckpt.rng_state()})
@@ -317,6 +355,7 @@ def _main(argv=None):
             # chunk until every rank is done with its host work
             pdist.host_barrier()
         sys.stdout.flush()
+    resolve()
     trace.__exit__(None, None, None)
     if writer:
         writer.close()
