@@ -237,6 +237,7 @@ def _stall_worker(rank, world, port, q):
         ar.allreduce_sgd_(0, n, **kw)  # one healthy step first
         torch.cuda.synchronize(dev)
         ar.check()
+        ar.poll()  # non-blocking check: captures the (clean) word for the next poll
         _fill(buf, rank, 2)
         snap = [t.clone() for t in (p, m, buf)]
         dist.barrier()
@@ -259,12 +260,20 @@ def _stall_worker(rank, world, port, q):
         ar.allreduce_sgd_(0, n, **kw)
         torch.cuda.synchronize(dev)
         after = time.perf_counter() - t1
-        q.put((rank, elapsed, unchanged, raised, after))
+        # poll() reports the word captured by the PREVIOUS poll: clean, then the failure
+        polls = []
+        for _ in range(2):
+            try:
+                ar.poll()
+                polls.append("ok")
+            except XgmiTimeout:
+                polls.append("raise")
+        q.put((rank, elapsed, unchanged, raised, after, polls))
         dist.barrier()
         ar.close()
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001
-        q.put((rank, repr(e), False, False, None))
+        q.put((rank, repr(e), False, False, None, None))
         raise
 
 
@@ -278,9 +287,10 @@ def test_xgmi_timeout_fails_fast_without_updates():
     res = sorted(q.get(timeout=240) for _ in range(2))
     for p in ps:
         p.join(60)
-    for rank, elapsed, unchanged, raised, after in res:
+    for rank, elapsed, unchanged, raised, after, polls in res:
         assert not isinstance(elapsed, str), elapsed
         assert raised, (rank, "error word not set")
+        assert polls == ["ok", "raise"], (rank, polls)
         assert unchanged, (rank, "params/momentum/grads written by a failed all-reduce")
         assert after < 0.1, (rank, after)
     # rank 0: one 300 ms timeout for 8 launches, not one per barrier
