@@ -74,7 +74,8 @@ constexpr int AR_MAX_RANKS = 8;
 constexpr int AR_MAX_BLOCKS = 64;
 constexpr int AR_CHANNELS = 2;
 constexpr int AR_THREADS = 512;
-constexpr int AR_MAX_REP = 16;  // gradient replicas folded before barrier 1
+constexpr int AR_MAX_REP = 256;  // gradient replicas folded before barrier 1 (launcher check)
+constexpr int AR_REP_CHUNK = 16;  // replica loads in flight at once
 constexpr long long AR_ONESHOT_MAX = 65536;  // floats (256 KB): one-shot path
 constexpr long long AR_TICKS_PER_MS = 100000LL;  // wall_clock64 runs at 100 MHz
 long long g_timeout_ticks = 500 * AR_TICKS_PER_MS;  // pto_ar_set_timeout_ms
@@ -158,16 +159,18 @@ struct ArSgd {
 __device__ __forceinline__ void fold_rep(const ArSgd& f, float* g, long long fi) {
   if (!f.rep || f.nrep <= 1 || fi < f.rep_from || fi >= f.rep_from + f.rep_stride) return;
   const long long k = fi - f.rep_from;
-  float4 v[AR_MAX_REP - 1];
-#pragma unroll
-  for (int r = 0; r < AR_MAX_REP - 1; ++r)
-    v[r] = *reinterpret_cast<const float4*>(f.rep + (long long)min(r, f.nrep - 2) * f.rep_stride + k);
   float4 a = *reinterpret_cast<const float4*>(g + fi);
+  for (int r0 = 0; r0 < f.nrep - 1; r0 += AR_REP_CHUNK) {  // replica order
+    float4 v[AR_REP_CHUNK];
 #pragma unroll
-  for (int r = 0; r < AR_MAX_REP - 1; ++r) {
-    if (r >= f.nrep - 1) break;
-    a.x += v[r].x; a.y += v[r].y; a.z += v[r].z; a.w += v[r].w;
-    *reinterpret_cast<float4*>(f.rep + (long long)r * f.rep_stride + k) = float4{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < AR_REP_CHUNK; ++r)
+      v[r] = *reinterpret_cast<const float4*>(f.rep + (long long)min(r0 + r, f.nrep - 2) * f.rep_stride + k);
+#pragma unroll
+    for (int r = 0; r < AR_REP_CHUNK; ++r) {
+      if (r0 + r >= f.nrep - 1) break;
+      a.x += v[r].x; a.y += v[r].y; a.z += v[r].z; a.w += v[r].w;
+      *reinterpret_cast<float4*>(f.rep + (long long)(r0 + r) * f.rep_stride + k) = float4{0.f, 0.f, 0.f, 0.f};
+    }
   }
   *reinterpret_cast<float4*>(g + fi) = a;
 }

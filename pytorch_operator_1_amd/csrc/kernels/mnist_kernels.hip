@@ -77,7 +77,8 @@ struct LazyConv1 {
   const float* rep;     // extra gradient replicas (k_bwd_all): g + sum_r rep[r*rep_stride + i], r < nrep-1
   int nrep, rep_stride;
 };
-constexpr int C1_MAXREP = 16;  // max conv1 gradient replicas (launchers check)
+constexpr int C1_MAXREP = 256;  // max conv1 gradient replicas (launchers check)
+constexpr int REP_CHUNK = 16;   // replica loads the readers keep in flight at once
 struct Conv1Commit {
   float* p;             // flat conv1 range [0, n) of params / grads / momentum
   float* g;
@@ -99,15 +100,17 @@ PTO_DEV void commit4(const Conv1Commit& cm, int i, float lr) {
     return;
   }
   float4 gs = *reinterpret_cast<const float4*>(cm.g + i);
-  float4 v[C1_MAXREP - 1];  // every replica load in flight before the first add
+  for (int r0 = 0; r0 < cm.nrep - 1; r0 += REP_CHUNK) {
+    float4 v[REP_CHUNK];  // a chunk of replica loads in flight before the first add
 #pragma unroll
-  for (int r = 0; r < C1_MAXREP - 1; ++r)
-    v[r] = *reinterpret_cast<const float4*>(cm.rep + (size_t)min(r, cm.nrep - 2) * cm.rep_stride + i);
+    for (int r = 0; r < REP_CHUNK; ++r)
+      v[r] = *reinterpret_cast<const float4*>(cm.rep + (size_t)min(r0 + r, cm.nrep - 2) * cm.rep_stride + i);
 #pragma unroll
-  for (int r = 0; r < C1_MAXREP - 1; ++r) {
-    if (r >= cm.nrep - 1) break;
-    gs.x += v[r].x; gs.y += v[r].y; gs.z += v[r].z; gs.w += v[r].w;
-    *reinterpret_cast<float4*>(cm.rep + (size_t)r * cm.rep_stride + i) = float4{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < REP_CHUNK; ++r) {
+      if (r0 + r >= cm.nrep - 1) break;
+      gs.x += v[r].x; gs.y += v[r].y; gs.z += v[r].z; gs.w += v[r].w;
+      *reinterpret_cast<float4*>(cm.rep + (size_t)(r0 + r) * cm.rep_stride + i) = float4{0.f, 0.f, 0.f, 0.f};
+    }
   }
   float4 pv = *reinterpret_cast<float4*>(cm.p + i);
   float4 mv = *reinterpret_cast<float4*>(cm.m + i);
@@ -120,18 +123,20 @@ PTO_DEV void commit4(const Conv1Commit& cm, int i, float lr) {
   *reinterpret_cast<float4*>(cm.g + i) = float4{0.f, 0.f, 0.f, 0.f};
 }
 
-// Sum of the nrep-1 extra conv1 gradient replicas at index i (0 if !live).
-// All C1_MAXREP-1 loads are issued before the first add (clamped addresses,
-// branch-free): a runtime-bound loop here compiled to one dependent memory
-// round trip per replica, ~1 us of F12's critical path at nrep = 8.
+// Sum of the nrep-1 extra conv1 gradient replicas at index i (0 if !live),
+// in replica order.  REP_CHUNK loads are issued before the first add
+// (clamped addresses, branch-free): a plain runtime-bound loop compiled to
+// one dependent memory round trip per replica, ~1 us of F12's critical path
+// at nrep = 8.
 PTO_DEV float rep_sum(const float* __restrict__ rep, int nrep, int stride, int i, bool live) {
-  if (nrep <= 1) return 0.f;
-  float v[C1_MAXREP - 1];
-#pragma unroll
-  for (int r = 0; r < C1_MAXREP - 1; ++r) v[r] = rep[(size_t)min(r, nrep - 2) * stride + i];
   float s = 0.f;
+  for (int r0 = 0; r0 < nrep - 1; r0 += REP_CHUNK) {
+    float v[REP_CHUNK];
 #pragma unroll
-  for (int r = 0; r < C1_MAXREP - 1; ++r) s += (live && r < nrep - 1) ? v[r] : 0.f;
+    for (int r = 0; r < REP_CHUNK; ++r) v[r] = rep[(size_t)min(r0 + r, nrep - 2) * stride + i];
+#pragma unroll
+    for (int r = 0; r < REP_CHUNK; ++r) s += (live && r0 + r < nrep - 1) ? v[r] : 0.f;
+  }
   return s;
 }
 
@@ -1292,7 +1297,8 @@ PTO_DEV void wave_halving26(const float acc[26], int lane, float* out) {
 // fp32 atomics into gw2.
 template <int CH>
 PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, const uint8_t* __restrict__ code2,
-                            const float* __restrict__ a1p, float* __restrict__ gw2, int B) {
+                            const float* __restrict__ a1p, float* __restrict__ gw2, int B,
+                            float* __restrict__ part = nullptr) {
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // ---- part A: weight gradient.  ONE staging round: the block's K-tile
   // (16 (ic,kh,kw) columns) touches at most 2 input channels, so for all 8
@@ -1381,7 +1387,12 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
   for (int rr = 0; rr < 4; ++rr) {
     const int m = wv * 16 + (lane >> 4) * 4 + rr;
     const int n = nt * 16 + (lane & 15);
-    if (m < C2 && n < 500) atomicAdd(gw2 + m * 500 + n, acc[rr]);
+    if (m < C2 && n < 500) {
+      if (part)  // deterministic mode: this chunk's partial tile, summed in chunk order by the last arriver
+        part[(bid / 32) * (C2 * 500) + m * 500 + n] = acc[rr];
+      else
+        atomicAdd(gw2 + m * 500 + n, acc[rr]);
+    }
   }
 }
 
@@ -1606,8 +1617,13 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
   if (tid < 52 && !(ktail & 512)) {
     const int icl = tid / 26, k = tid - icl * 26, oc1 = icg * 2 + icl;
     const float v = part[(2 * icl) * 26 + k] + part[(2 * icl + 1) * 26 + k];
-    if (k < 25) atomicAdd(gw1 + oc1 * 25 + k, v);
-    else atomicAdd(gb1 + oc1, v);
+    if (ktail & 2048) {  // deterministic mode: one slot per sample, every element written once
+      if (k < 25) gw1[oc1 * 25 + k] = v;
+      else gb1[oc1] = v;
+    } else {
+      if (k < 25) atomicAdd(gw1 + oc1 * 25 + k, v);
+      else atomicAdd(gb1 + oc1, v);
+    }
   }
 }
 
@@ -1885,6 +1901,11 @@ struct BwdAllArgs {
   int B, nA, nB, nC, nD, nF, ktail;
   int skip;  // timing probes only (PTO_BWD_ALL_SKIP): 1 = no conv1 wgrad, 4 = no conv2 tile SGD
   int order;  // block-range order (PTO_BWD_ORDER): 0 wgrad,dgrad,dW1; 1 dgrad,wgrad,dW1; 2 wgrad,dW1,dgrad
+  // deterministic mode (wpart != nullptr): no floating-point atomics.  The
+  // conv2 wgrad chunks store partial tiles into wpart[chunk] and the last
+  // arriver per tile sums them in chunk order; conv1 grads go to one
+  // replica per sample (nrep == B), each element stored once.
+  float* wpart;
   // conv1 grads are accumulated into nrep replicas (sample b -> b % nrep;
   // replica 0 = gw1/gb1, replica r >= 1 at c1rep + (r-1)*rep_stride, same
   // layout as the flat conv1 range: weights at 0, bias at bias_off), so
@@ -1970,28 +1991,51 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
     else if (bid >= A.nA + A.nD && bid < A.nA + A.nD + A.nB) bid -= A.nD;
   }
   if (bid < A.nA) {
-    c2_wgrad_block<CH>(bid, smem, A.g2, A.code2, A.a1p, A.g2w, A.B);
-    if (A.grads_only || (A.skip & 1024)) return;  // 1024: timing probe, no arrival / tile SGD
+    const bool det = A.wpart != nullptr;
+    c2_wgrad_block<CH>(bid, smem, A.g2, A.code2, A.a1p, A.g2w, A.B, A.wpart);
+    if ((A.grads_only && !det) || (A.skip & 1024)) return;  // 1024: timing probe, no arrival / tile SGD
     // arrival: every lane's atomics have been performed at the memory side
+    // (deterministic mode: the partial-tile stores are written back first)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int nt = bid % 32, nchunk = A.nA / 32;
     if (threadIdx.x == 0) {
+      if (det) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       const int old = __hip_atomic_fetch_add(A.ctr + nt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_last = old == nchunk - 1;
-      if (s_last) __hip_atomic_store(A.ctr + nt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (s_last) {
+        __hip_atomic_store(A.ctr + nt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (det) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
     }
     __syncthreads();
     if (!s_last || (A.skip & 4)) return;
-    const float lr = *A.a.lr;
     int idx[4];
     float gv[4], pv[4], mv[4];
+    if (det) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = threadIdx.x + 256 * q, row = e >> 4, col = nt * 16 + (e & 15);
+        idx[q] = (e < C2 * 16 && col < 500) ? row * 500 + col : -1;
+        float g = 0.f;
+        if (idx[q] >= 0)
+          for (int c = 0; c < nchunk; ++c) g += A.wpart[c * (C2 * 500) + idx[q]];  // chunk order
+        gv[q] = g;
+      }
+      if (A.grads_only) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (idx[q] >= 0) A.g2w[idx[q]] = gv[q];
+        return;
+      }
+    }
+    const float lr = *A.a.lr;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {  // 50 rows x 16 columns = 800 elements
       const int e = threadIdx.x + 256 * q, row = e >> 4, col = nt * 16 + (e & 15);
       idx[q] = (e < C2 * 16 && col < 500) ? row * 500 + col : -1;
       if (idx[q] >= 0) {
-        gv[q] = atomicExch(A.g2w + idx[q], 0.f);
+        if (!det) gv[q] = atomicExch(A.g2w + idx[q], 0.f);
         pv[q] = A.p2w[idx[q]];
         mv[q] = A.m2w[idx[q]];
       }
@@ -2508,9 +2552,10 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
                         long long off_fc1b, long long off_c2w, long long off_c2b, long long off_c1w,
                         long long off_c1b, int* ctr, long long* bidx, long long nbatches, int* pending, int B,
                         const float* lr, float mom, float wd, float gscale, int nesterov, float* c1rep, int nrep,
-                        int rep_stride, int grads_only, hipStream_t s) {
+                        int rep_stride, int grads_only, float* wpart, hipStream_t s) {
   if (!grads_only && (!bidx || !pending || !ctr || nbatches < 1)) return -1;
   if (B < 1 || nrep < 1 || nrep > C1_MAXREP || (nrep > 1 && !c1rep)) return -1;
+  if (wpart && (nrep != B || !ctr)) return -1;  // deterministic mode: one conv1 replica per sample
   BwdAllArgs A;
   A.g2 = g2; A.code2 = code2; A.a1p = a1p; A.w2f = w2f; A.x = x; A.code1 = code1;
   A.gw1 = g + off_c1w; A.gb1 = g + off_c1b;
@@ -2543,12 +2588,13 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   A.nC = (C2 + 3) / 4;
   A.nD = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
   A.nF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9;
-  A.ktail = 3;
+  A.ktail = 3 | (wpart ? 2048 : 0);
   static const int skip = [] {
     const char* e = getenv("PTO_BWD_ALL_SKIP");  // timing probes: parts left out (wrong numerics)
     return e ? atoi(e) : 0;
   }();
   A.skip = skip;
+  A.wpart = wpart;
   static const int order = [] {
     const char* e = getenv("PTO_BWD_ORDER");
     return e ? atoi(e) : 0;

@@ -101,7 +101,7 @@ _SIGS = {
     # fused-optimizer schedule of the single-process MNIST step
     "pto_conv12_fwd_lazy": [_P] * 9 + [_I, _P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _I, _P],
     "pto_conv12_fwd_lazy_x": [_P] * 9 + [_I, _P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _P, _P, _P, _I, _I, _P],
-    "pto_bwd_all": [_P] * 13 + [_L] * 8 + [_P, _P, _L, _P, _I, _P, _F, _F, _F, _I, _P, _I, _I, _I, _P],
+    "pto_bwd_all": [_P] * 13 + [_L] * 8 + [_P, _P, _L, _P, _I, _P, _F, _F, _F, _I, _P, _I, _I, _I, _P, _P],
     "pto_fc2_ce_commit": [_P] * 7 + [_I, _F, _P, _P, _P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _P],
     "pto_conv1_commit": [_P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _P, _I, _I, _P],
     "pto_fc_bwd_adv": [_P] * 10 + [_I, _P, _L, _P, _P],

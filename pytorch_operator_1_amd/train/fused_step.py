@@ -156,6 +156,12 @@ class FusedMnistTrainer:
         self.bwd_all = self.merge_f4 and os.environ.get("PTO_BWD_ALL", "1") == "1"
         self.w2f = torch.empty(50 * 500, device=device) if self.bwd_all else None
         self.c2_ctr = torch.zeros(32, device=device, dtype=torch.int32) if self.bwd_all else None
+        # deterministic mode (PTO_DETERMINISTIC=1): no floating-point atomics
+        # in the backward -- conv2 wgrad chunks store partial tiles summed in
+        # chunk order by the last arriver, conv1 grads one replica per
+        # sample summed in replica order -- so B=64 steps are bitwise
+        # reproducible run to run and across a checkpoint/resume
+        self.deterministic = os.environ.get("PTO_DETERMINISTIC", "0") == "1"
         # multi-GPU step: the same single backward launch in grads-only mode
         # (every gradient into the flat buffer, no parameter touched) after
         # F12 / fc1 / F4dx -> 4 launches + the all-reduce (whose SGD
@@ -167,6 +173,14 @@ class FusedMnistTrainer:
         # before its exchange (multi-GPU; RCCL: 1 replica, see ddp_nrep)
         self.c1_nrep = (min(16, max(1, int(os.environ.get("PTO_C1_REPLICAS", "8"))))
                         if (self.bwd_all or self.ddp_bwd_all) else 1)
+        self.wpart = None
+        if self.deterministic:
+            if not (self.bwd_all or self.ddp_bwd_all) or self.B > 256:
+                raise RuntimeError("PTO_DETERMINISTIC=1 needs the k_bwd_all schedule and batch <= 256")
+            self.c1_nrep = self.B
+            self.wpart = torch.empty(((self.B + 3) // 4) * 50 * 500, device=device)  # >= chunks x conv2.weight
+            if self.c2_ctr is None:
+                self.c2_ctr = torch.zeros(32, device=device, dtype=torch.int32)
         self.c1_stride = self.numel - offs["conv1.weight"][0]
         self.c1rep = torch.zeros(max(1, self.c1_nrep - 1) * self.c1_stride, **f32)
         self.ddp_nrep = 1
@@ -203,6 +217,9 @@ class FusedMnistTrainer:
         self._side = torch.cuda.Stream(device) if self._xgmi is not None else None
         if self.ddp_bwd_all and self._xgmi is not None and self.ar_fused_sgd:
             self.ddp_nrep = self.c1_nrep  # the all-reduce's SGD launch folds them
+        elif self.deterministic and self.ddp:
+            raise RuntimeError("PTO_DETERMINISTIC=1 on several ranks needs the xGMI all-reduce with its SGD "
+                               "epilogue (it folds the per-sample conv1 replicas in order)")
         # graph modes: "full" = the whole step (collectives included) is one
         # HIP graph; "split" = collectives issued eagerly between graphs;
         # "none" = eager launches.  The xGMI kernel and RCCL all-reduces are
@@ -370,7 +387,7 @@ class FusedMnistTrainer:
                             self.grads.data_ptr(), self.mom.data_ptr(), *o, _lib.ptr(self.c2_ctr),
                             None if go else bi, self.n_batches, None if go else self.pending.data_ptr(), B,
                             *self._opt_args(), self.c1rep.data_ptr(), self.ddp_nrep if go else self.c1_nrep, self.c1_stride,
-                            int(go), s), "bwd_all")
+                            int(go), _lib.ptr(self.wpart), s), "bwd_all")
             return
         if self.merge_f4:  # + B3's all-row reductions (dW2, db1, db2)
             c(L.pto_conv2_bwd_fc(self.da2p.data_ptr(), self.code2.data_ptr(), self.a1p.data_ptr(),

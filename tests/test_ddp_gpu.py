@@ -33,6 +33,9 @@ def _worker(rank, world, port, q, comm):
     if comm == "xgmi-overlap":  # fc bucket on a side stream under the conv backward, conv bucket after
         comm = "xgmi"
         os.environ["PTO_COMM_OVERLAP"] = "1"
+    if comm == "xgmi-det":  # deterministic backward: per-sample conv1 replicas folded by the all-reduce
+        comm = "xgmi"
+        os.environ["PTO_DETERMINISTIC"] = "1"
     import torch.distributed as dist
 
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
@@ -56,7 +59,7 @@ def _worker(rank, world, port, q, comm):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("comm", ["rccl", "xgmi", "xgmi-sgd-launch", "xgmi-overlap"])
+@pytest.mark.parametrize("comm", ["rccl", "xgmi", "xgmi-sgd-launch", "xgmi-overlap", "xgmi-det"])
 def test_fused_ddp_two_ranks_matches_reference(comm):
     """comm=rccl: host collectives (gloo here) between split graphs;
     comm=xgmi: one peer-memory all-reduce of the whole buffer with the SGD

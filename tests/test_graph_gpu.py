@@ -183,3 +183,43 @@ def test_bwd_all_matches_separate_launches(monkeypatch, B):
     offs = __import__("pytorch_operator_1_amd.models.mnist", fromlist=["param_offsets"]).param_offsets()[0]
     c2 = offs["conv2.weight"][0]
     assert float(g[c2:c2 + 25000].abs().max()) == 0.0  # consumed gradients re-zeroed
+
+
+def test_deterministic_mode_b64_bitwise_and_resume(monkeypatch):
+    """PTO_DETERMINISTIC=1: no floating-point atomics in k_bwd_all (conv2
+    wgrad partial tiles summed in chunk order by the last arriver, conv1
+    grads one replica per sample summed in replica order).  At B=64 two runs
+    are bitwise identical, a checkpoint/resume in the middle reproduces the
+    uninterrupted run bit for bit, and the trajectory matches the default
+    (atomic) schedule within fp32 reordering noise."""
+    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+
+    dev = torch.device("cuda", 0)
+    kw = dict(batch_size=64, dataset_size=64 * 9, seed=4, unroll=4)
+    monkeypatch.setenv("PTO_DETERMINISTIC", "1")
+
+    a = FusedMnistTrainer(dev, **kw)
+    assert a.deterministic and a.c1_nrep == 64 and a.wpart is not None
+    a.run(10)
+    b = FusedMnistTrainer(dev, **kw)
+    b.run(10)
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params), "two deterministic runs differ"
+    assert torch.equal(a.mom, b.mom)
+
+    c = FusedMnistTrainer(dev, **kw)
+    c.run(4)
+    sd = c.state_dict()
+    d = FusedMnistTrainer(dev, **kw)
+    d.load_state_dict(sd)
+    d.run(6)
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, d.params), "resume from step 4 diverged from the uninterrupted run"
+    assert int(a.c2_ctr.abs().sum().item()) == 0  # counters re-armed
+
+    monkeypatch.setenv("PTO_DETERMINISTIC", "0")
+    e = FusedMnistTrainer(dev, **kw)
+    e.run(10)
+    torch.cuda.synchronize()
+    for name in a.p:
+        assert rel(a.p[name], e.p[name]) < 2e-4, name
