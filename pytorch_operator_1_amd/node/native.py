@@ -9,6 +9,7 @@ long-running daemon.
 """
 from __future__ import annotations
 
+import fcntl
 import json
 import os
 import shutil
@@ -25,17 +26,28 @@ BIN = os.path.join(PKG_DIR, "_lib", "pto-node-agent")
 def build(force: bool = False, verbose: bool = False, sanitize: bool = False) -> str:
     out = BIN + ("-san" if sanitize else "")
     deps = [SRC, os.path.join(os.path.dirname(SRC), "json.hpp")]
-    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
+    def fresh() -> bool:
+        return os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps)
+
+    if not force and fresh():
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cxx = os.environ.get("CXX") or shutil.which("g++") or "c++"
-    cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-o", out + ".tmp", SRC]
-    if sanitize:
-        cmd[1:1] = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
-    os.replace(out + ".tmp", out)
+    # Concurrent builders (pytest-xdist workers) serialise on a lock file and
+    # each writes its own temp name, so nobody execs a half-written binary
+    # ("Text file busy") or renames another builder's output.
+    with open(out + ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not force and fresh():
+            return out
+        tmp = f"{out}.tmp{os.getpid()}"
+        cxx = os.environ.get("CXX") or shutil.which("g++") or "c++"
+        cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-o", tmp, SRC]
+        if sanitize:
+            cmd[1:1] = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        os.replace(tmp, out)
     return out
 
 
