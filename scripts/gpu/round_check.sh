@@ -11,6 +11,6 @@ grep -E "passed|failed|submit ->" gpurun_out/pytest_gpu.log | tail -5
 timeout -k 10 200 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || { tail -20 gpurun_out/bench_default.err; exit 1; }
 cat gpurun_out/bench_default.json
 R="$GRAFT_REPO_ROOT"
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_fused" -o run -- python3 "$R/bench.py" --steps 200 --warmup 20 > "$R/gpurun_out/fused_prof.log" 2>&1
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_fused" -o run -- python3 "$R/bench.py" --steps 200 --warmup 20 --no-latency > "$R/gpurun_out/fused_prof.log" 2>&1
 python3 "$R/tools/rocprof_summary.py" "$R/gpurun_out/prof_fused" --top 12
 echo done
