@@ -157,6 +157,7 @@ class ShardedCheckpointer:
                                                                 barrier_timeout_s))
         self._thread = None
         self._error = None
+        self.resumed_from = None
 
     # ---------------------------------------------------------------- save
     def save(self, step: int, tensors: dict[str, torch.Tensor], meta: dict | None = None):
@@ -218,7 +219,20 @@ class ShardedCheckpointer:
         not exist before the first step).  Every rank reads its own shard;
         each tensor is then broadcast from its owner.  Returns the manifest
         (``step``, ``meta``) or None when there is nothing to resume."""
-        path = path or self.latest()
+        import torch.distributed as dist
+
+        dist_on = self.world > 1 and dist.is_available() and dist.is_initialized()
+        if path is None:
+            path = self.latest()
+            if dist_on:
+                # rank 0's choice for everyone: a replica restarted early can
+                # otherwise see an older committed step than one whose save
+                # was still committing, and the ranks would resume at
+                # different steps (mismatched collectives)
+                box = [path]
+                dist.broadcast_object_list(box, src=0)
+                path = box[0]
+        self.resumed_from = path
         if path is None:
             return None
         with open(os.path.join(path, "manifest.json")) as f:
@@ -230,9 +244,6 @@ class ShardedCheckpointer:
         if self.world == 1 or any(t["owner"] == self.rank for t in man["tensors"].values()):
             shard = torch.load(os.path.join(path, man["shards"][self.rank]), map_location="cpu",
                                weights_only=True)
-        import torch.distributed as dist
-
-        dist_on = self.world > 1 and dist.is_available() and dist.is_initialized()
         for name in sorted(man["tensors"]):
             info = man["tensors"][name]
             dst = tensors.get(name)

@@ -87,7 +87,7 @@ def _main(argv=None):
         if man is not None:
             trainer.after_load(man["meta"])
             start = int(man["step"])
-            print(f"Resumed from {saver.latest()} at step {start}", flush=True)
+            print(f"Resumed from {saver.resumed_from} at step {start}", flush=True)
     fail = args.fail_at_step if (args.fail_at_step and rank == args.fail_rank and start == 0) else 0
     t_last, steps_since = time.time(), 0
     for step in range(start, args.steps):

@@ -116,3 +116,46 @@ def test_keep_prunes_old_steps(tmp_path, keep):
         ck.save(step, {"a": torch.full((4,), float(step))})
     ck.close()
     assert [int(p.rsplit("-", 1)[1]) for p in list_sharded(str(tmp_path))] == [3 - i for i in range(keep)][::-1]
+
+
+def _agree_worker(rank, port, dirs, out):
+    import torch.distributed as dist
+
+    from pytorch_operator_1_amd.train.checkpoint import ShardedCheckpointer
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    try:
+        ck = ShardedCheckpointer(dirs[rank], rank, 2)
+        dst = {"a": torch.zeros(4)}
+        man = ck.load_into(dst)
+        out.put((rank, man["step"], ck.resumed_from, dst["a"].tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_resume_point_is_rank0s_choice(tmp_path):
+    """Ranks whose view of the checkpoint directory differs (rank 1 sees
+    only an older committed step) still resume from ONE step: rank 0's."""
+    import multiprocessing as mp
+
+    from pytorch_operator_1_amd.train.checkpoint import ShardedCheckpointer
+
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    for d, steps in ((a, (1, 2)), (b, (1,))):
+        for r in range(2):
+            ck = ShardedCheckpointer(d, r, 2, async_write=False, barrier=lambda step: None)
+            for s in steps:
+                ck.save(s, {"a": torch.full((4,), float(s))})
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_agree_worker, args=(r, port, [a, b], q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [2, 2]
+    assert res[0][2] == res[1][2] and res[0][2].startswith(a)
+    assert res[1][3] == [2.0] * 4
