@@ -178,7 +178,7 @@ class Kubelet:
         self.extra_env = extra_env or {}
         self.pods: dict[str, PodRuntime] = {}
         self.job_ports: dict[str, int] = {}
-        self._port_locks: list[int] = []  # flock fds of the reserved ports (released at exit)
+        self._port_locks: dict[int, int] = {}  # port -> flock fd of its host-wide reservation
         self.pod_informer = Informer(client, "pods")
         self.svc_informer = Informer(client, "services")
         self.pod_informer.add_event_handler(on_delete=self._on_pod_delete)
@@ -253,6 +253,7 @@ class Kubelet:
             live = {key_of(p) for p in pods}
             for k in [k for k in self.pods if k not in live]:
                 self._teardown(self.pods.pop(k))
+            self._release_job_ports(pods)
 
     def _on_pod_delete(self, pod):
         with self._lock:
@@ -390,9 +391,13 @@ class Kubelet:
                 except FileNotFoundError:
                     pass
 
-    def _job_port(self, pod, wanted: int) -> int:
+    @staticmethod
+    def _job_key(pod) -> str:
         job = (pod["metadata"].get("labels") or {}).get(C.LABEL_JOB_NAME) or name_of(pod)
-        jk = f"{namespace_of(pod)}/{job}"
+        return f"{namespace_of(pod)}/{job}"
+
+    def _job_port(self, pod, wanted: int) -> int:
+        jk = self._job_key(pod)
         if jk in self.job_ports:
             return self.job_ports[jk]
         used = set(self.job_ports.values())
@@ -401,11 +406,27 @@ class Kubelet:
             if port not in used and _port_free(port):
                 fd = _reserve_port(port)
                 if fd is not None:
-                    self._port_locks.append(fd)
+                    self._port_locks[port] = fd
                     break
             port += 1
         self.job_ports[jk] = port
         return port
+
+    def _release_job_ports(self, pods):
+        """Give back the virtual master port (and its host-wide lock) of every
+        job that no longer has a pod on this node.  A job keeps its port while
+        any of its pods exists, so a replica restarted next to live peers
+        gets the port they rendezvous on; a job whose pods are all gone (or
+        re-submitted later) takes a fresh reservation."""
+        live = {self._job_key(p) for p in pods}
+        for jk in [jk for jk in self.job_ports if jk not in live]:
+            port = self.job_ports.pop(jk)
+            fd = self._port_locks.pop(port, None)
+            if fd is not None:
+                try:
+                    os.close(fd)  # drops the flock
+                except OSError:
+                    pass
 
     def _resolve_env(self, pod, c, rt) -> dict:
         env = {k: v for k, v in os.environ.items() if not k.startswith(("MASTER_", "RANK", "WORLD_SIZE",

@@ -117,3 +117,27 @@ def test_training_gauges_scraped_for_finished_gloo_job(tmp_path):
     assert s2f is not None and 0 < s2f < 120
     assert series['pytorchjob_gpu_hbm_used_bytes{gpu="card1"}'] == float(2 << 30)
     assert series['pytorchjob_gpu_hbm_total_bytes{gpu="card0"}'] == float(288 << 30)
+
+
+def test_job_port_released_after_job_deleted(tmp_path):
+    """A job's virtual master port (and its host-wide lock) is given back
+    once the job's pods are gone, so a long-running node does not walk the
+    port range one job at a time."""
+    import time
+
+    with LocalCluster(gpus=0, log_dir=str(tmp_path)) as c:
+        k = c.kubelet
+        c.submit(new_job("port-a", image="pto/python:rocm", master_args=["-c", "print('ok')"], workers=0, gpus=0))
+        j = c.wait_for_condition("port-a", timeout=60)
+        assert j["status"]["conditions"][-1]["type"] == "Succeeded", j["status"]
+        assert "default/port-a" in k.job_ports
+        port = k.job_ports["default/port-a"]
+        assert port in k._port_locks
+        c.store.delete("pytorchjobs", "default", "port-a")
+        end = time.time() + 30
+        while time.time() < end and "default/port-a" in k.job_ports:
+            time.sleep(0.05)
+        assert "default/port-a" not in k.job_ports and port not in k._port_locks
+        c.submit(new_job("port-b", image="pto/python:rocm", master_args=["-c", "print('ok')"], workers=0, gpus=0))
+        c.wait_for_condition("port-b", timeout=60)
+        assert k.job_ports["default/port-b"] == port  # the same base port is free again
