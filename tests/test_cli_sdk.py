@@ -147,3 +147,18 @@ def test_metrics_exposition(cluster):
                  "pytorch_operator_jobs_deleted_total", "pytorch_operator_jobs_successful_total",
                  "pytorch_operator_jobs_failed_total", "pytorch_operator_jobs_restarted_total"):
         assert name in text
+
+
+def test_sdk_walkthrough_example():
+    """examples/sdk/pytorchjob_sdk.py (the reference notebook's flow:
+    create -> get -> get_job_status -> wait_for_job(watch) ->
+    is_job_succeeded -> get_logs -> delete) on an in-process stack."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "examples", "sdk", "pytorchjob_sdk.py"), "--steps", "20"],
+                       capture_output=True, text=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "succeeded: True" in r.stdout and "deleted" in r.stdout
+    assert "Train Epoch: 1" in r.stdout
