@@ -618,6 +618,201 @@ __global__ __launch_bounds__(NT, 1) void k_attn_bwd_dkdv(const __bf16* __restric
     }
 }
 
+
+// ------------------------------------- dK/dV kernel, producer / consumer
+// Same block (batch, kv head, 128 keys) and query sweep, 8 waves in two
+// roles on the same 4 x 32 keys (wave w and w + 4 share a SIMD):
+//   producers (waves 0-3): S = Q K^T and dP = dO V^T (accumulators
+//     initialised with the row constants), P = exp2(c S'), dS = P dP', and
+//     the bf16 B operands of the dV^T / dK^T products -> LDS;
+//   consumers (waves 4-7): dV^T += dO^T P, dK^T += Q^T dS from those
+//     operands, one step behind.
+// 16 MFMAs per 32-row query slice on each side and no recomputation; the
+// producers' softmax VALU issues beside the consumers' MFMAs on the same
+// SIMD.  Each wave holds either K/V fragments + S/dP or the two
+// accumulators, so the kernel fits 256 registers (two waves per SIMD).
+// One 32-row slice per step; Q/dO tiles in a 3-slot ring (staged for t+1,
+// read by the producers for t and by the consumers for t-1), operands in a
+// 2-slot ring; one barrier per step.
+constexpr int PC_TB = QT * 256;  // one 32 x 128 bf16 tile (bytes)
+constexpr int PC_OPB = NW * 4 * 64 * 16;  // operands of one step: 4 waves x 4 frags x 64 lanes x 16 B
+constexpr int PC_LDS = 3 * 2 * PC_TB + 3 * 2 * QT * 4 + 2 * PC_OPB;
+
+__global__ __launch_bounds__(2 * NT) void k_attn_bwd_dkdv_pc(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                             const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
+                                                             const float* __restrict__ lse, const float* __restrict__ delta,
+                                                             __bf16* __restrict__ dk, __bf16* __restrict__ dv,
+                                                             long long dkv_rs, AttnShape sh) {
+  constexpr int NTH = 2 * NT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // [3 slots][Q tile | dO tile], [3 slots][lse 32 | delta 32], [2 slots][operands]
+  float* rowc = reinterpret_cast<float*>(smem + 3 * 2 * PC_TB);
+  char* opnd = smem + 3 * 2 * PC_TB + 3 * 2 * QT * 4;
+  const int G = sh.H / sh.Hkv;
+  const int nkb = sh.S / KB;
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  int lin = bid;
+  if ((nblk & 7) == 0) lin = (bid & 7) * (nblk >> 3) + (bid >> 3);
+  const int pair = lin / nkb, kbi = lin % nkb;
+  const int b = pair / sh.Hkv, kvh = pair % sh.Hkv;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, hi = lane >> 5, kl = lane & 31;
+  const bool producer = w < NW;  // wave-uniform
+  const int kw = w & (NW - 1);
+  const int kb0 = kbi * KB, key = kb0 + 32 * kw + kl;
+  const long long tok0 = (long long)b * sh.S;
+  const float sl = sh.scale * LOG2E;
+  const float inv_sl = 1.f / sl;
+  const int nqt = (sh.S - kb0) / QT;
+  const int nsteps = G * nqt;
+
+  uint4 rq, rd;
+  float rc = 0.f;
+  auto stage = [&](int s) {
+    const int g = s / nqt, qt = s % nqt, h = kvh * G + g;
+    const long long tok = tok0 + kb0 + (long long)qt * QT;
+    rq = tile_piece_load<NTH>(q + tok * sh.q_rs + (long long)h * HD, sh.q_rs, 0);
+    rd = tile_piece_load<NTH>(dout + tok * sh.o_rs + (long long)h * HD, sh.o_rs, 0);
+    const long long li = ((long long)b * sh.H + h) * sh.S + kb0 + (long long)qt * QT;
+    rc = threadIdx.x < QT ? lse[li + threadIdx.x] : (threadIdx.x < 2 * QT ? delta[li + threadIdx.x - QT] : 0.f);
+  };
+  auto commit = [&](int slot) {
+    char* qtile = smem + slot * 2 * PC_TB;
+    tile_piece_store<NTH>(qtile, 0, rq);
+    tile_piece_store<NTH>(qtile + PC_TB, 0, rd);
+    if (threadIdx.x < 2 * QT) rowc[slot * 2 * QT + threadIdx.x] = rc;
+  };
+  // wave-uniform activity / diagonal of query slice `qt` for this wave's keys
+  auto active = [&](int qt) { return kb0 + qt * QT + QT - 1 >= kb0 + 32 * kw; };
+  auto diagonal = [&](int qt) { return kb0 + qt * QT < kb0 + 32 * kw + 31; };
+
+  auto produce = [&](int t, int tslot, int oslot, const bf16x8* kf, const bf16x8* vf) {
+    const int qt = t % nqt;
+    if (!active(qt)) return;
+    const char* qtile = smem + tslot * 2 * PC_TB;
+    const char* dtile = qtile + PC_TB;
+    const float* lrow = rowc + tslot * 2 * QT;
+    f32x16 sa, pa;
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const float4 l4 = *reinterpret_cast<const float4*>(lrow + 8 * gg + 4 * hi);
+      const float4 d4 = *reinterpret_cast<const float4*>(lrow + QT + 8 * gg + 4 * hi);
+      sa[4 * gg] = -l4.x * inv_sl; sa[4 * gg + 1] = -l4.y * inv_sl;
+      sa[4 * gg + 2] = -l4.z * inv_sl; sa[4 * gg + 3] = -l4.w * inv_sl;
+      pa[4 * gg] = -d4.x; pa[4 * gg + 1] = -d4.y; pa[4 * gg + 2] = -d4.z; pa[4 * gg + 3] = -d4.w;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      sa = mfma(row_operand(qtile, 0, ks), kf[ks], sa);
+      pa = mfma(row_operand(dtile, 0, ks), vf[ks], pa);
+    }
+    if (diagonal(qt)) {
+      const int q0 = kb0 + qt * QT;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qr = q0 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+        if (key > qr) sa[i] = -INFINITY;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = __builtin_amdgcn_exp2f(sa[i] * sl);
+      sa[i] = p;
+      pa[i] = p * pa[i];  // dS
+    }
+    bf16x8* o = reinterpret_cast<bf16x8*>(opnd + oslot * PC_OPB + kw * (4 * 64 * 16)) + lane;
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      float t0[8], t1[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        t0[j] = sa[8 * qs + j];
+        t1[j] = pa[8 * qs + j];
+      }
+      o[64 * qs] = acc_to_operand(t0);        // P fragments 0, 1
+      o[64 * (2 + qs)] = acc_to_operand(t1);  // dS fragments 2, 3
+    }
+  };
+  auto consume = [&](int t, int tslot, int oslot, f32x16* dka, f32x16* dva) {
+    const int qt = t % nqt;
+    if (!active(qt)) return;
+    const char* qtile = smem + tslot * 2 * PC_TB;
+    const char* dtile = qtile + PC_TB;
+    const bf16x8* o = reinterpret_cast<const bf16x8*>(opnd + oslot * PC_OPB + kw * (4 * 64 * 16)) + lane;
+    bf16x8 pf[2], sf[2];
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      pf[qs] = o[64 * qs];
+      sf[qs] = o[64 * (2 + qs)];
+    }
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        dva[db] = mfma(tr_operand(dtile, 16 * qs, 32 * db), pf[qs], dva[db]);
+        dka[db] = mfma(tr_operand(qtile, 16 * qs, 32 * db), sf[qs], dka[db]);
+      }
+  };
+
+  stage(0);
+  commit(0);
+  __syncthreads();
+  // iteration t: stage step t+1, producers step t, consumers step t-1.  The
+  // two roles run separate loops with the same barrier count (nsteps + 1),
+  // so the K/V fragments (producers) and the dK/dV accumulators (consumers)
+  // are never live together.
+  if (producer) {
+    bf16x8 kf[8], vf[8];
+    {
+      const __bf16* kr = k + (tok0 + key) * sh.k_rs + (long long)kvh * HD + 8 * hi;
+      const __bf16* vr = v + (tok0 + key) * sh.v_rs + (long long)kvh * HD + 8 * hi;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        kf[ks] = *reinterpret_cast<const bf16x8*>(kr + 16 * ks);
+        vf[ks] = *reinterpret_cast<const bf16x8*>(vr + 16 * ks);
+      }
+    }
+    int ts = 0;  // tile slot of step t (t mod 3)
+    for (int t = 0; t <= nsteps; ++t) {
+      const int tn = ts == 2 ? 0 : ts + 1;
+      if (t + 1 < nsteps) stage(t + 1);
+      if (t < nsteps) produce(t, ts, t & 1, kf, vf);
+      if (t + 1 < nsteps) commit(tn);
+      __syncthreads();
+      ts = tn;
+    }
+    return;
+  }
+  f32x16 dka[4], dva[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    dka[db] = (f32x16){};
+    dva[db] = (f32x16){};
+  }
+  int ts = 0;
+  for (int t = 0; t <= nsteps; ++t) {
+    const int tn = ts == 2 ? 0 : ts + 1;
+    const int tp = ts == 0 ? 2 : ts - 1;
+    if (t + 1 < nsteps) stage(t + 1);
+    if (t >= 1) consume(t - 1, tp, (t - 1) & 1, dka, dva);
+    if (t + 1 < nsteps) commit(tn);
+    __syncthreads();
+    ts = tn;
+  }
+  // consumers: dK^T / dV^T, lane = key, registers = d (32db + 8g + 4hi + 0..3)
+  __bf16* dkr = dk + (tok0 + key) * dkv_rs + (long long)kvh * HD + 4 * hi;
+  __bf16* dvr = dv + (tok0 + key) * dkv_rs + (long long)kvh * HD + 4 * hi;
+  const float c = sh.scale;
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      u32x2 pk = {pack2(dka[db][4 * g] * c, dka[db][4 * g + 1] * c), pack2(dka[db][4 * g + 2] * c, dka[db][4 * g + 3] * c)};
+      *reinterpret_cast<u32x2*>(dkr + 32 * db + 8 * g) = pk;
+      u32x2 pv = {pack2(dva[db][4 * g], dva[db][4 * g + 1]), pack2(dva[db][4 * g + 2], dva[db][4 * g + 3])};
+      *reinterpret_cast<u32x2*>(dvr + 32 * db + 8 * g) = pv;
+    }
+}
+
 }  // namespace
 
 #define PTO_API extern "C" __attribute__((visibility("default")))
@@ -678,6 +873,17 @@ static void launch_attn_dq(const void* q, const void* k, const void* v, const vo
                      (__bf16*)dq, dqkv_rs, sh);
 }
 
+// dK/dV kernel: PTO_ATTN_DKDV_PC=1 -> k_attn_bwd_dkdv_pc (8 waves, producer /
+// consumer roles), 0 -> k_attn_bwd_dkdv (4 waves, one wave per SIMD).
+static bool attn_dkdv_pc() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PTO_ATTN_DKDV_PC");
+    v = e ? (atoi(e) != 0) : 1;
+  }
+  return v != 0;
+}
+
 PTO_API int pto_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H,
                          int Hkv, long long q_rs, long long k_rs, long long v_rs, long long o_rs, float scale,
                          hipStream_t s) {
@@ -707,9 +913,20 @@ PTO_API int pto_attn_bwd(const void* q, const void* k, const void* v, const void
   const long long rows = (long long)B * S * H;
   hipLaunchKernelGGL(k_attn_bwd_delta, dim3((unsigned)((rows + 7) / 8)), dim3(256), 0, s, (const __bf16*)o,
                      (const __bf16*)dout, delta, sh);
-  hipLaunchKernelGGL(k_attn_bwd_dkdv, dim3(B * Hkv * (S / KB)), dim3(NT), 4 * QTB + 2 * 128 * 4, s,
-                     (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta,
-                     (__bf16*)dk, (__bf16*)dv, dqkv_rs, sh);
+  if (attn_dkdv_pc()) {
+    static bool attr2 = false;
+    if (!attr2) {
+      (void)hipFuncSetAttribute((const void*)k_attn_bwd_dkdv_pc, hipFuncAttributeMaxDynamicSharedMemorySize, PC_LDS);
+      attr2 = true;
+    }
+    hipLaunchKernelGGL(k_attn_bwd_dkdv_pc, dim3(B * Hkv * (S / KB)), dim3(2 * NT), PC_LDS, s, (const __bf16*)q,
+                       (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk,
+                       (__bf16*)dv, dqkv_rs, sh);
+  } else {
+    hipLaunchKernelGGL(k_attn_bwd_dkdv, dim3(B * Hkv * (S / KB)), dim3(NT), 4 * QTB + 2 * 128 * 4, s,
+                       (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta,
+                       (__bf16*)dk, (__bf16*)dv, dqkv_rs, sh);
+  }
   if (attn_waves(sh) == 8)
     launch_attn_dq<8>(q, k, v, dout, lse, delta, dq, dqkv_rs, sh, s);
   else

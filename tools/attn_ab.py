@@ -42,7 +42,7 @@ def main():
     tb = timed(lambda: torch.autograd.grad(o, a, go, retain_graph=True))
     fl = 4.0 * B * H * S * S * 128 / 2
     g = torch.autograd.grad(o, a, go, retain_graph=True)[0]
-    print(json.dumps({"dkdv_split": os.environ.get("PTO_ATTN_DKDV_SPLIT", "default"), "B": B, "S": S,
+    print(json.dumps({"dkdv_pc": os.environ.get("PTO_ATTN_DKDV_PC", "default"), "B": B, "S": S,
                       "fwd_ms": round(tf, 4), "bwd_ms": round(tb, 4), "fwd_tflops": round(fl / tf / 1e9, 1),
                       "bwd_tflops": round(2.5 * fl / tb / 1e9, 1),
                       "grad_checksum": float(g.float().abs().sum().item())}), flush=True)
