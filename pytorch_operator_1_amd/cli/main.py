@@ -383,6 +383,54 @@ def cmd_crd(args):
     return 0
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def cmd_bench(args):
+    """bench.py (BASELINE metric contract) at one world size or a sweep:
+    N = 1 runs it directly, N > 1 under ``torch.distributed.run`` (one rank
+    per GPU, rendezvous on 127.0.0.1) -- the driver's launch lines.  Each run
+    is a child process; its JSON line is printed, and for a sweep a table of
+    aggregate / per-GPU throughput and weak-scaling efficiency against the
+    smallest N follows."""
+    import json
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    bench = os.path.join(root, "bench.py")
+    if not os.path.exists(bench):
+        print(f"pto bench: {bench} not found (run from a source checkout)", file=sys.stderr)
+        return 2
+    sizes = [int(x) for x in args.scale.split(",")] if args.scale else [args.gpus]
+    extra = [a for a in (args.bench_args or []) if a != "--"]
+    rows = []
+    for n in sizes:
+        if n == 1:
+            cmd = [sys.executable, bench, "--gpus", "1"] + extra
+        else:
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                   "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", bench, "--gpus", str(n)] + extra
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{"metric"')]
+        if r.returncode != 0 or not lines:
+            print(f"pto bench: N={n} failed (exit {r.returncode})\n{r.stderr[-2000:]}", file=sys.stderr)
+            return r.returncode or 1
+        print(lines[-1], flush=True)
+        rows.append(json.loads(lines[-1]))
+    if len(rows) > 1:
+        base = rows[0]["value"] / rows[0]["n_gpus"]
+        print(f"{'N':>3} {'value':>14} {'per GPU':>12} {'ms/step':>9} {'efficiency':>10}")
+        for d in rows:
+            per = d["value"] / d["n_gpus"]
+            print(f"{d['n_gpus']:>3} {d['value']:>14,.1f} {per:>12,.1f} {d['ms_per_step']:>9.4f} {per / base:>10.1%}")
+    return 0
+
+
 def main(argv=None):
     p = argparse.ArgumentParser(prog="pto", description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--server", default=None, help="API server URL")
@@ -461,6 +509,12 @@ def main(argv=None):
 
     cr = sub.add_parser("crd", help="print the CRD manifest")
     cr.set_defaults(fn=cmd_crd)
+
+    bn = sub.add_parser("bench", help="run bench.py at one world size or a scaling sweep (e.g. --scale 1,2,4,8)")
+    bn.add_argument("--gpus", type=int, default=1)
+    bn.add_argument("--scale", default=None, help="comma-separated world sizes")
+    bn.add_argument("bench_args", nargs=argparse.REMAINDER, help="passed to bench.py (e.g. -- --steps 200 --cpu)")
+    bn.set_defaults(fn=cmd_bench)
 
     v = sub.add_parser("version")
     v.set_defaults(fn=lambda a: print(version_string()) or 0)

@@ -51,3 +51,18 @@ def test_bench_single_rank_reports_submit_to_first_step():
     assert "error" not in lat, lat
     assert lat["job_state"] == "Succeeded" and lat["zygote_warm"] is True
     assert 0 < d["submit_to_first_step_s"] < 60
+
+
+def test_pto_bench_scaling_sweep_cpu():
+    """`pto bench --scale 1,2` launches bench.py the driver's way (direct at
+    N=1, torch.distributed.run at N>1), prints each JSON line and a
+    weak-scaling table."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "2"
+    cmd = [sys.executable, "-m", "pytorch_operator_1_amd", "bench", "--scale", "1,2", "--", "--cpu", "--steps", "4",
+           "--warmup", "1", "--dataset-size", "640", "--no-latency"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(ln) for ln in out.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert [d["n_gpus"] for d in lines] == [1, 2]
+    assert "efficiency" in out.stdout and "100.0%" in out.stdout
