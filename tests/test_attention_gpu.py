@@ -57,3 +57,38 @@ def test_flash_attention_first_rows_exact_softmax():
     v0 = qkv[0, (H + Hkv) * D:]
     for h in range(H):
         torch.testing.assert_close(o[0, h * D:(h + 1) * D], v0, atol=1e-2, rtol=1e-2)
+
+
+_DKDV_CHILD = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[2])
+from pytorch_operator_1_amd.ops import llm
+torch.manual_seed(0)
+B, S, H, Hkv = 2, 512, 8, 2
+qkv = torch.randn(B * S, (H + 2 * Hkv) * 128, device="cuda", dtype=torch.bfloat16).requires_grad_()
+o = llm.flash_attention(qkv, B, S, H, Hkv)
+torch.manual_seed(1)
+o.backward(torch.randn_like(o))
+torch.save(qkv.grad.cpu(), sys.argv[1])
+"""
+
+
+def test_dkdv_producer_consumer_matches_single_wave_kernel(tmp_path):
+    """The producer/consumer dK/dV kernel (default) and the one-wave-per-SIMD
+    kernel (PTO_ATTN_DKDV_PC=0) accumulate in the same MFMA order: the QKV
+    gradients must be bitwise equal.  The switch is read once per process,
+    hence one child process per kernel."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    grads = []
+    for pc in ("1", "0"):
+        out = str(tmp_path / f"g{pc}.pt")
+        env = dict(os.environ, PTO_ATTN_DKDV_PC=pc)
+        r = subprocess.run([sys.executable, "-c", _DKDV_CHILD, out, root], capture_output=True, text=True,
+                           timeout=300, env=env)
+        assert r.returncode == 0, r.stderr[-2000:]
+        grads.append(torch.load(out, weights_only=True))
+    assert torch.equal(grads[0], grads[1])
