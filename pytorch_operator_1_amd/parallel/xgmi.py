@@ -10,9 +10,11 @@ per-workgroup barriers) instead of an RCCL ring.  Setup is collective:
    and an uncached flag page; handles are exchanged over the process group;
 2. every rank maps all peers; success is agreed with an all-reduce so all
    ranks take the same path;
-3. :meth:`XgmiAllReduce.autotune` checks the result bit-exactly against
-   RCCL and times both on the real bucket sizes (max over ranks); the
-   faster one is kept (``PTO_XGMI_AR=1`` forces xGMI, ``0`` disables it).
+3. :meth:`XgmiAllReduce.autotune` checks the result against RCCL (within
+   1e-5 relative, bit-identical on every rank) and times it against
+   RCCL on the real bucket sizes (max over ranks); the
+   faster one is kept (``PTO_COMM=xgmi`` forces xGMI, ``PTO_COMM=rccl`` disables it,
+   default ``auto``).
 
 The kernel is HIP-graph capturable (all pointers fixed at setup, epochs on
 the device), so the fused MNIST step keeps its whole-step graph.
