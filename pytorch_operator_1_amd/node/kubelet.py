@@ -75,6 +75,7 @@ DEFAULT_IMAGES = {
     "pto/pytorch-sendrecv:rocm": [sys.executable, "-m", "pytorch_operator_1_amd.train.sendrecv"],
     "gcr.io/kubeflow-ci/pytorch-dist-sendrecv-test:1.0": [sys.executable, "-m",
                                                           "pytorch_operator_1_amd.train.sendrecv"],
+    "pto/pytorch-lm:rocm": [sys.executable, "-m", "pytorch_operator_1_amd.train.lm"],
     "pto/bench:rocm": [sys.executable, os.path.join(REPO_ROOT, "bench.py")],
     "pto/python:rocm": [sys.executable],
 }

@@ -115,3 +115,30 @@ def test_clean_pod_policy_running_and_delete_cascade(cluster):
     assert "cleanup-worker-0" not in names and "cleanup-master-0" in names
     cluster.store.delete("pytorchjobs", "default", "cleanup")
     assert not [p for p in cluster.store.list("pods")["items"] if p["metadata"]["labels"].get("job-name") == "cleanup"]
+
+
+def test_llama_manifest_scaled_down_runs_through_operator(cluster, tmp_path):
+    """examples/llama/pytorch_job_llama3_8b.yaml (BASELINE config 4's job
+    shape: ExitCode restarts, sharded checkpoints, pto/pytorch-lm:rocm image)
+    with the model, replica count and resources scaled to a CPU: Master=1
+    Worker=1 on gloo, llama3-tiny, a checkpoint mid-run."""
+    import yaml
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    job = yaml.safe_load(open(os.path.join(root, "examples", "llama", "pytorch_job_llama3_8b.yaml")))
+    job["metadata"]["name"] = "llama-tiny-e2e"
+    ck = str(tmp_path / "ck")
+    specs = job["spec"]["pytorchReplicaSpecs"]
+    specs["Worker"]["replicas"] = 1
+    for spec in specs.values():
+        c = spec["template"]["spec"]["containers"][0]
+        assert c["image"] == "pto/pytorch-lm:rocm" and spec["restartPolicy"] == "ExitCode"
+        c["args"] = ["--no-cuda", "--backend", "gloo", "--model", "llama3-tiny", "--seq-len", "64", "--steps", "6",
+                     "--log-interval", "2", "--checkpoint-dir", ck, "--checkpoint-interval", "3"]
+        c.pop("resources")
+    cluster.submit(job)
+    j = cluster.wait_for_condition("llama-tiny-e2e", timeout=240)
+    assert j["status"]["conditions"][-1]["type"] == "Succeeded", j["status"]
+    log0 = cluster.pod_log("default", "llama-tiny-e2e-master-0")
+    assert "step 6/6" in log0 and "final_loss=" in log0
+    assert os.path.exists(os.path.join(ck, "step-000000003", "manifest.json"))
