@@ -88,6 +88,7 @@ _EFFECTIVE_KEYS = ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE", "LOCAL_RA
                    "HIP_VISIBLE_DEVICES", "PTO_MASTER_SERVICE", "PTO_MASTER_PORT_REQUESTED")
 GPU_VISIBILITY_MODES = ("node", "isolated")
 NODE_ADDRESS = "127.0.0.1"
+PORT_QUARANTINE_S = float(os.environ.get("PTO_PORT_QUARANTINE_S", "60"))
 
 
 def _port_free(port: int) -> bool:
@@ -180,6 +181,7 @@ class Kubelet:
         self.pods: dict[str, PodRuntime] = {}
         self.job_ports: dict[str, int] = {}
         self._port_locks: dict[int, int] = {}  # port -> flock fd of its host-wide reservation
+        self._quarantine: dict[int, float] = {}  # released port -> time it may be reused
         self.pod_informer = Informer(client, "pods")
         self.svc_informer = Informer(client, "services")
         self.pod_informer.add_event_handler(on_delete=self._on_pod_delete)
@@ -401,7 +403,7 @@ class Kubelet:
         jk = self._job_key(pod)
         if jk in self.job_ports:
             return self.job_ports[jk]
-        used = set(self.job_ports.values())
+        used = set(self.job_ports.values()) | set(self._quarantine)
         port = wanted
         while True:
             if port not in used and _port_free(port):
@@ -418,10 +420,16 @@ class Kubelet:
         job that no longer has a pod on this node.  A job keeps its port while
         any of its pods exists, so a replica restarted next to live peers
         gets the port they rendezvous on; a job whose pods are all gone (or
-        re-submitted later) takes a fresh reservation."""
+        re-submitted later) takes a fresh reservation.  A released port stays
+        locked and out of use for ``PORT_QUARANTINE_S`` (processes of deleted
+        pods may still be shutting down with connections to it; a new job's
+        rendezvous store on the same port must not see them)."""
         live = {self._job_key(p) for p in pods}
+        now = time.time()
         for jk in [jk for jk in self.job_ports if jk not in live]:
-            port = self.job_ports.pop(jk)
+            self._quarantine[self.job_ports.pop(jk)] = now + PORT_QUARANTINE_S
+        for port in [p for p, t in self._quarantine.items() if t <= now]:
+            del self._quarantine[port]
             fd = self._port_locks.pop(port, None)
             if fd is not None:
                 try:
