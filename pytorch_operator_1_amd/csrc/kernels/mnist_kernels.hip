@@ -123,13 +123,15 @@ PTO_DEV void commit4(const Conv1Commit& cm, int i, float lr) {
   *reinterpret_cast<float4*>(cm.g + i) = float4{0.f, 0.f, 0.f, 0.f};
 }
 
-// Sum of the nrep-1 extra conv1 gradient replicas at index i (0 if !live),
-// in replica order.  REP_CHUNK loads are issued before the first add
-// (clamped addresses, branch-free): a plain runtime-bound loop compiled to
-// one dependent memory round trip per replica, ~1 us of F12's critical path
-// at nrep = 8.
-PTO_DEV float rep_sum(const float* __restrict__ rep, int nrep, int stride, int i, bool live) {
-  float s = 0.f;
+// s0 + the nrep-1 extra conv1 gradient replicas at index i (s0 if !live),
+// added one by one in replica order starting from the primary slot s0 --
+// the association commit4 and the xGMI fold use, so the lazily applied and
+// the committed update are bit-identical (deterministic resume).  REP_CHUNK
+// loads are issued before the first add (clamped addresses, branch-free): a
+// plain runtime-bound loop compiled to one dependent memory round trip per
+// replica, ~1 us of F12's critical path at nrep = 8.
+PTO_DEV float rep_sum(const float* __restrict__ rep, int nrep, int stride, int i, bool live, float s0) {
+  float s = s0;
   for (int r0 = 0; r0 < nrep - 1; r0 += REP_CHUNK) {
     float v[REP_CHUNK];
 #pragma unroll
@@ -315,8 +317,8 @@ __global__ __launch_bounds__(256) void k_conv12_fwd(const float* __restrict__ x,
       for (int q = 0; q < 3; ++q) {
         const int e = tid + 256 * q;
         const int fi = e < C1 * 25 ? e : lz.bias_off + (e - C1 * 25);
-        float gsum = e < C1 * 26 ? lz.g[fi] : 0.f;
-        gsum += rep_sum(lz.rep, lz.nrep, lz.rep_stride, e < C1 * 26 ? fi : 0, e < C1 * 26);
+        const float gsum = rep_sum(lz.rep, lz.nrep, lz.rep_stride, e < C1 * 26 ? fi : 0, e < C1 * 26,
+                                   e < C1 * 26 ? lz.g[fi] : 0.f);
         gq[q] = gsum;
         mq[q] = e < C1 * 26 ? lz.m[fi] : 0.f;
       }
@@ -464,8 +466,8 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
       for (int q = 0; q < QW1; ++q) {
         const int e = tid + NTH * q;
         const int fi = e < C1 * 25 ? e : lz.bias_off + (e - C1 * 25);
-        float gsum = e < C1 * 26 ? lz.g[fi] : 0.f;
-        gsum += rep_sum(lz.rep, lz.nrep, lz.rep_stride, e < C1 * 26 ? fi : 0, e < C1 * 26);
+        const float gsum = rep_sum(lz.rep, lz.nrep, lz.rep_stride, e < C1 * 26 ? fi : 0, e < C1 * 26,
+                                   e < C1 * 26 ? lz.g[fi] : 0.f);
         gq[q] = gsum;
         mq[q] = e < C1 * 26 ? lz.m[fi] : 0.f;
       }

@@ -20,6 +20,8 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -164,7 +166,7 @@ def synthetic_mnist(n: int, device, seed: int = 1, dtype=torch.float32):
     numpy twin produces the bit-identical set.
     """
     device = torch.device(device)
-    if device.type == "cuda":
+    if device.type == "cuda" and os.environ.get("PTO_SYNTH_HOST") != "1":
         from ..ops import _lib
 
         imgs = torch.empty((n, 1, 28, 28), device=device, dtype=torch.float32)

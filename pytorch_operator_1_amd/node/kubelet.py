@@ -126,6 +126,7 @@ def _reserve_port(port: int):
 class PodRuntime:
     def __init__(self, pod):
         self.key = key_of(pod)
+        self.job_key = Kubelet._job_key(pod)
         self.uid = pod["metadata"].get("uid")
         self.stage = "admit"  # admit -> init -> run -> done
         self.gpus: list[int] = []
@@ -182,6 +183,7 @@ class Kubelet:
         self.job_ports: dict[str, int] = {}
         self._port_locks: dict[int, int] = {}  # port -> flock fd of its host-wide reservation
         self._quarantine: dict[int, float] = {}  # released port -> time it may be reused
+        self._dying: dict[str, int] = {}  # job -> torn-down pods whose processes are still exiting
         self.pod_informer = Informer(client, "pods")
         self.svc_informer = Informer(client, "services")
         self.pod_informer.add_event_handler(on_delete=self._on_pod_delete)
@@ -270,10 +272,13 @@ class Kubelet:
                 self.agent.kill(pid, signal=15, grace=self.grace)
             except Exception:
                 pass
-        threading.Thread(target=self._reap_later, args=(list(rt.proc_ids), rt.key), daemon=True).start()
+        if rt.proc_ids:
+            with self._lock:
+                self._dying[rt.job_key] = self._dying.get(rt.job_key, 0) + 1
+        threading.Thread(target=self._reap_later, args=(list(rt.proc_ids), rt.key, rt.job_key), daemon=True).start()
         rt.deleted = True
 
-    def _reap_later(self, ids, owner):
+    def _reap_later(self, ids, owner, job_key):
         try:
             end = time.time() + self.grace + 5
             while time.time() < end and not self._stop.is_set():
@@ -286,12 +291,27 @@ class Kubelet:
             self.agent.free(owner)
         except Exception:  # agent already shut down (node stopping)
             pass
+        finally:
+            if ids:
+                with self._lock:
+                    n = self._dying.get(job_key, 0) - 1
+                    if n > 0:
+                        self._dying[job_key] = n
+                    else:
+                        self._dying.pop(job_key, None)
 
     # ------------------------------------------------------------ stages
     def _advance(self, pod, rt: PodRuntime, procs):
         if rt.stage == "done":
             return
         if rt.stage == "admit":
+            # a job's recreated replicas start only once every process of its
+            # deleted ones has exited: a new worker must not rendezvous with
+            # an old master's TCPStore that is still shutting down on the
+            # job's port (the store deletes pods at once; a real kubelet's
+            # graceful deletion gives the same ordering)
+            if self._dying.get(rt.job_key):
+                return
             if not self._admit(pod, rt):
                 return
             rt.stage = "init"
