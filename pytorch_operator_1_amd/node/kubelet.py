@@ -89,6 +89,7 @@ _EFFECTIVE_KEYS = ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE", "LOCAL_RA
 GPU_VISIBILITY_MODES = ("node", "isolated")
 NODE_ADDRESS = "127.0.0.1"
 PORT_QUARANTINE_S = float(os.environ.get("PTO_PORT_QUARANTINE_S", "60"))
+PORT_RELEASE = os.environ.get("PTO_PORT_RELEASE", "1") == "1"
 
 
 def _port_free(port: int) -> bool:
@@ -127,6 +128,7 @@ class PodRuntime:
     def __init__(self, pod):
         self.key = key_of(pod)
         self.job_key = Kubelet._job_key(pod)
+        self.gen = 0  # rendezvous generation (Kubelet._job_port)
         self.uid = pod["metadata"].get("uid")
         self.stage = "admit"  # admit -> init -> run -> done
         self.gpus: list[int] = []
@@ -184,6 +186,9 @@ class Kubelet:
         self._port_locks: dict[int, int] = {}  # port -> flock fd of its host-wide reservation
         self._quarantine: dict[int, float] = {}  # released port -> time it may be reused
         self._dying: dict[str, int] = {}  # job -> torn-down pods whose processes are still exiting
+        self._job_gen: dict[str, int] = {}  # job -> current rendezvous generation
+        self._port_gen: dict[str, int] = {}  # job -> generation of its current port
+        self._old_ports: dict[str, list[int]] = {}  # job -> ports of earlier generations (still reserved)
         self.pod_informer = Informer(client, "pods")
         self.svc_informer = Informer(client, "services")
         self.pod_informer.add_event_handler(on_delete=self._on_pod_delete)
@@ -249,16 +254,24 @@ class Kubelet:
                 k = key_of(pod)
                 rt = self.pods.get(k)
                 if rt is None or rt.uid != pod["metadata"].get("uid"):
-                    if rt is not None:  # same name, new incarnation
-                        self._teardown(rt)
+                    old = rt
+                    if old is not None:  # same name, new incarnation
+                        self._teardown(old)
                     if (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
                         continue  # finished before we knew it (e.g. kubelet restart)
                     rt = self.pods[k] = PodRuntime(pod)
+                    if old is not None:
+                        # a replica recreated after a failure opens the job's
+                        # next rendezvous generation (every replica recreated
+                        # in the same wave lands on the same one)
+                        self._job_gen[rt.job_key] = max(self._job_gen.get(rt.job_key, 0), old.gen + 1)
+                    rt.gen = self._job_gen.get(rt.job_key, 0)
                 self._advance(pod, rt, procs)
             live = {key_of(p) for p in pods}
             for k in [k for k in self.pods if k not in live]:
                 self._teardown(self.pods.pop(k))
-            self._release_job_ports(pods)
+            if PORT_RELEASE:
+                self._release_job_ports(pods)
 
     def _on_pod_delete(self, pod):
         with self._lock:
@@ -419,11 +432,20 @@ class Kubelet:
         job = (pod["metadata"].get("labels") or {}).get(C.LABEL_JOB_NAME) or name_of(pod)
         return f"{namespace_of(pod)}/{job}"
 
-    def _job_port(self, pod, wanted: int) -> int:
+    def _job_port(self, pod, wanted: int, gen: int = 0) -> int:
+        """The job's virtual master port for rendezvous generation ``gen``.
+        Replicas recreated after a failure (ExitCode / backoff restarts)
+        rendezvous on a fresh port: a fast-starting new worker must never
+        reach a TCPStore that an old replica still serves on the previous
+        port (it would hang the new master's store creation).  Ports of
+        earlier generations stay reserved until the job is gone."""
         jk = self._job_key(pod)
-        if jk in self.job_ports:
+        if jk in self.job_ports and self._port_gen.get(jk, 0) >= gen:
             return self.job_ports[jk]
-        used = set(self.job_ports.values()) | set(self._quarantine)
+        if jk in self.job_ports:
+            self._old_ports.setdefault(jk, []).append(self.job_ports[jk])
+        used = (set(self.job_ports.values()) | set(self._quarantine)
+                | {p for ps in self._old_ports.values() for p in ps})
         port = wanted
         while True:
             if port not in used and _port_free(port):
@@ -433,6 +455,7 @@ class Kubelet:
                     break
             port += 1
         self.job_ports[jk] = port
+        self._port_gen[jk] = gen
         return port
 
     def _release_job_ports(self, pods):
@@ -448,6 +471,10 @@ class Kubelet:
         now = time.time()
         for jk in [jk for jk in self.job_ports if jk not in live]:
             self._quarantine[self.job_ports.pop(jk)] = now + PORT_QUARANTINE_S
+            for p in self._old_ports.pop(jk, []):
+                self._quarantine[p] = now + PORT_QUARANTINE_S
+            self._port_gen.pop(jk, None)
+            self._job_gen.pop(jk, None)
         for port in [p for p, t in self._quarantine.items() if t <= now]:
             del self._quarantine[port]
             fd = self._port_locks.pop(port, None)
@@ -479,7 +506,7 @@ class Kubelet:
             env["MASTER_ADDR"] = NODE_ADDRESS
         if "MASTER_PORT" in env:
             env["PTO_MASTER_PORT_REQUESTED"] = env["MASTER_PORT"]
-            env["MASTER_PORT"] = str(self._job_port(pod, int(env["MASTER_PORT"])))
+            env["MASTER_PORT"] = str(self._job_port(pod, int(env["MASTER_PORT"]), rt.gen))
         # GPU pinning (module doc): one process per allocated GPU
         if gpus_requested(c) > 0 or rt.gpus:
             mine = sorted({g // self.gpu_share for g in rt.gpus})  # allocator slot -> device

@@ -115,6 +115,17 @@ def _wait_verbose(c, name, timeout, dump_after=None):
                 raise
             if dump_after and time.time() > start + dump_after and not dumped:
                 dumped = True  # PTO_FAULTHANDLER pods dump every thread's stack on SIGUSR2
+                try:  # who listens where (rendezvous stalls)
+                    import subprocess
+
+                    print(subprocess.run(["ss", "-ltnp"], capture_output=True, text=True, timeout=10).stdout,
+                          flush=True)
+                    for n in _replicas(name):
+                        pod = c.store.get("pods", "default", n)
+                        print(n, (pod["metadata"].get("annotations") or {}).get("pto.amd.com/effective-env"),
+                              flush=True)
+                except Exception as e:  # noqa: BLE001
+                    print(f"listener dump failed: {e}", flush=True)
                 for n in _replicas(name):
                     try:
                         c.kubelet.inject_fault("default", n, signal=12)
