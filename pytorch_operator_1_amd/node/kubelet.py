@@ -536,6 +536,12 @@ class Kubelet:
         # resolver times out, every rank of a 4-replica job was seen stuck in
         # the ProcessGroupGloo constructor for minutes)
         env.setdefault("GLOO_SOCKET_IFNAME", "lo")
+        # c10d's TCPStore reverse-resolves every peer socket (getnameinfo) and
+        # only logs the result; on a box whose resolver times out that costs
+        # the full resolver timeout per connection (EAI_AGAIN, "hostname of
+        # the client socket cannot be retrieved"), tens of seconds for a
+        # 4-replica rendezvous.  Fail such lookups fast (glibc RES_OPTIONS).
+        env.setdefault("RES_OPTIONS", "timeout:1 attempts:1")
         env["PTO_POD_NAME"] = name_of(pod)
         env["PTO_NAMESPACE"] = namespace_of(pod)
         env["PTO_JOB_NAME"] = (pod["metadata"].get("labels") or {}).get(C.LABEL_JOB_NAME, "")
