@@ -128,7 +128,6 @@ class PodRuntime:
     def __init__(self, pod):
         self.key = key_of(pod)
         self.job_key = Kubelet._job_key(pod)
-        self.gen = 0  # rendezvous generation (Kubelet._job_port)
         self.uid = pod["metadata"].get("uid")
         self.stage = "admit"  # admit -> init -> run -> done
         self.gpus: list[int] = []
@@ -186,9 +185,6 @@ class Kubelet:
         self._port_locks: dict[int, int] = {}  # port -> flock fd of its host-wide reservation
         self._quarantine: dict[int, float] = {}  # released port -> time it may be reused
         self._dying: dict[str, int] = {}  # job -> torn-down pods whose processes are still exiting
-        self._job_gen: dict[str, int] = {}  # job -> current rendezvous generation
-        self._port_gen: dict[str, int] = {}  # job -> generation of its current port
-        self._old_ports: dict[str, list[int]] = {}  # job -> ports of earlier generations (still reserved)
         self.pod_informer = Informer(client, "pods")
         self.svc_informer = Informer(client, "services")
         self.pod_informer.add_event_handler(on_delete=self._on_pod_delete)
@@ -260,12 +256,6 @@ class Kubelet:
                     if (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
                         continue  # finished before we knew it (e.g. kubelet restart)
                     rt = self.pods[k] = PodRuntime(pod)
-                    if old is not None:
-                        # a replica recreated after a failure opens the job's
-                        # next rendezvous generation (every replica recreated
-                        # in the same wave lands on the same one)
-                        self._job_gen[rt.job_key] = max(self._job_gen.get(rt.job_key, 0), old.gen + 1)
-                    rt.gen = self._job_gen.get(rt.job_key, 0)
                 self._advance(pod, rt, procs)
             live = {key_of(p) for p in pods}
             for k in [k for k in self.pods if k not in live]:
@@ -432,20 +422,15 @@ class Kubelet:
         job = (pod["metadata"].get("labels") or {}).get(C.LABEL_JOB_NAME) or name_of(pod)
         return f"{namespace_of(pod)}/{job}"
 
-    def _job_port(self, pod, wanted: int, gen: int = 0) -> int:
-        """The job's virtual master port for rendezvous generation ``gen``.
-        Replicas recreated after a failure (ExitCode / backoff restarts)
-        rendezvous on a fresh port: a fast-starting new worker must never
-        reach a TCPStore that an old replica still serves on the previous
-        port (it would hang the new master's store creation).  Ports of
-        earlier generations stay reserved until the job is gone."""
+    def _job_port(self, pod, wanted: int) -> int:
+        """The job's virtual master port: one per job for its whole life
+        (replicas recreated after a failure rendezvous where their peers
+        do; they start only once the deleted replicas' processes are gone,
+        see ``_dying``)."""
         jk = self._job_key(pod)
-        if jk in self.job_ports and self._port_gen.get(jk, 0) >= gen:
-            return self.job_ports[jk]
         if jk in self.job_ports:
-            self._old_ports.setdefault(jk, []).append(self.job_ports[jk])
-        used = (set(self.job_ports.values()) | set(self._quarantine)
-                | {p for ps in self._old_ports.values() for p in ps})
+            return self.job_ports[jk]
+        used = set(self.job_ports.values()) | set(self._quarantine)
         port = wanted
         while True:
             if port not in used and _port_free(port):
@@ -455,7 +440,6 @@ class Kubelet:
                     break
             port += 1
         self.job_ports[jk] = port
-        self._port_gen[jk] = gen
         return port
 
     def _release_job_ports(self, pods):
@@ -471,10 +455,6 @@ class Kubelet:
         now = time.time()
         for jk in [jk for jk in self.job_ports if jk not in live]:
             self._quarantine[self.job_ports.pop(jk)] = now + PORT_QUARANTINE_S
-            for p in self._old_ports.pop(jk, []):
-                self._quarantine[p] = now + PORT_QUARANTINE_S
-            self._port_gen.pop(jk, None)
-            self._job_gen.pop(jk, None)
         for port in [p for p, t in self._quarantine.items() if t <= now]:
             del self._quarantine[port]
             fd = self._port_locks.pop(port, None)
@@ -506,7 +486,7 @@ class Kubelet:
             env["MASTER_ADDR"] = NODE_ADDRESS
         if "MASTER_PORT" in env:
             env["PTO_MASTER_PORT_REQUESTED"] = env["MASTER_PORT"]
-            env["MASTER_PORT"] = str(self._job_port(pod, int(env["MASTER_PORT"]), rt.gen))
+            env["MASTER_PORT"] = str(self._job_port(pod, int(env["MASTER_PORT"])))
         # GPU pinning (module doc): one process per allocated GPU
         if gpus_requested(c) > 0 or rt.gpus:
             mine = sorted({g // self.gpu_share for g in rt.gpus})  # allocator slot -> device

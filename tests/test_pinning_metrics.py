@@ -147,26 +147,3 @@ def test_job_port_released_after_job_deleted(tmp_path):
         k._release_job_ports(c.store.list("pods", None)["items"])
         assert port not in k._port_locks and port not in k._quarantine
 
-
-def test_restart_generation_gets_fresh_rendezvous_port(tmp_path):
-    """Replicas recreated after a failure rendezvous on a new port (a new
-    worker must never reach the TCPStore an old replica still serves); the
-    previous generation's port stays reserved until the job is gone."""
-    with LocalCluster(gpus=0, log_dir=str(tmp_path)) as c:
-        k = c.kubelet
-        k._stop.set()  # no sync loop releasing the pod-less job's ports under the test
-        k._thread.join(5)
-        pod = {"metadata": {"name": "g-master-0", "namespace": "default",
-                            "labels": {"training.kubeflow.org/job-name": "g", "job-name": "g",
-                                       "pytorch-job-name": "g"}}}
-        from pytorch_operator_1_amd.api import constants as C
-
-        pod["metadata"]["labels"][C.LABEL_JOB_NAME] = "g"
-        p0 = k._job_port(pod, 23456, 0)
-        assert k._job_port(pod, 23456, 0) == p0
-        p1 = k._job_port(pod, 23456, 1)
-        assert p1 != p0 and k._job_port(pod, 23456, 1) == p1
-        assert k._job_port(pod, 23456, 0) == p1  # a late old-generation spawn joins the current one
-        assert p0 in k._port_locks and p0 in k._old_ports["default/g"]
-        k._release_job_ports([])  # job gone: both generations quarantined
-        assert {p0, p1} <= set(k._quarantine)
