@@ -90,7 +90,7 @@ _SHARED_ARGS = ["--backend", "gloo", "--impl", "fused", "--comm", "xgmi", "--log
 # no schedule race (4 ranks share one GPU); a rendezvous that stalls (seen
 # intermittently on some boxes: the new master blocked creating its TCPStore
 # while the workers were already connected) times out in 45 s and exits 138,
-# so the ExitCode policy recreates the replicas on a fresh rendezvous port
+# so the ExitCode policy recreates the replicas and they rendezvous again
 _SHARED_ENV = {"PTO_COMM_OVERLAP": "0", "PTO_FAULTHANDLER": "1", "PTO_PG_TIMEOUT": "45"}
 
 
