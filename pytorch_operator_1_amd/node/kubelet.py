@@ -128,6 +128,9 @@ class PodRuntime:
     def __init__(self, pod):
         self.key = key_of(pod)
         self.job_key = Kubelet._job_key(pod)
+        self.replacement = False  # a new incarnation of a pod name seen before
+        self.t_created = time.time()
+        self.t_started = None  # when its containers were spawned
         self.uid = pod["metadata"].get("uid")
         self.stage = "admit"  # admit -> init -> run -> done
         self.gpus: list[int] = []
@@ -256,6 +259,7 @@ class Kubelet:
                     if (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
                         continue  # finished before we knew it (e.g. kubelet restart)
                     rt = self.pods[k] = PodRuntime(pod)
+                    rt.replacement = old is not None
                 self._advance(pod, rt, procs)
             live = {key_of(p) for p in pods}
             for k in [k for k in self.pods if k not in live]:
@@ -315,6 +319,17 @@ class Kubelet:
             # graceful deletion gives the same ordering)
             if self._dying.get(rt.job_key):
                 return
+            # a replica recreated after a failure also waits for the job's
+            # other replicas that were started before it to exit: an old
+            # master that has not noticed the failure yet still serves the
+            # job's rendezvous store, and a new worker that joined it would
+            # leave the next rendezvous one rank short
+            if rt.replacement and any(
+                    o is not rt and o.job_key == rt.job_key and o.t_started is not None
+                    and o.t_started < rt.t_created
+                    and any((procs.get(i) or {}).get("state") == "running" for i in o.proc_ids)
+                    for o in self.pods.values()):
+                return
             if not self._admit(pod, rt):
                 return
             rt.stage = "init"
@@ -326,6 +341,7 @@ class Kubelet:
             if not self._run_init(pod, rt, procs):
                 return
             self._start_containers(pod, rt)
+            rt.t_started = time.time()
             rt.stage = "run"
             procs = self.agent.status()
         if rt.stage == "run":
