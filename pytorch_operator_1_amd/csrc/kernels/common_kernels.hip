@@ -168,38 +168,6 @@ __global__ __launch_bounds__(1024) void k_gridbar(unsigned* ctr, int rounds, int
   }
 }
 
-
-// Synthetic MNIST-shaped data (models/mnist.py synthetic_mnist): a
-// counter-based hash per (seed, element), so the set is generated in place
-// on the device in one launch (no host RNG, no upload, no lazy loading of
-// library kernels on the submit -> first-step path) and bit-identical to
-// the numpy twin on CPU (_synthetic_mnist_host).  Arithmetic is kept to
-// correctly rounded single operations (no contraction) for that reason.
-__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x7feb352du;
-  x ^= x >> 15;
-  x *= 0x846ca68bu;
-  x ^= x >> 16;
-  return x;
-}
-
-__global__ __launch_bounds__(256) void k_synth_mnist(float* __restrict__ img, int64_t* __restrict__ labels, int n,
-                                                     uint32_t kimg, uint32_t klab) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)n * 784) return;
-  const int s = (int)(i / 784), p = (int)(i % 784), y = p / 28, x = p % 28;
-  const int lab = (int)(lowbias32((uint32_t)s ^ klab) % 10u);
-  if (p == 0) labels[s] = lab;
-  const int ys[10] = {2, 2, 2, 11, 11, 11, 20, 20, 20, 11};
-  const int xs[10] = {2, 11, 20, 2, 11, 20, 2, 11, 20, 8};
-  const float u = __fmul_rn((float)(lowbias32((uint32_t)i ^ kimg) >> 8), 5.9604644775390625e-08f);  // [0, 1)
-  float v = __fmul_rn(u, 0.3f);
-  if (y >= ys[lab] && y < ys[lab] + 6 && x >= xs[lab] && x < xs[lab] + 6) v = __fadd_rn(v, 0.7f);
-  v = fminf(fmaxf(v, 0.f), 1.f);
-  img[i] = __fdiv_rn(__fsub_rn(v, 0.1307f), 0.3081f);
-}
-
 }  // namespace
 
 #define PTO_API extern "C" __attribute__((visibility("default")))
@@ -267,13 +235,5 @@ PTO_API int pto_sum(const float* x, float* out, long long n, float scale, hipStr
 
 PTO_API int pto_noop(int blocks, hipStream_t s) {
   hipLaunchKernelGGL(k_noop, dim3(blocks), dim3(64), 0, s, nullptr);
-  return (int)hipGetLastError();
-}
-
-PTO_API int pto_synth_mnist(float* img, int64_t* labels, int n, unsigned kimg, unsigned klab, hipStream_t s) {
-  if (n <= 0 || (long long)n * 784 >= (1LL << 32)) return -1;
-  const long long total = (long long)n * 784;
-  hipLaunchKernelGGL(k_synth_mnist, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, img, labels, n,
-                     (uint32_t)kimg, (uint32_t)klab);
   return (int)hipGetLastError();
 }

@@ -111,68 +111,25 @@ class MnistNet(nn.Module):
         return F.log_softmax(x, dim=1)
 
 
-_BLOB_Y = (2, 2, 2, 11, 11, 11, 20, 20, 20, 11)
-_BLOB_X = (2, 11, 20, 2, 11, 20, 2, 11, 20, 8)
-
-
-def _lowbias32(x: torch.Tensor) -> torch.Tensor:
-    """32-bit integer hash on int64 tensors holding uint32 values (products
-    wrap in int64; the low 32 bits are exact)."""
-    m = 0xFFFFFFFF
-    x = x ^ (x >> 16)
-    x = (x * 0x7FEB352D) & m
-    x = x ^ (x >> 15)
-    x = (x * 0x846CA68B) & m
-    return x ^ (x >> 16)
-
-
-def _synth_keys(seed: int) -> tuple[int, int]:
-    k = _lowbias32(torch.tensor([(2 * seed) & 0xFFFFFFFF, (2 * seed + 1) & 0xFFFFFFFF], dtype=torch.int64))
-    return int(k[0]), int(k[1])
-
-
-def _synthetic_mnist_host(n: int, seed: int):
-    """CPU twin of the device kernel ``k_synth_mnist`` (common_kernels.hip):
-    the same hash and the same single-rounded float32 operations, so CPU and
-    GPU runs see bit-identical data."""
-    kimg, klab = _synth_keys(seed)
-    labels = _lowbias32(torch.arange(n, dtype=torch.int64) ^ klab) % 10
-    h = _lowbias32(torch.arange(n * 784, dtype=torch.int64) ^ kimg) >> 8
-    u = h.to(torch.float32) * torch.tensor(5.9604644775390625e-08, dtype=torch.float32)
-    v = (u * torch.tensor(0.3, dtype=torch.float32)).view(n, 28, 28)
-    r = torch.arange(28)
-    y0 = torch.tensor(_BLOB_Y)[labels][:, None]
-    x0 = torch.tensor(_BLOB_X)[labels][:, None]
-    rows = (r >= y0) & (r < y0 + 6)
-    cols = (r >= x0) & (r < x0 + 6)
-    v = torch.where(rows[:, :, None] & cols[:, None, :], v + torch.tensor(0.7, dtype=torch.float32), v)
-    v = v.clamp_(0, 1)
-    v = (v - torch.tensor(0.1307, dtype=torch.float32)) / torch.tensor(0.3081, dtype=torch.float32)
-    return v.view(n, 1, 28, 28), labels
-
-
 def synthetic_mnist(n: int, device, seed: int = 1, dtype=torch.float32):
     """Synthetic MNIST-shaped data (normalised like ``Normalize((0.1307,),
     (0.3081,))``) with a learnable label rule, resident on ``device``.
 
     There is no network in this environment, so real MNIST cannot be
     downloaded; the label is a deterministic function of the image (which
-    quadrant holds the brightest 6x6 blob) so training visibly converges.
-    Pixels and labels come from a counter-based hash of (seed, index): on a
-    GPU one kernel writes the set in place (``k_synth_mnist``; it is on the
-    submit -> first-step path: no host RNG, no 188 MB upload), on the CPU a
-    numpy twin produces the bit-identical set.
+    quadrant holds the brightest blob) so training visibly converges.
     """
-    device = torch.device(device)
-    if device.type == "cuda":
-        from ..ops import _lib
-
-        imgs = torch.empty((n, 1, 28, 28), device=device, dtype=torch.float32)
-        labels = torch.empty((n,), device=device, dtype=torch.int64)
-        kimg, klab = _synth_keys(seed)
-        with torch.cuda.device(device):
-            _lib.check(_lib.lib().pto_synth_mnist(imgs.data_ptr(), labels.data_ptr(), n, kimg, klab,
-                                                  _lib.stream_ptr(device)), "synth_mnist")
-    else:
-        imgs, labels = _synthetic_mnist_host(n, seed)
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    labels = torch.randint(0, NUM_CLASSES, (n,), generator=g)
+    imgs = torch.rand((n, 1, 28, 28), generator=g) * 0.3
+    # Paint a class-dependent 6x6 blob: 10 classes -> 10 fixed positions.
+    ys = torch.tensor([2, 2, 2, 11, 11, 11, 20, 20, 20, 11])
+    xs = torch.tensor([2, 11, 20, 2, 11, 20, 2, 11, 20, 8])
+    # one broadcast mask instead of per-class fancy indexing (same values)
+    r = torch.arange(28)
+    y0, x0 = ys[labels][:, None], xs[labels][:, None]
+    rows = (r >= y0) & (r < y0 + 6)
+    cols = (r >= x0) & (r < x0 + 6)
+    imgs[:, 0].add_((rows[:, :, None] & cols[:, None, :]).to(imgs.dtype), alpha=0.7)
+    imgs = (imgs.clamp_(0, 1) - 0.1307) / 0.3081
     return imgs.to(device=device, dtype=dtype), labels.to(device)

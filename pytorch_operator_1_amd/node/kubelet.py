@@ -88,8 +88,6 @@ _EFFECTIVE_KEYS = ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE", "LOCAL_RA
                    "HIP_VISIBLE_DEVICES", "PTO_MASTER_SERVICE", "PTO_MASTER_PORT_REQUESTED")
 GPU_VISIBILITY_MODES = ("node", "isolated")
 NODE_ADDRESS = "127.0.0.1"
-PORT_QUARANTINE_S = float(os.environ.get("PTO_PORT_QUARANTINE_S", "60"))
-PORT_RELEASE = os.environ.get("PTO_PORT_RELEASE", "1") == "1"
 
 
 def _port_free(port: int) -> bool:
@@ -127,10 +125,6 @@ def _reserve_port(port: int):
 class PodRuntime:
     def __init__(self, pod):
         self.key = key_of(pod)
-        self.job_key = Kubelet._job_key(pod)
-        self.replacement = False  # a new incarnation of a pod name seen before
-        self.t_created = time.time()
-        self.t_started = None  # when its containers were spawned
         self.uid = pod["metadata"].get("uid")
         self.stage = "admit"  # admit -> init -> run -> done
         self.gpus: list[int] = []
@@ -186,8 +180,6 @@ class Kubelet:
         self.pods: dict[str, PodRuntime] = {}
         self.job_ports: dict[str, int] = {}
         self._port_locks: dict[int, int] = {}  # port -> flock fd of its host-wide reservation
-        self._quarantine: dict[int, float] = {}  # released port -> time it may be reused
-        self._dying: dict[str, int] = {}  # job -> torn-down pods whose processes are still exiting
         self.pod_informer = Informer(client, "pods")
         self.svc_informer = Informer(client, "services")
         self.pod_informer.add_event_handler(on_delete=self._on_pod_delete)
@@ -253,19 +245,16 @@ class Kubelet:
                 k = key_of(pod)
                 rt = self.pods.get(k)
                 if rt is None or rt.uid != pod["metadata"].get("uid"):
-                    old = rt
-                    if old is not None:  # same name, new incarnation
-                        self._teardown(old)
+                    if rt is not None:  # same name, new incarnation
+                        self._teardown(rt)
                     if (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
                         continue  # finished before we knew it (e.g. kubelet restart)
                     rt = self.pods[k] = PodRuntime(pod)
-                    rt.replacement = old is not None
                 self._advance(pod, rt, procs)
             live = {key_of(p) for p in pods}
             for k in [k for k in self.pods if k not in live]:
                 self._teardown(self.pods.pop(k))
-            if PORT_RELEASE:
-                self._release_job_ports(pods)
+            self._release_job_ports(pods)
 
     def _on_pod_delete(self, pod):
         with self._lock:
@@ -279,13 +268,10 @@ class Kubelet:
                 self.agent.kill(pid, signal=15, grace=self.grace)
             except Exception:
                 pass
-        if rt.proc_ids:
-            with self._lock:
-                self._dying[rt.job_key] = self._dying.get(rt.job_key, 0) + 1
-        threading.Thread(target=self._reap_later, args=(list(rt.proc_ids), rt.key, rt.job_key), daemon=True).start()
+        threading.Thread(target=self._reap_later, args=(list(rt.proc_ids), rt.key), daemon=True).start()
         rt.deleted = True
 
-    def _reap_later(self, ids, owner, job_key):
+    def _reap_later(self, ids, owner):
         try:
             end = time.time() + self.grace + 5
             while time.time() < end and not self._stop.is_set():
@@ -298,38 +284,12 @@ class Kubelet:
             self.agent.free(owner)
         except Exception:  # agent already shut down (node stopping)
             pass
-        finally:
-            if ids:
-                with self._lock:
-                    n = self._dying.get(job_key, 0) - 1
-                    if n > 0:
-                        self._dying[job_key] = n
-                    else:
-                        self._dying.pop(job_key, None)
 
     # ------------------------------------------------------------ stages
     def _advance(self, pod, rt: PodRuntime, procs):
         if rt.stage == "done":
             return
         if rt.stage == "admit":
-            # a job's recreated replicas start only once every process of its
-            # deleted ones has exited: a new worker must not rendezvous with
-            # an old master's TCPStore that is still shutting down on the
-            # job's port (the store deletes pods at once; a real kubelet's
-            # graceful deletion gives the same ordering)
-            if self._dying.get(rt.job_key):
-                return
-            # a replica recreated after a failure also waits for the job's
-            # other replicas that were started before it to exit: an old
-            # master that has not noticed the failure yet still serves the
-            # job's rendezvous store, and a new worker that joined it would
-            # leave the next rendezvous one rank short
-            if rt.replacement and any(
-                    o is not rt and o.job_key == rt.job_key and o.t_started is not None
-                    and o.t_started < rt.t_created
-                    and any((procs.get(i) or {}).get("state") == "running" for i in o.proc_ids)
-                    for o in self.pods.values()):
-                return
             if not self._admit(pod, rt):
                 return
             rt.stage = "init"
@@ -341,7 +301,6 @@ class Kubelet:
             if not self._run_init(pod, rt, procs):
                 return
             self._start_containers(pod, rt)
-            rt.t_started = time.time()
             rt.stage = "run"
             procs = self.agent.status()
         if rt.stage == "run":
@@ -439,14 +398,10 @@ class Kubelet:
         return f"{namespace_of(pod)}/{job}"
 
     def _job_port(self, pod, wanted: int) -> int:
-        """The job's virtual master port: one per job for its whole life
-        (replicas recreated after a failure rendezvous where their peers
-        do; they start only once the deleted replicas' processes are gone,
-        see ``_dying``)."""
         jk = self._job_key(pod)
         if jk in self.job_ports:
             return self.job_ports[jk]
-        used = set(self.job_ports.values()) | set(self._quarantine)
+        used = set(self.job_ports.values())
         port = wanted
         while True:
             if port not in used and _port_free(port):
@@ -463,16 +418,10 @@ class Kubelet:
         job that no longer has a pod on this node.  A job keeps its port while
         any of its pods exists, so a replica restarted next to live peers
         gets the port they rendezvous on; a job whose pods are all gone (or
-        re-submitted later) takes a fresh reservation.  A released port stays
-        locked and out of use for ``PORT_QUARANTINE_S`` (processes of deleted
-        pods may still be shutting down with connections to it; a new job's
-        rendezvous store on the same port must not see them)."""
+        re-submitted later) takes a fresh reservation."""
         live = {self._job_key(p) for p in pods}
-        now = time.time()
         for jk in [jk for jk in self.job_ports if jk not in live]:
-            self._quarantine[self.job_ports.pop(jk)] = now + PORT_QUARANTINE_S
-        for port in [p for p, t in self._quarantine.items() if t <= now]:
-            del self._quarantine[port]
+            port = self.job_ports.pop(jk)
             fd = self._port_locks.pop(port, None)
             if fd is not None:
                 try:
@@ -532,12 +481,6 @@ class Kubelet:
         # resolver times out, every rank of a 4-replica job was seen stuck in
         # the ProcessGroupGloo constructor for minutes)
         env.setdefault("GLOO_SOCKET_IFNAME", "lo")
-        # c10d's TCPStore reverse-resolves every peer socket (getnameinfo) and
-        # only logs the result; on a box whose resolver times out that costs
-        # the full resolver timeout per connection (EAI_AGAIN, "hostname of
-        # the client socket cannot be retrieved"), tens of seconds for a
-        # 4-replica rendezvous.  Fail such lookups fast (glibc RES_OPTIONS).
-        env.setdefault("RES_OPTIONS", "timeout:1 attempts:1")
         env["PTO_POD_NAME"] = name_of(pod)
         env["PTO_NAMESPACE"] = namespace_of(pod)
         env["PTO_JOB_NAME"] = (pod["metadata"].get("labels") or {}).get(C.LABEL_JOB_NAME, "")

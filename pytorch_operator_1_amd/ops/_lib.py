@@ -112,7 +112,6 @@ _SIGS = {
     "pto_conv2_bwd_fc": [_P] * 7 + [_I] + [_P] * 7,
     "pto_fc_bwd_adv_nodw1": [_P] * 9 + [_I, _P, _L, _P, _P],
     "pto_sgd_flat": [_P, _P, _P, _L, _L, _P, _F, _F, _F, _I, _P],
-    "pto_synth_mnist": [_P, _P, _I, ctypes.c_uint, ctypes.c_uint, _P],
     "pto_fc_bwd_part": [_P] * 10 + [_I, _P, _L, _P, _I, _P],
     "pto_eval_head": [_P, _P, _P, _I, _P],
     "pto_sgd_block_count": [_L],

@@ -83,10 +83,6 @@ def init_distributed(backend: str | None = None, use_gpu: bool | None = None,
     if use_gpu is None:
         use_gpu = torch.cuda.is_available()
     if use_gpu:
-        # initialise HIP first: torch only caches device_count() once HIP is
-        # up, and every uncached call goes through amdsmi (~0.1 s each, on
-        # the submit -> first-step path)
-        torch.cuda.init()
         n = torch.cuda.device_count()
         device = torch.device("cuda", env.local_rank % max(n, 1))
         torch.cuda.set_device(device)

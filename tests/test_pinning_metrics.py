@@ -137,13 +137,7 @@ def test_job_port_released_after_job_deleted(tmp_path):
         end = time.time() + 30
         while time.time() < end and "default/port-a" in k.job_ports:
             time.sleep(0.05)
-        assert "default/port-a" not in k.job_ports and port in k._quarantine
-        # quarantined: a job submitted right away gets another port
+        assert "default/port-a" not in k.job_ports and port not in k._port_locks
         c.submit(new_job("port-b", image="pto/python:rocm", master_args=["-c", "print('ok')"], workers=0, gpus=0))
         c.wait_for_condition("port-b", timeout=60)
-        assert k.job_ports["default/port-b"] != port
-        # after the quarantine the lock is dropped and the port is reusable
-        k._quarantine[port] = 0.0
-        k._release_job_ports(c.store.list("pods", None)["items"])
-        assert port not in k._port_locks and port not in k._quarantine
-
+        assert k.job_ports["default/port-b"] == port  # the same base port is free again
