@@ -108,6 +108,9 @@ def add_operator_flags(p):
     p.add_argument("--burst", type=int, default=10)
     p.add_argument("--alsologtostderr", action="store_true", help="accepted for manifest compatibility")
     p.add_argument("-v", type=int, default=0, help="accepted for manifest compatibility")
+    p.add_argument("--restart-scope", choices=["job", "pod"], default="job",
+                   help="ExitCode restarts of a multi-replica job: job = recreate every replica when one fails "
+                        "retryably (a DDP world restarts as a whole); pod = only the failed pod (reference)")
 
 
 def _server_url(args) -> str:
@@ -146,7 +149,7 @@ def cmd_operator(args):
     cfg = ControllerConfig(enable_gang_scheduling=args.enable_gang_scheduling,
                            gang_scheduler_name=args.gang_scheduler_name,
                            init_container_image=args.init_container_image, threadiness=args.threadiness,
-                           namespace=args.namespace or None)
+                           namespace=args.namespace or None, restart_scope=args.restart_scope)
     ctl = PyTorchController(client, cfg, metrics=metrics)
 
     def lead():
@@ -221,7 +224,7 @@ def cmd_up(args):
 
     c = LocalCluster(gpus=args.gpus, port=args.port, wal_path=args.wal, log_dir=args.log_dir,
                      enable_gang_scheduling=args.enable_gang_scheduling, hbm_per_gpu=_hbm(args),
-                     gpu_visibility=args.gpu_visibility)
+                     gpu_visibility=args.gpu_visibility, restart_scope=args.restart_scope)
     c.start()
     serve_metrics(c.metrics, args.monitoring_port)
     print(f"pto: API server {c.url}  metrics :{args.monitoring_port}/metrics  "
@@ -457,7 +460,8 @@ def main(argv=None):
     nd.add_argument("--log-dir", default=None)
     nd.add_argument("--gpu-visibility", choices=["node", "isolated"], default=None,
                     help="node: replicas see every GPU and pick theirs via LOCAL_RANK (peer IPC/P2P reachable); "
-                         "isolated: HIP_VISIBLE_DEVICES = the replica's own GPUs (default: $PTO_GPU_VISIBILITY or node)")
+                         "isolated: HIP_VISIBLE_DEVICES = the replica's own GPUs (default: $PTO_GPU_VISIBILITY or "
+                         "isolated); a pod overrides it with the pto.amd.com/gpu-visibility annotation")
     nd.add_argument("--monitoring-port", type=int, default=0,
                     help="serve the pytorchjob_* training/HBM gauges on this port (0: off)")
     nd.add_argument("--node-name", default="mi355x-0")
@@ -474,6 +478,8 @@ def main(argv=None):
     up.add_argument("--enable-gang-scheduling", action="store_true")
     up.add_argument("--gpu-visibility", choices=["node", "isolated"], default=None,
                     help="GPU pinning model (see pto node --help)")
+    up.add_argument("--restart-scope", choices=["job", "pod"], default="job",
+                    help="ExitCode restarts of multi-replica jobs (see pto operator --help)")
     up.set_defaults(fn=cmd_up)
 
     a = sub.add_parser("apply")

@@ -28,14 +28,14 @@ class LocalCluster:
     def __init__(self, gpus: int | None = None, port: int = 0, wal_path: str | None = None,
                  log_dir: str | None = None, enable_gang_scheduling: bool = False, serve_http: bool = True,
                  extra_env: dict | None = None, threadiness: int = 2, hbm_per_gpu: float | None = None,
-                 gpu_visibility: str | None = None, gpu_share: int | None = None):
+                 gpu_visibility: str | None = None, gpu_share: int | None = None, restart_scope: str = "job"):
         self.store = Store(wal_path=wal_path)
         self.client = LocalClient(self.store)
         self.server = ApiServer(self.store, port=port) if serve_http else None
         self.metrics = OperatorMetrics()
         self.controller = PyTorchController(
             self.client, ControllerConfig(enable_gang_scheduling=enable_gang_scheduling, threadiness=threadiness,
-                                          job_resync_period=5.0), metrics=self.metrics)
+                                          job_resync_period=5.0, restart_scope=restart_scope), metrics=self.metrics)
         kw = {"hbm_per_gpu": hbm_per_gpu} if hbm_per_gpu else {}
         if gpu_visibility:
             kw["gpu_visibility"] = gpu_visibility

@@ -88,6 +88,10 @@ class ControllerConfig:
     threadiness: int = 1
     namespace: str | None = None
     job_resync_period: float = C.JOB_RESYNC_PERIOD_S
+    # ExitCode restarts of a multi-replica job: "job" deletes every replica
+    # when one fails retryably (a DDP world restarts as a whole); "pod"
+    # deletes only the failed pod, as the reference does (pod.go:91-109)
+    restart_scope: str = "job"
 
 
 class Recorder:
@@ -515,6 +519,7 @@ class PyTorchController:
                     control.sync_pod_group(self.client, job, total)
                 except ApiError as e:
                     log.warning("Sync PodGroup %s: %s", name_of(job), e)
+            self.restart_wave(job, pods, total)
             for rtype, spec in replica_specs(job).items():
                 self.reconcile_pods(job, pods, rtype, spec)
                 if rtype != C.REPLICA_MASTER:
@@ -549,6 +554,56 @@ class PyTorchController:
         return time.time() - parse_rfc3339(start) >= float(ads)
 
     # ---------------------------------------------------------- pods
+    @staticmethod
+    def _exit_code(pod) -> int | None:
+        """Terminated exit code of the ``pytorch`` container (pod.go:91-101)."""
+        for cs in pod.get("status", {}).get("containerStatuses") or []:
+            term = (cs.get("state") or {}).get("terminated")
+            if cs.get("name") == C.DEFAULT_CONTAINER_NAME and term:
+                return int(term.get("exitCode", 0))
+        return None
+
+    def restart_wave(self, job, pods, total: int):
+        """Job-level restart (``restart_scope="job"``).
+
+        The reference deletes only the failed pod of an ``ExitCode`` replica
+        (pod.go:91-109).  For a DDP world that is not enough: the surviving
+        ranks keep the rendezvous store and communicators of the old world,
+        sit in a collective with a dead peer until a timeout, and the
+        recreated rank joins their store instead of a new one.  So when any
+        replica failed with a retryable code, every other replica of the
+        job is deleted in the same pass; the next reconcile recreates all of
+        them, and the node manager starts the new pods only after every
+        process of the old ones has exited (node/kubelet.py, restart gate).
+        The failed pod itself goes through :meth:`reconcile_pods` as usual,
+        which keeps the reference's ``ExitedWithCode`` events and the
+        ``Restarting`` condition."""
+        if self.config.restart_scope != "job" or total <= 1:
+            return
+        specs = replica_specs(job)
+        failed = []
+        for p in pods:
+            if p.get("status", {}).get("phase") != "Failed":
+                continue
+            rt = (p["metadata"].get("labels") or {}).get(C.LABEL_REPLICA_TYPE, "")
+            spec = next((s for t, s in specs.items() if t.lower() == rt), None)
+            code = self._exit_code(p)
+            if (spec is None or spec.get("restartPolicy") != C.RESTART_POLICY_EXIT_CODE or code is None
+                    or not is_retryable_exit_code(code)):
+                return  # a permanent failure: the job fails (reconcile_pods), nothing is restarted
+            failed.append(name_of(p))
+        if not failed:
+            return
+        others = [p for p in pods if name_of(p) not in failed and not p["metadata"].get("deletionTimestamp")]
+        if not others:
+            return
+        msg = (f"PyTorchJob {name_of(job)}: {', '.join(sorted(failed))} failed with a retryable exit code; "
+               f"restarting all {total} replicas")
+        log.info(msg)
+        self.recorder.event(job, "Normal", C.REASON_RESTARTING, msg)
+        for p in others:
+            self.pod_control.delete_pod(namespace_of(p), name_of(p), job)
+
     def reconcile_pods(self, job, pods, rtype, spec):
         rt = rtype.lower()
         pods = _filter_for_rtype(pods, rt)

@@ -15,6 +15,14 @@
 //   * the worker init-container gate: a TCP connect probe of
 //     MASTER_ADDR:MASTER_PORT (the DNS wait of the reference's
 //     init-pytorch container, pkg/common/config/config.go:9-20);
+//   * restart groups (gang restart): the containers of one multi-replica
+//     job share a group.  A DDP world cannot take back one restarted rank
+//     (its peers hold the old rendezvous store and communicators), so when a
+//     member fails and its policy restarts it, the agent SIGKILLs every other
+//     running member, holds them all until the last one has been reaped (the
+//     old rendezvous port is then closed), and restarts the whole group at
+//     once with PTO_RESTART_GENERATION=<base>.<wave> -- one rendezvous per
+//     wave, never a new rank joining an old store;
 //   * warm starts (--zygote PYTHON): a pre-imported interpreter
 //     (node/zygote.py) forks `python -m MODULE` / `python SCRIPT.py`
 //     containers instead of a cold fork/exec (import torch is ~1.5-2 s of
@@ -93,6 +101,18 @@ struct Proc {
   double last_finished_at = 0;
   std::string launcher;  // "zygote" | "exec"
   bool exec_only = false;  // spawn request "launcher": "exec" -- never fork from the zygote
+  std::string group;       // restart group ("" = restarts alone)
+  std::string gen_base;    // PTO_RESTART_GENERATION given at spawn
+  bool held = false;       // restart owed, waiting for its group to drain
+  double held_delay = 0;   // its own CrashLoopBackOff delay
+};
+
+// One restart wave at a time per group: `draining` from the first failing
+// member until every member has exited, then all held members restart.
+struct Group {
+  int wave = 0;
+  bool draining = false;
+  double drain_started = 0;
 };
 
 // ---------------------------------------------------------------- zygote --
@@ -238,6 +258,7 @@ struct Zygote {
 
 struct Agent {
   std::map<std::string, Proc> procs;
+  std::map<std::string, Group> groups;
   // GPU allocator
   int n_gpus = 0;
   double hbm_per_gpu = 288e9;
@@ -391,6 +412,9 @@ struct Agent {
     p.restart_policy = req["restart_policy"].str("Never");
     p.exec_only = req["launcher"].str("auto") == "exec";
     for (auto& c : req["cpus"].a) p.cpus.push_back((int)c.num());
+    p.group = req["group"].str("");
+    auto g = p.env.find("PTO_RESTART_GENERATION");
+    p.gen_base = g == p.env.end() ? "0" : g->second;
     procs[id] = p;
     start(procs[id]);
     Json r = ok();
@@ -457,6 +481,14 @@ struct Agent {
         p.state = "waiting";
         p.reason = "CrashLoopBackOff";
         p.restart_at = mono_s() + delay;
+        if (!p.group.empty()) {
+          Group& g = groups[p.group];
+          if (!g.draining && p.exit_code != 0) begin_wave(p.group, p.id);
+          if (g.draining) {  // restarts with the rest of its group
+            p.held = true;
+            p.held_delay = delay;
+          }
+        }
       } else {
         p.state = "terminated";
         p.reason = p.exit_code == 0 ? "Completed" : (p.stopping ? "Killed" : "Error");
@@ -465,11 +497,64 @@ struct Agent {
     }
   }
 
+  // A member failed: every other running member of its group is killed
+  // (it would otherwise sit in a collective with a dead peer, and the
+  // restarted rank would rendezvous with a store that belongs to it).
+  void begin_wave(const std::string& name, const std::string& culprit) {
+    Group& g = groups[name];
+    g.draining = true;
+    g.wave += 1;
+    g.drain_started = mono_s();
+    int killed = 0;
+    for (auto& kv : procs) {
+      Proc& q = kv.second;
+      if (q.group != name || q.id == culprit || q.stopping) continue;
+      if (q.state == "running" && q.pid > 0) {
+        ::kill(-q.pid, SIGKILL);
+        ++killed;
+      } else if (q.state == "waiting" && q.reason == "CrashLoopBackOff") {
+        q.held = true;  // already owed a restart: it joins this wave
+        q.held_delay = std::max(0.0, q.restart_at - mono_s());
+      }
+    }
+    fprintf(stderr, "pto-node-agent: group %s: %s failed, restart wave %d (%d member(s) stopped)\n",
+            name.c_str(), culprit.c_str(), g.wave, killed);
+  }
+
+  // Restart a drained group: all held members at once, after the longest
+  // back-off any of them is owed, under the wave's generation.
+  void release_groups() {
+    for (auto& gkv : groups) {
+      Group& g = gkv.second;
+      if (!g.draining) continue;
+      bool live = false;
+      double delay = 0;
+      for (auto& kv : procs) {
+        const Proc& q = kv.second;
+        if (q.group != gkv.first) continue;
+        if (q.state == "running") live = true;
+        if (q.held) delay = std::max(delay, q.held_delay);
+      }
+      if (live) continue;
+      const double at = mono_s() + delay;
+      for (auto& kv : procs) {
+        Proc& q = kv.second;
+        if (q.group != gkv.first || !q.held) continue;
+        q.held = false;
+        q.restart_at = at;
+        q.env["PTO_RESTART_GENERATION"] = q.gen_base + "." + std::to_string(g.wave);
+      }
+      g.draining = false;
+    }
+  }
+
   void tick() {
+    release_groups();
     double t = mono_s();
     for (auto& kv : procs) {
       Proc& p = kv.second;
-      if (p.state == "waiting" && p.reason == "CrashLoopBackOff" && !p.stopping && t >= p.restart_at) start(p);
+      if (p.state == "waiting" && p.reason == "CrashLoopBackOff" && !p.stopping && !p.held && t >= p.restart_at)
+        start(p);
       if (p.state == "running" && p.kill_deadline > 0 && t >= p.kill_deadline && p.pid > 0) {
         ::kill(-p.pid, SIGKILL);
         p.kill_deadline = 0;
@@ -497,6 +582,10 @@ struct Agent {
       j["last_exit_code"] = p.last_exit_code;
       j["last_finished_at"] = p.last_finished_at;
       j["launcher"] = p.launcher;
+      j["group"] = p.group;
+      j["held"] = p.held;
+      auto g = p.env.find("PTO_RESTART_GENERATION");
+      j["generation"] = g == p.env.end() ? std::string() : g->second;
       list.push(j);
     }
     out["procs"] = list;

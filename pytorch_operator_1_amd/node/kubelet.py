@@ -23,24 +23,39 @@ Per pod:
      ``MASTER_PORT=23456``, pod.go:245-274), the process sees
      ``127.0.0.1`` and the job's port.
 
-GPU pinning (``gpu_visibility``):
-  * ``node`` (default) — every replica sees ALL of the node's GPUs
+GPU pinning (``gpu_visibility``, per pod: the ``pto.amd.com/gpu-visibility``
+annotation):
+  * ``isolated`` (default) — the process sees only its own GPUs
+    (``HIP_VISIBLE_DEVICES`` = its allocation, ``LOCAL_RANK=0``), the
+    Kubernetes device-plugin model: any image that just uses ``cuda:0``
+    lands on its own GPU.
+  * ``node`` — every replica sees ALL of the node's GPUs
     (``HIP_VISIBLE_DEVICES`` = the node's list, identical in every
     replica) and selects its own through ``LOCAL_RANK`` = the index of its
     allocated GPU.  This is what torchrun does, and it keeps the peers'
     devices enumerable by HIP: ``hipIpcOpenMemHandle`` of a peer buffer
     (the xGMI all-reduce) and RCCL's P2P transport both work on devices
     the process can see.  The allocator still hands each GPU to exactly
-    one replica.
-  * ``isolated`` — the process sees only its own GPUs
-    (``HIP_VISIBLE_DEVICES`` = its allocation, ``LOCAL_RANK=0``), the
-    Kubernetes device-plugin model.  RCCL then has to use its IPC path for
-    peers it cannot enumerate; the fused trainer's xGMI autotune falls back
-    to RCCL if the peer mapping fails on any rank.
+    one replica.  Jobs that all-reduce over peer memory (the fused trainer's
+    xGMI transport) ask for it with the annotation; with ``isolated`` the
+    xGMI autotune falls back to RCCL if the peer mapping fails on any rank.
   4. status — phase, containerStatuses (state, restartCount, exitCode),
      podIP/hostIP, written back through the status subresource.
   5. deletion — SIGTERM the process group, SIGKILL after the grace period,
      free the GPUs.
+
+Restarts of a multi-replica job (a DDP world cannot take back one
+restarted rank; docs/multi_gpu.md "Restarts"):
+  * in place (``OnFailure``/``Always``): the job's containers form one
+    restart group in the agent -- a failing member takes the others down,
+    and all restart together once the last has exited;
+  * recreated pods (``ExitCode``: the controller deletes every replica of
+    the job, controller/pytorch.py ``restart_scope``): a new pod of the job
+    is held Pending (``PreviousIncarnationRunning``) until every process of
+    the job's torn-down pods has exited, so its master binds a closed port
+    and no replica can reach the old incarnation's rendezvous store;
+  * every wave gets ``PTO_RESTART_GENERATION`` (``<pod generation>.<in-place
+    wave>``), which the trainers put in front of their rendezvous keys.
 """
 from __future__ import annotations
 
@@ -87,6 +102,9 @@ EFFECTIVE_ENV_ANNOTATION = "pto.amd.com/effective-env"
 _EFFECTIVE_KEYS = ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
                    "HIP_VISIBLE_DEVICES", "PTO_MASTER_SERVICE", "PTO_MASTER_PORT_REQUESTED")
 GPU_VISIBILITY_MODES = ("node", "isolated")
+# per-pod choice of the visibility model (pod template annotation); the
+# node-wide default is --gpu-visibility / PTO_GPU_VISIBILITY
+GPU_VISIBILITY_ANNOTATION = "pto.amd.com/gpu-visibility"
 NODE_ADDRESS = "127.0.0.1"
 
 
@@ -126,6 +144,11 @@ class PodRuntime:
     def __init__(self, pod):
         self.key = key_of(pod)
         self.uid = pod["metadata"].get("uid")
+        # agent process ids and the GPU owner are per pod INCARNATION: a pod
+        # recreated under the same name must never be confused with the
+        # previous one, whose teardown may still be reaping its processes
+        self.owner = _owner(pod)
+        self.job_key = Kubelet._job_key(pod)
         self.stage = "admit"  # admit -> init -> run -> done
         self.gpus: list[int] = []
         self.init_index = 0
@@ -149,11 +172,14 @@ class Kubelet:
                  log_dir: str | None = None, images: dict | None = None, gpus: int | None = None,
                  poll_interval: float = 0.05, grace_seconds: float = 5.0, extra_env: dict | None = None,
                  hbm_per_gpu: float = C.HBM_PER_GPU_BYTES, gpu_visibility: str | None = None, metrics=None,
-                 sysfs_root: str | None = None, gpu_share: int | None = None):
+                 sysfs_root: str | None = None, gpu_share: int | None = None, group_restarts: bool = True):
         self.client = client
-        self.gpu_visibility = gpu_visibility or os.environ.get("PTO_GPU_VISIBILITY", "node")
+        self.gpu_visibility = gpu_visibility or os.environ.get("PTO_GPU_VISIBILITY", "isolated")
         if self.gpu_visibility not in GPU_VISIBILITY_MODES:
             raise ValueError(f"gpu_visibility must be one of {GPU_VISIBILITY_MODES}")
+        # in-place restarts (OnFailure/Always) of a multi-replica job's
+        # containers as one group (False: each container alone, as a kubelet)
+        self.group_restarts = group_restarts
         # OperatorMetrics to feed with the trainers' reports and node HBM
         self.metrics = metrics
         self.sysfs_root = sysfs_root or os.environ.get("PTO_SYSFS_ROOT", "/sys")
@@ -178,6 +204,12 @@ class Kubelet:
         self.grace = grace_seconds
         self.extra_env = extra_env or {}
         self.pods: dict[str, PodRuntime] = {}
+        # restart generations (module doc, "Restarts"): agent ids of the
+        # processes of torn-down pods, per job, until they have all exited;
+        # jobs whose previous incarnation has just drained; generation per job
+        self.retired: dict[str, set[str]] = {}
+        self._drained: set[str] = set()
+        self.job_gen: dict[str, int] = {}
         self.job_ports: dict[str, int] = {}
         self._port_locks: dict[int, int] = {}  # port -> flock fd of its host-wide reservation
         self.pod_informer = Informer(client, "pods")
@@ -254,6 +286,10 @@ class Kubelet:
             live = {key_of(p) for p in pods}
             for k in [k for k in self.pods if k not in live]:
                 self._teardown(self.pods.pop(k))
+            for jk in [jk for jk, ids in self.retired.items()
+                       if all((procs.get(i) or {}).get("state") != "running" for i in ids)]:
+                del self.retired[jk]
+                self._drained.add(jk)
             self._release_job_ports(pods)
 
     def _on_pod_delete(self, pod):
@@ -263,12 +299,14 @@ class Kubelet:
                 self._teardown(rt)
 
     def _teardown(self, rt: PodRuntime):
+        if rt.proc_ids and not rt.deleted:
+            self.retired.setdefault(rt.job_key, set()).update(rt.proc_ids)
         for pid in rt.proc_ids:
             try:
                 self.agent.kill(pid, signal=15, grace=self.grace)
             except Exception:
                 pass
-        threading.Thread(target=self._reap_later, args=(list(rt.proc_ids), rt.key), daemon=True).start()
+        threading.Thread(target=self._reap_later, args=(list(rt.proc_ids), rt.owner), daemon=True).start()
         rt.deleted = True
 
     def _reap_later(self, ids, owner):
@@ -290,7 +328,7 @@ class Kubelet:
         if rt.stage == "done":
             return
         if rt.stage == "admit":
-            if not self._admit(pod, rt):
+            if not self._previous_incarnation_gone(pod, rt, procs) or not self._admit(pod, rt):
                 return
             rt.stage = "init"
             rt.started_at = now_rfc3339()
@@ -306,13 +344,43 @@ class Kubelet:
         if rt.stage == "run":
             self._report(pod, rt, procs)
 
+    def _previous_incarnation_gone(self, pod, rt, procs) -> bool:
+        """Restart gate: a pod of a job whose earlier pods were torn down
+        starts only once every process of those pods has exited.  Until
+        then an old master may still be serving the job's rendezvous store
+        on its port, and a new replica would join THAT world (the cause of
+        the round-2 kill/rejoin stall, docs/multi_gpu.md "Restarts").  The
+        first pod admitted after the drain opens a new restart generation
+        for the job (PTO_RESTART_GENERATION), and if something outside the
+        job still holds its port, the job moves to a fresh one."""
+        jk = rt.job_key
+        ids = self.retired.get(jk)
+        if ids:
+            live = sorted(i for i in ids if (procs.get(i) or {}).get("state") == "running")
+            if live:
+                self._write_status(pod, rt, {"phase": "Pending", "conditions": [
+                    {"type": "PodScheduled", "status": "False", "reason": "PreviousIncarnationRunning",
+                     "message": f"waiting for {len(live)} process(es) of the job's previous pods to exit"}]})
+                return False
+            del self.retired[jk]
+            self._drained.add(jk)
+        if jk in self._drained:
+            self._drained.discard(jk)
+            self.job_gen[jk] = self.job_gen.get(jk, 0) + 1
+            port = self.job_ports.get(jk)
+            peers = [r for r in self.pods.values() if r.job_key == jk and r is not rt and r.stage in ("init", "run")]
+            if port is not None and not peers and not _port_free(port):
+                log.warning("job %s: port %d still bound after its pods exited; taking a new one", jk, port)
+                self._drop_job_port(jk)
+        return True
+
     def _admit(self, pod, rt) -> bool:
         n = sum(gpus_requested(c) for c in pod.get("spec", {}).get("containers") or [])
         ann = pod["metadata"].get("annotations") or {}
         group = ann.get(C.ANNOTATION_GANG_GROUP)
         if n == 0 and not group:
             return True
-        requests = [{"owner": rt.key, "count": n, "hbm": _pod_hbm(pod)}]
+        requests = [{"owner": rt.owner, "count": n, "hbm": _pod_hbm(pod)}]
         if group:
             members = [p for p in self.pod_informer.list(namespace_of(pod))
                        if (p["metadata"].get("annotations") or {}).get(C.ANNOTATION_GANG_GROUP) == group]
@@ -324,13 +392,13 @@ class Kubelet:
             if len(members) < min_member:
                 self._set_unschedulable(pod, rt, f"{len(members)}/{min_member} gang members present")
                 return False
-            requests = [{"owner": key_of(m), "count": sum(gpus_requested(c) for c in m["spec"].get("containers", [])),
+            requests = [{"owner": _owner(m), "count": sum(gpus_requested(c) for c in m["spec"].get("containers", [])),
                          "hbm": _pod_hbm(m)} for m in members]
         r = self.agent.alloc(requests)
         if not r.get("ok"):
             self._set_unschedulable(pod, rt, r.get("error", "insufficient amd.com/gpu"))
             return False
-        rt.gpus = list(r["assigned"].get(rt.key, []))
+        rt.gpus = list(r["assigned"].get(rt.owner, []))
         return True
 
     def _set_unschedulable(self, pod, rt, msg):
@@ -351,7 +419,7 @@ class Kubelet:
                     return False
                 rt.init_index += 1
                 continue
-            pid = f"{rt.key}/init/{c.get('name')}"
+            pid = f"{rt.owner}/init/{c.get('name')}"
             st = procs.get(pid)
             if st is None:
                 self._spawn(pod, rt, c, pid, restart_policy="Never")
@@ -420,14 +488,17 @@ class Kubelet:
         gets the port they rendezvous on; a job whose pods are all gone (or
         re-submitted later) takes a fresh reservation."""
         live = {self._job_key(p) for p in pods}
-        for jk in [jk for jk in self.job_ports if jk not in live]:
-            port = self.job_ports.pop(jk)
-            fd = self._port_locks.pop(port, None)
-            if fd is not None:
-                try:
-                    os.close(fd)  # drops the flock
-                except OSError:
-                    pass
+        for jk in [jk for jk in self.job_ports if jk not in live and jk not in self.retired]:
+            self._drop_job_port(jk)
+
+    def _drop_job_port(self, jk):
+        port = self.job_ports.pop(jk)
+        fd = self._port_locks.pop(port, None)
+        if fd is not None:
+            try:
+                os.close(fd)  # drops the flock
+            except OSError:
+                pass
 
     def _resolve_env(self, pod, c, rt) -> dict:
         env = {k: v for k, v in os.environ.items() if not k.startswith(("MASTER_", "RANK", "WORLD_SIZE",
@@ -455,7 +526,10 @@ class Kubelet:
         # GPU pinning (module doc): one process per allocated GPU
         if gpus_requested(c) > 0 or rt.gpus:
             mine = sorted({g // self.gpu_share for g in rt.gpus})  # allocator slot -> device
-            if self.gpu_visibility == "node":
+            mode = (pod["metadata"].get("annotations") or {}).get(GPU_VISIBILITY_ANNOTATION) or self.gpu_visibility
+            if mode not in GPU_VISIBILITY_MODES:
+                mode = self.gpu_visibility
+            if mode == "node":
                 n = int(self.agent.gpus()["count"]) // self.gpu_share
                 env["HIP_VISIBLE_DEVICES"] = _physical_ids(list(range(n)))
                 env["LOCAL_RANK"] = str(mine[0] if mine else 0)
@@ -481,6 +555,7 @@ class Kubelet:
         # resolver times out, every rank of a 4-replica job was seen stuck in
         # the ProcessGroupGloo constructor for minutes)
         env.setdefault("GLOO_SOCKET_IFNAME", "lo")
+        env["PTO_RESTART_GENERATION"] = str(self.job_gen.get(rt.job_key, 0))
         env["PTO_POD_NAME"] = name_of(pod)
         env["PTO_NAMESPACE"] = namespace_of(pod)
         env["PTO_JOB_NAME"] = (pod["metadata"].get("labels") or {}).get(C.LABEL_JOB_NAME, "")
@@ -500,7 +575,7 @@ class Kubelet:
             argv[0] = sys.executable
         return argv
 
-    def _spawn(self, pod, rt, c, pid, restart_policy):
+    def _spawn(self, pod, rt, c, pid, restart_policy, group=""):
         log_path = self._log_path(pod) if c.get("name") == C.DEFAULT_CONTAINER_NAME else \
             self._log_path(pod, c.get("name"))
         try:
@@ -516,9 +591,14 @@ class Kubelet:
         # store server hung in its constructor (observed on the GPU box:
         # master stuck in _create_c10d_store while the 3 workers had
         # connected; replicas that are only store clients were fine).
-        hosts_store = env.get("RANK") == "0" and int(env.get("WORLD_SIZE", "1") or 1) > 1
+        multi = int(env.get("WORLD_SIZE", "1") or 1) > 1
+        hosts_store = env.get("RANK") == "0" and multi
+        # the replicas of a multi-rank job restart in place as one group
+        # (node_agent.cpp "restart groups"): a DDP world cannot take back a
+        # single restarted rank
         self.agent.spawn(pid, argv, env=env, cwd=c.get("workingDir") or REPO_ROOT,
-                         log=log_path, restart_policy=restart_policy, launcher="exec" if hosts_store else "auto")
+                         log=log_path, restart_policy=restart_policy, launcher="exec" if hosts_store else "auto",
+                         group=rt.job_key if (group and multi) else "")
         rt.proc_ids.append(pid)
         if c.get("name") == C.DEFAULT_CONTAINER_NAME:
             eff = {k: env[k] for k in _EFFECTIVE_KEYS if k in env}
@@ -527,13 +607,14 @@ class Kubelet:
     def _start_containers(self, pod, rt):
         policy = pod.get("spec", {}).get("restartPolicy") or "Always"
         for c in pod["spec"].get("containers") or []:
-            self._spawn(pod, rt, c, f"{rt.key}/{c.get('name')}", restart_policy=policy)
+            self._spawn(pod, rt, c, f"{rt.owner}/{c.get('name')}", restart_policy=policy,
+                        group=rt.job_key if self.group_restarts else "")
 
     def _report(self, pod, rt, procs):
         statuses = []
         running = terminated_ok = terminated_bad = waiting = 0
         for c in pod["spec"].get("containers") or []:
-            st = procs.get(f"{rt.key}/{c.get('name')}")
+            st = procs.get(f"{rt.owner}/{c.get('name')}")
             cs = {"name": c.get("name"), "image": c.get("image"), "restartCount": 0, "ready": False}
             if st is None:
                 cs["state"] = {"waiting": {"reason": "ContainerCreating"}}
@@ -583,7 +664,7 @@ class Kubelet:
         self._write_status(pod, rt, status)
         if phase in ("Succeeded", "Failed"):
             rt.stage = "done"
-            self.agent.free(rt.key)
+            self.agent.free(rt.owner)
 
     def _read_metrics(self, pod, rt):
         """Tail the trainer's metrics stream ($PTO_METRICS_FILE): first
@@ -683,8 +764,14 @@ class Kubelet:
         """SIGKILL (or other signal) a running replica: the fault-injection
         hook for the kill/rejoin path.  The process may be
         restarted by its restart policy (exit 137 is retryable)."""
-        pid = f"{namespace}/{name}/{container}"
-        return self.agent.kill(pid, signal=signal, restartable=True)
+        rt = self.pods.get(f"{namespace}/{name}")
+        if rt is None:
+            raise KeyError(f"pod {namespace}/{name} is not running on this node")
+        return self.agent.kill(f"{rt.owner}/{container}", signal=signal, restartable=True)
+
+
+def _owner(pod) -> str:
+    return f"{key_of(pod)}@{pod['metadata'].get('uid', '')}"
 
 
 def read_hbm(sysfs_root: str = "/sys") -> list[tuple[str, int, int]]:

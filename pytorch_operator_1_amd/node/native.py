@@ -106,11 +106,14 @@ class AgentClient:
         return r
 
     # convenience wrappers
-    def spawn(self, id, argv, env=None, cwd=None, log=None, restart_policy="Never", cpus=None, launcher="auto"):
+    def spawn(self, id, argv, env=None, cwd=None, log=None, restart_policy="Never", cpus=None, launcher="auto",
+              group=""):
         """``launcher``: "auto" (zygote when eligible) or "exec" (always
-        fork/exec a fresh interpreter)."""
+        fork/exec a fresh interpreter).  ``group``: restart group -- a failed
+        member that is restarted takes every other member down with it and
+        the whole group restarts together (node_agent.cpp, restart groups)."""
         return self.ok("spawn", id=id, argv=list(argv), env=dict(env or {}), cwd=cwd or "", log=log or "",
-                       restart_policy=restart_policy, cpus=list(cpus or []), launcher=launcher)
+                       restart_policy=restart_policy, cpus=list(cpus or []), launcher=launcher, group=group or "")
 
     def kill(self, id, signal=15, grace=10.0, restartable=False):
         return self.call("kill", id=id, signal=signal, grace=grace, restartable=restartable)

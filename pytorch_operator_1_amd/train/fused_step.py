@@ -578,6 +578,10 @@ class FusedMnistTrainer:
         snap = [t.clone() for t in state]
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
+        # the xGMI barriers spin for PTO_XGMI_TIMEOUT_MS only: every rank
+        # arrives here after its own checkpoint load / earlier captures, so
+        # they line up on the host first (skew > 500 ms tripped it)
+        self._align_ranks("warmup")
         with torch.cuda.stream(s):
             self._eager_step()
         torch.cuda.current_stream(self.device).wait_stream(s)
@@ -620,12 +624,14 @@ class FusedMnistTrainer:
             # peers, which replay the same graphs)
             torch.cuda.synchronize(self.device)
             snap = [t.clone() for t in state]
+            self._align_ranks("warm-replay")
             for g in list(self._graph_pow.values()) + list(self._graph_close.values()):
                 g.replay()
             torch.cuda.synchronize(self.device)
             for dst, src in zip(state, snap):
                 dst.copy_(src)
             torch.cuda.synchronize(self.device)
+            self._align_ranks("captured")
         else:  # split: collectives outside the graphs, overlapped with conv bwd
             ga, gb, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(ga):
@@ -636,6 +642,14 @@ class FusedMnistTrainer:
                 self.optimizer_step()
             graphs = [ga, gb, gc]
         self._graphs = graphs
+
+    def _align_ranks(self, tag: str):
+        """Host-side barrier before device work whose cross-rank spins are
+        short-bounded (the xGMI all-reduce); a no-op otherwise."""
+        if self._xgmi is not None:
+            from ..utils import dist as pdist
+
+            pdist.host_barrier(tag=f"xgmi-{tag}")
 
     def _graph_sizes(self) -> list[int]:
         if self.fused_opt and self._close_graphs:

@@ -98,8 +98,47 @@ def init_distributed(backend: str | None = None, use_gpu: bool | None = None,
         kwargs = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kwargs["device_id"] = device
+        store = generation_store(env, timeout_s)
+        if store is not None:
+            kwargs.update(store=store, rank=env.rank, world_size=env.world_size)
         dist.init_process_group(**kwargs)
     return env, device
+
+
+class StaleRendezvous(RuntimeError):
+    """This replica reached the rendezvous store of another restart
+    generation (an old incarnation's master still serving the port)."""
+
+
+GENERATION_KEY = "pto/restart-generation"
+
+
+def generation_store(env: DistEnv, timeout_s: float):
+    """Rendezvous store of one restart generation, or None outside the
+    operator (no ``PTO_RESTART_GENERATION``: plain ``env://``).
+
+    The node manager tags every restart wave of a job with
+    ``PTO_RESTART_GENERATION`` (node/kubelet.py, "Restarts").  Rank 0 hosts
+    the TCPStore and publishes its generation; every other rank connects,
+    reads it, and refuses a store of a different generation
+    (:class:`StaleRendezvous`, which the trainers turn into the retryable
+    exit) instead of joining an old world.  Every key of the process group
+    and of the trainers (resume path, host barriers) lives under the
+    generation's prefix, so nothing of an earlier wave is ever read."""
+    gen = os.environ.get("PTO_RESTART_GENERATION")
+    if gen is None or not env.is_distributed:
+        return None
+    store = dist.TCPStore(env.master_addr, env.master_port, env.world_size, env.is_master,
+                          timeout=datetime.timedelta(seconds=timeout_s), wait_for_workers=False,
+                          use_libuv=os.environ.get("USE_LIBUV", "1") == "1")
+    if env.is_master:
+        store.set(GENERATION_KEY, gen)
+    else:
+        theirs = store.get(GENERATION_KEY).decode()
+        if theirs != gen:
+            raise StaleRendezvous(f"rendezvous at {env.master_addr}:{env.master_port} belongs to restart "
+                                  f"generation {theirs}, this replica is generation {gen}")
+    return dist.PrefixStore(f"pto/g{gen}", store)
 
 
 def barrier(device: torch.device | None = None) -> None:
@@ -120,13 +159,13 @@ def host_barrier(timeout_s: float | None = None, tag: str = "hb") -> None:
     short spin timeouts (the xGMI all-reduce): no rank launches its next
     chunk of steps before every rank is back.  A rank that died makes the
     others raise after ``timeout_s`` (``PTO_HOST_BARRIER_TIMEOUT``, default
-    60 s) instead of blocking until the process-group timeout; the caller
+    30 s) instead of blocking until the process-group timeout; the caller
     maps that to the retryable exit."""
     global _host_barrier_seq
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return
     if timeout_s is None:
-        timeout_s = float(os.environ.get("PTO_HOST_BARRIER_TIMEOUT", "60"))
+        timeout_s = float(os.environ.get("PTO_HOST_BARRIER_TIMEOUT", "30"))
     store = dist.distributed_c10d._get_default_store()
     _host_barrier_seq += 1
     key = f"pto/{tag}/{_host_barrier_seq}"

@@ -5,6 +5,11 @@ import pytest
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+# multi-process operator tests (minutes, many replicas): run after every
+# kernel / graph / collective numerics test, so one stalled job can never
+# hide the numerics results behind `-x`
+_LAST = ("test_e2e_gpu.py", "test_e2e_cpu.py", "test_restart_wave.py")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device); run with -m gpu")
@@ -12,6 +17,7 @@ def pytest_configure(config):
 
 
 def pytest_collection_modifyitems(config, items):
+    items.sort(key=lambda it: 1 if os.path.basename(str(it.fspath)) in _LAST else 0)  # stable
     import torch
 
     if torch.cuda.is_available():

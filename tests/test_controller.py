@@ -174,8 +174,12 @@ def test_running_then_succeeded_marks_running_false():
     assert h.pc.metrics.jobs_successful._value.get() == 1
 
 
-def test_exitcode_retryable_restarts():
-    h = Harness()
+@pytest.mark.parametrize("scope", ["job", "pod"])
+def test_exitcode_retryable_restarts(scope):
+    """A retryable failure -> Restarting.  ``pod`` scope (the reference,
+    pod.go:91-109) deletes only the failed pod; the default ``job`` scope
+    deletes every replica of the job in the same pass (restart wave)."""
+    h = Harness(restart_scope=scope)
     job = new_job("x", workers=2, restart_policy="ExitCode")
     j = h.add_job(job)
     h.set_pods(j, "Master", active=1)
@@ -185,10 +189,26 @@ def test_exitcode_retryable_restarts():
     last = h.last()
     assert last["status"]["conditions"][-1]["type"] == "Restarting"
     assert "restarting because 1 Worker replica(s) failed" in last["status"]["conditions"][-1]["message"]
-    assert h.pods.delete_pod_names == ["x-worker-0"]
+    if scope == "pod":
+        assert h.pods.delete_pod_names == ["x-worker-0"]
+    else:
+        assert sorted(h.pods.delete_pod_names) == ["x-master-0", "x-worker-0"]
     assert h.pc.metrics.jobs_restarted._value.get() == 1
     # pods created with restartPolicy Never for ExitCode
     assert all(t["spec"]["restartPolicy"] == "Never" for t in h.pods.templates)
+
+
+def test_exitcode_wave_not_started_by_permanent_failure():
+    """A permanent failure next to a retryable one fails the job; nothing
+    else is deleted for a restart."""
+    h = Harness()
+    j = h.add_job(new_job("p", workers=2, restart_policy="ExitCode"))
+    h.set_pods(j, "Master", failed=1, exit_code=1)
+    h.set_pods(j, "Worker", failed=1, exit_code=137)
+    h.set_services(j)
+    h.sync(j)
+    assert h.last()["status"]["conditions"][-1]["type"] == "Failed"
+    assert "p-master-0" not in h.pods.delete_pod_names and "p-worker-1" not in h.pods.delete_pod_names
 
 
 def test_exitcode_permanent_fails():

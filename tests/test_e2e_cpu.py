@@ -96,8 +96,33 @@ def test_exitcode_policy_kill_rejoin_resume(cluster, tmp_path):
            if e["involvedObject"]["name"] == "elastic"]
     assert "PyTorchJobRestarting" in evs or "ExitedWithCode" in evs
     assert any(f.startswith("ckpt-") for f in os.listdir(ck))
-    log0 = cluster.pod_log("default", "elastic-worker-0")
-    assert "Resumed from" in log0
+    for pod in ("elastic-master-0", "elastic-worker-0"):  # the whole world was recreated and resumed
+        assert "Resumed from" in cluster.pod_log("default", pod), pod
+
+
+def test_onfailure_kill_rejoin_every_rank_resumes(cluster, tmp_path):
+    """BASELINE config 5 as worded: restartPolicy OnFailure, Master=1
+    Worker=1.  Worker 0 SIGKILLs itself mid-epoch; the node agent's restart
+    group stops the master too and restarts both in place together (new
+    restart generation), they agree on the step-10 checkpoint, resume, and
+    the job succeeds with restartCount >= 1 on the killed pod."""
+    import re
+
+    ck = str(tmp_path / "ckpt")
+    job = _mnist_job("onfail", 1, extra=["--checkpoint-dir", ck, "--checkpoint-interval", "5", "--fail-at-step",
+                                         "12", "--fail-rank", "1", "--max-steps", "30"], restart="OnFailure")
+    job["spec"]["backoffLimit"] = 6
+    cluster.submit(job)
+    j = cluster.wait_for_condition("onfail", timeout=300)
+    logs = {n: cluster.pod_log("default", n) for n in ("onfail-master-0", "onfail-worker-0")}
+    assert j["status"]["conditions"][-1]["type"] == "Succeeded", (j["status"], logs)
+    for n, log in logs.items():
+        m = re.search(r"Resumed from \S+ at step (\d+)", log)
+        assert m and int(m.group(1)) == 10, (n, log[-2000:])
+        assert "[fault-injection]" in log or n.startswith("onfail-master"), n
+    pod = cluster.store.get("pods", "default", "onfail-worker-0")
+    assert pod["status"]["containerStatuses"][0]["restartCount"] >= 1
+    assert pod["status"]["phase"] == "Succeeded"
 
 
 def test_clean_pod_policy_running_and_delete_cascade(cluster):
