@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void k_sum(const float* __restrict__ x, float*
 }
 
 // Empty kernel: measures the cost of one more launch boundary inside a
-// replayed graph (tools: PTO_PROBE_NOOPS in fused_step.py).
+// replayed graph (tools/kernel_floor_probe.py, tools/graph_launch_probe.py).
 __global__ void k_noop(int* p) {
   if (p && threadIdx.x == 0 && blockIdx.x == 0) *p = 0;
 }

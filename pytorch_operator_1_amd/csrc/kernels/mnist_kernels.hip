@@ -1,17 +1,20 @@
 // Fused fp32 kernels for the reference MNIST CNN training step on gfx950.
 //
 // Workload parity: reference examples/mnist/mnist.py:17-43 (Net + SGD step);
-// op inventory K1..K10 in SURVEY.md §2.9.  The step is 8 launches:
+// op inventory K1..K10 in SURVEY.md §2.9.  The training step is 4 launches
+// (train/fused_step.py):
 //
-//   F1 conv1+bias+ReLU+maxpool (VALU direct conv, K=25 too small for MFMA)
-//   F2 conv2+bias+ReLU+maxpool (MFMA implicit GEMM, pool done in-register)
-//   F3 fc1+bias+ReLU            (MFMA, split-K over the 4 waves of a block)
-//   F4 fc2+log_softmax+NLL+dlogits+dh1 (one wave per row, fully fused)
-//   B3 fc1/fc2 weight+bias grads and d(a2p)  (one launch, 4 block ranges)
-//   B2 conv2 wgrad (split-K atomics), dgrad via col2im in LDS, conv2 bias
-//   B1 conv1 wgrad+bias (ReLU/pool mask applied on the fly)
-//   SGD fused momentum update over the flat parameter buffer
-//       (common_kernels.hip; it also advances the device batch cursor)
+//   F12  conv1+bias+ReLU+maxpool (VALU) and conv2+bias+ReLU+maxpool (MFMA
+//        implicit GEMM, pool in registers), k_conv12_fwd2_t
+//   F3   fc1+bias+ReLU (MFMA, split-K over 16 waves), k_linear_fwd_vec16
+//   F4dx fc2+log_softmax+NLL+dlogits+dh1 on the matrix cores, then
+//        d(a2p) = dh1 W1 per tile, k_fc2_ce_dx_mf
+//   B    the whole backward (+ every parameter update in the one-process
+//        schedule), k_bwd_all
+//
+// The single-op kernels (k_conv1_fwd, k_conv2_fwd, k_fc2_ce, k_conv2_bwd,
+// k_conv1_bwd, ...) serve the evaluation pass and the autograd module path
+// (ops/nn.py).
 //
 // Pool/ReLU backward never materialises a scattered tensor: each pooled
 // output stores a 1-byte argmax code (0..3 = window position, 4 = no
@@ -30,7 +33,6 @@
 // the dataset without any copy kernels.
 #include "mfma_f32.h"
 #include "sgd_f32.h"
-#include <stdlib.h>
 
 namespace {
 
@@ -56,16 +58,16 @@ PTO_DEV const float* batch_ptr(const float* base, const long long* bidx, int per
 // "Fused optimizer" schedule of the single-process step (no gradient
 // all-reduce between backward and the update): the optimizer runs inside
 // launches that already exist instead of a separate SGD launch.
-//   * fc + conv2 parameters: their grads are final after B3 / B2 and no
-//     later launch of the step reads those parameters, so extra blocks of
-//     the B1 launch update them (k_conv1_bwd_sgd).
-//   * conv1 parameters: their grads are final only when B1 ends, and F1
-//     of the NEXT step is their first reader.  F1 applies the pending update
-//     on the fly while staging the weights (LazyConv1), and F4 of that step
-//     (which does not read conv1) commits it: p, m written, g zeroed
-//     (Conv1Commit).  `pending` (set by B3) says whether an update is owed;
-//     the host flushes it before anyone reads the parameters.
-//   * batch cursor: F4 snapshots it for B1, B3 advances it.
+//   * fc + conv2 parameters: updated inside k_bwd_all by the block that
+//     finishes their gradient (no later launch of the step reads them).
+//   * conv1 parameters: their grads are final only when k_bwd_all ends, and
+//     F12 of the NEXT step is their first reader.  F12 applies the pending
+//     update on the fly while staging the weights (LazyConv1), and F4dx of
+//     that step (which does not read conv1) commits it: p, m written, g
+//     zeroed (Conv1Commit).  `pending` (set by k_bwd_all) says whether an
+//     update is owed; the host flushes it before anyone reads the parameters.
+//   * batch cursor: advanced by k_bwd_all (nothing later in the step reads
+//     it: F12 copied the images out for the backward).
 struct LazyConv1 {
   const float* g;       // flat conv1 grads: weights [0, 500), bias [bias_off, +20)
   const float* m;       // flat conv1 momentum, same layout
@@ -86,8 +88,6 @@ struct Conv1Commit {
   int n;                // multiple of 4
   const int* pending;   // nullptr: no commit
   SgdArgs a;
-  const long long* bidx;
-  long long* bidx_snap;
   float* rep;           // extra gradient replicas, summed into the update and re-zeroed
   int nrep, rep_stride;
 };
@@ -274,156 +274,21 @@ __global__ __launch_bounds__(256) void k_conv2_fwd(const float* __restrict__ a1p
 
 // -------------------------------------------------------------- F1+F2 ----
 // conv1 and conv2 forward in ONE launch.  Block = (sample, 16-channel conv2
-// tile); each block recomputes the sample's whole pooled conv1 map straight
-// into LDS (2880 outputs x 100 FMAs, ~1 us of VALU: cheaper than a kernel
-// boundary) and the nt == 0 block also writes it (+ argmax codes) to HBM
-// for the backward pass.  Then the conv2 implicit GEMM of k_conv2_fwd.
-__global__ __launch_bounds__(256) void k_conv12_fwd(const float* __restrict__ x, const float* __restrict__ w1,
-                                                    const float* __restrict__ b1, const float* __restrict__ w2,
-                                                    const float* __restrict__ b2, float* __restrict__ a1p,
-                                                    uint8_t* __restrict__ code1, float* __restrict__ a2p,
-                                                    uint8_t* __restrict__ code2, int B,
-                                                    const long long* __restrict__ bidx, LazyConv1 lz) {
-  __shared__ float ws[16 * WS_LD];
-  __shared__ __attribute__((aligned(16))) float in_s[A1P];
-  __shared__ __attribute__((aligned(16))) float xs[784];
-  __shared__ float w1s[C1 * 25 + C1];
-  const int b = blockIdx.x >> 2, nt = blockIdx.x & 3;
-  const int tid = threadIdx.x;
-  {
-    x = batch_ptr(x, bidx, B * 784);
-    const int nrows = min(16, C2 - nt * 16);
-    const float4* wsrc = reinterpret_cast<const float4*>(w2 + nt * 16 * 500);
-    float4 wv[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int e = tid + 256 * q;
-      wv[q] = (e < nrows * 125) ? wsrc[e] : float4{0.f, 0.f, 0.f, 0.f};
-    }
-    const float4 xv = tid < 196 ? reinterpret_cast<const float4*>(x + b * 784)[tid] : float4{0.f, 0.f, 0.f, 0.f};
-    float wq[3], gq[3], mq[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int e = tid + 256 * q;
-      wq[q] = e < C1 * 25 ? w1[e] : (e < C1 * 26 ? b1[e - C1 * 25] : 0.f);
-    }
-    // the previous step's conv1 update, loaded in the same memory round
-    int pend = 0;
-    float lr = 0.f;
-    if (lz.pending) {
-      pend = *lz.pending;
-      lr = *lz.a.lr;
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int e = tid + 256 * q;
-        const int fi = e < C1 * 25 ? e : lz.bias_off + (e - C1 * 25);
-        const float gsum = rep_sum(lz.rep, lz.nrep, lz.rep_stride, e < C1 * 26 ? fi : 0, e < C1 * 26,
-                                   e < C1 * 26 ? lz.g[fi] : 0.f);
-        gq[q] = gsum;
-        mq[q] = e < C1 * 26 ? lz.m[fi] : 0.f;
-      }
-    }
-    if (pend) {
-#pragma unroll
-      for (int q = 0; q < 3; ++q) sgd_elem(wq[q], gq[q], mq[q], lr, lz.a.mom, lz.a.wd, lz.a.gscale, lz.a.nesterov);
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int e = tid + 256 * q;
-      if (e < 2000) {
-        const int row = e / 125, col = (e - row * 125) * 4;
-        float* d = ws + row * WS_LD + col;
-        d[0] = wv[q].x; d[1] = wv[q].y; d[2] = wv[q].z; d[3] = wv[q].w;
-      }
-    }
-    if (tid < 196) reinterpret_cast<float4*>(xs)[tid] = xv;
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-      if (tid + 256 * q < C1 * 26) w1s[tid + 256 * q] = wq[q];
-  }
-  __syncthreads();
-  // conv1 + bias + ReLU + pool: item = (4-channel group, pooled pixel)
-  for (int it = tid; it < 5 * 144; it += 256) {
-    const int cg = it / 144, pix = it - cg * 144;
-    const int ph = pix / 12, pw = pix - ph * 12;
-    float p[6][6];
-#pragma unroll
-    for (int r = 0; r < 6; ++r)
-#pragma unroll
-      for (int c = 0; c < 6; ++c) p[r][c] = xs[(2 * ph + r) * 28 + 2 * pw + c];
-#pragma unroll
-    for (int cc = 0; cc < 4; ++cc) {
-      const int oc = cg * 4 + cc;
-      const float* wc = w1s + oc * 25;
-      float v[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int dy = q >> 1, dx = q & 1;
-        float sacc = w1s[C1 * 25 + oc];
-#pragma unroll
-        for (int kh = 0; kh < 5; ++kh)
-#pragma unroll
-          for (int kw = 0; kw < 5; ++kw) sacc = fmaf(p[dy + kh][dx + kw], wc[kh * 5 + kw], sacc);
-        v[q] = sacc;
-      }
-      float o;
-      uint8_t cd;
-      relu_pool4(v, o, cd);
-      in_s[oc * 144 + pix] = o;
-      if (nt == 0) {
-        a1p[b * A1P + oc * 144 + pix] = o;
-        code1[b * A1P + oc * 144 + pix] = cd;
-      }
-    }
-  }
-  __syncthreads();
-  const int t = tid >> 6, lane = tid & 63;
-  const int i = lane & 15, g = lane >> 4;
-  const int pw = i >> 2, dy = (i >> 1) & 1, dx = i & 1;
-  const int n = nt * 16 + (lane & 15);
-  const float* wl = ws + (lane & 15) * WS_LD + 5 * g;
-  const float* il = in_s + (2 * t + dy) * 12 + 2 * pw + dx;
-  f32x4 acc0 = zero4(), acc1 = zero4();
-#pragma unroll
-  for (int G = 0; G < 25; ++G) {
-    const int R = 4 * G + g;
-    const int ic = R / 5, kh = R - ic * 5;
-    const float* arow = il + ic * 144 + kh * 12;
-    const float* brow = wl + 20 * G;
-    acc0 = mfma16x16x4(arow[0], brow[0], acc0);
-    acc1 = mfma16x16x4(arow[1], brow[1], acc1);
-    acc0 = mfma16x16x4(arow[2], brow[2], acc0);
-    acc1 = mfma16x16x4(arow[3], brow[3], acc1);
-    acc0 = mfma16x16x4(arow[4], brow[4], acc0);
-  }
-  const f32x4 acc = acc0 + acc1;
-  if (n >= C2 || b >= B) return;
-  const float bn = b2[n];
-  float v[4] = {acc[0] + bn, acc[1] + bn, acc[2] + bn, acc[3] + bn};
-  float o;
-  uint8_t cd;
-  relu_pool4(v, o, cd);
-  const int oi = b * F1IN + n * 16 + t * 4 + (lane >> 4);
-  a2p[oi] = o;
-  code2[oi] = cd;
-}
-
-// F1+F2, 512-thread version: the same work as k_conv12_fwd laid out for
-// two waves per SIMD.
-//  * conv1: a wave owns (4-channel group, 64 pooled pixels), so its 100
-//    weights + 4 biases are wave-uniform: read ONCE per task from LDS as
-//    broadcast ds_read_b128 into VGPRs (channel rows padded to 28 floats),
-//    instead of 100 ds_read_b32 per pooled pixel; the 6x6 input patch is 18
-//    ds_read_b64.
-//  * conv2 GEMM: K split over the two halves of the block (waves w and w+4
-//    own the same pooled row), partial tiles combined through LDS, so each
-//    SIMD interleaves two independent MFMA chains.
+// tile), 1024 threads; each block recomputes the sample's whole pooled conv1
+// map straight into LDS (2880 outputs x 100 FMAs: cheaper than a kernel
+// boundary) and the nt == 0 block also writes it (+ argmax codes) to HBM for
+// the backward pass.
+//  * conv1: a wave owns (2-channel pair, 64 pooled pixels), so its weights
+//    are wave-uniform: read ONCE per task from LDS as broadcast ds_read_b128
+//    into VGPRs (channel rows padded to 28 floats); the 6x6 input patch is 18
+//    ds_read_b64.  The last 16 pixels of each 4-channel group run as quarter
+//    tasks (lane = channel*16 + pixel): 20 full + 5 quarter tasks.
+//  * conv2 implicit GEMM (k_conv2_fwd's lane maps): K split over the four
+//    wave sets (7+6+6+6 groups of 5 MFMAs), partial tiles combined through
+//    LDS, so each SIMD interleaves independent MFMA chains.
+//  * lazy conv1 update (one-process schedule, LazyConv1), the image copy
+//    for the backward (xout) and the conv2.weight snapshot (w2out).
 constexpr int W1LD = 28;
-// Balanced layout's task slots per wave (waves w and w+4 share a SIMD): per
-// SIMD 3 full, 3 full, 2 full + 3 quarter, 2 full + 2 quarter tasks
-// (1200/1200/1100/1000 FMA units vs 1300/1300/1000/900 for task += 8).
-__constant__ signed char kConv1Slots[8][3] = {{0, 1, -1}, {3, 4, -1},  {6, 10, 11}, {8, 13, -1},
-                                              {2, -1, -1}, {5, -1, -1}, {7, 12, -1}, {9, 14, -1}};
 template <int NTH>
 __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__ x, const float* __restrict__ w1,
                                                      const float* __restrict__ b1, const float* __restrict__ w2,
@@ -511,23 +376,15 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
   // chunks; tasks 10-14 = the last 16 pixels of one channel group with the
   // group's 4 channels spread over the lanes (lane = channel*16 + pixel), a
   // quarter of a full task's FMAs instead of a full task's lockstep cost.
-  const bool bal = NTH == 1024 || !(lz.a.variant & 2);  // bit 2: legacy 15-task layout (512 threads)
-  const bool slots = NTH == 512 && bal && (lz.a.variant & 4);
-  // 1024 threads: full tasks hold 2 channels' weights (VGPR budget of 4
-  // waves/SIMD): 20 full tasks (10 channel pairs x 2 chunks) + 5 quarter
-  // tasks, 25 over 16 waves.  512 threads: 4-channel tasks, 10 + 5.
-  constexpr int CPT = NTH == 1024 ? 2 : 4;
-  constexpr int NFULL = 2 * C1 / CPT, NTASK = NTH == 1024 ? NFULL + 5 : 15;
-  for (int si = 0; si < 3; ++si) {
-    int task;
-    if (slots) {
-      task = kConv1Slots[wid][si];
-      if (task < 0) break;
-    } else {
-      task = wid + NWV * si;
-      if (task >= NTASK) break;
-    }
-    if (bal && task >= NFULL) {
+  // full tasks hold 2 channels' weights (VGPR budget of 4 waves/SIMD): 20
+  // full tasks (10 channel pairs x 2 chunks) + 5 quarter tasks over 16 waves
+  static_assert(NTH == 1024, "F12 is laid out for 16 waves");
+  constexpr int CPT = 2;
+  constexpr int NFULL = 2 * C1 / CPT, NTASK = NFULL + 5;
+  for (int si = 0; si < 2; ++si) {
+    const int task = wid + NWV * si;
+    if (task >= NTASK) break;
+    if (task >= NFULL) {
       const int oc = (task - NFULL) * 4 + (lane >> 4), pix = 128 + (lane & 15);
       float wr1[W1LD];
 #pragma unroll
@@ -567,8 +424,8 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
       }
       continue;
     }
-    const int cg = bal ? task >> 1 : task / 3;
-    const int pix = (bal ? (task & 1) : task - cg * 3) * 64 + lane;
+    const int cg = task >> 1;
+    const int pix = (task & 1) * 64 + lane;
     float wr[CPT][W1LD], bz[CPT];
 #pragma unroll
     for (int cc = 0; cc < CPT; ++cc) {
@@ -590,7 +447,6 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
         p[r][c] = v.x;
         p[r][c + 1] = v.y;
       }
-    const bool skip1 = lz.a.variant & 8;  // timing probe (PTO_F12_PROBE): no conv1 FMAs
 #pragma unroll
     for (int cc = 0; cc < CPT; ++cc) {
       const int oc = cg * CPT + cc;
@@ -599,12 +455,10 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
       for (int q = 0; q < 4; ++q) {
         const int dy = q >> 1, dx = q & 1;
         float sacc = bz[cc];
-        if (!skip1) {
 #pragma unroll
-          for (int kh = 0; kh < 5; ++kh)
+        for (int kh = 0; kh < 5; ++kh)
 #pragma unroll
-            for (int kw = 0; kw < 5; ++kw) sacc = fmaf(p[dy + kh][dx + kw], wr[cc][kh * 5 + kw], sacc);
-        }
+          for (int kw = 0; kw < 5; ++kw) sacc = fmaf(p[dy + kh][dx + kw], wr[cc][kh * 5 + kw], sacc);
         v[q] = sacc;
       }
       float o;
@@ -638,8 +492,7 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
     acc1 = mfma16x16x4(arow[3], brow[3], acc1);
     acc0 = mfma16x16x4(arow[4], brow[4], acc0);
   };
-  if (lz.a.variant & 16) {  // timing probe: no conv2 MFMAs
-  } else if (NPART == 2) {
+  if (NPART == 2) {
     if (half == 0) {
 #pragma unroll
       for (int G = 0; G < 13; ++G) group(G);
@@ -703,20 +556,11 @@ __global__ __launch_bounds__(256) void k_linear_fwd(const float* __restrict__ x,
                                           EpiBiasRelu{bias, y, N, relu != 0});
 }
 
-// Same with float4 operand loads and K split over 8 waves (512 threads);
-// requires K % 4 == 0 and 16-byte aligned x / w (checked by the launcher).
-__global__ __launch_bounds__(512) void k_linear_fwd_vec(const float* __restrict__ x, const float* __restrict__ w,
-                                                        const float* __restrict__ bias, float* __restrict__ y, int M,
-                                                        int N, int K, int relu) {
-  __shared__ float red[8 * 256];
-  block_gemm_splitk<LAY_ROWK, LAY_ROWK, EpiBiasRelu, 8, true, true>(x, K, w, K, M, N, K, blockIdx.x, red,
-                                                                    EpiBiasRelu{bias, y, N, relu != 0});
-}
-
-// 16-wave variant (1024 threads, 4 waves per SIMD): each wave owns a 64-deep
-// K slice (NG = 4 groups, all 8 loads per lane in flight at once), so the
-// serial chain per wave is one memory round trip + 16 MFMAs instead of
-// 32.  Same tile count as k_linear_fwd_vec (fc1 at B=64: 128 blocks).
+// float4 operand loads, 16 waves (1024 threads, 4 waves per SIMD): each wave
+// owns a 64-deep K slice (NG = 4 groups, all 8 loads per lane in flight at
+// once), so the serial chain per wave is one memory round trip + 16 MFMAs
+// (fc1 at B=64: 128 blocks).  Requires K % 4 == 0 and 16-byte aligned x / w
+// (checked by the launcher).
 // XCD-aware tile order: workgroup i runs on XCD i % 8, so tile index
 // (i % 8) * (T / 8) + i / 8 puts T/8 consecutive tiles -- the m-tiles that
 // share one weight tile -- on one XCD, and each weight tile is fetched into
@@ -728,14 +572,12 @@ __global__ __launch_bounds__(1024) void k_linear_fwd_vec16(const float* __restri
                                                            int M, int N, int K, int relu) {
   __shared__ float red[16 * 256];
   const int mtiles = (M + 15) >> 4;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x, relu & 2);
+  const int tile = xcd_tile(blockIdx.x, gridDim.x, true);
   const int mt = tile % mtiles, nt = tile / mtiles;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int kc = (((K + 15) / 16) + 15) & ~15;
-  f32x4 acc = zero4();
-  if (!(relu & 4))  // bit 4: timing probe (PTO_FC1_PROBE), no loads / MFMAs
-    acc = wave_tile_16x16<LAY_ROWK, LAY_ROWK, 4, true, true>(x, K, w, K, M, N, K, mt * 16, nt * 16, wv * kc,
-                                                             (wv + 1) * kc);
+  const f32x4 acc = wave_tile_16x16<LAY_ROWK, LAY_ROWK, 4, true, true>(x, K, w, K, M, N, K, mt * 16, nt * 16,
+                                                                       wv * kc, (wv + 1) * kc);
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) red[wv * 256 + ((lane >> 4) * 4 + rr) * 16 + (lane & 15)] = acc[rr];
   __syncthreads();
@@ -745,7 +587,7 @@ __global__ __launch_bounds__(1024) void k_linear_fwd_vec16(const float* __restri
 #pragma unroll
     for (int q = 0; q < 16; ++q) v += red[q * 256 + t];
     const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
-    if (m < M && n < N) EpiBiasRelu{bias, y, N, (relu & 1) != 0}(m, n, v);
+    if (m < M && n < N) EpiBiasRelu{bias, y, N, relu != 0}(m, n, v);
   }
 }
 
@@ -782,8 +624,7 @@ __global__ __launch_bounds__(256) void k_relu_bwd(const float* __restrict__ g, c
 PTO_DEV void fc2_ce_row(int row, int lane, const float* __restrict__ h1, const float* __restrict__ w,
                         const float* __restrict__ bias, const int64_t* __restrict__ labels,
                         float* __restrict__ logp, float* __restrict__ loss_rows, float* __restrict__ dlogits,
-                        float* __restrict__ dh1, int B, float inv_b, const long long* __restrict__ bidx,
-                        float* dh1_row_lds = nullptr, bool halving = true) {
+                        float* __restrict__ dh1, int B, float inv_b, const long long* __restrict__ bidx) {
   float h[8], wv[NCLS][8], bz[NCLS];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -807,7 +648,7 @@ PTO_DEV void fc2_ce_row(int row, int lane, const float* __restrict__ h1, const f
     for (int j = 0; j < 8; ++j) s = fmaf(h[j], wv[c][j], s);
     z[c] = s;
   }
-  if (halving) {
+  {
     // recursive halving (10 sums padded to 16): 8+4+2+1 shuffles leave lane l
     // with class idx = bits 5..2 of l summed over 16 lanes, two butterflies
     // finish it, and each class is broadcast back with one readlane:
@@ -840,12 +681,6 @@ PTO_DEV void fc2_ce_row(int row, int lane, const float* __restrict__ h1, const f
       const int src = ((c >> 3) & 1) * 32 + ((c >> 2) & 1) * 16 + ((c >> 1) & 1) * 8 + (c & 1) * 4;
       z[c] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h1), src));
     }
-  } else {
-    // 10 butterfly reductions interleaved (independent chains)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-      for (int c = 0; c < NCLS; ++c) z[c] += __shfl_xor(z[c], o, 64);
   }
 #pragma unroll
   for (int c = 0; c < NCLS; ++c) z[c] += bz[c];
@@ -874,7 +709,7 @@ PTO_DEV void fc2_ce_row(int row, int lane, const float* __restrict__ h1, const f
       if (c == y) zy = z[c];
     loss_rows[row] = lse - zy;
   }
-  if (!dh1 && !dh1_row_lds) return;
+  if (!dh1) return;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int k = lane + 64 * j;
@@ -882,9 +717,7 @@ PTO_DEV void fc2_ce_row(int row, int lane, const float* __restrict__ h1, const f
       float s = 0.f;
 #pragma unroll
       for (int c = 0; c < NCLS; ++c) s = fmaf(dl[c], wv[c][j], s);
-      const float v = h[j] > 0.f ? s : 0.f;
-      if (dh1) dh1[row * F1OUT + k] = v;
-      if (dh1_row_lds) dh1_row_lds[k] = v;
+      dh1[row * F1OUT + k] = h[j] > 0.f ? s : 0.f;
     }
   }
 }
@@ -893,105 +726,23 @@ __global__ __launch_bounds__(256) void k_fc2_ce(const float* __restrict__ h1, co
                                                 const float* __restrict__ bias, const int64_t* __restrict__ labels,
                                                 float* __restrict__ logp, float* __restrict__ loss_rows,
                                                 float* __restrict__ dlogits, float* __restrict__ dh1, int B,
-                                                float inv_b, const long long* __restrict__ bidx, Conv1Commit cm) {
-  if (blockIdx.x == (unsigned)((B + 3) >> 2)) {  // extra block: conv1 commit + cursor snapshot
-    const int t = threadIdx.x;
-    if (t == 0 && cm.bidx_snap) *cm.bidx_snap = *cm.bidx;
-    if (cm.pending && *cm.pending) {
-      const float lr = *cm.a.lr;
-      for (int i = 4 * t; i < cm.n; i += 1024) commit4(cm, i, lr);
-    }
-    return;
-  }
+                                                float inv_b, const long long* __restrict__ bidx) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= B) return;
   fc2_ce_row(row, lane, h1, w, bias, labels, logp, loss_rows, dlogits, dh1, B, inv_b, bidx);
 }
 
-// F4 + the critical part of B3 in one launch (single-process schedule with
-// fc1's weight gradient in B1): block (mt, nt) = 16 waves; wave w runs the
-// fc2 + log_softmax + NLL + dlogits + dh1 head of row mt*16+w into LDS (the
-// nt == 0 blocks also store loss/dlogits/dh1 for B2/B1), then the 16 waves
-// split K = 500 of the d(a2p) tile [16 rows, 16 cols] = dh1 W1.  The head is
-// recomputed per column tile (50x, ~1 us of dependent latency either way)
-// so the F4 -> B3 launch boundary disappears.  The all-row reductions of B3
-// (dW2, db1, db2) run in B2's launch.  Extra last block: conv1 commit.
 constexpr int FDX_WAVES = 16;
-__global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx(
-    const float* __restrict__ h1, const float* __restrict__ w2, const float* __restrict__ b2,
-    const int64_t* __restrict__ labels, const float* __restrict__ w1, float* __restrict__ loss_rows,
-    float* __restrict__ dlogits, float* __restrict__ dh1, float* __restrict__ da2p, int B, float inv_b,
-    const long long* __restrict__ bidx, Conv1Commit cm) {
-  __shared__ __attribute__((aligned(16))) float dh1s[16 * F1OUT];
-  __shared__ float red[FDX_WAVES * 256];
-  const int mtiles = (B + 15) >> 4, ntiles = (F1IN + 15) >> 4;
-  const int t = threadIdx.x;
-  if (blockIdx.x == (unsigned)(mtiles * ntiles)) {  // conv1 commit (F1 of this step applied it on the fly)
-    if (cm.pending && *cm.pending) {
-      const float lr = *cm.a.lr;
-      for (int i = 4 * t; i < cm.n; i += 4 * FDX_WAVES * 64) commit4(cm, i, lr);
-    }
-    return;
-  }
-  const int mt = blockIdx.x % mtiles, nt = blockIdx.x / mtiles;
-  const int w = t >> 6, lane = t & 63;
-  const int row = mt * 16 + w;
-  float* srow = dh1s + w * F1OUT;
-  constexpr int KC = ((F1OUT + FDX_WAVES - 1) / FDX_WAVES + 15) & ~15;  // 32
-  constexpr int NGK = KC / 16;
-  const bool pre = (cm.a.variant & 1) != 0;
-  // variant 1: the wave's W1 operand slice (K-rows [w*KC, (w+1)*KC) of 16
-  // columns, 8 floats per lane) is loaded BEFORE the head, so its memory
-  // round trip overlaps the head's instead of following the barrier.
-  const int r = lane & 15, gq = lane >> 4;
-  const int kb = w * KC, kend = min((w + 1) * KC, F1OUT);
-  float bw[NGK][4];
-  if (pre) {
-#pragma unroll
-    for (int q = 0; q < NGK; ++q) load4<LAY_KROW>(w1, F1IN, nt * 16 + r, F1IN, kb + 16 * q + 4 * gq, kend, bw[q]);
-  }
-  if (row < B) {
-    const bool st = nt == 0;
-    fc2_ce_row(row, lane, h1, w2, b2, labels, nullptr, st ? loss_rows : nullptr, st ? dlogits : nullptr,
-               st ? dh1 : nullptr, B, inv_b, bidx, srow, !(cm.a.variant & 2));  // bit 2: legacy butterflies
-  } else {
-    for (int k = lane; k < F1OUT; k += 64) srow[k] = 0.f;
-  }
-  __syncthreads();
-  f32x4 acc;
-  if (pre) {
-    f32x4 acc0 = zero4(), acc1 = zero4();
-#pragma unroll
-    for (int q = 0; q < NGK; ++q) {
-      float av[4];
-      load4<LAY_ROWK>(dh1s, F1OUT, r, 16, kb + 16 * q + 4 * gq, kend, av);
-      acc0 = mfma16x16x4(av[0], bw[q][0], acc0);
-      acc1 = mfma16x16x4(av[1], bw[q][1], acc1);
-      acc0 = mfma16x16x4(av[2], bw[q][2], acc0);
-      acc1 = mfma16x16x4(av[3], bw[q][3], acc1);
-    }
-    acc = acc0 + acc1;
-  } else {
-    acc = wave_tile_16x16<LAY_ROWK, LAY_KROW, NGK>(dh1s, F1OUT, w1, F1IN, 16, F1IN, F1OUT, 0, nt * 16, kb,
-                                                   (w + 1) * KC);
-  }
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) red[w * 256 + ((lane >> 4) * 4 + rr) * 16 + (lane & 15)] = acc[rr];
-  __syncthreads();
-  if (t < 256) {
-    float v = 0.f;
-#pragma unroll
-    for (int q = 0; q < FDX_WAVES; ++q) v += red[q * 256 + t];
-    const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
-    if (m < B && n < F1IN) da2p[m * F1IN + n] = v;
-  }
-}
 
-// k_fc2_ce_dx with the head on the matrix cores.  The per-wave head above
-// reads all of W2 (80 scalar loads per lane, 16 waves per block => ~1600
-// VMEM instructions per block, most of them the same 20 KB); here the block
-// stages its 16 h1 rows and W2 into LDS with one round of float4 loads and
-// runs the head as two tiny GEMMs:
+// F4dx: F4 + d(a2p) in one launch.  Block (mt, nt) = 16 waves: the fc2 +
+// log_softmax + NLL + dlogits + dh1 head of its 16 rows (recomputed per
+// column tile -- ~1 us of dependent latency either way -- so the F4 -> B3
+// launch boundary disappears; the nt == 0 blocks store loss/dlogits/dh1),
+// then the d(a2p) tile [16 rows, 16 cols] = dh1 W1 split-K over the waves.
+// The head runs on the matrix cores (a per-wave VALU head read all of W2
+// with 80 scalar loads per lane, ~1600 VMEM instructions per block,
+// profiles/fdx_mfma_head_r2.md): the block stages its 16 h1 rows and W2 into
+// LDS with one round of float4 loads and runs two tiny GEMMs:
 //   Z[16 x 16]   = h1_tile[16 x 500] W2^T   (split-K over the 16 waves)
 //   dh1[16 x 500] = dL[16 x 16] W2[16 x 500] (2 column tiles per wave, K=16)
 // with the softmax between them done by 256 threads, 16 lanes per row.
@@ -1021,7 +772,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     }
     return;
   }
-  const int tile = xcd_tile(blockIdx.x, mtiles * ntiles, cm.a.variant & 4);
+  const int tile = xcd_tile(blockIdx.x, mtiles * ntiles, true);
   const int mt = tile % mtiles, nt = tile / mtiles;
   const int w = t >> 6, lane = t & 63;
   const int r = lane & 15, gq = lane >> 4;
@@ -1157,84 +908,6 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
     if (m < B && n < F1IN) da2p[m * F1IN + n] = v;
   }
-}
-
-// F3+F4 in one launch: the fc1 tiles as k_linear_fwd_vec, then the LAST
-// block to finish a 16-row group (per-group arrival counter) runs
-// fc2 + log_softmax + NLL + dlogits + dh1 for those 16 rows.  Hand-off per
-// MI355X_MICROARCH.md "inter-workgroup visibility": producers wait for
-// their stores, barrier, one agent release + counter add; the last arriver
-// does one agent acquire, waits, barriers, then loads h1.  The last block
-// re-arms the counter, so graph replays need no reset launch.
-__global__ __launch_bounds__(512) void k_fc12_ce(const float* __restrict__ a2p, const float* __restrict__ w1,
-                                                 const float* __restrict__ b1, float* __restrict__ h1,
-                                                 const float* __restrict__ w2, const float* __restrict__ b2,
-                                                 const int64_t* __restrict__ labels, float* __restrict__ loss_rows,
-                                                 float* __restrict__ dlogits, float* __restrict__ dh1, int B,
-                                                 float inv_b, const long long* __restrict__ bidx,
-                                                 unsigned* __restrict__ counters) {
-  __shared__ float red[8 * 256];
-  __shared__ int is_last;
-  block_gemm_splitk<LAY_ROWK, LAY_ROWK, EpiBiasRelu, 8, true, true>(a2p, F1IN, w1, F1IN, B, F1OUT, F1IN, blockIdx.x,
-                                                                    red, EpiBiasRelu{b1, h1, F1OUT, true});
-  const int mtiles = (B + 15) >> 4, ntiles = (F1OUT + 15) >> 4;
-  const int mt = blockIdx.x % mtiles;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = atomicAdd(&counters[mt], 1u);
-    is_last = prev == (unsigned)(ntiles - 1);
-    if (is_last) {
-      counters[mt] = 0u;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!is_last) return;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int row = mt * 16 + w; row < min(B, mt * 16 + 16); row += 8)
-    fc2_ce_row(row, lane, h1, w2, b2, labels, nullptr, loss_rows, dlogits, dh1, B, inv_b, bidx);
-}
-
-// ---------------------------------------------------------------- B3 ----
-// Four block ranges in one launch (all depend only on F4's outputs):
-//   [0, nA)       dW1 = dh1^T a2p      (1600 tiles, 4 per block, K = B)
-//   [nA, +nB)     d(a2p) = dh1 W1      (split-K 4, K = 500)
-//   [.., +nW)     dW2 = dlogits^T h1   (32 tiles, 4 per block, K = B)
-//   [.., +nS)     db1 / db2 column sums
-__global__ __launch_bounds__(256) void k_fc_bwd(const float* __restrict__ dh1, const float* __restrict__ a2p,
-                                                const float* __restrict__ w1, const float* __restrict__ h1,
-                                                const float* __restrict__ dlogits, float* __restrict__ gw1,
-                                                float* __restrict__ gb1, float* __restrict__ gw2,
-                                                float* __restrict__ gb2, float* __restrict__ da2p, int B, int nA,
-                                                int nB, int nW, long long* __restrict__ bidx, long long nbatches,
-                                                int* __restrict__ pending) {
-  __shared__ float red[4 * 256];
-  int bid = blockIdx.x;
-  if (bid == 0 && threadIdx.x == 0) {  // fused-optimizer schedule: F1/F4 of this step have read the cursor
-    if (bidx) *bidx = (*bidx + 1) % nbatches;
-    if (pending) *pending = 1;        // conv1's update (after B1) is owed to the next F1
-  }
-  if (bid < nA) {
-    block_gemm_4tiles<LAY_KROW, LAY_KROW>(dh1, F1OUT, a2p, F1IN, F1OUT, F1IN, B, bid, EpiStore{gw1, F1IN});
-    return;
-  }
-  bid -= nA;
-  if (bid < nB) {
-    block_gemm_splitk4<LAY_ROWK, LAY_KROW>(dh1, F1OUT, w1, F1IN, B, F1IN, F1OUT, bid, red, EpiStore{da2p, F1IN});
-    return;
-  }
-  bid -= nB;
-  if (bid < nW) {
-    block_gemm_4tiles<LAY_KROW, LAY_KROW>(dlogits, NCLS, h1, F1OUT, NCLS, F1OUT, B, bid, EpiStore{gw2, F1OUT});
-    return;
-  }
-  bid -= nW;
-  if (bid < 8) block_colsum64(dh1, F1OUT, B, F1OUT, bid * 64, red, gb1);
-  else block_colsum64(dlogits, NCLS, B, NCLS, 0, red, gb2);
 }
 
 // ---------------------------------------------------------------- B2 ----
@@ -1404,7 +1077,7 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
 PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, const uint8_t* __restrict__ code2,
                             const float* __restrict__ w2, float* __restrict__ da1p, int B, const float* __restrict__ x,
                             const long long* __restrict__ bidx, const uint8_t* __restrict__ code1,
-                            float* __restrict__ gw1, float* __restrict__ gb1, int ktail) {
+                            float* __restrict__ gw1, float* __restrict__ gb1, bool det) {
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // ---- part B: data gradient via col2im.  Block = (sample, pair of input
   // channels): 640 blocks at B=64, so each block's serial chain (one
@@ -1488,9 +1161,9 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
     for (int q = 0; q < 4; ++q) acc[q] = zero4();
 #pragma unroll
     for (int k0 = 0; k0 < 4; ++k0) {
-      if (k0 == 3 && (ktail & 1)) {
+      if (k0 == 3) {
         // K tail (k = 48..51): one k per lane group, so 4 MFMAs instead of
-        // 16 with three quarters of their K padding
+        // 16 with three quarters of their K padding (profiles/conv2_ktail_ab_r1.md)
         const int k = 48 + gg;
         const float a = k < C2 ? dys[k * B2_DLD + wv * 16 + r] : 0.f;
 #pragma unroll
@@ -1522,7 +1195,7 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
     }
   }
   __syncthreads();
-  if (ktail & 2) {
+  {
     // 288 outputs on 256 threads: one full output per thread, then the last
     // 32 outputs split 8 ways over all threads (<= 4 taps each, 3-step
     // shuffle sum) instead of a second full round on half a wave
@@ -1561,24 +1234,6 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
         dsum[o] = sacc;
       }
     }
-  } else
-  for (int o = tid; o < 2 * 144; o += 256) {
-    const int icl = o / 144, pix = o - icl * 144;
-    const int y = pix / 12, xx = pix - y * 12;
-    float s = 0.f;
-#pragma unroll
-    for (int kh = 0; kh < 5; ++kh) {
-      const int sy = y - kh;
-      if (sy < 0 || sy >= 8) continue;
-#pragma unroll
-      for (int kw = 0; kw < 5; ++kw) {
-        const int sx = xx - kw;
-        if (sx < 0 || sx >= 8) continue;
-        s += ts[(sy * 8 + sx) * TLD + icl * 25 + kh * 5 + kw];
-      }
-    }
-    if (da1p) da1p[b * A1P + (icg * 2 + icl) * 144 + pix] = s;
-    dsum[o] = s;
   }
   if (!fuse1) return;
   // ---- conv1 weight+bias grad of this sample's 2 channels (replaces the
@@ -1586,7 +1241,7 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
   // quarter); pooled grad expanded through the conv1 argmax code.
   __syncthreads();
   float* part = ws;  // [4][26] wave totals (free after the GEMM)
-  if (!(ktail & 256)) {
+  {
     // pixel-major: wave w owns channel w>>1 and 72 of its 144 pooled pixels
     // (lanes 0..63, then lanes 0..7 again); a lane expands its pixel's
     // (grad, code) once and accumulates the 25 taps + bias in registers;
@@ -1612,14 +1267,12 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
       }
     }
     wave_halving26(acc, lane, part + wv * 26);
-  } else if (tid < 104) {
-    part[tid] = 0.f;
   }
   __syncthreads();
-  if (tid < 52 && !(ktail & 512)) {
+  if (tid < 52) {
     const int icl = tid / 26, k = tid - icl * 26, oc1 = icg * 2 + icl;
     const float v = part[(2 * icl) * 26 + k] + part[(2 * icl + 1) * 26 + k];
-    if (ktail & 2048) {  // deterministic mode: one slot per sample, every element written once
+    if (det) {  // deterministic mode: one slot per sample, every element written once
       if (k < 25) gw1[oc1 * 25 + k] = v;
       else gb1[oc1] = v;
     } else {
@@ -1657,10 +1310,7 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
                                                    float* __restrict__ da1p, int B, int nA, int nB, int nC,
                                                    const float* __restrict__ x, const long long* __restrict__ bidx,
                                                    const uint8_t* __restrict__ code1, float* __restrict__ gw1,
-                                                   float* __restrict__ gb1, int nF, const float* __restrict__ fdh1,
-                                                   const float* __restrict__ fh1, const float* __restrict__ fdl,
-                                                   float* __restrict__ fgw2, float* __restrict__ fgb1,
-                                                   float* __restrict__ fgb2, int ktail = 1) {
+                                                   float* __restrict__ gb1) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int bid = blockIdx.x;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1670,7 +1320,7 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
   }
   bid -= nA;
   if (bid < nB) {
-    c2_dgrad_block(bid, smem, g2, code2, w2, da1p, B, x, bidx, code1, gw1, gb1, ktail);
+    c2_dgrad_block(bid, smem, g2, code2, w2, da1p, B, x, bidx, code1, gw1, gb1, false);
     return;
   }
   bid -= nB;
@@ -1680,19 +1330,7 @@ __global__ __launch_bounds__(256) void k_conv2_bwd(const float* __restrict__ g2,
     if (oc >= C2) return;
     const float s = c2_bias_sum(oc, g2, code2, B);
     if (lane == 0) gb2[oc] = s;
-    return;
   }
-  bid -= nC;
-  if (bid >= nF) return;
-  // ---- part F (k_fc2_ce_dx schedule): B3's all-row reductions dW2, db1, db2
-  constexpr int NWF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4;
-  if (bid < NWF) {
-    block_gemm_4tiles<LAY_KROW, LAY_KROW>(fdl, NCLS, fh1, F1OUT, NCLS, F1OUT, B, bid, EpiStore{fgw2, F1OUT});
-    return;
-  }
-  bid -= NWF;
-  if (bid < 8) block_colsum64(fdh1, F1OUT, B, F1OUT, bid * 64, smem, fgb1);
-  else block_colsum64(fdl, NCLS, B, NCLS, 0, smem, fgb2);
 }
 
 // One wave: a 16x16 tile of dW1 = dh1^T a2p (K = B) consumed straight from
@@ -1714,12 +1352,10 @@ PTO_DEV void dw1_sgd_tile(int tile, const float* __restrict__ dh1, const float* 
     mv[rr] = ok ? mw[r * F1IN + n] : 0.f;
   }
   const float lr = *a.lr;
-  // variant 1: 4 k-groups per memory round (K = B = 64 exactly, 32 loads
-  // per lane in flight) instead of 8 with half of them masked off
+  // 4 k-groups per memory round (K = B = 64 exactly, 32 loads per lane in
+  // flight; 8 groups with half of them masked off was slower)
   const f32x4 acc =
-      (a.variant & 1)
-          ? wave_tile_16x16<LAY_KROW, LAY_KROW, 4>(dh1, F1OUT, a2p, F1IN, F1OUT, F1IN, B, mt * 16, nt * 16, 0, B)
-          : wave_tile_16x16<LAY_KROW, LAY_KROW, 8>(dh1, F1OUT, a2p, F1IN, F1OUT, F1IN, B, mt * 16, nt * 16, 0, B);
+      wave_tile_16x16<LAY_KROW, LAY_KROW, 4>(dh1, F1OUT, a2p, F1IN, F1OUT, F1IN, B, mt * 16, nt * 16, 0, B);
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
     const int r = mt * 16 + (lane >> 4) * 4 + rr;
@@ -1740,7 +1376,7 @@ PTO_DEV void dw1_sgd_tile(int tile, const float* __restrict__ dh1, const float* 
 constexpr int B1_CHUNK = 4;
 PTO_DEV void conv1_bwd_block(int vb, const float* __restrict__ g1, const uint8_t* __restrict__ code1,
                              const float* __restrict__ x, float* __restrict__ gw1, float* __restrict__ gb1, int B,
-                             const long long* __restrict__ bidx, bool halving = true) {
+                             const long long* __restrict__ bidx) {
   // One memory round: the chunk's 4 input images (12.5 KB, coalesced
   // float4) go to LDS together with each thread's (grad, code) pairs; the
   // 25-tap patches are then read from LDS.
@@ -1792,21 +1428,7 @@ PTO_DEV void conv1_bwd_block(int vb, const float* __restrict__ g1, const uint8_t
     acc[25] += gq;
   }
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (halving) {
-    wave_halving26(acc, lane, part[wv]);
-  } else {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-      for (int k = 0; k < 26; ++k) acc[k] += __shfl_xor(acc[k], o, 64);
-    if (lane < 26) {
-      float v = acc[0];
-#pragma unroll
-      for (int k = 1; k < 26; ++k)
-        if (lane == k) v = acc[k];
-      part[wv][lane] = v;
-    }
-  }
+  wave_halving26(acc, lane, part[wv]);
   __syncthreads();
   if (threadIdx.x < 26) {
     const int q = threadIdx.x;
@@ -1821,43 +1443,6 @@ __global__ __launch_bounds__(256) void k_conv1_bwd(const float* __restrict__ g1,
                                                    float* __restrict__ gb1, int B,
                                                    const long long* __restrict__ bidx) {
   conv1_bwd_block(blockIdx.x, g1, code1, x, gw1, gb1, B, bidx);
-}
-
-// B1 + the optimizer for every parameter whose gradient is final before B1
-// (fc and conv2: the flat range [0, nflat), 1024 elements per extra block).
-// The extra blocks touch no byte the conv1 blocks read or write.  Grads
-// below `zero_from` (fc: B3 stores every element each step) are not zeroed;
-// the atomically accumulated conv2 weight grads are.
-__global__ __launch_bounds__(256) void k_conv1_bwd_sgd(const float* __restrict__ g1,
-                                                       const uint8_t* __restrict__ code1,
-                                                       const float* __restrict__ x, float* __restrict__ gw1,
-                                                       float* __restrict__ gb1, int B,
-                                                       const long long* __restrict__ bidx, int nconv,
-                                                       float* __restrict__ p, float* __restrict__ g,
-                                                       float* __restrict__ m, long long nflat, long long zero_from,
-                                                       SgdArgs a, int ndw, const float* __restrict__ dh1,
-                                                       const float* __restrict__ a2p, long long skip_lo,
-                                                       long long skip_hi, int nsgd_lo, long long* __restrict__ adv,
-                                                       long long nbatches, int* __restrict__ set_pending) {
-  int bid = blockIdx.x;
-  if (bid == 0 && threadIdx.x == 0) {  // no block of this launch reads the cursor (x comes from xout)
-    if (adv) *adv = (*adv + 1) % nbatches;
-    if (set_pending) *set_pending = 1;
-  }
-  if (bid < nconv) {
-    conv1_bwd_block(bid, g1, code1, x, gw1, gb1, B, bidx, !(a.variant & 2));  // bit 2: legacy 6x26-shuffle reduction
-    return;
-  }
-  bid -= nconv;
-  if (bid < ndw) {  // dW1 = dh1^T a2p (K = B, 4 tiles per block) consumed by SGD on fc1.weight = [skip_lo, skip_hi)
-    dw1_sgd_tile(bid * 4 + (threadIdx.x >> 6), dh1, a2p, p + skip_lo, m + skip_lo, B, a);
-    return;
-  }
-  bid -= ndw;
-  // flat SGD over [0, nflat) minus [skip_lo, skip_hi): nsgd_lo blocks below, the rest above
-  const long long i = bid < nsgd_lo ? ((long long)bid * 256 + threadIdx.x) * 4
-                                    : skip_hi + ((long long)(bid - nsgd_lo) * 256 + threadIdx.x) * 4;
-  if (bid < nsgd_lo ? i < skip_lo : i < nflat) sgd_flat4(p, g, m, i, *a.lr, a, i >= zero_from);
 }
 
 // ------------------------------------------------------ B (all-in-one) ----
@@ -1900,9 +1485,7 @@ struct BwdAllArgs {
   long long* bidx;
   long long nbatches;
   int* pending;
-  int B, nA, nB, nC, nD, nF, ktail;
-  int skip;  // timing probes only (PTO_BWD_ALL_SKIP): 1 = no conv1 wgrad, 4 = no conv2 tile SGD
-  int order;  // block-range order (PTO_BWD_ORDER): 0 wgrad,dgrad,dW1; 1 dgrad,wgrad,dW1; 2 wgrad,dW1,dgrad
+  int B, nA, nB, nC, nD, nF;
   // deterministic mode (wpart != nullptr): no floating-point atomics.  The
   // conv2 wgrad chunks store partial tiles into wpart[chunk] and the last
   // arriver per tile sums them in chunk order; conv1 grads go to one
@@ -1946,7 +1529,8 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   }
   // block order: the short independent ranges first (they must not queue
   // behind the LDS-heavy conv2 blocks for a CU slot), then conv2 wgrad,
-  // conv2 dgrad, dW1
+  // conv2 dgrad, dW1 (dgrad-first and dW1-before-dgrad measured 0.9 and
+  // 1.4 us slower, profiles/bwd_all_r2.md)
   if (bid < A.nC) {
     const int oc = bid * 4 + wv;
     if (oc >= C2) return;
@@ -1985,17 +1569,10 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
     return;
   }
   bid -= A.nF;
-  if (A.order == 1) {  // dgrad range dispatched before the wgrad range
-    if (bid < A.nB) bid += A.nA;
-    else if (bid < A.nB + A.nA) bid -= A.nB;
-  } else if (A.order == 2) {  // wgrad, dW1, dgrad
-    if (bid >= A.nA && bid < A.nA + A.nD) bid += A.nB;
-    else if (bid >= A.nA + A.nD && bid < A.nA + A.nD + A.nB) bid -= A.nD;
-  }
   if (bid < A.nA) {
     const bool det = A.wpart != nullptr;
     c2_wgrad_block<CH>(bid, smem, A.g2, A.code2, A.a1p, A.g2w, A.B, A.wpart);
-    if ((A.grads_only && !det) || (A.skip & 1024)) return;  // 1024: timing probe, no arrival / tile SGD
+    if (A.grads_only && !det) return;
     // arrival: every lane's atomics have been performed at the memory side
     // (deterministic mode: the partial-tile stores are written back first)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2011,7 +1588,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
       }
     }
     __syncthreads();
-    if (!s_last || (A.skip & 4)) return;
+    if (!s_last) return;
     int idx[4];
     float gv[4], pv[4], mv[4];
     if (det) {
@@ -2056,8 +1633,8 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
     const int r = (bid / B2_ICG) % A.nrep;
     float* gw1 = r == 0 ? A.gw1 : A.c1rep + (r - 1) * A.rep_stride;
     float* gb1 = r == 0 ? A.gb1 : A.c1rep + (r - 1) * A.rep_stride + A.bias_off;
-    c2_dgrad_block(bid, smem, A.g2, A.code2, A.w2f, nullptr, A.B, A.x, nullptr, A.code1,
-                   (A.skip & 1) ? nullptr : gw1, gb1, A.ktail);
+    c2_dgrad_block(bid, smem, A.g2, A.code2, A.w2f, nullptr, A.B, A.x, nullptr, A.code1, gw1, gb1,
+                   A.wpart != nullptr);
     return;
   }
   bid -= A.nB;
@@ -2149,15 +1726,6 @@ PTO_API int pto_conv2_fwd(const float* a1p, const float* w, const float* b, floa
   LAUNCH_CHECK();
 }
 
-PTO_API int pto_conv12_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
-                           float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B, const long long* bidx,
-                           hipStream_t s) {
-  LazyConv1 lz{};
-  hipLaunchKernelGGL(k_conv12_fwd, dim3(B * 4), dim3(256), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B, bidx,
-                     lz);
-  LAUNCH_CHECK();
-}
-
 static SgdArgs sgd_args(const float* lr, float mom, float wd, float gscale, int nesterov) {
   SgdArgs a;
   a.lr = lr;
@@ -2169,67 +1737,22 @@ static SgdArgs sgd_args(const float* lr, float mom, float wd, float gscale, int 
   return a;
 }
 
-// F1 with conv1's owed SGD update applied on the fly (fused-optimizer
-// schedule).  g1f/m1f: flat conv1 grads/momentum (weights at 0, bias at
-// bias_off); lr: device scalar.
-// Block size of the fused forward: 512 (two K halves) or 1024 threads
-// threads (default: 2-channel conv1 tasks, four K parts).
-static int fwd_threads() {
-  static const int n = [] {
-    const char* e = getenv("PTO_FWD_THREADS");  // 512 = two K halves, 4-channel conv1 tasks (A/B)
-    return e ? atoi(e) : 1024;
-  }();
-  return n;
-}
-
-PTO_API int pto_conv12_fwd_lazy(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
-                                float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B, const long long* bidx,
-                                const float* g1f, const float* m1f, int bias_off, const int* pending, const float* lr,
-                                float mom, float wd, float gscale, int nesterov, int version, hipStream_t s) {
-  LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off, nullptr, nullptr};
-  if (version == 2 && fwd_threads() == 1024)
-    hipLaunchKernelGGL(k_conv12_fwd2_t<1024>, dim3(B * 4), dim3(1024), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p,
-                       code2, B, bidx, lz);
-  else if (version == 2)
-    hipLaunchKernelGGL(k_conv12_fwd2_t<512>, dim3(B * 4), dim3(512), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2,
-                       B, bidx, lz);
-  else
-    hipLaunchKernelGGL(k_conv12_fwd, dim3(B * 4), dim3(256), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B,
-                       bidx, lz);
-  LAUNCH_CHECK();
-}
-
-// Version-2 F1+F2 launch that also copies the batch's images to xout, so
-// the conv1 weight-gradient blocks of B1 read them without the dependent
-// batch-cursor load.
+// F12: conv1 + conv2 forward.  g1f/m1f/pending non-null: conv1's owed SGD
+// update is applied on the fly (flat conv1 grads/momentum, weights at 0,
+// bias at bias_off, `nrep` gradient replicas at rep + r*rep_stride); xout:
+// the batch's images copied out for the backward; w2out: the conv2.weight
+// snapshot k_bwd_all's dgrad blocks read.
 PTO_API int pto_conv12_fwd_lazy_x(const float* x, const float* w1, const float* b1, const float* w2,
                                   const float* b2, float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B,
                                   const long long* bidx, const float* g1f, const float* m1f, int bias_off,
                                   const int* pending, const float* lr, float mom, float wd, float gscale, int nesterov,
                                   float* xout, float* w2out, const float* rep, int nrep, int rep_stride,
                                   hipStream_t s) {
+  if (nrep < 1 || nrep > C1_MAXREP || (nrep > 1 && !rep) || (pending && (!g1f || !m1f || !lr))) return -1;
   LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off, xout, w2out, rep, nrep,
                rep_stride};
-  static const int bal = [] {
-    const char* e = getenv("PTO_CONV1_BALANCED");  // 0 = 15 lockstep tasks (A/B)
-    return e ? atoi(e) : 1;
-  }();
-  static const int slots = [] {
-    const char* e = getenv("PTO_CONV1_SLOTS");
-    return e ? atoi(e) : 0;
-  }();
-  static const int probe = [] {
-    const char* e = getenv("PTO_F12_PROBE");  // timing probes, numerics wrong: 8 no conv1 FMAs, 16 no conv2 MFMAs
-    return e ? atoi(e) : 0;
-  }();
-  lz.a.variant = (bal ? 0 : 2) | (slots ? 4 : 0) | (probe & 24);  // conv1 task layout (the lazy SGD ignores it)
-  if (probe & 32) bidx = nullptr;  // timing probe: no batch-cursor hop before the image load
-  if (fwd_threads() == 1024)
-    hipLaunchKernelGGL(k_conv12_fwd2_t<1024>, dim3(B * 4), dim3(1024), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p,
-                       code2, B, bidx, lz);
-  else
-    hipLaunchKernelGGL(k_conv12_fwd2_t<512>, dim3(B * 4), dim3(512), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2,
-                       B, bidx, lz);
+  hipLaunchKernelGGL(k_conv12_fwd2_t<1024>, dim3(B * 4), dim3(1024), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2,
+                     B, bidx, lz);
   LAUNCH_CHECK();
 }
 
@@ -2237,23 +1760,8 @@ PTO_API int pto_linear_fwd(const float* x, const float* w, const float* b, float
                            hipStream_t s) {
   const int tiles = ((M + 15) / 16) * ((N + 15) / 16);
   const bool vec = (K % 4) == 0 && ((((uintptr_t)x) | ((uintptr_t)w)) & 15) == 0;
-  static const int waves = [] {
-    const char* e = getenv("PTO_LINEAR_WAVES");  // 8 = the 512-thread kernel (A/B)
-    return e ? atoi(e) : 16;
-  }();
-  static const int swz = [] {
-    const char* e = getenv("PTO_XCD_SWZ");  // 0 = linear tile order (A/B)
-    return e ? atoi(e) : 1;
-  }();
-  static const int probe = [] {
-    const char* e = getenv("PTO_FC1_PROBE");
-    return e ? atoi(e) : 0;
-  }();
-  if (vec && waves == 16)
-    hipLaunchKernelGGL(k_linear_fwd_vec16, dim3(tiles), dim3(1024), 0, s, x, w, b, y, M, N, K,
-                       (relu ? 1 : 0) | (swz ? 2 : 0) | (probe & 4));
-  else if (vec)
-    hipLaunchKernelGGL(k_linear_fwd_vec, dim3(tiles), dim3(512), 0, s, x, w, b, y, M, N, K, relu);
+  if (vec)
+    hipLaunchKernelGGL(k_linear_fwd_vec16, dim3(tiles), dim3(1024), 0, s, x, w, b, y, M, N, K, relu);
   else
     hipLaunchKernelGGL(k_linear_fwd, dim3(tiles), dim3(256), 0, s, x, w, b, y, M, N, K, relu);
   LAUNCH_CHECK();
@@ -2281,23 +1789,8 @@ PTO_API int pto_relu_bwd(const float* g, const float* y, float* out, int n, hipS
 PTO_API int pto_fc2_ce(const float* h1, const float* w, const float* b, const int64_t* labels, float* logp,
                        float* loss_rows, float* dlogits, float* dh1, int B, float inv_b, const long long* bidx,
                        hipStream_t s) {
-  Conv1Commit cm{};
   hipLaunchKernelGGL(k_fc2_ce, dim3((B + 3) / 4), dim3(256), 0, s, h1, w, b, labels, logp, loss_rows, dlogits, dh1,
-                     B, inv_b, bidx, cm);
-  LAUNCH_CHECK();
-}
-
-// F4 + one extra block: commit conv1's owed update (flat range p1/g1/m1 of
-// n1 floats, n1 % 4 == 0, 16-byte aligned) and snapshot the batch cursor
-// into bidx_snap for B1.
-PTO_API int pto_fc2_ce_commit(const float* h1, const float* w, const float* b, const int64_t* labels,
-                              float* loss_rows, float* dlogits, float* dh1, int B, float inv_b, const long long* bidx,
-                              long long* bidx_snap, float* p1, float* g1, float* m1, int n1, const int* pending,
-                              const float* lr, float mom, float wd, float gscale, int nesterov, hipStream_t s) {
-  if (n1 % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1)) & 15)) return -1;
-  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), bidx, bidx_snap};
-  hipLaunchKernelGGL(k_fc2_ce, dim3((B + 3) / 4 + 1), dim3(256), 0, s, h1, w, b, labels, nullptr, loss_rows, dlogits,
-                     dh1, B, inv_b, bidx, cm);
+                     B, inv_b, bidx);
   LAUNCH_CHECK();
 }
 
@@ -2306,44 +1799,8 @@ PTO_API int pto_conv1_commit(float* p1, float* g1, float* m1, int n1, int* pendi
                              hipStream_t s) {
   if (n1 % 4 || rep_stride % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1) | ((uintptr_t)rep)) & 15))
     return -1;
-  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), nullptr, nullptr, rep, nrep,
-                 rep_stride};
+  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), rep, nrep, rep_stride};
   hipLaunchKernelGGL(k_conv1_commit, dim3(1), dim3(256), 0, s, cm, pending);
-  LAUNCH_CHECK();
-}
-
-// counters: >= (B+15)/16 zero-initialised uint32 (re-armed by the kernel).
-PTO_API int pto_fc12_ce(const float* a2p, const float* w1, const float* b1, float* h1, const float* w2,
-                        const float* b2, const int64_t* labels, float* loss_rows, float* dlogits, float* dh1, int B,
-                        float inv_b, const long long* bidx, unsigned* counters, hipStream_t s) {
-  const int tiles = ((B + 15) / 16) * ((F1OUT + 15) / 16);
-  hipLaunchKernelGGL(k_fc12_ce, dim3(tiles), dim3(512), 0, s, a2p, w1, b1, h1, w2, b2, labels, loss_rows, dlogits,
-                     dh1, B, inv_b, bidx, counters);
-  LAUNCH_CHECK();
-}
-
-PTO_API int pto_fc_bwd(const float* dh1, const float* a2p, const float* w1, const float* h1, const float* dlogits,
-                       float* gw1, float* gb1, float* gw2, float* gb2, float* da2p, int B, hipStream_t s) {
-  const int nA = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
-  const int nB = ((B + 15) / 16) * ((F1IN + 15) / 16);
-  const int nW = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4;
-  const int nS = 8 + 1;
-  hipLaunchKernelGGL(k_fc_bwd, dim3(nA + nB + nW + nS), dim3(256), 0, s, dh1, a2p, w1, h1, dlogits, gw1, gb1, gw2,
-                     gb2, da2p, B, nA, nB, nW, nullptr, 1LL, nullptr);
-  LAUNCH_CHECK();
-}
-
-// B3 of the fused-optimizer schedule: also advances the batch cursor and
-// marks conv1's update as owed.
-PTO_API int pto_fc_bwd_adv(const float* dh1, const float* a2p, const float* w1, const float* h1,
-                           const float* dlogits, float* gw1, float* gb1, float* gw2, float* gb2, float* da2p, int B,
-                           long long* bidx, long long nbatches, int* pending, hipStream_t s) {
-  const int nA = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
-  const int nB = ((B + 15) / 16) * ((F1IN + 15) / 16);
-  const int nW = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4;
-  const int nS = 8 + 1;
-  hipLaunchKernelGGL(k_fc_bwd, dim3(nA + nB + nW + nS), dim3(256), 0, s, dh1, a2p, w1, h1, dlogits, gw1, gb1, gw2,
-                     gb2, da2p, B, nA, nB, nW, bidx, nbatches, pending);
   LAUNCH_CHECK();
 }
 
@@ -2362,35 +1819,12 @@ PTO_API int pto_conv2_bwd(const float* g2, const uint8_t* code2, const float* a1
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;
   if (nA + nB + nC == 0) return 0;
   hipLaunchKernelGGL(k_conv2_bwd, dim3(nA + nB + nC), dim3(256), lds, s, g2, code2, a1p, w2, gw2, gb2, da1p, B, nA,
-                     nB, nC, x, bidx, code1, (parts & 2) ? gw1 : nullptr, gb1, 0, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, 1);
+                     nB, nC, x, bidx, code1, (parts & 2) ? gw1 : nullptr, gb1);
   LAUNCH_CHECK();
 }
 
-// Full conv2 backward + the fc layers' all-row reductions (dW2 = dlogits^T
-// h1, db1, db2) for the k_fc2_ce_dx schedule.
-PTO_API int pto_conv2_bwd_fc(const float* g2, const uint8_t* code2, const float* a1p, const float* w2, float* gw2,
-                             float* gb2, float* da1p, int B, const float* dh1, const float* h1, const float* dlogits,
-                             float* fgw2, float* fgb1, float* fgb2, hipStream_t s) {
-  const int nA = ((B + B2_CHUNK - 1) / B2_CHUNK) * 32;
-  const int nB = B * B2_ICG;
-  const int nC = (C2 + 3) / 4;
-  const int nF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9;
-  const size_t ldsA = B2_CHUNK * (288 + F1IN + F1IN / 4) * sizeof(float);
-  const size_t ldsB = B2_LDS_FLOATS * sizeof(float);
-  const size_t lds = ldsA > ldsB ? ldsA : ldsB;
-  static const int ktail = [] {
-    const char* e = getenv("PTO_C2_KTAIL");  // 0 = padded 16-deep K tail (A/B)
-    const char* c = getenv("PTO_C2_COL2IM_SPLIT");  // 0 = two full col2im rounds (A/B)
-    return (e ? atoi(e) : 1) | ((c ? atoi(c) : 1) ? 2 : 0);
-  }();
-  hipLaunchKernelGGL(k_conv2_bwd, dim3(nA + nB + nC + nF), dim3(256), lds, s, g2, code2, a1p, w2, gw2, gb2, da1p, B,
-                     nA, nB, nC, nullptr, nullptr, nullptr, nullptr, nullptr, nF, dh1, h1, dlogits, fgw2, fgb1, fgb2,
-                     ktail);
-  LAUNCH_CHECK();
-}
-
-// F4 + d(a2p) (k_fc2_ce_dx) + the conv1 commit block.
+// F4dx (k_fc2_ce_dx_mf) + one extra block committing conv1's owed update
+// (pending != nullptr; flat range p1/g1/m1 of n1 floats + replicas).
 PTO_API int pto_fc2_ce_dx(const float* h1, const float* w2, const float* b2, const int64_t* labels, const float* w1,
                           float* loss_rows, float* dlogits, float* dh1, float* da2p, int B, float inv_b,
                           const long long* bidx, float* p1, float* g1, float* m1, int n1, const int* pending,
@@ -2398,32 +1832,11 @@ PTO_API int pto_fc2_ce_dx(const float* h1, const float* w2, const float* b2, con
                           int rep_stride, hipStream_t s) {
   if (n1 % 4 || rep_stride % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1) | ((uintptr_t)rep)) & 15))
     return -1;
-  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), nullptr, nullptr, rep, nrep,
-                 rep_stride};
-  static const int prefetch = [] {
-    const char* e = getenv("PTO_FDX_PREFETCH");  // 0 = operand loads after the barrier (A/B)
-    return e ? atoi(e) : 1;
-  }();
-  static const int head_halving = [] {
-    const char* e = getenv("PTO_HEAD_HALVING");  // 0 = 6 x 10 butterfly shuffles (A/B)
-    return e ? atoi(e) : 1;
-  }();
-  static const int swz = [] {
-    const char* e = getenv("PTO_XCD_SWZ");
-    return e ? atoi(e) : 1;
-  }();
-  cm.a.variant = (prefetch ? 1 : 0) | (head_halving ? 0 : 2) | (swz ? 4 : 0);  // read only by k_fc2_ce_dx's tile loop (the commit SGD ignores it)
-  static const int mf = [] {
-    const char* e = getenv("PTO_FDX_MF");  // 0 = per-wave VALU head (A/B)
-    return e ? atoi(e) : 1;
-  }();
+  if ((((uintptr_t)h1) | ((uintptr_t)w2)) & 15) return -1;  // float4 staging of the h1 tile and W2
+  if (nrep < 1 || nrep > C1_MAXREP || (nrep > 1 && !rep)) return -1;
+  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), rep, nrep, rep_stride};
   const int nblk = ((B + 15) / 16) * ((F1IN + 15) / 16);
-  if (mf && !((((uintptr_t)h1) | ((uintptr_t)w2)) & 15)) {
-    hipLaunchKernelGGL(k_fc2_ce_dx_mf, dim3(nblk + 1), dim3(FDX_WAVES * 64), 0, s, h1, w2, b2, labels, w1,
-                       loss_rows, dlogits, dh1, da2p, B, inv_b, bidx, cm);
-    LAUNCH_CHECK();
-  }
-  hipLaunchKernelGGL(k_fc2_ce_dx, dim3(nblk + 1), dim3(FDX_WAVES * 64), 0, s, h1, w2, b2, labels, w1, loss_rows,
+  hipLaunchKernelGGL(k_fc2_ce_dx_mf, dim3(nblk + 1), dim3(FDX_WAVES * 64), 0, s, h1, w2, b2, labels, w1, loss_rows,
                      dlogits, dh1, da2p, B, inv_b, bidx, cm);
   LAUNCH_CHECK();
 }
@@ -2433,105 +1846,6 @@ PTO_API int pto_conv1_bwd(const float* g1, const uint8_t* code1, const float* x,
                           const long long* bidx, hipStream_t s) {
   const int nblk = C1 * ((B + B1_CHUNK - 1) / B1_CHUNK);
   hipLaunchKernelGGL(k_conv1_bwd, dim3(nblk), dim3(256), 0, s, g1, code1, x, gw1, gb1, B, bidx);
-  LAUNCH_CHECK();
-}
-
-// B1 + SGD over the flat range [0, nflat) of (p, g, m) (nflat % 4 == 0,
-// 16-byte aligned); zeroes the grads in [zero_from, nflat).
-PTO_API int pto_conv1_bwd_sgd(const float* g1, const uint8_t* code1, const float* x, float* gw1, float* gb1, int B,
-                              const long long* bidx, float* p, float* g, float* m, long long nflat,
-                              long long zero_from, const float* lr, float mom, float wd, float gscale, int nesterov,
-                              hipStream_t s) {
-  if (nflat % 4 || zero_from % 4 || ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m)) & 15)) return -1;
-  const int nconv = C1 * ((B + B1_CHUNK - 1) / B1_CHUNK);
-  const int nsgd = (int)((nflat / 4 + 255) / 256);
-  hipLaunchKernelGGL(k_conv1_bwd_sgd, dim3(nconv + nsgd), dim3(256), 0, s, g1, code1, x, gw1, gb1, B, bidx, nconv, p,
-                     g, m, nflat, zero_from, sgd_args(lr, mom, wd, gscale, nesterov), 0, nullptr, nullptr, nflat,
-                     nflat, nsgd, nullptr, 1LL, nullptr);
-  LAUNCH_CHECK();
-}
-
-// B1 with fc1's weight gradient moved out of B3: extra blocks compute
-// dW1 = dh1^T a2p and apply SGD to fc1.weight (flat range [w1_off,
-// w1_off + 500*800)) straight from the MMA accumulators, so that gradient is
-// never written or re-read (and its grad slot is left untouched).  The flat
-// SGD blocks skip that range.  Single-process schedule only: with DDP the
-// gradient must exist for the all-reduce.
-PTO_API int pto_conv1_bwd_sgd_dw1(const float* g1, const uint8_t* code1, const float* x, float* gw1, float* gb1,
-                                  int B, const long long* bidx, float* p, float* g, float* m, long long nflat,
-                                  long long zero_from, const float* dh1, const float* a2p, long long w1_off,
-                                  long long* adv, long long nbatches, int* set_pending, const float* lr, float mom,
-                                  float wd, float gscale, int nesterov, hipStream_t s) {
-  if (adv && bidx) return -1;  // the advance would race with the conv1 blocks' cursor reads
-  const long long w1_end = w1_off + (long long)F1OUT * F1IN;
-  if (nflat % 4 || zero_from % 4 || w1_off % 4 || w1_end > nflat ||
-      ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m)) & 15))
-    return -1;
-  const int nconv = C1 * ((B + B1_CHUNK - 1) / B1_CHUNK);
-  const int ndw = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
-  const int nsgd_lo = (int)((w1_off / 4 + 255) / 256);
-  const int nsgd_hi = (int)(((nflat - w1_end) / 4 + 255) / 256);
-  static const int dw1_ng = [] {
-    const char* e = getenv("PTO_DW1_NG");  // 8 = previous loop shape (A/B)
-    return e ? atoi(e) : 4;
-  }();
-  static const int c1_halving = [] {
-    const char* e = getenv("PTO_CONV1_HALVING");  // 0 = legacy reduction (A/B)
-    return e ? atoi(e) : 1;
-  }();
-  SgdArgs sa = sgd_args(lr, mom, wd, gscale, nesterov);
-  sa.variant = (dw1_ng == 4 ? 1 : 0) | (c1_halving ? 0 : 2);
-  hipLaunchKernelGGL(k_conv1_bwd_sgd, dim3(nconv + ndw + nsgd_lo + nsgd_hi), dim3(256), 0, s, g1, code1, x, gw1, gb1,
-                     B, bidx, nconv, p, g, m, nflat, zero_from, sa, ndw, dh1, a2p,
-                     w1_off, w1_end, nsgd_lo, adv, nbatches > 0 ? nbatches : 1LL, set_pending);
-  LAUNCH_CHECK();
-}
-
-// B3 without fc1's weight gradient (it moved into pto_conv1_bwd_sgd_dw1).
-PTO_API int pto_fc_bwd_adv_nodw1(const float* dh1, const float* a2p, const float* w1, const float* h1,
-                                 const float* dlogits, float* gb1, float* gw2, float* gb2, float* da2p, int B,
-                                 long long* bidx, long long nbatches, int* pending, hipStream_t s) {
-  const int nB = ((B + 15) / 16) * ((F1IN + 15) / 16);
-  const int nW = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4;
-  const int nS = 8 + 1;
-  hipLaunchKernelGGL(k_fc_bwd, dim3(nB + nW + nS), dim3(256), 0, s, dh1, a2p, w1, h1, dlogits, nullptr, gb1, gw2,
-                     gb2, da2p, B, 0, nB, nW, bidx, nbatches, pending);
-  LAUNCH_CHECK();
-}
-
-// Optimizer-only launch of k_conv1_bwd_sgd (no conv1 blocks): SGD-momentum
-// over a flat (p, g, m) range of n floats, gradients zeroed from zero_from.
-PTO_API int pto_sgd_flat(float* p, float* g, float* m, long long n, long long zero_from, const float* lr, float mom,
-                         float wd, float gscale, int nesterov, hipStream_t s) {
-  if (n % 4 || zero_from % 4 || ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m)) & 15)) return -1;
-  if (n == 0) return 0;
-  const int nsgd = (int)((n / 4 + 255) / 256);
-  hipLaunchKernelGGL(k_conv1_bwd_sgd, dim3(nsgd), dim3(256), 0, s, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
-                     nullptr, 0, p, g, m, n, zero_from, sgd_args(lr, mom, wd, gscale, nesterov), 0, nullptr, nullptr,
-                     n, n, nsgd, nullptr, 1LL, nullptr);
-  LAUNCH_CHECK();
-}
-
-// B3 split in two launches for the two-stream backward of the fused-
-// optimizer schedule: part 1 = d(a2p) = dh1 W1 (what conv2's backward
-// needs) + the cursor advance / pending flag; part 2 = the fc weight and
-// bias gradients (only the optimizer needs them), run on a side stream
-// concurrently with part 1 and the conv backward.
-PTO_API int pto_fc_bwd_part(const float* dh1, const float* a2p, const float* w1, const float* h1,
-                            const float* dlogits, float* gw1, float* gb1, float* gw2, float* gb2, float* da2p, int B,
-                            long long* bidx, long long nbatches, int* pending, int part, hipStream_t s) {
-  const int nA = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
-  const int nB = ((B + 15) / 16) * ((F1IN + 15) / 16);
-  const int nW = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4;
-  const int nS = 8 + 1;
-  if (part == 1)
-    hipLaunchKernelGGL(k_fc_bwd, dim3(nB), dim3(256), 0, s, dh1, a2p, w1, h1, dlogits, gw1, gb1, gw2, gb2, da2p, B, 0,
-                       nB, 0, bidx, nbatches, pending);
-  else if (part == 2)
-    hipLaunchKernelGGL(k_fc_bwd, dim3(nA + nW + nS), dim3(256), 0, s, dh1, a2p, w1, h1, dlogits, gw1, gb1, gw2, gb2,
-                       da2p, B, nA, 0, nW, nullptr, 1LL, nullptr);
-  else
-    return -1;
   LAUNCH_CHECK();
 }
 
@@ -2546,7 +1860,12 @@ PTO_API int pto_eval_head(const float* logp, const int64_t* labels, float* stats
   LAUNCH_CHECK();
 }
 
-// The all-in-one backward + optimizer launch (k_bwd_all).  Flat-buffer
+// Samples per conv2-wgrad block of k_bwd_all: 6 -> 30.2 KB of LDS, 5 blocks
+// per CU next to the 31.5 KB dgrad blocks (sweep 4..8: 21.7, 20.8, 17.6,
+// 18.1, 23.4 us, profiles/bwd_all_r2.md).
+constexpr int BWD_WCHUNK = 6;
+
+// The all-in-one backward (+ optimizer) launch (k_bwd_all).  Flat-buffer
 // views: p/g/m + offsets of each parameter (elements); ctr: 32 zeroed ints.
 PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p, const float* w2f, const float* x,
                         const uint8_t* code1, const float* dh1, const float* a2p, const float* h1, const float* dl,
@@ -2555,9 +1874,10 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
                         long long off_c1b, int* ctr, long long* bidx, long long nbatches, int* pending, int B,
                         const float* lr, float mom, float wd, float gscale, int nesterov, float* c1rep, int nrep,
                         int rep_stride, int grads_only, float* wpart, hipStream_t s) {
-  if (!grads_only && (!bidx || !pending || !ctr || nbatches < 1)) return -1;
+  if (!ctr) return -1;
+  if (!grads_only && (!bidx || !pending || !w2f || nbatches < 1)) return -1;
   if (B < 1 || nrep < 1 || nrep > C1_MAXREP || (nrep > 1 && !c1rep)) return -1;
-  if (wpart && (nrep != B || !ctr)) return -1;  // deterministic mode: one conv1 replica per sample
+  if (wpart && nrep != B) return -1;  // deterministic mode: one conv1 replica per sample
   BwdAllArgs A;
   A.g2 = g2; A.code2 = code2; A.a1p = a1p; A.w2f = w2f; A.x = x; A.code1 = code1;
   A.gw1 = g + off_c1w; A.gb1 = g + off_c1b;
@@ -2569,7 +1889,6 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   A.pfw = p + off_fc2w; A.mfw = m + off_fc2w;
   A.pfb = p + off_fc2b; A.mfb = m + off_fc2b;
   A.a = sgd_args(lr, mom, wd, gscale, nesterov);
-  A.a.variant = 1;  // dW1 tiles: 4 k-groups per memory round
   A.c1rep = c1rep;
   A.nrep = nrep;
   A.rep_stride = rep_stride;
@@ -2578,45 +1897,15 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   A.g2b = g + off_c2b; A.g1w = g + off_fc1w; A.g1b = g + off_fc1b; A.gfw = g + off_fc2w; A.gfb = g + off_fc2b;
   if (grads_only) A.w2f = p + off_c2w;  // nothing updates conv2.weight in this launch
   A.bidx = bidx; A.nbatches = nbatches; A.pending = pending; A.B = B;
-  static const int chunk = [] {
-    // samples per conv2-wgrad block, 4..8 (A/B, profiles/bwd_all_r2.md):
-    // 6 -> 30.2 KB of LDS, 5 blocks per CU with the 31.5 KB dgrad blocks
-    const char* e = getenv("PTO_BWD_CHUNK");
-    const int v = e ? atoi(e) : 6;
-    return v < 4 ? 4 : (v > 8 ? 8 : v);
-  }();
-  A.nA = ((B + chunk - 1) / chunk) * 32;
+  A.nA = ((B + BWD_WCHUNK - 1) / BWD_WCHUNK) * 32;
   A.nB = B * B2_ICG;
   A.nC = (C2 + 3) / 4;
   A.nD = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
   A.nF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9;
-  A.ktail = 3 | (wpart ? 2048 : 0);
-  static const int skip = [] {
-    const char* e = getenv("PTO_BWD_ALL_SKIP");  // timing probes: parts left out (wrong numerics)
-    return e ? atoi(e) : 0;
-  }();
-  A.skip = skip;
   A.wpart = wpart;
-  static const int order = [] {
-    const char* e = getenv("PTO_BWD_ORDER");
-    return e ? atoi(e) : 0;
-  }();
-  A.order = order;
-  A.ktail |= ((skip >> 6) & 3) << 8;  // 64: no conv1 loop, 128: no conv1 atomics
-  if (skip & 2) A.nD = 0;
-  if (skip & 8) A.nB = 0;
-  if (skip & 16) A.nA = 0;
-  if (skip & 32) A.nF = 0, A.nC = 0;
-  const size_t ldsA = chunk * (288 + F1IN + F1IN / 4) * sizeof(float);
+  const size_t ldsA = BWD_WCHUNK * (288 + F1IN + F1IN / 4) * sizeof(float);
   const size_t ldsB = B2_LDS_FLOATS * sizeof(float);
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;
-  const dim3 grid(A.nA + A.nB + A.nC + A.nD + A.nF);
-  switch (chunk) {
-    case 4: hipLaunchKernelGGL(k_bwd_all<4>, grid, dim3(256), lds, s, A); break;
-    case 5: hipLaunchKernelGGL(k_bwd_all<5>, grid, dim3(256), lds, s, A); break;
-    case 6: hipLaunchKernelGGL(k_bwd_all<6>, grid, dim3(256), lds, s, A); break;
-    case 8: hipLaunchKernelGGL(k_bwd_all<8>, grid, dim3(256), lds, s, A); break;
-    default: hipLaunchKernelGGL(k_bwd_all<7>, grid, dim3(256), lds, s, A); break;
-  }
+  hipLaunchKernelGGL(k_bwd_all<BWD_WCHUNK>, dim3(A.nA + A.nB + A.nC + A.nD + A.nF), dim3(256), lds, s, A);
   LAUNCH_CHECK();
 }

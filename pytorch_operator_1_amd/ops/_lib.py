@@ -88,31 +88,18 @@ _L = ctypes.c_longlong
 _SIGS = {
     "pto_conv1_fwd": [_P, _P, _P, _P, _P, _I, _P, _P],
     "pto_conv2_fwd": [_P, _P, _P, _P, _P, _I, _P],
-    "pto_conv12_fwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     "pto_linear_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
     "pto_linear_bwd": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
     "pto_relu_bwd": [_P, _P, _P, _I, _P],
     "pto_fc2_ce": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _P, _P],
-    "pto_fc12_ce": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _P, _P, _P],
-    "pto_fc_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P],
     "pto_conv2_bwd": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P],
     "pto_conv1_bwd": [_P, _P, _P, _P, _P, _I, _P, _P],
     "pto_conv1_bwd_data": [_P, _P, _P, _P, _I, _P],
     # fused-optimizer schedule of the single-process MNIST step
-    "pto_conv12_fwd_lazy": [_P] * 9 + [_I, _P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _I, _P],
     "pto_conv12_fwd_lazy_x": [_P] * 9 + [_I, _P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _P, _P, _P, _I, _I, _P],
     "pto_bwd_all": [_P] * 13 + [_L] * 8 + [_P, _P, _L, _P, _I, _P, _F, _F, _F, _I, _P, _I, _I, _I, _P, _P],
-    "pto_fc2_ce_commit": [_P] * 7 + [_I, _F, _P, _P, _P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _P],
     "pto_conv1_commit": [_P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _P, _I, _I, _P],
-    "pto_fc_bwd_adv": [_P] * 10 + [_I, _P, _L, _P, _P],
-    "pto_conv1_bwd_sgd": [_P] * 5 + [_I, _P, _P, _P, _P, _L, _L, _P, _F, _F, _F, _I, _P],
-    "pto_conv1_bwd_sgd_dw1": [_P] * 5 + [_I, _P, _P, _P, _P, _L, _L, _P, _P, _L, _P, _L, _P, _P, _F, _F, _F, _I,
-                                         _P],
     "pto_fc2_ce_dx": [_P] * 9 + [_I, _F, _P, _P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _P, _I, _I, _P],
-    "pto_conv2_bwd_fc": [_P] * 7 + [_I] + [_P] * 7,
-    "pto_fc_bwd_adv_nodw1": [_P] * 9 + [_I, _P, _L, _P, _P],
-    "pto_sgd_flat": [_P, _P, _P, _L, _L, _P, _F, _F, _F, _I, _P],
-    "pto_fc_bwd_part": [_P] * 10 + [_I, _P, _L, _P, _I, _P],
     "pto_eval_head": [_P, _P, _P, _I, _P],
     "pto_sgd_block_count": [_L],
     "pto_sgd_multi": [_P, _P, _I, _I, _P, _F, _F, _F, _F, _I, _I, _P, _L, _P],

@@ -20,7 +20,7 @@ from ..models.mnist import MnistNet, synthetic_mnist
 
 class EagerMnistTrainer:
     def __init__(self, device, batch_size=64, lr=0.01, momentum=0.5, dataset_size=60000, seed=1,
-                 impl="torch", rank=0, data=None, target=None):
+                 impl="torch", rank=0, data=None, target=None, weight_decay=0.0):
         torch.manual_seed(seed)
         self.device = device
         self.batch_size = batch_size
@@ -29,7 +29,7 @@ class EagerMnistTrainer:
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             kw = {"device_ids": [device.index]} if device.type == "cuda" else {}
             self.model = torch.nn.parallel.DistributedDataParallel(self.module, **kw)
-        self.opt = torch.optim.SGD(self.model.parameters(), lr=lr, momentum=momentum)
+        self.opt = torch.optim.SGD(self.model.parameters(), lr=lr, momentum=momentum, weight_decay=weight_decay)
         if data is None:
             data, target = synthetic_mnist(dataset_size, device, seed=seed + 1000 * rank)
         self.data, self.target = data, target

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Per-kernel stats of the MNIST step under rocprofv3 for one or more env
-# settings: kstats.sh "PTO_BWD_ALL=1" "PTO_BWD_ALL=0" ...  Keeps only the
+# settings: kstats.sh "PTO_DETERMINISTIC=0" "PTO_DETERMINISTIC=1" ...  Keeps only the
 # stats CSVs (the traces are large).
 set -e
 cd "$GRAFT_REPO_ROOT"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # LDS counters of the MNIST step kernels per env setting:
-#   lds_pmc.sh "PTO_F12_PROBE=0" "PTO_F12_PROBE=8" ...
+#   lds_pmc.sh "PTO_DETERMINISTIC=0" "PTO_DETERMINISTIC=1" ...
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

@@ -1,8 +1,11 @@
 """Data-parallel fused trainer on the GPU: 2 ranks share the box's one
-MI355X (gloo carries the HBM-resident grads between the two processes,
-exercising the same bucketed/overlapped all-reduce code path the RCCL run
-uses).  Checked against a single-process stock-PyTorch reference that
-averages the two ranks' gradients by hand."""
+MI355X.  RCCL refuses two ranks on one device, so the process group is
+gloo: ``host-allreduce`` exercises the grads-only step + a host-side
+all-reduce between split graphs (the RCCL schedule's structure, not RCCL
+itself); ``xgmi`` / ``xgmi-det`` run the peer-memory all-reduce kernel with
+its SGD epilogue inside the whole-step graph.  Checked against a
+single-process stock-PyTorch reference that averages the two ranks'
+gradients by hand."""
 import os
 import socket
 
@@ -27,15 +30,11 @@ def _free_port():
 
 def _worker(rank, world, port, q, comm):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    if comm == "xgmi-sgd-launch":  # all-reduce kernel without the optimizer epilogue + separate SGD launch
-        comm = "xgmi"
-        os.environ["PTO_AR_FUSED_SGD"] = "0"
-    if comm == "xgmi-overlap":  # fc bucket on a side stream under the conv backward, conv bucket after
-        comm = "xgmi"
-        os.environ["PTO_COMM_OVERLAP"] = "1"
     if comm == "xgmi-det":  # deterministic backward: per-sample conv1 replicas folded by the all-reduce
         comm = "xgmi"
         os.environ["PTO_DETERMINISTIC"] = "1"
+    if comm == "host-allreduce":
+        comm = "rccl"  # "not xGMI": with a gloo group the collective is gloo's host all-reduce
     import torch.distributed as dist
 
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
@@ -44,28 +43,31 @@ def _worker(rank, world, port, q, comm):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=N, seed=1, rank=rank, comm=comm)
-    assert comm != "xgmi" or (tr.comm_info["transport"] == "xgmi" and tr.graph_mode == "full")
+    if comm == "xgmi":
+        assert tr.comm_info["transport"] == "xgmi" and tr.graph_mode == "full" and tr.schedule == "ddp-xgmi"
+    else:
+        assert tr.comm_info["transport"] == "host-allreduce (gloo)" and tr.graph_mode == "split"
+    assert tr.comm_info["world_size"] == 2
     for _ in range(STEPS):
         tr.step()
     torch.cuda.synchronize()
     assert int(tr.batch_idx.item()) == STEPS % (N // 64)
-    assert float(tr.grads[tr._split():].abs().max()) == 0.0  # atomically accumulated range zeroed
-    if comm == "xgmi" and os.environ.get("PTO_AR_FUSED_SGD", "1") == "1" and os.environ.get("PTO_COMM_OVERLAP") != "1":
+    assert float(tr.grads[tr._split:].abs().max()) == 0.0  # atomically accumulated range zeroed
+    if comm == "xgmi":
         # conv1 gradient replicas: folded by the all-reduce before the exchange, then zeroed
-        assert tr.ddp_nrep == tr.c1_nrep > 1
+        assert tr.c1_nrep > 1
         assert float(tr.c1rep.abs().max()) == 0.0
     q.put((rank, tr.params.cpu()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("comm", ["rccl", "xgmi", "xgmi-sgd-launch", "xgmi-overlap", "xgmi-det"])
+@pytest.mark.parametrize("comm", ["host-allreduce", "xgmi", "xgmi-det"])
 def test_fused_ddp_two_ranks_matches_reference(comm):
-    """comm=rccl: host collectives (gloo here) between split graphs;
-    comm=xgmi: one peer-memory all-reduce of the whole buffer with the SGD
-    epilogue inside the whole-step graph (no optimizer launch);
-    xgmi-sgd-launch: plain all-reduce kernel + the multi-tensor SGD launch;
-    xgmi-overlap: fc bucket on a side stream, conv bucket after."""
+    """host-allreduce: grads-only step, gloo all-reduce between split graphs,
+    SGD launch; xgmi: one peer-memory all-reduce of the whole buffer with the
+    SGD epilogue inside the whole-step graph (no optimizer launch); xgmi-det:
+    the same with the deterministic backward."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -90,7 +90,7 @@ def test_gpu_kill_rejoin_resumes_fused_trainer(cluster, tmp_path):
 
 _SHARED_ARGS = ["--backend", "gloo", "--impl", "fused", "--comm", "xgmi", "--log-interval", "50", "--no-test",
                 "--train-size", "16384"]
-_SHARED_ENV = {"PTO_COMM_OVERLAP": "0", "PTO_FAULTHANDLER": "1"}  # no schedule race (4 ranks share one GPU)
+_SHARED_ENV = {"PTO_FAULTHANDLER": "1"}  # SIGUSR2 dumps every thread's stack (PTO_TEST_DUMP_AFTER)
 
 
 @pytest.fixture(scope="module")

@@ -15,19 +15,17 @@ def rel(a, b):
     return ((a - b).abs().max() / b.abs().max()).item()
 
 
-@pytest.mark.parametrize("B,tol,bwd_all", [(4, 0.0, "0"), (1, 0.0, "1"), (64, 2e-3, "1")])
-def test_unrolled_graph_matches_single_steps(monkeypatch, B, tol, bwd_all):
+@pytest.mark.parametrize("B,tol", [(4, 0.0), (1, 0.0), (64, 2e-3)])
+def test_unrolled_graph_matches_single_steps(B, tol):
     """U-step graph replays walk the same trajectory as single steps.  When
     every fp32-atomic gradient address receives exactly one add the step is
-    bitwise deterministic and the two must agree exactly: B=4 with the
-    separate conv2-backward/B1 launches (conv2 wgrad chunks are 7 samples,
-    conv1 chunks 4), B=1 with the all-in-one backward (its conv1 wgrad adds
-    once per sample).  At B=64 the atomics' arrival order varies run to run
+    bitwise deterministic and the two must agree exactly: at B <= 6 there is
+    one conv2-wgrad chunk per tile and every sample adds into its own conv1
+    gradient replica.  At B=64 the atomics' arrival order varies run to run
     and a ReLU at the edge can flip, which amplifies last-bit differences
     chaotically over 21 steps; there the check is a loose trajectory check."""
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
 
-    monkeypatch.setenv("PTO_BWD_ALL", bwd_all)
     dev = torch.device("cuda", 0)
     a = FusedMnistTrainer(dev, batch_size=B, dataset_size=B * 12, seed=2, unroll=8)
     b = FusedMnistTrainer(dev, batch_size=B, dataset_size=B * 12, seed=2, unroll=1)
@@ -86,23 +84,24 @@ def test_captured_rccl_allreduce_in_graph():
 
 @pytest.mark.parametrize("graph,unroll", [("none", 1), (None, 1), (None, 4)])
 def test_fused_optimizer_schedule_matches_sgd_launch(graph, unroll):
-    """The fused-optimizer schedule (no SGD launch; conv1's update applied on
-    the fly by the next step and committed by its fc2 launch) leaves the
-    parameters, momentum and batch cursor of the separate SGD launch at every
-    point the host can observe them (params / state_dict / evaluate),
-    including an LR change and a checkpoint reload mid-run.  (Not bitwise:
-    the schedules evaluate the same update in a different op order; a missed
-    or doubled conv1 update would be off by ~lr*grad, orders of magnitude
-    above the tolerance.)"""
+    """The one-process schedule (no SGD launch: every update inside
+    k_bwd_all, conv1's applied on the fly by the next step's F12 and
+    committed by its F4dx) leaves the parameters, momentum and batch cursor
+    of the DDP code path (grads-only backward + the multi-tensor SGD launch,
+    force_ddp at world size 1) at every point the host can observe them
+    (params / state_dict / evaluate), including an LR change and a
+    checkpoint reload mid-run.  (Not bitwise: the schedules evaluate the
+    same update in a different op order; a missed or doubled conv1 update
+    would be off by ~lr*grad, orders of magnitude above the tolerance.)"""
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
 
     dev = torch.device("cuda", 0)
     # B=4: one fp32-atomic add per gradient address (see the unroll test),
     # so neither schedule has run-to-run noise to amplify
     kw = dict(batch_size=4, dataset_size=4 * 9, seed=4, graph=graph, unroll=unroll, weight_decay=1e-4)
-    a = FusedMnistTrainer(dev, fused_opt=True, **kw)
-    b = FusedMnistTrainer(dev, fused_opt=False, **kw)
-    assert a.fused_opt and not b.fused_opt
+    a = FusedMnistTrainer(dev, **kw)
+    b = FusedMnistTrainer(dev, force_ddp=True, **kw)
+    assert a.schedule == "fused-opt" and b.schedule == "ddp-rccl"
     for t in (a, b):
         t.run(7)
     torch.cuda.synchronize()
@@ -130,59 +129,32 @@ def test_fused_optimizer_schedule_matches_sgd_launch(graph, unroll):
     assert abs(a.last_loss() - b.last_loss()) < 1e-4
 
 
-@pytest.mark.gpu
-def test_dw1_sgd_epilogue_matches_b3_path(monkeypatch):
-    """fc1's weight gradient consumed by the SGD epilogue inside B1
-    (PTO_DW1_SGD=1, never stored) updates the parameters exactly like the
-    path that stores it in B3 and re-reads it in B1's SGD blocks."""
-    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
-
-    dev = torch.device("cuda", 0)
-    kw = dict(batch_size=4, dataset_size=4 * 9, seed=5, graph="full", unroll=4, weight_decay=1e-4)
-    monkeypatch.setenv("PTO_DW1_SGD", "1")
-    a = FusedMnistTrainer(dev, fused_opt=True, **kw)
-    monkeypatch.setenv("PTO_DW1_SGD", "0")
-    b = FusedMnistTrainer(dev, fused_opt=True, **kw)
-    assert a.dw1_sgd and not b.dw1_sgd and a.xcur is not None
-    for t in (a, b):
-        t.run(9)
-    torch.cuda.synchronize()
-    for name in a.p:
-        assert rel(a.p[name], b.p[name]) < 1e-5, name
-    assert rel(a.mom, b.mom) < 1e-4
-    assert abs(a.last_loss() - b.last_loss()) < 1e-5
-
-
 @pytest.mark.parametrize("B", [8, 64])
-def test_bwd_all_matches_separate_launches(monkeypatch, B):
+def test_bwd_all_matches_stock_pytorch(B):
     """The all-in-one backward launch (k_bwd_all: conv2.weight updated by the
     last-arriving wgrad chunk of each tile, dgrad from F12's weight
-    snapshot, every other update in its producer's epilogue) walks the same
-    trajectory as the conv2-backward + B1 launches.  B=8: two wgrad chunks
-    per tile, so the arrival counters and the atomic-exchange consume run;
-    B=64: ten.  fp32 atomics: not bitwise, loose trajectory check."""
+    snapshot, every other update in its producer's epilogue) walks the
+    trajectory of stock PyTorch fp32 (nn.Conv2d/Linear + SGD momentum, same
+    init and batches).  B=8: two wgrad chunks per tile, so the arrival
+    counters and the atomic-exchange consume run; B=64: eleven."""
+    from pytorch_operator_1_amd.models.mnist import param_offsets
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+    from pytorch_operator_1_amd.train.runner import EagerMnistTrainer
 
     dev = torch.device("cuda", 0)
-    kw = dict(batch_size=B, dataset_size=B * 9, seed=6, unroll=4, weight_decay=1e-4)
-    monkeypatch.setenv("PTO_BWD_ALL", "1")
-    a = FusedMnistTrainer(dev, **kw)
-    monkeypatch.setenv("PTO_BWD_ALL", "0")
-    b = FusedMnistTrainer(dev, **kw)
-    assert a.bwd_all and not b.bwd_all
-    for t in (a, b):
-        t.run(7)
+    a = FusedMnistTrainer(dev, batch_size=B, dataset_size=B * 9, seed=6, unroll=4, weight_decay=1e-4)
+    ref = EagerMnistTrainer(dev, batch_size=B, dataset_size=B * 9, seed=6, weight_decay=1e-4)
+    a.run(7)
+    for _ in range(7):
+        ref.step()
     torch.cuda.synchronize()
-    for name in a.p:
-        assert rel(a.p[name], b.p[name]) < 2e-4, name
-    assert rel(a.mom, b.mom) < 2e-3
-    assert abs(a.last_loss() - b.last_loss()) < 1e-3
-    assert int(a.batch_idx.item()) == int(b.batch_idx.item()) == 7 % 9
+    for name, t in ref.model.state_dict().items():
+        assert rel(a.p[name], t) < 2e-4, name
+    assert abs(a.last_loss() - ref.last_loss()) < 1e-3
+    assert int(a.batch_idx.item()) == 7 % 9
     assert int(a.c2_ctr.abs().sum().item()) == 0  # counters re-armed
-    g = a.grads
-    offs = __import__("pytorch_operator_1_amd.models.mnist", fromlist=["param_offsets"]).param_offsets()[0]
-    c2 = offs["conv2.weight"][0]
-    assert float(g[c2:c2 + 25000].abs().max()) == 0.0  # consumed gradients re-zeroed
+    c2 = param_offsets()[0]["conv2.weight"][0]
+    assert float(a.grads[c2:c2 + 25000].abs().max()) == 0.0  # consumed gradients re-zeroed
 
 
 def test_deterministic_mode_b64_bitwise_and_resume(monkeypatch):

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Per-step time of the fused MNIST trainer's MULTI-GPU schedule at world
-size 1 (``force_ddp``: the RCCL all-reduce of a 1-rank group is a no-op, so
-this is the compute + optimizer part of the DDP step), for A/B of
-PTO_DDP_BWD_ALL and friends.  Prints one JSON line.
+size 1 (``force_ddp``: grads-only backward, the RCCL all-reduce of a 1-rank
+group, the multi-tensor SGD launch -- the compute + optimizer part of the
+DDP step), next to the one-process fused-optimizer step.  Prints one JSON
+line.
 
 Usage: python tools/ddp_step_bench.py [--steps 2000] [--warmup 200]
 """
@@ -36,15 +37,18 @@ def main():
     dist.init_process_group("nccl", device_id=dev)
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
 
-    tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=60000, force_ddp=True)
-    tr.run(a.warmup)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    tr.run(a.steps)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / a.steps
-    print(json.dumps({"ddp_step_us": round(dt * 1e6, 2), "ddp_bwd_all": tr.ddp_bwd_all,
-                      "graph_mode": tr.graph_mode, "loss": round(tr.last_loss(), 4)}))
+    out = {}
+    for key, force in (("ddp_step_us", True), ("single_gpu_step_us", False)):
+        tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=60000, force_ddp=force)
+        tr.run(a.warmup)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tr.run(a.steps)
+        torch.cuda.synchronize()
+        out[key] = round((time.perf_counter() - t0) / a.steps * 1e6, 2)
+        out[key.replace("_step_us", "_schedule")] = tr.schedule
+        out[key.replace("_step_us", "_loss")] = round(tr.last_loss(), 4)
+    print(json.dumps(out))
     dist.destroy_process_group()
 
 
