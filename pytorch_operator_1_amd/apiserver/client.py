@@ -68,6 +68,10 @@ class LocalClient(Client):
     def record_event(self, involved, etype, reason, message):
         return self.store.record_event(involved, etype, reason, message)
 
+    def created_unix(self, resource, namespace, name) -> float | None:
+        """Sub-second creation time of an object (None if unknown)."""
+        return self.store.created_unix(self.store.get(resource, namespace, name)["metadata"].get("uid"))
+
 
 class _LocalWatch:
     def __init__(self, w, timeout):
@@ -137,6 +141,17 @@ class RestClient(Client):
 
     def get(self, resource, namespace, name):
         return self._do("GET", self._url(resource, namespace or "default", name))
+
+    def created_unix(self, resource, namespace, name) -> float | None:
+        """Sub-second creation time of an object, from the API server's
+        ``X-Pto-Created-Unix`` response header (None if it has none)."""
+        from .store import CREATED_UNIX_HEADER
+
+        r = self.session.get(self._url(resource, namespace or "default", name), timeout=self.timeout)
+        if r.status_code >= 400:
+            return None
+        v = r.headers.get(CREATED_UNIX_HEADER)
+        return float(v) if v else None
 
     def list(self, resource, namespace=None, label_selector=None, field_selector=None):
         params = {}

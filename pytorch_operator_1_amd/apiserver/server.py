@@ -27,7 +27,7 @@ import threading
 from aiohttp import web
 
 from ..api import crd
-from .store import RESOURCES, ApiError, Store
+from .store import CREATED_UNIX_HEADER, RESOURCES, ApiError, Store
 
 GROUP_PATHS = {
     ("kubeflow.org", "v1"): {"pytorchjobs"},
@@ -117,7 +117,12 @@ class ApiServer:
                 return _json(st.list(resource, ns, q.get("labelSelector"), q.get("fieldSelector")))
             if sub == "log":
                 return await self._log(request, ns, name)
-            return _json(st.get(resource, ns, name))
+            obj = st.get(resource, ns, name)
+            resp = _json(obj)
+            t = st.created_unix(obj.get("metadata", {}).get("uid"))
+            if t is not None:
+                resp.headers[CREATED_UNIX_HEADER] = f"{t:.6f}"
+            return resp
         body = await request.json() if m in ("POST", "PUT", "PATCH") and request.can_read_body else None
         if m == "POST":
             if name is not None:

@@ -32,9 +32,10 @@ from dataclasses import dataclass
 
 from ..api.types import now_rfc3339
 
-# sub-second creation time of a PyTorchJob (creationTimestamp has 1 s
-# resolution); read by the node manager for submit -> first-step
-CREATED_UNIX_ANNOTATION = "pto.amd.com/created-unix"
+# response header carrying an object's sub-second creation time
+# (creationTimestamp has 1 s resolution); read by the node manager for the
+# submit -> first-step metric
+CREATED_UNIX_HEADER = "X-Pto-Created-Unix"
 
 
 class ApiError(Exception):
@@ -182,6 +183,7 @@ class Store:
     def __init__(self, wal_path: str | None = None):
         self._lock = threading.RLock()
         self._objs: dict[tuple[str, str, str], dict] = {}
+        self._created_unix: dict[str, float] = {}  # uid -> creation time (s, sub-second)
         self._rv = 0
         self._history: deque[WatchEvent] = deque(maxlen=self.HISTORY)
         self._watches: list[Watch] = []
@@ -260,8 +262,10 @@ class Store:
                 raise AlreadyExists(resource, md["name"])
             md["uid"] = str(uuid.uuid4())
             md["creationTimestamp"] = now_rfc3339()
-            if resource == "pytorchjobs":  # sub-second submit time for the submit -> first-step metric
-                md.setdefault("annotations", {})[CREATED_UNIX_ANNOTATION] = f"{time.time():.6f}"
+            # sub-second creation time for the submit -> first-step metric,
+            # kept next to the object (never written into it: the user's
+            # object comes back as submitted); served as a response header
+            self._created_unix[md["uid"]] = time.time()
             md["generation"] = 1
             md.pop("deletionTimestamp", None)
             rv = self._bump(obj)
@@ -269,6 +273,11 @@ class Store:
             self._log("put", key, obj, rv)
             self._emit("ADDED", resource, obj)
             return copy.deepcopy(obj)
+
+    def created_unix(self, uid: str | None) -> float | None:
+        """Sub-second creation time of the object with this uid (objects
+        created by this process only; None otherwise)."""
+        return self._created_unix.get(uid) if uid else None
 
     def get(self, resource: str, namespace: str | None, name: str) -> dict:
         with self._lock:

@@ -74,7 +74,7 @@ from ..api import constants as C
 from ..api.types import key_of, name_of, namespace_of, now_rfc3339, parse_rfc3339
 from ..api.validation import gpus_requested
 from ..apiserver.server import LOG_ANNOTATION
-from ..apiserver.store import CREATED_UNIX_ANNOTATION, ApiError
+from ..apiserver.store import ApiError
 from ..controller.informer import Informer
 from .native import AgentClient
 
@@ -717,16 +717,17 @@ class Kubelet:
             self._annotate(pod, ann)
 
     def _job_created(self, pod, job) -> float | None:
-        """Job creationTimestamp (unix seconds, sub-second when recorded)."""
+        """Job creation time (unix seconds): sub-second from the API server
+        when it has it, else creationTimestamp."""
+        fn = getattr(self.client, "created_unix", None)
         try:
+            t = fn("pytorchjobs", namespace_of(pod), job) if fn else None
+            if t is not None:
+                return t
             j = self.client.get("pytorchjobs", namespace_of(pod), job)
-        except ApiError:
+        except (ApiError, OSError):
             return None
-        md = j.get("metadata", {})
-        ann = md.get("annotations") or {}
-        if CREATED_UNIX_ANNOTATION in ann:
-            return float(ann[CREATED_UNIX_ANNOTATION])
-        return parse_rfc3339(md.get("creationTimestamp"))
+        return parse_rfc3339(j.get("metadata", {}).get("creationTimestamp"))
 
     def update_node_metrics(self):
         """Per-GPU HBM used/total from the amdgpu sysfs counters

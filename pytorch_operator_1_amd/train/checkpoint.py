@@ -192,6 +192,8 @@ class ShardedCheckpointer:
                 os.replace(tmp, os.path.join(d, "manifest.json"))
                 for old in list_sharded(self.dir)[:-self.keep]:
                     _rmtree(old)
+                for orphan in list_uncommitted(self.dir, before=step):
+                    _rmtree(orphan)  # a save killed before its manifest (~128 GB per crash at 8B)
         except BaseException as e:  # noqa: BLE001 - re-raised on the training thread by commit()
             self._error = e
 
@@ -282,6 +284,22 @@ def list_sharded(ckpt_dir: str) -> list[str]:
     """Committed (manifest present) sharded steps, oldest first."""
     ds = glob.glob(os.path.join(ckpt_dir, "step-*", "manifest.json"))
     return sorted((os.path.dirname(d) for d in ds), key=lambda p: int(p.rsplit("-", 1)[1]))
+
+
+def list_uncommitted(ckpt_dir: str, before: int) -> list[str]:
+    """Step directories older than ``before`` that never got a manifest: a
+    save that was killed mid-write.  Saves are sequential and the restart
+    gate ends every process of the previous incarnation before the next one
+    starts, so none of them can still be in flight."""
+    out = []
+    for d in glob.glob(os.path.join(ckpt_dir, "step-*")):
+        try:
+            n = int(d.rsplit("-", 1)[1])
+        except ValueError:
+            continue
+        if n < before and not os.path.exists(os.path.join(d, "manifest.json")):
+            out.append(d)
+    return sorted(out)
 
 
 def _rmtree(d: str):

@@ -144,3 +144,18 @@ def test_local_client_matches_interface():
     c = LocalClient(Store())
     c.create("services", {"metadata": {"name": "s"}, "spec": {"clusterIP": "None"}})
     assert c.get("services", "default", "s")["spec"]["clusterIP"] == "None"
+
+
+def test_created_unix_kept_out_of_the_object(server):
+    """The sub-second creation time (submit -> first-step metric) lives next
+    to the object, not in its metadata: a job comes back as submitted
+    (ADVICE r2), and both clients can still read the time."""
+    before = time.time()
+    rc = RestClient(server.url)
+    obj = rc.create("pytorchjobs", new_job("ts-job", workers=0))
+    assert "annotations" not in obj["metadata"] or not obj["metadata"]["annotations"]
+    assert "annotations" not in rc.get("pytorchjobs", "default", "ts-job")["metadata"]
+    t_rest = rc.created_unix("pytorchjobs", "default", "ts-job")
+    t_local = LocalClient(server.store).created_unix("pytorchjobs", "default", "ts-job")
+    assert t_rest is not None and abs(t_rest - t_local) < 1e-5
+    assert before - 1e-3 <= t_local <= time.time()

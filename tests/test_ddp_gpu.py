@@ -39,6 +39,17 @@ def _worker(rank, world, port, q, comm):
 
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
 
+    verify_fail = comm == "xgmi-verify-fail"
+    if verify_fail:
+        # first-run safety on a new node: the xGMI kernel maps the peers but
+        # returns wrong sums (here: it does nothing) -> autotune's check
+        # against the host all-reduce fails on every rank -> every rank
+        # falls back to the collective, and says so in comm_info
+        from pytorch_operator_1_amd.parallel import xgmi
+
+        xgmi.XgmiAllReduce.allreduce_ = lambda self, *a, **k: None
+        comm = "auto"
+
     dist.init_process_group("gloo")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -47,6 +58,9 @@ def _worker(rank, world, port, q, comm):
         assert tr.comm_info["transport"] == "xgmi" and tr.graph_mode == "full" and tr.schedule == "ddp-xgmi"
     else:
         assert tr.comm_info["transport"] == "host-allreduce (gloo)" and tr.graph_mode == "split"
+        assert tr.schedule == "ddp-rccl"
+    if verify_fail:
+        assert tr.comm_info["correct"] is False and tr.comm_info["use_xgmi"] is False, tr.comm_info
     assert tr.comm_info["world_size"] == 2
     for _ in range(STEPS):
         tr.step()
@@ -62,12 +76,14 @@ def _worker(rank, world, port, q, comm):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("comm", ["host-allreduce", "xgmi", "xgmi-det"])
+@pytest.mark.parametrize("comm", ["host-allreduce", "xgmi", "xgmi-det", "xgmi-verify-fail"])
 def test_fused_ddp_two_ranks_matches_reference(comm):
     """host-allreduce: grads-only step, gloo all-reduce between split graphs,
     SGD launch; xgmi: one peer-memory all-reduce of the whole buffer with the
     SGD epilogue inside the whole-step graph (no optimizer launch); xgmi-det:
-    the same with the deterministic backward."""
+    the same with the deterministic backward; xgmi-verify-fail: the kernel
+    fails autotune's verification and every rank falls back to the host
+    all-reduce."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -67,6 +67,55 @@ def _captured_ddp_worker(port, q):
     dist.destroy_process_group()
 
 
+def _capture_fail_worker(port, q):
+    """First-run safety: RCCL refuses graph capture of its all-reduce (as an
+    older RCCL or driver would).  The trainer falls back to split graphs
+    (collective between two graphs), records it in comm_info, and trains on
+    with the same numerics."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    import torch.distributed as dist
+
+    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    orig = FusedMnistTrainer._allreduce_update
+    failed = []
+
+    def refuse_capture(self):
+        if torch.cuda.is_current_stream_capturing() and not failed:
+            failed.append(1)
+            raise RuntimeError("simulated: RCCL refused stream capture")
+        return orig(self)
+
+    FusedMnistTrainer._allreduce_update = refuse_capture
+    ddp = FusedMnistTrainer(dev, batch_size=4, dataset_size=4 * 10, seed=3, force_ddp=True, unroll=4)
+    ref = FusedMnistTrainer(dev, batch_size=4, dataset_size=4 * 10, seed=3, graph="none")
+    ddp.run(10)
+    for _ in range(10):
+        ref.step()
+    torch.cuda.synchronize()
+    q.put((failed == [1], ddp.graph_mode, ddp.comm_info.get("graph_mode"), rel(ddp.params, ref.params)))
+    dist.destroy_process_group()
+
+
+def test_rccl_capture_failure_falls_back_to_split_graphs():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_capture_fail_worker, args=(port, q))
+    p.start()
+    refused, mode, info, err = q.get(timeout=300)
+    p.join(60)
+    assert p.exitcode == 0
+    assert refused and mode == "split" and info == "split (capture failed)"
+    assert err < 1e-5
+
+
 def test_captured_rccl_allreduce_in_graph():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

@@ -118,6 +118,25 @@ def test_keep_prunes_old_steps(tmp_path, keep):
     assert [int(p.rsplit("-", 1)[1]) for p in list_sharded(str(tmp_path))] == [3 - i for i in range(keep)][::-1]
 
 
+def test_orphaned_uncommitted_step_is_deleted(tmp_path):
+    """A save killed before its manifest leaves a step directory nobody
+    resumes from; the next committed save deletes it (older steps only)."""
+    import os
+
+    from pytorch_operator_1_amd.train.checkpoint import ShardedCheckpointer, list_sharded
+
+    ck = ShardedCheckpointer(str(tmp_path), keep=2)
+    ck.save(1, {"a": torch.ones(4)})
+    ck.commit()
+    crashed = tmp_path / "step-000000002"
+    crashed.mkdir()
+    (crashed / "shard-00000-of-00001.pt").write_bytes(b"partial")
+    ck.save(3, {"a": torch.ones(4)})
+    ck.close()
+    assert not crashed.exists()
+    assert [os.path.basename(p) for p in list_sharded(str(tmp_path))] == ["step-000000001", "step-000000003"]
+
+
 def _agree_worker(rank, port, dirs, out):
     import torch.distributed as dist
 
