@@ -42,8 +42,7 @@
 // exits with the retryable code 138.
 //
 // Two independent "channels" (flag sets + epochs) let two buckets be in
-// flight at once on different streams (fc bucket overlapped with the conv
-// backward, then the conv bucket).
+// flight at once on different streams.
 //
 // Small buckets (<= AR_ONESHOT_MAX floats, e.g. MNIST's 100 KB conv bucket,
 // which sits on the step's critical path) use a one-shot variant instead:
@@ -57,8 +56,7 @@
 // momentum with it (same element formula as the multi-tensor SGD launch,
 // sgd_f32.h) and zeroes the local gradient from `zero_from` on (the
 // atomically accumulated range).  The DDP step then needs no optimizer
-// launch, and the fc bucket's update runs on the side stream under the conv
-// backward (which reads no fc parameter).  Zeroing is safe in stage 2: every
+// launch.  Zeroing is safe in stage 2: every
 // peer read this rank's gradient in its stage 1, before barrier 2.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -71,7 +69,10 @@
 namespace {
 
 constexpr int AR_MAX_RANKS = 8;
-constexpr int AR_MAX_BLOCKS = 64;
+// workgroups per launch: ceil(chunk / AR_THREADS) up to this cap, so every
+// thread handles ONE float4 per stage down to world 1-2 on MNIST's 1.7 MB
+// (64 left a 3-round dependent chain per stage at world 1: 18.8 us)
+constexpr int AR_MAX_BLOCKS = 256;
 constexpr int AR_CHANNELS = 2;
 constexpr int AR_THREADS = 512;
 constexpr int AR_MAX_REP = 256;  // gradient replicas folded before barrier 1 (launcher check)
@@ -355,10 +356,11 @@ PTO_API int pto_ar_blocks(long long n, int world) {
 
 // In-place SUM all-reduce of n floats at float offset `off` of the registered
 // input buffers.  peers: device copy of ArPeers.  Requires n % 4 == 0,
-// off % 4 == 0, 1 < world <= 8, chan < 2.
+// off % 4 == 0, 1 <= world <= 8 (world 1: the one-process measurement of the
+// multi-GPU step, no peers), chan < 2.
 PTO_API int pto_ar_allreduce(const void* peers, long long off, long long n, int rank, int world, int chan,
                              void* epochs, void* err, hipStream_t s) {
-  if (n % 4 || off % 4 || world < 2 || world > AR_MAX_RANKS || chan < 0 || chan >= AR_CHANNELS || rank < 0 ||
+  if (n % 4 || off % 4 || world < 1 || world > AR_MAX_RANKS || chan < 0 || chan >= AR_CHANNELS || rank < 0 ||
       rank >= world)
     return -1;
   if (n == 0) return 0;
@@ -384,7 +386,7 @@ PTO_API int pto_ar_allreduce_sgd(const void* peers, long long off, long long n, 
                                  float gscale, int nesterov, long long zero_from, long long* bidx,
                                  long long nbatches, float* rep, int nrep, int rep_stride, long long rep_from,
                                  hipStream_t s) {
-  if (n % 4 || off % 4 || world < 2 || world > AR_MAX_RANKS || chan < 0 || chan >= AR_CHANNELS || rank < 0 ||
+  if (n % 4 || off % 4 || world < 1 || world > AR_MAX_RANKS || chan < 0 || chan >= AR_CHANNELS || rank < 0 ||
       rank >= world || !p || !m || !lr || ((((uintptr_t)p) | ((uintptr_t)m)) & 15) || (bidx && nbatches < 1))
     return -1;
   if (rep && (nrep < 1 || nrep > AR_MAX_REP || rep_stride % 4 || rep_from % 4 || (((uintptr_t)rep) & 15)))

@@ -52,10 +52,13 @@ class XgmiAllReduce:
         if buf.dtype != torch.float32 or not buf.is_cuda or not buf.is_contiguous():
             raise ValueError("XgmiAllReduce: contiguous fp32 HIP buffer required")
         self.group = group
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
+        pg = dist.is_available() and dist.is_initialized()
+        # world size 1 (no process group needed): the multi-GPU step's
+        # launches in one process, for measuring its per-rank cost
+        self.rank = dist.get_rank(group) if pg else 0
+        self.world = dist.get_world_size(group) if pg else 1
         L = _lib.lib()
-        if self.world < 2 or self.world > L.pto_ar_max_ranks():
+        if self.world > L.pto_ar_max_ranks():
             raise ValueError(f"XgmiAllReduce: world size {self.world} unsupported")
         import os
 
@@ -70,6 +73,10 @@ class XgmiAllReduce:
         self._flags = fl.value
         self.epochs = torch.zeros(L.pto_ar_epoch_words(), dtype=torch.int32, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        if self.world == 1:
+            self._opened = []
+            self._set_peers(L, [[buf.data_ptr()], [self.tmp.data_ptr()], [self._flags]])
+            return
         hs = L.pto_ar_ipc_handle_size()
         mine = []
         for p in (buf.data_ptr(), self.tmp.data_ptr(), self._flags):
@@ -99,6 +106,11 @@ class XgmiAllReduce:
         if int(flag.item()) != 1:
             self.close()
             raise RuntimeError("XgmiAllReduce: peer memory could not be mapped on every rank")
+        self._set_peers(L, ptrs)
+        dist.barrier(group=group)
+
+    def _set_peers(self, L, ptrs):
+        """Device copy of the ArPeers table: [input, scratch, flags] x rank."""
         nmax = L.pto_ar_max_ranks()
         words = []
         for k in range(3):
@@ -107,7 +119,6 @@ class XgmiAllReduce:
         assert host.numel() * 8 == L.pto_ar_peers_bytes()
         self.peers = host.to(self.device)
         torch.cuda.synchronize(self.device)
-        dist.barrier(group=group)
 
     def allreduce_(self, offset: int, n: int, chan: int = 0, stream=None):
         """SUM in place over ``buf[offset:offset+n]`` on every rank."""
@@ -192,6 +203,8 @@ class XgmiAllReduce:
         """Verify against RCCL and time both over ``ranges`` [(offset, n)],
         returning ``{"use_xgmi": bool, "xgmi_us": t, "rccl_us": t}`` — the
         same decision on every rank (times are max over ranks)."""
+        if self.world == 1:
+            return self._autotune_single(ranges, iters)
         saved = self.buf.clone()
         g = torch.Generator(device=self.device).manual_seed(1234 + self.rank)
         self.buf.copy_(torch.randn(self.buf.shape, generator=g, device=self.device))
@@ -249,6 +262,26 @@ class XgmiAllReduce:
         result.update(correct=ok_after, use_xgmi=bool(ok_after and tx < tr), xgmi_us=round(tx, 2),
                       rccl_us=round(tr, 2), timed_out=not ok_after)
         return result
+
+    def _autotune_single(self, ranges, iters: int) -> dict:
+        """World size 1: the sum over one rank is the input itself."""
+        saved = self.buf.clone()
+        self.buf.copy_(torch.randn(self.buf.shape, device=self.device))
+        ref = self.buf.clone()
+        for c, (off, n) in enumerate(ranges):
+            self.allreduce_(off, n, chan=c % 2)
+        torch.cuda.synchronize(self.device)
+        ok = bool(torch.equal(self.buf, ref)) and int(self.err.item()) == 0
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            for c, (off, n) in enumerate(ranges):
+                self.allreduce_(off, n, chan=c % 2)
+        torch.cuda.synchronize(self.device)
+        tx = (time.perf_counter() - t0) / iters * 1e6
+        self.buf.copy_(saved)
+        torch.cuda.synchronize(self.device)
+        return {"use_xgmi": ok, "correct": ok, "max_abs_err": 0.0 if ok else float("nan"), "timed_out": False,
+                "xgmi_us": round(tx, 2), "rccl_us": None}
 
     def close(self):
         L = _lib.lib()

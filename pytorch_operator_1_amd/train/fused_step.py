@@ -149,8 +149,8 @@ class FusedMnistTrainer:
 
         # gradient transport (same decision on every rank)
         self._xgmi, self.comm_info = None, {"transport": "none" if self.world == 1 else "rccl"}
-        if self.world > 1 and self.comm in ("xgmi", "auto"):
-            self._setup_xgmi()
+        if (self.world > 1 and self.comm in ("xgmi", "auto")) or (self.ddp and self.comm == "xgmi"):
+            self._setup_xgmi()  # world 1 + force_ddp + comm="xgmi": the xGMI step's launches in one process
         if self.deterministic and self.ddp and self._xgmi is None:
             raise RuntimeError("PTO_DETERMINISTIC=1 with DDP needs the xGMI all-reduce (its SGD epilogue folds the "
                                "per-sample conv1 replicas in order)")

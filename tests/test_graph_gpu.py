@@ -178,6 +178,27 @@ def test_fused_optimizer_schedule_matches_sgd_launch(graph, unroll):
     assert abs(a.last_loss() - b.last_loss()) < 1e-4
 
 
+def test_xgmi_step_at_world_1_matches_sgd_launch():
+    """The multi-GPU xGMI step run in one process (grads-only backward + the
+    all-reduce kernel with its SGD epilogue over one rank: replica fold,
+    update, gradient zeroing, cursor advance) trains like the grads-only
+    step + the multi-tensor SGD launch."""
+    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+
+    dev = torch.device("cuda", 0)
+    kw = dict(batch_size=4, dataset_size=4 * 9, seed=8, unroll=4, weight_decay=1e-4, force_ddp=True)
+    a = FusedMnistTrainer(dev, comm="xgmi", **kw)
+    b = FusedMnistTrainer(dev, comm="rccl", **kw)
+    assert a.schedule == "ddp-xgmi" and a.comm_info["correct"] and b.schedule == "ddp-rccl"
+    for t in (a, b):
+        t.run(7)
+    torch.cuda.synchronize()
+    assert rel(a.params, b.params) < 1e-5
+    assert rel(a.mom, b.mom) < 1e-4
+    assert int(a.batch_idx.item()) == int(b.batch_idx.item()) == 7 % 9
+    assert float(a.c1rep.abs().max()) == 0.0 and float(a.grads[a._split:].abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("B", [8, 64])
 def test_bwd_all_matches_stock_pytorch(B):
     """The all-in-one backward launch (k_bwd_all: conv2.weight updated by the

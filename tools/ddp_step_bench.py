@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Per-step time of the fused MNIST trainer's MULTI-GPU schedule at world
-size 1 (``force_ddp``: grads-only backward, the RCCL all-reduce of a 1-rank
-group, the multi-tensor SGD launch -- the compute + optimizer part of the
-DDP step), next to the one-process fused-optimizer step.  Prints one JSON
-line.
+size 1 (``force_ddp``: grads-only backward, then either the RCCL
+all-reduce of a 1-rank group + the multi-tensor SGD launch, or the xGMI
+all-reduce kernel with its SGD epilogue over one rank -- the per-rank
+launches of the N>1 step without the peer traffic), next to the one-process
+fused-optimizer step.  Prints one JSON line.
 
 Usage: python tools/ddp_step_bench.py [--steps 2000] [--warmup 200]
 """
@@ -26,6 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--only", choices=["ddp", "xgmi", "single"], default=None, help="time one schedule (for rocprof)")
     a = ap.parse_args()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -38,8 +40,16 @@ def main():
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
 
     out = {}
-    for key, force in (("ddp_step_us", True), ("single_gpu_step_us", False)):
-        tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=60000, force_ddp=force)
+    # ddp: grads-only step + RCCL all-reduce of the 1-rank group + SGD launch;
+    # xgmi: grads-only step + the xGMI all-reduce kernel with its SGD
+    # epilogue over one rank (the N>1 step's launches minus the peer reads)
+    runs = (("ddp_step_us", "ddp", dict(force_ddp=True, comm="rccl")),
+            ("ddp_xgmi_step_us", "xgmi", dict(force_ddp=True, comm="xgmi")),
+            ("single_gpu_step_us", "single", {}))
+    for key, tag, kw in runs:
+        if a.only and a.only != tag:
+            continue
+        tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=60000, **kw)
         tr.run(a.warmup)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
