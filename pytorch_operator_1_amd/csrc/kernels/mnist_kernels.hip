@@ -786,12 +786,15 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
   const int nrow = min(16, B - mt * 16);
   const float4* hg = reinterpret_cast<const float4*>(h1 + (size_t)mt * 16 * F1OUT);
   const float4* wg = reinterpret_cast<const float4*>(w2);
+  // a zero RVALUE: with an lvalue zero, `ok ? *p : z4` is an lvalue
+  // conditional, which the compiler lowers to a flat load from a select
+  // between p and a scratch copy of the zero
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   const int h4n = nrow * (F1OUT / 4);
-  const float4 hv0 = t < h4n ? hg[t] : z4;
-  const float4 hv1 = (t + NT < H4 && t + NT < h4n) ? hg[t + NT] : z4;
-  const float4 wv0 = t < W4 ? wg[t] : z4;
-  const float4 wv1 = t + NT < W4 ? wg[t + NT] : z4;
+  const float4 hv0 = t < h4n ? hg[t] : float4(z4);
+  const float4 hv1 = (t + NT < H4 && t + NT < h4n) ? hg[t + NT] : float4(z4);
+  const float4 wv0 = t < W4 ? wg[t] : float4(z4);
+  const float4 wv1 = t + NT < W4 ? wg[t + NT] : float4(z4);
   float bw[NGK][4];
 #pragma unroll
   for (int q = 0; q < NGK; ++q) load4<LAY_KROW>(w1, F1IN, nt * 16 + r, F1IN, kb + 16 * q + 4 * gq, kend, bw[q]);
@@ -819,8 +822,8 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     for (int q = 0; q < NGK; ++q) {
       const int k0 = kb + 16 * q + 4 * gq;
       const bool ok = k0 < F1OUT;
-      const float4 a = ok ? *reinterpret_cast<const float4*>(hs + r * HLD + k0) : z4;
-      const float4 b = (ok && r < NCLS) ? *reinterpret_cast<const float4*>(w2s + r * HLD + k0) : z4;
+      const float4 a = ok ? *reinterpret_cast<const float4*>(hs + r * HLD + k0) : float4(z4);
+      const float4 b = (ok && r < NCLS) ? *reinterpret_cast<const float4*>(w2s + r * HLD + k0) : float4(z4);
       acc0 = mfma16x16x4(a.x, b.x, acc0);
       acc1 = mfma16x16x4(a.y, b.y, acc1);
       acc0 = mfma16x16x4(a.z, b.z, acc0);
@@ -967,42 +970,57 @@ PTO_DEV void wave_halving26(const float acc[26], int lane, float* out) {
   if (!(lane & 1) && idx < 26) out[idx] = h1;
 }
 
-// conv2 weight-gradient block (part A of the conv2 backward): one 16-column
-// K-tile x all 64 (padded) output channels x a chunk of B2_CHUNK samples,
-// fp32 atomics into gw2.
-template <int CH>
+// conv2 weight-gradient block (part A of the conv2 backward): NTW 16-column
+// K-tiles x all 64 (padded) output channels x a chunk of CH samples, fp32
+// atomics into gw2 (or, deterministic mode, the chunk's partial tile).
+// ONE staging round: the block's 16*NTW (ic,kh,kw) columns touch at most
+// NCH input channels, so for every sample of the chunk it stages NCH x 144
+// pooled conv1 values + the 800 pooled grads + 800 codes with coalesced
+// 16-byte loads, then runs its MFMAs from LDS.  NTW = 2 shares that staging
+// (and every A-operand read) between two column tiles.
+template <int NTW>
+constexpr int wgrad_nch() { return NTW == 1 ? 2 : 3; }  // 16 cols span <= 2 channels, 32 cols <= 3
+template <int CH, int NTW>
+constexpr int wgrad_lds_floats() { return CH * (wgrad_nch<NTW>() * 144 + F1IN + F1IN / 4); }
+template <int CH, int NTW = 1>
 PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, const uint8_t* __restrict__ code2,
                             const float* __restrict__ a1p, float* __restrict__ gw2, int B,
                             float* __restrict__ part = nullptr) {
+  constexpr int NT = 32 / NTW;           // column tiles of one sample chunk
+  constexpr int NCH = wgrad_nch<NTW>();  // input channels staged per sample
+  static_assert(32 % NTW == 0, "500 columns = 32 tiles of 16");
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // ---- part A: weight gradient.  ONE staging round: the block's K-tile
-  // (16 (ic,kh,kw) columns) touches at most 2 input channels, so for all 8
-  // samples of the chunk it stages 2x144 pooled conv1 values + the 800
-  // pooled grads + 800 codes (41 KB) with coalesced 16-byte loads, then
-  // runs its 128 MFMAs from LDS.
-  const int nt = bid % 32, chunk = bid / 32;
+  const int nt = bid % NT, chunk = bid / NT;
+  const int col0 = nt * 16 * NTW;
   const int oc = wv * 16 + (lane & 15);
   const int g = lane >> 4;
-  const int kk = nt * 16 + (lane & 15);
-  const bool kvalid = kk < 500;
-  const int ic0 = (nt * 16) / 25;
-  const int ic = kvalid ? kk / 25 : ic0, r25 = kvalid ? kk - ic * 25 : 0;
-  const int kh = r25 / 5, kw = r25 - kh * 5;
+  const int ic0 = col0 / 25;
+  int koff[NTW];
+  bool kvalid[NTW];
+#pragma unroll
+  for (int u = 0; u < NTW; ++u) {
+    const int kk = col0 + 16 * u + (lane & 15);
+    kvalid[u] = kk < 500;
+    const int ic = kvalid[u] ? kk / 25 : ic0, r25 = kvalid[u] ? kk - ic * 25 : 0;
+    const int kh = r25 / 5, kw = r25 - kh * 5;
+    koff[u] = (ic - ic0) * 144 + kh * 12 + kw;
+  }
   const bool ocvalid = oc < C2;
   const int b0 = chunk * CH, nb = min(B, b0 + CH) - b0;
-  float* as = smem;                                   // [8][2][144]
-  float* gs = smem + CH * 288;                  // [8][800]
-  uint8_t* cs = reinterpret_cast<uint8_t*>(gs + CH * F1IN);  // [8][800] bytes
+  float* as = smem;                                           // [CH][NCH][144]
+  float* gs = smem + CH * NCH * 144;                          // [CH][800]
+  uint8_t* cs = reinterpret_cast<uint8_t*>(gs + CH * F1IN);  // [CH][800] bytes
   const int tid = threadIdx.x;
   {
-    constexpr int NVA = (CH * 72 + 255) / 256, NVG = (CH * (F1IN / 4) + 255) / 256;
+    constexpr int A4 = NCH * 36;  // float4 per sample
+    constexpr int NVA = (CH * A4 + 255) / 256, NVG = (CH * (F1IN / 4) + 255) / 256;
     float4 va[NVA], vg[NVG];
     uint32_t vc[NVG];
 #pragma unroll
     for (int q = 0; q < NVA; ++q) {
       const int e = tid + 256 * q;  // float4 index over [s][ch][36]
-      const int smp = e / 72, rr = e - smp * 72, ch = rr / 36, off = (rr - ch * 36) * 4;
-      const bool ok = e < nb * 72 && ic0 + ch < C1;
+      const int smp = e / A4, rr = e - smp * A4, ch = rr / 36, off = (rr - ch * 36) * 4;
+      const bool ok = e < nb * A4 && ic0 + ch < C1;
       va[q] = ok ? *reinterpret_cast<const float4*>(a1p + (b0 + smp) * A1P + (ic0 + ch) * 144 + off)
                  : float4{0.f, 0.f, 0.f, 0.f};
     }
@@ -1016,7 +1034,7 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
 #pragma unroll
     for (int q = 0; q < NVA; ++q) {
       const int e = tid + 256 * q;
-      if (e < CH * 72) reinterpret_cast<float4*>(as)[e] = va[q];
+      if (e < CH * A4) reinterpret_cast<float4*>(as)[e] = va[q];
     }
 #pragma unroll
     for (int q = 0; q < NVG; ++q) {
@@ -1036,37 +1054,46 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
     }
   }
   __syncthreads();
-  f32x4 acc0 = zero4(), acc1 = zero4();
-  const int koff = (ic - ic0) * 144 + kh * 12 + kw;
+  // K order: lane group g = pooled pixel 4G+g, MFMA j = window position j,
+  // so one (grad, code) expansion feeds 4 MFMAs per column tile
+  f32x4 acc0[NTW], acc1[NTW];
+#pragma unroll
+  for (int u = 0; u < NTW; ++u) acc0[u] = acc1[u] = zero4();
   const int goff = (ocvalid ? oc : 0) * 16;
 #pragma unroll 2
   for (int smp = 0; smp < nb; ++smp) {
-    const float* ap0 = as + smp * 288 + koff;
 #pragma unroll
     for (int G = 0; G < 4; ++G) {
       const int pp = 4 * G + g;
       const float gv = ocvalid ? gs[smp * F1IN + goff + ((G ^ ((oc >> 1) & 3)) << 2) + (g ^ (((oc >> 3) & 1) << 1))]
                                : 0.f;
       const int cd = ocvalid ? (int)cs[smp * F1IN + goff + ((G ^ ((oc >> 3) & 1)) << 2) + g] : 4;
-      const float* ap = ap0 + 2 * (pp >> 2) * 12 + 2 * (pp & 3);
-      const float bv0 = kvalid ? ap[0] : 0.f, bv1 = kvalid ? ap[1] : 0.f;
-      const float bv2 = kvalid ? ap[12] : 0.f, bv3 = kvalid ? ap[13] : 0.f;
-      acc0 = mfma16x16x4(cd == 0 ? gv : 0.f, bv0, acc0);
-      acc1 = mfma16x16x4(cd == 1 ? gv : 0.f, bv1, acc1);
-      acc0 = mfma16x16x4(cd == 2 ? gv : 0.f, bv2, acc0);
-      acc1 = mfma16x16x4(cd == 3 ? gv : 0.f, bv3, acc1);
+      const float a0 = cd == 0 ? gv : 0.f, a1 = cd == 1 ? gv : 0.f, a2 = cd == 2 ? gv : 0.f, a3 = cd == 3 ? gv : 0.f;
+#pragma unroll
+      for (int u = 0; u < NTW; ++u) {
+        const float* ap = as + smp * (NCH * 144) + koff[u] + 2 * (pp >> 2) * 12 + 2 * (pp & 3);
+        const float bv0 = kvalid[u] ? ap[0] : 0.f, bv1 = kvalid[u] ? ap[1] : 0.f;
+        const float bv2 = kvalid[u] ? ap[12] : 0.f, bv3 = kvalid[u] ? ap[13] : 0.f;
+        acc0[u] = mfma16x16x4(a0, bv0, acc0[u]);
+        acc1[u] = mfma16x16x4(a1, bv1, acc1[u]);
+        acc0[u] = mfma16x16x4(a2, bv2, acc0[u]);
+        acc1[u] = mfma16x16x4(a3, bv3, acc1[u]);
+      }
     }
   }
-  const f32x4 acc = acc0 + acc1;
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const int m = wv * 16 + (lane >> 4) * 4 + rr;
-    const int n = nt * 16 + (lane & 15);
-    if (m < C2 && n < 500) {
-      if (part)  // deterministic mode: this chunk's partial tile, summed in chunk order by the last arriver
-        part[(bid / 32) * (C2 * 500) + m * 500 + n] = acc[rr];
-      else
-        atomicAdd(gw2 + m * 500 + n, acc[rr]);
+  for (int u = 0; u < NTW; ++u) {
+    const f32x4 acc = acc0[u] + acc1[u];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int m = wv * 16 + (lane >> 4) * 4 + rr;
+      const int n = col0 + 16 * u + (lane & 15);
+      if (m < C2 && n < 500) {
+        if (part)  // deterministic mode: this chunk's partial tile, summed in chunk order by the last arriver
+          part[chunk * (C2 * 500) + m * 500 + n] = acc[rr];
+        else
+          atomicAdd(gw2 + m * 500 + n, acc[rr]);
+      }
     }
   }
 }
@@ -1517,7 +1544,7 @@ struct EpiSgd {
   }
 };
 
-template <int CH>
+template <int CH, int NTW>
 __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int s_last;
@@ -1571,13 +1598,14 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   bid -= A.nF;
   if (bid < A.nA) {
     const bool det = A.wpart != nullptr;
-    c2_wgrad_block<CH>(bid, smem, A.g2, A.code2, A.a1p, A.g2w, A.B, A.wpart);
+    c2_wgrad_block<CH, NTW>(bid, smem, A.g2, A.code2, A.a1p, A.g2w, A.B, A.wpart);
     if (A.grads_only && !det) return;
     // arrival: every lane's atomics have been performed at the memory side
     // (deterministic mode: the partial-tile stores are written back first)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const int nt = bid % 32, nchunk = A.nA / 32;
+    constexpr int NT = 32 / NTW, TC = 16 * NTW;  // column tiles per chunk, columns per tile
+    const int nt = bid % NT, nchunk = A.nA / NT;
     if (threadIdx.x == 0) {
       if (det) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       const int old = __hip_atomic_fetch_add(A.ctr + nt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1589,13 +1617,14 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
     }
     __syncthreads();
     if (!s_last) return;
-    int idx[4];
-    float gv[4], pv[4], mv[4];
+    constexpr int NQ = (C2 * TC + 255) / 256;  // tile elements per thread
+    int idx[NQ];
+    float gv[NQ], pv[NQ], mv[NQ];
     if (det) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int e = threadIdx.x + 256 * q, row = e >> 4, col = nt * 16 + (e & 15);
-        idx[q] = (e < C2 * 16 && col < 500) ? row * 500 + col : -1;
+      for (int q = 0; q < NQ; ++q) {
+        const int e = threadIdx.x + 256 * q, row = e / TC, col = nt * TC + (e % TC);
+        idx[q] = (e < C2 * TC && col < 500) ? row * 500 + col : -1;
         float g = 0.f;
         if (idx[q] >= 0)
           for (int c = 0; c < nchunk; ++c) g += A.wpart[c * (C2 * 500) + idx[q]];  // chunk order
@@ -1603,16 +1632,16 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
       }
       if (A.grads_only) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < NQ; ++q)
           if (idx[q] >= 0) A.g2w[idx[q]] = gv[q];
         return;
       }
     }
     const float lr = *A.a.lr;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {  // 50 rows x 16 columns = 800 elements
-      const int e = threadIdx.x + 256 * q, row = e >> 4, col = nt * 16 + (e & 15);
-      idx[q] = (e < C2 * 16 && col < 500) ? row * 500 + col : -1;
+    for (int q = 0; q < NQ; ++q) {  // 50 rows x TC columns
+      const int e = threadIdx.x + 256 * q, row = e / TC, col = nt * TC + (e % TC);
+      idx[q] = (e < C2 * TC && col < 500) ? row * 500 + col : -1;
       if (idx[q] >= 0) {
         if (!det) gv[q] = atomicExch(A.g2w + idx[q], 0.f);
         pv[q] = A.p2w[idx[q]];
@@ -1620,7 +1649,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
       }
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < NQ; ++q)
       if (idx[q] >= 0) {
         sgd_elem(pv[q], gv[q], mv[q], lr, A.a.mom, A.a.wd, A.a.gscale, A.a.nesterov);
         A.p2w[idx[q]] = pv[q];
@@ -1864,6 +1893,10 @@ PTO_API int pto_eval_head(const float* logp, const int64_t* labels, float* stats
 // per CU next to the 31.5 KB dgrad blocks (sweep 4..8: 21.7, 20.8, 17.6,
 // 18.1, 23.4 us, profiles/bwd_all_r2.md).
 constexpr int BWD_WCHUNK = 6;
+// 16-column tiles per conv2-wgrad block of k_bwd_all.  2 shares the staged
+// grads/codes (and the A-operand reads) between two tiles but halves the
+// wgrad blocks: k_bwd_all 16.5 -> 18.4 us (r3), so 1
+constexpr int BWD_WNTW = 1;
 
 // The all-in-one backward (+ optimizer) launch (k_bwd_all).  Flat-buffer
 // views: p/g/m + offsets of each parameter (elements); ctr: 32 zeroed ints.
@@ -1897,15 +1930,15 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   A.g2b = g + off_c2b; A.g1w = g + off_fc1w; A.g1b = g + off_fc1b; A.gfw = g + off_fc2w; A.gfb = g + off_fc2b;
   if (grads_only) A.w2f = p + off_c2w;  // nothing updates conv2.weight in this launch
   A.bidx = bidx; A.nbatches = nbatches; A.pending = pending; A.B = B;
-  A.nA = ((B + BWD_WCHUNK - 1) / BWD_WCHUNK) * 32;
+  A.nA = ((B + BWD_WCHUNK - 1) / BWD_WCHUNK) * (32 / BWD_WNTW);
   A.nB = B * B2_ICG;
   A.nC = (C2 + 3) / 4;
   A.nD = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
   A.nF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9;
   A.wpart = wpart;
-  const size_t ldsA = BWD_WCHUNK * (288 + F1IN + F1IN / 4) * sizeof(float);
+  const size_t ldsA = wgrad_lds_floats<BWD_WCHUNK, BWD_WNTW>() * sizeof(float);
   const size_t ldsB = B2_LDS_FLOATS * sizeof(float);
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;
-  hipLaunchKernelGGL(k_bwd_all<BWD_WCHUNK>, dim3(A.nA + A.nB + A.nC + A.nD + A.nF), dim3(256), lds, s, A);
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bwd_all<BWD_WCHUNK, BWD_WNTW>), dim3(A.nA + A.nB + A.nC + A.nD + A.nF), dim3(256), lds, s, A);
   LAUNCH_CHECK();
 }
