@@ -1687,6 +1687,28 @@ __global__ __launch_bounds__(256) void k_conv1_commit(Conv1Commit cm, int* __res
   if (threadIdx.x == 0) *pending = 0;
 }
 
+// The RCCL schedule's optimizer launch (ddp-rccl).  The all-reduce covers
+// the flat gradient buffer AND the conv1 replica tail allocated right after
+// it (one message), so k_bwd_all spreads conv1's same-address atomics over
+// C1_REPLICAS copies on this schedule too; this launch folds them in replica
+// order (commit4's association), applies SGD to the flat params/momentum,
+// zeroes the atomically accumulated range [zero_from, n) and the replicas,
+// and advances the batch cursor.  One float4 per thread.
+__global__ __launch_bounds__(256) void k_ddp_sgd(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                                                 int n, int c1, int zero_from, float* __restrict__ rep, int nrep,
+                                                 SgdArgs a, long long* __restrict__ bidx, long long nbatches) {
+  if (bidx && blockIdx.x == 0 && threadIdx.x == 0) *bidx = (*bidx + 1) % nbatches;
+  const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= n) return;
+  const float lr = *a.lr;
+  if (i >= c1) {
+    const Conv1Commit cm{p + c1, g + c1, m + c1, n - c1, nullptr, a, rep, nrep, n - c1};
+    commit4(cm, i - c1, lr);
+  } else {
+    sgd_flat4(p, g, m, i, lr, a, i >= zero_from);
+  }
+}
+
 // conv1 data gradient (only needed when the input requires grad, e.g. the
 // nn.Module path under autograd checks).  dx[b][y][x] = sum dY1 * w.
 __global__ __launch_bounds__(256) void k_conv1_bwd_data(const float* __restrict__ g1,
@@ -1830,6 +1852,20 @@ PTO_API int pto_conv1_commit(float* p1, float* g1, float* m1, int n1, int* pendi
     return -1;
   Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), rep, nrep, rep_stride};
   hipLaunchKernelGGL(k_conv1_commit, dim3(1), dim3(256), 0, s, cm, pending);
+  LAUNCH_CHECK();
+}
+
+// ddp-rccl optimizer launch (k_ddp_sgd): flat buffers of n floats, conv1
+// range [c1, n), replicas r >= 1 at rep + (r-1)*(n-c1).
+PTO_API int pto_mnist_ddp_sgd(float* p, float* g, float* m, int n, int c1, int zero_from, float* rep, int nrep,
+                              const float* lr, float mom, float wd, float gscale, int nesterov, long long* bidx,
+                              long long nbatches, hipStream_t s) {
+  if (n % 4 || c1 % 4 || zero_from % 4 || c1 < 0 || c1 >= n || !lr || nrep < 1 || nrep > C1_MAXREP ||
+      (nrep > 1 && !rep) || (bidx && nbatches < 1))
+    return -1;
+  if ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)rep)) & 15) return -1;
+  hipLaunchKernelGGL(k_ddp_sgd, dim3((n / 4 + 255) / 256), dim3(256), 0, s, p, g, m, n, c1, zero_from, rep, nrep,
+                     sgd_args(lr, mom, wd, gscale, nesterov), bidx, nbatches);
   LAUNCH_CHECK();
 }
 

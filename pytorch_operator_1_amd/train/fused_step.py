@@ -31,9 +31,10 @@ knobs):
   ``ddp-xgmi``: the same four launches with ``k_bwd_all`` in grads-only
       mode, then ONE xGMI all-reduce of the flat buffer whose epilogue is the
       SGD update (+ conv1 replica fold, gradient zeroing, cursor advance).
-  ``ddp-rccl``: the grads-only step, one RCCL all-reduce, one multi-tensor
-      SGD launch.  With a host-side backend (gloo) the collective runs
-      between two captured graphs ("split").
+  ``ddp-rccl``: the grads-only step, one RCCL all-reduce of the gradients
+      and their conv1 replica tail, one SGD launch (``k_ddp_sgd``: replica
+      fold, update, zeroing, cursor).  With a host-side backend (gloo) the
+      collective runs between two captured graphs ("split").
   deterministic (``PTO_DETERMINISTIC=1``): ``k_bwd_all`` without floating-
       point atomics (conv2 wgrad partial tiles summed in chunk order, one
       conv1 gradient replica per sample); bitwise reproducible runs.
@@ -140,9 +141,6 @@ class FusedMnistTrainer:
         self.target = target[: self.n_batches * B].reshape(self.n_batches, B).contiguous()
         self.batch_idx = torch.zeros(1, device=device, dtype=torch.int64)
 
-        from ..ops.optim import SgdTable
-
-        self.sgd = SgdTable([(self._params, self.grads, self.mom)], device)
         self.lr_dev = torch.tensor([self.lr], **f32)
         self.steps_done = 0
         self._owed = False  # host view: a conv1 update may be owed (fused-opt)
@@ -154,12 +152,23 @@ class FusedMnistTrainer:
         if self.deterministic and self.ddp and self._xgmi is None:
             raise RuntimeError("PTO_DETERMINISTIC=1 with DDP needs the xGMI all-reduce (its SGD epilogue folds the "
                                "per-sample conv1 replicas in order)")
-        # conv1 replicas: fused-opt readers and the xGMI epilogue fold them;
-        # the RCCL path all-reduces a single copy
-        self.c1_nrep = B if self.deterministic else (C1_REPLICAS if (not self.ddp or self._xgmi) else 1)
+        # conv1 replicas: fused-opt readers and the xGMI epilogue fold them
+        # locally; on the RCCL schedule they are a tail of the gradient
+        # allocation, all-reduced with it in one message and folded by the
+        # optimizer launch (k_ddp_sgd)
+        self.c1_nrep = B if self.deterministic else C1_REPLICAS
         self.c1_stride = self.numel - self._c1
-        self.c1rep = torch.zeros(max(1, self.c1_nrep - 1) * self.c1_stride, **f32)
         self.schedule = "fused-opt" if not self.ddp else ("ddp-xgmi" if self._xgmi is not None else "ddp-rccl")
+        nrep_tail = max(1, self.c1_nrep - 1) * self.c1_stride
+        if self.schedule == "ddp-rccl":
+            self._ar_buf = torch.zeros(total + nrep_tail, **f32)
+            self.grads = self._ar_buf[:total]
+            for name, (off, shape) in offs.items():
+                self.g[name] = self.grads[off:off + math.prod(shape)].view(shape)
+            self.c1rep = self._ar_buf[total:]
+        else:
+            self._ar_buf = self.grads
+            self.c1rep = torch.zeros(nrep_tail, **f32)
 
         # graph modes: "full" = whole steps (collectives included) in HIP
         # graphs; "split" = the collective issued between two graphs (a
@@ -261,12 +270,14 @@ class FusedMnistTrainer:
                                       replicas=self.c1rep, n_replicas=self.c1_nrep, rep_from=self._c1)
             return
         if _pg_ready():
-            dist.all_reduce(self.grads)
+            dist.all_reduce(self._ar_buf)  # gradients + conv1 replica tail, one message
         self._sgd_launch()
 
     def _sgd_launch(self):
-        self.sgd.step(self.lr_dev, self.lr, self.momentum, self.weight_decay, 1.0 / self.world, self.nesterov,
-                      zero_grad=True, stream=self._s(), batch_cursor=self.batch_idx, n_batches=self.n_batches)
+        _lib.check(self.L.pto_mnist_ddp_sgd(self._params.data_ptr(), self.grads.data_ptr(), self.mom.data_ptr(),
+                                            self.numel, self._c1, self._split, self.c1rep.data_ptr(), self.c1_nrep,
+                                            *self._opt_args(), self.batch_idx.data_ptr(), self.n_batches, self._s()),
+                   "ddp_sgd")
 
     def _eager_step(self):
         self._forward()
@@ -443,7 +454,7 @@ class FusedMnistTrainer:
             else:  # split: the host collective between the two graphs
                 self._graphs[0].replay()
                 if _pg_ready():
-                    dist.all_reduce(self.grads)
+                    dist.all_reduce(self._ar_buf)
                 self._graphs[1].replay()
         self.steps_done += 1
         self._owed = self.fused_opt

@@ -68,7 +68,7 @@ def main():
             G["conv1.weight"].data_ptr() if f else None, G["conv1.bias"].data_ptr() if f else None, s))
     launches["conv1_bwd"] = lambda: L.pto_conv1_bwd(da1p.data_ptr(), tr.code1.data_ptr(), tr.data.data_ptr(),
                                                     G["conv1.weight"].data_ptr(), G["conv1.bias"].data_ptr(), B, bi, s)
-    launches["sgd"] = lambda: tr.sgd.step(tr.lr_dev, 0.0, 0.0, 0.0, 1.0, False, zero_grad=False, stream=s)
+    launches["sgd"] = lambda: tr._sgd_launch()  # ddp-rccl optimizer launch (k_ddp_sgd)
     launches["empty(sgd n=1)"] = None
     tiny = torch.zeros(4, device=dev)
     from pytorch_operator_1_amd.ops.optim import SgdTable
