@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Which roles of ``k_bwd_all`` set its time: the launch with whole block
+ranges left out (tools/probes/bwd_roles.hip, its own .so; the shipped
+kernel is unchanged).  Each variant: a HIP graph of 40 launches, replayed,
+median us per launch.  Usage: python tools/bwd_roles_probe.py [--build]
+(--build compiles the probe .so, on the CPU host, before the GPU run)."""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+SRC = os.path.join(ROOT, "tools", "probes", "bwd_roles.hip")
+SO = os.path.join(ROOT, "tools", "probes", "libbwd_roles.so")
+ROLES = {1: "C conv2-bias", 2: "F fc2/bias", 4: "A conv2-wgrad", 8: "B dgrad+conv1-wgrad", 16: "D dW1"}
+
+
+def build():
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-I", os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "kernels"), "-o", SO, SRC]
+    subprocess.check_call(cmd)
+    print("built", SO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--reps", type=int, default=15)
+    a = ap.parse_args()
+    if a.build:
+        build()
+        return
+    import torch
+
+    from pytorch_operator_1_amd.ops import _lib
+    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+
+    P_, I_, L_ = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong
+    lib = ctypes.CDLL(SO)
+    fn = lib.probe_bwd_all
+    fn.argtypes = [P_] * 13 + [L_] * 8 + [P_, P_, L_, P_, I_, P_, P_, I_, I_, I_, P_]
+    fn.restype = ctypes.c_int
+    dev = torch.device("cuda", 0)
+    tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=64 * 16, graph="none")
+    for _ in range(3):
+        tr.step()
+    torch.cuda.synchronize()
+
+    def launch(mask):
+        rc = fn(tr.da2p.data_ptr(), tr.code2.data_ptr(), tr.a1p.data_ptr(), tr.w2f.data_ptr(), tr.xcur.data_ptr(),
+                tr.code1.data_ptr(), tr.dh1.data_ptr(), tr.a2p.data_ptr(), tr.h1.data_ptr(), tr.dlogits.data_ptr(),
+                tr._params.data_ptr(), tr.grads.data_ptr(), tr.mom.data_ptr(), *tr._offs, tr.c2_ctr.data_ptr(),
+                tr.batch_idx.data_ptr(), tr.n_batches, tr.pending.data_ptr(), tr.B, tr.lr_dev.data_ptr(),
+                tr.c1rep.data_ptr(), tr.c1_nrep, tr.c1_stride, mask, _lib.stream_ptr(dev))
+        assert rc == 0, rc
+
+    masks = [31, 1 | 2, 4, 8, 16, 31 & ~4, 31 & ~8, 31 & ~16, 4 | 8]
+    graphs = {}
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        for mk in masks:
+            launch(mk)
+    torch.cuda.synchronize()
+    for mk in masks:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(40):
+                launch(mk)
+        graphs[mk] = g
+    res = {mk: [] for mk in masks}
+    for _ in range(a.reps):
+        for mk in masks:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            graphs[mk].replay()
+            e1.record()
+            e1.synchronize()
+            res[mk].append(e0.elapsed_time(e1) * 1000 / 40)
+    out = {}
+    for mk in masks:
+        v = sorted(res[mk])[len(res[mk]) // 2]
+        name = "+".join(ROLES[b].split()[0] for b in ROLES if mk & b) or "empty grid (noop)"
+        out[name] = round(v, 2)
+        print(f"{name:>24s}  {v:7.2f} us/launch")
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
