@@ -34,6 +34,13 @@
 #include "mfma_f32.h"
 #include "sgd_f32.h"
 
+// Phase timestamps for the timing probes under tools/probes (which define
+// PTO_STAMP before including this file); nothing in the shipped library.
+#ifndef PTO_STAMP
+#define PTO_STAMP(k) ((void)0)
+#define PTO_STAMP_SCOPE()
+#endif
+
 namespace {
 
 constexpr int C1 = 20, C2 = 50, P1 = 12, F1OUT = 500, F1IN = 800, NCLS = 10;
@@ -928,10 +935,10 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
 //  part C: db2[oc] = sum of unmasked pooled grads (one wave per channel).
 constexpr int B2_CHUNK = 7;  // samples per weight-grad block (7: LDS <= 40 KB -> 4 blocks/CU, all parts co-resident)
 constexpr int B2_ICG = 10;   // input-channel pairs per sample in the dgrad part
-// LDS of a dgrad block: R1 = max(W2 slice [52][68] + stage 1000, T [64][65])
-// + R2 = dY2 [64][52] (c2_dgrad_block)
+// LDS of a dgrad block: R1 = T [64][65] (first the W2 slice [50][68]) +
+// R2 = dY2^T [50][68] (c2_dgrad_block)
 constexpr int B2_DLD = 68;  // dY^T row stride (64 positions + 4): conflict-free writes and GEMM reads
-constexpr int B2_LDS_FLOATS = ((52 * 68 + 1000) > 64 * 65 ? (52 * 68 + 1000) : 64 * 65) + C2 * B2_DLD;
+constexpr int B2_LDS_FLOATS = 64 * 65 + C2 * B2_DLD;
 
 // Recursive-halving wave reduction of 26 (padded to 32) per-lane sums: at
 // each step a lane keeps half of its live accumulators (chosen by its lane
@@ -1054,33 +1061,97 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
     }
   }
   __syncthreads();
+  PTO_STAMP(1);
   // K order: lane group g = pooled pixel 4G+g, MFMA j = window position j,
-  // so one (grad, code) expansion feeds 4 MFMAs per column tile
+  // so one (grad, code) expansion feeds 4 MFMAs per column tile.
+  // Branch-free operand reads over all CH staged samples (the slots of
+  // samples past nb were staged as zero grads with code 4); columns
+  // kk >= 500 read column offset 0 -- finite values whose output columns are
+  // never stored -- so every read of a sample can be issued before its
+  // MFMAs (exec-masked reads compiled to one LDS round trip per pixel
+  // group).  Waves 0-2 run rows 0..47 on the matrix cores; wave 3 runs rows
+  // 48, 49 on the VALU.
+  if (wv == C2 / 16) {
+    // rows 48..49 (the only valid rows of the 4th 16-row tile) on the VALU:
+    // lane = column c (16) x row 48 + rr (2) x sample half h (2); per
+    // (sample, pooled pixel) one (grad, code) pair and the one patch value
+    // its code selects -- a quarter of the FLOPs of the zero-padded MFMA
+    // tile, and no MFMA issue on this wave's SIMD
+    static_assert(C2 % 16 == 2, "VALU tail covers exactly 2 rows");
+    const int c = lane & 15, rr = (lane >> 4) & 1, h = lane >> 5;
+    const int ocx = C2 - 2 + rr;
+    const int xg = ocx * 16, xgsw = (ocx >> 1) & 3, xghs = ((ocx >> 3) & 1) << 1, xcsw = (ocx >> 3) & 1;
+    float sum[NTW];
+#pragma unroll
+    for (int u = 0; u < NTW; ++u) sum[u] = 0.f;
+#pragma unroll
+    for (int i = 0; i < (CH + 1) / 2; ++i) {
+      const int smp = 2 * i + h;
+      if (smp >= CH) break;
+#pragma unroll
+      for (int pp = 0; pp < 16; ++pp) {
+        const int G = pp >> 2, gq = pp & 3;
+        const float gv = gs[smp * F1IN + xg + ((G ^ xgsw) << 2) + (gq ^ xghs)];
+        const int cd = cs[smp * F1IN + xg + ((G ^ xcsw) << 2) + gq];
+        const int po = (cd >> 1) * 12 + (cd & 1);  // window position of the code (cd 4: masked)
+#pragma unroll
+        for (int u = 0; u < NTW; ++u) {
+          const float* ap = as + smp * (NCH * 144) + koff[u] + 24 * G + 2 * gq;
+          const float bvx = ap[cd < 4 ? po : 0];
+          sum[u] = fmaf(cd < 4 ? gv : 0.f, bvx, sum[u]);
+        }
+      }
+    }
+    PTO_STAMP(2);
+#pragma unroll
+    for (int u = 0; u < NTW; ++u) {
+      const float v = sum[u] + __shfl_xor(sum[u], 32, 64);
+      const int n = col0 + 16 * u + c;
+      if (h == 0 && n < 500) {
+        if (part)
+          part[chunk * (C2 * 500) + ocx * 500 + n] = v;
+        else
+          atomicAdd(gw2 + ocx * 500 + n, v);
+      }
+    }
+    return;
+  }
   f32x4 acc0[NTW], acc1[NTW];
 #pragma unroll
   for (int u = 0; u < NTW; ++u) acc0[u] = acc1[u] = zero4();
-  const int goff = (ocvalid ? oc : 0) * 16;
-#pragma unroll 2
-  for (int smp = 0; smp < nb; ++smp) {
+  const int ocr = oc;
+  const int goff = ocr * 16, gsw = (ocr >> 1) & 3, ghs = ((ocr >> 3) & 1) << 1, csw = (ocr >> 3) & 1;
+#pragma unroll
+  for (int smp = 0; smp < CH; ++smp) {
+    float gv[4], bv[NTW][4][4];
+    int cd[4];
 #pragma unroll
     for (int G = 0; G < 4; ++G) {
-      const int pp = 4 * G + g;
-      const float gv = ocvalid ? gs[smp * F1IN + goff + ((G ^ ((oc >> 1) & 3)) << 2) + (g ^ (((oc >> 3) & 1) << 1))]
-                               : 0.f;
-      const int cd = ocvalid ? (int)cs[smp * F1IN + goff + ((G ^ ((oc >> 3) & 1)) << 2) + g] : 4;
-      const float a0 = cd == 0 ? gv : 0.f, a1 = cd == 1 ? gv : 0.f, a2 = cd == 2 ? gv : 0.f, a3 = cd == 3 ? gv : 0.f;
+      gv[G] = gs[smp * F1IN + goff + ((G ^ gsw) << 2) + (g ^ ghs)];
+      cd[G] = cs[smp * F1IN + goff + ((G ^ csw) << 2) + g];
 #pragma unroll
       for (int u = 0; u < NTW; ++u) {
-        const float* ap = as + smp * (NCH * 144) + koff[u] + 2 * (pp >> 2) * 12 + 2 * (pp & 3);
-        const float bv0 = kvalid[u] ? ap[0] : 0.f, bv1 = kvalid[u] ? ap[1] : 0.f;
-        const float bv2 = kvalid[u] ? ap[12] : 0.f, bv3 = kvalid[u] ? ap[13] : 0.f;
-        acc0[u] = mfma16x16x4(a0, bv0, acc0[u]);
-        acc1[u] = mfma16x16x4(a1, bv1, acc1[u]);
-        acc0[u] = mfma16x16x4(a2, bv2, acc0[u]);
-        acc1[u] = mfma16x16x4(a3, bv3, acc1[u]);
+        const float* ap = as + smp * (NCH * 144) + koff[u] + 24 * G + 2 * g;
+        bv[u][G][0] = ap[0];
+        bv[u][G][1] = ap[1];
+        bv[u][G][2] = ap[12];
+        bv[u][G][3] = ap[13];
+      }
+    }
+#pragma unroll
+    for (int G = 0; G < 4; ++G) {
+      const float a0 = cd[G] == 0 ? gv[G] : 0.f, a1 = cd[G] == 1 ? gv[G] : 0.f;
+      const float a2 = cd[G] == 2 ? gv[G] : 0.f, a3 = cd[G] == 3 ? gv[G] : 0.f;
+#pragma unroll
+      for (int u = 0; u < NTW; ++u) {
+        acc0[u] = mfma16x16x4(a0, bv[u][G][0], acc0[u]);
+        acc1[u] = mfma16x16x4(a1, bv[u][G][1], acc1[u]);
+        acc0[u] = mfma16x16x4(a2, bv[u][G][2], acc0[u]);
+        acc1[u] = mfma16x16x4(a3, bv[u][G][3], acc1[u]);
       }
     }
   }
+  PTO_STAMP(2);
 #pragma unroll
   for (int u = 0; u < NTW; ++u) {
     const f32x4 acc = acc0[u] + acc1[u];
@@ -1088,7 +1159,7 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
     for (int rr = 0; rr < 4; ++rr) {
       const int m = wv * 16 + (lane >> 4) * 4 + rr;
       const int n = col0 + 16 * u + (lane & 15);
-      if (m < C2 && n < 500) {
+      if (n < 500) {
         if (part)  // deterministic mode: this chunk's partial tile, summed in chunk order by the last arriver
           part[chunk * (C2 * 500) + m * 500 + n] = acc[rr];
         else
@@ -1115,15 +1186,17 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
   constexpr int WLD = 68;   // 64 + 4: the 4 k-rows of a wave hit disjoint banks
   constexpr int TLD = 65;
   // Two LDS regions, each reused once the phase that reads it is over
-  // (31.5 KB in all: 5 blocks per CU):
-  //   R1: W2 slice [52][68] + grads/codes stage  -> after the GEMM: T [64][65]
+  // (30 KB in all):
+  //   R1: W2 slice [50][68]                     -> after the GEMM: T [64][65]
   //       -> after col2im: the conv1 wave partials
   //   R2: expanded dY2^T [50][68]               -> after the GEMM: input
   //       image [784] + conv1 codes [2][144] (held in registers until then)
   //       + d(a1p) of the two channels [288]
-  constexpr int R1 = (52 * WLD + F1IN + F1IN / 4) > 64 * TLD ? (52 * WLD + F1IN + F1IN / 4) : 64 * TLD;
+  // The W2 slice's pad columns 50..63 are never written: they only feed T
+  // columns col2im does not read; the K rows past 50 are masked at the read.
+  constexpr int R1 = 64 * TLD;
+  static_assert(50 * WLD <= R1, "W2 slice fits R1");
   float* ws = smem;                      // R1
-  float* gstage = ws + 52 * WLD;         // R1 tail: [800] grads + [800 B] codes
   float* ts = smem;                      // R1 after the GEMM
   float* dys = smem + R1;                // R2
   float* xs = dys;                       // R2 after the GEMM
@@ -1159,33 +1232,40 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
       const int e = tid + 256 * q, k = e / 50, n = e - k * 50;
       if (e < C2 * 50) ws[k * WLD + n] = wv_[q];
     }
-    for (int e = tid; e < 2 * WLD; e += 256) ws[50 * WLD + e] = 0.f;     // rows 50,51
-    for (int e = tid; e < 50 * 14; e += 256) ws[(e / 14) * WLD + 50 + e % 14] = 0.f;  // cols 50..63
+    // dY^T [oc][pos] expanded straight from the registers: thread t < 200
+    // holds pooled row ph = t & 3 of channel oc = t >> 2 (4 grads + 4 codes)
+    // and writes conv2-output rows 2ph and 2ph+1 (16 positions, 4 float4)
     if (tid < F1IN / 4) {
-      reinterpret_cast<float4*>(gstage)[tid] = gv4;
-      reinterpret_cast<uint32_t*>(gstage + F1IN)[tid] = cv;
-    }
-  }
-  __syncthreads();
-  {
-    const float* gst = gstage;
-    const uint8_t* cst = reinterpret_cast<const uint8_t*>(gstage + F1IN);
-    // dY^T [oc][pos]: lanes run over positions, so the 32 lanes of a
-    // ds_read group read 8 distinct (grad, code) words (broadcast) and write
-    // consecutive floats (the [pos][oc] order read gst at a 16-float stride:
-    // 16-way bank conflicts)
-    for (int e = tid; e < C2 * 64; e += 256) {
-      const int oc = e >> 6, pos = e & 63;
-      const int oh = pos >> 3, ow = pos & 7;
-      const int gi = oc * 16 + (oh >> 1) * 4 + (ow >> 1);
-      dys[oc * B2_DLD + pos] = (cst[gi] == ((oh & 1) * 2 + (ow & 1))) ? gst[gi] : 0.f;
-    }
-  }
-  __syncthreads();
-  {
-    f32x4 acc[4];
+      const int oc = tid >> 2, ph = tid & 3;
+      const float gq[4] = {gv4.x, gv4.y, gv4.z, gv4.w};
+      float e[2][8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = zero4();
+      for (int pw = 0; pw < 4; ++pw) {
+        const int cd = (cv >> (8 * pw)) & 0xff;
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 2; ++dx) e[dy][2 * pw + dx] = cd == dy * 2 + dx ? gq[pw] : 0.f;
+      }
+      float4* row = reinterpret_cast<float4*>(dys + oc * B2_DLD + 16 * ph);
+      row[0] = float4{e[0][0], e[0][1], e[0][2], e[0][3]};
+      row[1] = float4{e[0][4], e[0][5], e[0][6], e[0][7]};
+      row[2] = float4{e[1][0], e[1][1], e[1][2], e[1][3]};
+      row[3] = float4{e[1][4], e[1][5], e[1][6], e[1][7]};
+    }
+  }
+  __syncthreads();
+  PTO_STAMP(1);
+  {
+    // T columns 0..47 on the matrix cores (3 column tiles); the 2 valid
+    // columns of the 4th tile (48, 49) on the VALU: lane = position (16) x
+    // column (2) x K half (2), 25 FMAs, one shuffle -- a 13-MFMA tile that
+    // was 7/8 padding
+    static_assert(2 * 25 - 48 == 2, "VALU tail covers T columns 48, 49");
+    constexpr int NQ = 3;
+    f32x4 acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[q] = zero4();
 #pragma unroll
     for (int k0 = 0; k0 < 4; ++k0) {
       if (k0 == 3) {
@@ -1194,65 +1274,85 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
         const int k = 48 + gg;
         const float a = k < C2 ? dys[k * B2_DLD + wv * 16 + r] : 0.f;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = mfma16x16x4(a, ws[k * WLD + q * 16 + r], acc[q]);
+        for (int q = 0; q < NQ; ++q) acc[q] = mfma16x16x4(a, k < C2 ? ws[k * WLD + q * 16 + r] : 0.f, acc[q]);
         break;
       }
-      float av[4], bv[4][4];
+      float av[4], bv[NQ][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int k = 16 * k0 + 4 * gg + j;
-        av[j] = k < C2 ? dys[k * B2_DLD + wv * 16 + r] : 0.f;
+        av[j] = dys[k * B2_DLD + wv * 16 + r];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) bv[q][j] = k < 52 ? ws[k * WLD + q * 16 + r] : 0.f;
+        for (int q = 0; q < NQ; ++q) bv[q][j] = ws[k * WLD + q * 16 + r];
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < NQ; ++q)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[q] = mfma16x16x4(av[j], bv[q][j], acc[q]);
     }
+    float tail;
+    {
+      const int pos = wv * 16 + r, cc = 48 + (gg & 1), k0 = (gg >> 1) * 25;
+      float tv = 0.f;
+#pragma unroll
+      for (int k = 0; k < 25; ++k) tv = fmaf(dys[(k0 + k) * B2_DLD + pos], ws[(k0 + k) * WLD + cc], tv);
+      tail = tv + __shfl_xor(tv, 32, 64);
+    }
     __syncthreads();  // ts aliases ws, xs aliases dys: every wave's GEMM reads are done
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < NQ; ++q)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
         ts[(wv * 16 + gg * 4 + rr) * TLD + q * 16 + r] = acc[q][rr];
+    if (gg < 2) ts[(wv * 16 + r) * TLD + 48 + gg] = tail;
     if (fuse1) {
       if (tid < 196) reinterpret_cast<float4*>(xs)[tid] = xv;
       if (tid < 72) reinterpret_cast<uint32_t*>(c1s)[tid] = c1v;
     }
   }
   __syncthreads();
+  PTO_STAMP(3);
   {
     // 288 outputs on 256 threads: one full output per thread, then the last
     // 32 outputs split 8 ways over all threads (<= 4 taps each, 3-step
-    // shuffle sum) instead of a second full round on half a wave
+    // shuffle sum) instead of a second full round on half a wave.  Taps
+    // outside the 8x8 map read T[0][0] and are dropped by a select, so all
+    // of a thread's reads issue back to back (no exec-masked branches)
     {
       const int o = tid, icl = o / 144, pix = o - icl * 144;
       const int y = pix / 12, xx = pix - y * 12;
-      float sacc = 0.f;
+      float tv[25];
 #pragma unroll
-      for (int kh = 0; kh < 5; ++kh) {
-        const int sy = y - kh;
-        if (sy < 0 || sy >= 8) continue;
+      for (int kh = 0; kh < 5; ++kh)
 #pragma unroll
         for (int kw = 0; kw < 5; ++kw) {
-          const int sx = xx - kw;
-          if (sx < 0 || sx >= 8) continue;
-          sacc += ts[(sy * 8 + sx) * TLD + icl * 25 + kh * 5 + kw];
+          const int sy = y - kh, sx = xx - kw;
+          const bool ok = (unsigned)sy < 8u && (unsigned)sx < 8u;
+          tv[kh * 5 + kw] = ts[ok ? (sy * 8 + sx) * TLD + icl * 25 + kh * 5 + kw : 0];
+          tv[kh * 5 + kw] = ok ? tv[kh * 5 + kw] : 0.f;
         }
-      }
+      float sacc = 0.f;
+#pragma unroll
+      for (int t = 0; t < 25; ++t) sacc += tv[t];
       if (da1p) da1p[b * A1P + (icg * 2 + icl) * 144 + pix] = sacc;
       dsum[o] = sacc;
     }
     {
       const int o = 256 + (tid >> 3), part = tid & 7, pix = o - 144;  // icl = 1
       const int y = pix / 12, xx = pix - y * 12;
-      float sacc = 0.f;
+      float tv[4];
 #pragma unroll
-      for (int tt = part; tt < 25; tt += 8) {
+      for (int i = 0; i < 4; ++i) {
+        const int tt = part + 8 * i;
         const int kh = tt / 5, kw = tt - kh * 5, sy = y - kh, sx = xx - kw;
-        if (sy >= 0 && sy < 8 && sx >= 0 && sx < 8) sacc += ts[(sy * 8 + sx) * TLD + 25 + tt];
+        const bool ok = tt < 25 && (unsigned)sy < 8u && (unsigned)sx < 8u;
+        tv[i] = ts[ok ? (sy * 8 + sx) * TLD + 25 + tt : 0];
+        tv[i] = ok ? tv[i] : 0.f;
       }
+      float sacc = tv[0];  // tap order, as the sequential sum over valid taps
+      sacc += tv[1];
+      sacc += tv[2];
+      sacc += tv[3];
       sacc += __shfl_xor(sacc, 4, 64);
       sacc += __shfl_xor(sacc, 2, 64);
       sacc += __shfl_xor(sacc, 1, 64);
@@ -1267,6 +1367,7 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
   // separate conv1-backward launch): thread = (channel, tap, pixel
   // quarter); pooled grad expanded through the conv1 argmax code.
   __syncthreads();
+  PTO_STAMP(4);
   float* part = ws;  // [4][26] wave totals (free after the GEMM)
   {
     // pixel-major: wave w owns channel w>>1 and 72 of its 144 pooled pixels
@@ -1296,6 +1397,7 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
     wave_halving26(acc, lane, part + wv * 26);
   }
   __syncthreads();
+  PTO_STAMP(5);
   if (tid < 52) {
     const int icl = tid / 26, k = tid - icl * 26, oc1 = icg * 2 + icl;
     const float v = part[(2 * icl) * 26 + k] + part[(2 * icl + 1) * 26 + k];
@@ -1549,6 +1651,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int s_last;
   int bid = blockIdx.x;
+  PTO_STAMP_SCOPE();
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (bid == 0 && threadIdx.x == 0 && !A.grads_only) {  // no block of this launch reads the cursor
     *A.bidx = (*A.bidx + 1) % A.nbatches;
@@ -1604,6 +1707,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
     // (deterministic mode: the partial-tile stores are written back first)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    PTO_STAMP(3);
     constexpr int NT = 32 / NTW, TC = 16 * NTW;  // column tiles per chunk, columns per tile
     const int nt = bid % NT, nchunk = A.nA / NT;
     if (threadIdx.x == 0) {
@@ -1616,6 +1720,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
       }
     }
     __syncthreads();
+    PTO_STAMP(4);
     if (!s_last) return;
     constexpr int NQ = (C2 * TC + 255) / 256;  // tile elements per thread
     int idx[NQ];

@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""Per-phase timeline of ``k_bwd_all``'s roles: the shipped kernel source
+built with its PTO_STAMP marks compiled in (tools/probes/bwd_phases.hip, its
+own .so).  Thread 0 of every block stamps the chip-wide 100 MHz clock at
+entry, at each phase mark and at exit; the report gives, per role, the mean
+entry offset from the launch's first block, mean phase durations and mean
+exit, plus the launch span.  Usage: python tools/bwd_phases_probe.py
+[--build] [--mask 31]."""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+SRC = os.path.join(ROOT, "tools", "probes", "bwd_phases.hip")
+SO = os.path.join(ROOT, "tools", "probes", "libbwd_phases.so")
+SLOTS = 8
+PHASES = {"A": ["staged", "mfma", "atomics done", "counted", "exit"],
+          "B": ["staged+dY", "gemm+T", "col2im", "conv1 wgrad", "exit"]}
+MARKS = {"A": [0, 1, 2, 3, 4, 7], "B": [0, 1, 3, 4, 5, 7]}
+
+
+def build():
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                           "-I", os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "kernels"), "-o", SO, SRC])
+    print("built", SO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--mask", type=int, nargs="*", default=[31, 8, 4])
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    if a.build:
+        build()
+        return
+    import numpy as np
+    import torch
+
+    from pytorch_operator_1_amd.ops import _lib
+    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+
+    P_, I_, L_ = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong
+    lib = ctypes.CDLL(SO)
+    fn = lib.probe_bwd_all
+    fn.argtypes = [P_] * 13 + [L_] * 8 + [P_, P_, L_, P_, I_, P_, P_, I_, I_, I_, P_]
+    fn.restype = ctypes.c_int
+    rd = lib.probe_read_stamps
+    rd.argtypes = [P_, I_]
+    dev = torch.device("cuda", 0)
+    tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=64 * 16, graph="none")
+    for _ in range(3):
+        tr.step()
+    torch.cuda.synchronize()
+    counts = dict(C=13, F=17, A=352, B=640, D=400)
+    bits = dict(C=1, F=2, A=4, B=8, D=16)
+    report = {}
+    for mask in a.mask:
+        spans, per_role = [], {}
+        for _ in range(a.reps):
+            rc = fn(tr.da2p.data_ptr(), tr.code2.data_ptr(), tr.a1p.data_ptr(), tr.w2f.data_ptr(),
+                    tr.xcur.data_ptr(), tr.code1.data_ptr(), tr.dh1.data_ptr(), tr.a2p.data_ptr(), tr.h1.data_ptr(),
+                    tr.dlogits.data_ptr(), tr._params.data_ptr(), tr.grads.data_ptr(), tr.mom.data_ptr(),
+                    *tr._offs, tr.c2_ctr.data_ptr(), tr.batch_idx.data_ptr(), tr.n_batches, tr.pending.data_ptr(),
+                    tr.B, tr.lr_dev.data_ptr(), tr.c1rep.data_ptr(), tr.c1_nrep, tr.c1_stride, mask,
+                    _lib.stream_ptr(dev))
+            assert rc == 0
+            torch.cuda.synchronize()
+            nblk = sum(counts[r] for r in counts if mask & bits[r])
+            buf = (ctypes.c_ulonglong * (nblk * SLOTS))()
+            assert rd(buf, nblk * SLOTS) == 0
+            st = np.frombuffer(buf, dtype=np.uint64).reshape(nblk, SLOTS).astype(np.int64)
+            t0 = st[:, 0].min()
+            rel = (st - t0) * 10.0 / 1000.0  # 100 MHz ticks -> us
+            spans.append(float(rel[:, 7].max()))
+            i = 0
+            for r in ("C", "F", "A", "B", "D"):
+                if not mask & bits[r]:
+                    continue
+                blk = rel[i:i + counts[r]]
+                i += counts[r]
+                d = per_role.setdefault(r, {"entry": [], "exit": [], "entry_max": [], "exit_max": [], "ph": []})
+                d["entry"].append(blk[:, 0].mean())
+                d["entry_max"].append(blk[:, 0].max())
+                d["exit"].append(blk[:, 7].mean())
+                d["exit_max"].append(blk[:, 7].max())
+                if r in PHASES:
+                    marks = MARKS[r]
+                    durs = []
+                    for k0, k1 in zip(marks, marks[1:]):
+                        ok = (blk[:, k1] > 0) & (blk[:, k0] > 0)
+                        durs.append(float((blk[ok, k1] - blk[ok, k0]).mean()) if ok.any() else float("nan"))
+                    d["ph"].append(durs)
+        med = lambda v: float(np.median(v))
+        out = {"span_us": round(med(spans), 2)}
+        for r, d in per_role.items():
+            o = {"entry_mean": round(med(d["entry"]), 2), "entry_last": round(med(d["entry_max"]), 2),
+                 "exit_mean": round(med(d["exit"]), 2), "exit_last": round(med(d["exit_max"]), 2)}
+            if d["ph"]:
+                ph = np.median(np.array(d["ph"]), axis=0)
+                o["phases"] = {name: round(float(v), 2) for name, v in zip(PHASES[r], ph)}
+            out[r] = o
+        report[mask] = out
+        print(f"mask {mask}: {json.dumps(out)}")
+    print(json.dumps(report))
+
+
+if __name__ == "__main__":
+    main()
