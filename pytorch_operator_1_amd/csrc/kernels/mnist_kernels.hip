@@ -454,20 +454,31 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
         p[r][c] = v.x;
         p[r][c + 1] = v.y;
       }
+    // the task's two channels as one packed pair: every tap is one
+    // v_pk_fma_f32 (input pixel broadcast to both halves, the two channels'
+    // weights as the pair), 100 instead of 200 FMA issues per lane; each
+    // half is the same fmaf chain as a scalar sum (bitwise equal)
+    static_assert(CPT == 2, "conv1 full tasks pack two channels");
+    f32x2 s2[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int dy = q >> 1, dx = q & 1;
+      f32x2 acc2 = f32x2{bz[0], bz[1]};
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) {
+          const float pv = p[dy + kh][dx + kw];
+          acc2 = __builtin_elementwise_fma(f32x2{pv, pv}, f32x2{wr[0][kh * 5 + kw], wr[1][kh * 5 + kw]}, acc2);
+        }
+      s2[q] = acc2;
+    }
 #pragma unroll
     for (int cc = 0; cc < CPT; ++cc) {
       const int oc = cg * CPT + cc;
       float v[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int dy = q >> 1, dx = q & 1;
-        float sacc = bz[cc];
-#pragma unroll
-        for (int kh = 0; kh < 5; ++kh)
-#pragma unroll
-          for (int kw = 0; kw < 5; ++kw) sacc = fmaf(p[dy + kh][dx + kw], wr[cc][kh * 5 + kw], sacc);
-        v[q] = sacc;
-      }
+      for (int q = 0; q < 4; ++q) v[q] = s2[q][cc];
       float o;
       uint8_t cd;
       relu_pool4(v, o, cd);

@@ -59,6 +59,14 @@ from ..ops import _lib
 # update, the commit, the xGMI fold) sum them in replica order
 C1_REPLICAS = 8
 
+# Graph capture is thread-local: with "global" capture a HIP call from ANY
+# other thread of the process while a step is being captured -- e.g. the
+# RCCL process group's watchdog polling its events -- invalidates the
+# capture (hipErrorStreamCaptureInvalidated / "operation not permitted when
+# stream is capturing" on the watchdog), which the captured-RCCL GPU test hit
+# intermittently.  Only the capturing thread's own calls are checked now.
+_CAPTURE_MODE = "thread_local"
+
 
 def _pg_ready() -> bool:
     return dist.is_available() and dist.is_initialized()
@@ -353,10 +361,10 @@ class FusedMnistTrainer:
         torch.cuda.synchronize(self.device)
         if self.graph_mode == "split":
             ga, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(ga):
+            with torch.cuda.graph(ga, capture_error_mode=_CAPTURE_MODE):
                 self._forward()
                 self._backward()
-            with torch.cuda.graph(gc):
+            with torch.cuda.graph(gc, capture_error_mode=_CAPTURE_MODE):
                 self._sgd_launch()
             self._graphs = [ga, gc]
             return
@@ -367,7 +375,7 @@ class FusedMnistTrainer:
         self._graph_pow = {}
         for k in self._graph_sizes():
             gk = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gk):
+            with torch.cuda.graph(gk, capture_error_mode=_CAPTURE_MODE):
                 for _ in range(k):
                     self._eager_step()
             self._graph_pow[k] = gk
@@ -377,7 +385,7 @@ class FusedMnistTrainer:
         if self.fused_opt:
             for k in range(1, self.unroll + 1):
                 gk = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gk):
+                with torch.cuda.graph(gk, capture_error_mode=_CAPTURE_MODE):
                     for _ in range(k):
                         self._eager_step()
                     self._commit_launch()

@@ -10,6 +10,7 @@ import os
 import socket
 
 import pytest
+from mp_util import collect
 import torch
 import torch.multiprocessing as mp
 import torch.nn.functional as F
@@ -91,7 +92,7 @@ def test_fused_ddp_two_ranks_matches_reference(comm):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q, comm)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in range(2))
+    res = dict(collect(q, procs, 2))
     for p in procs:
         p.join(60)
         assert p.exitcode == 0

@@ -5,6 +5,7 @@ import os
 import socket
 
 import pytest
+from mp_util import collect
 import torch
 import torch.multiprocessing as mp
 
@@ -109,7 +110,7 @@ def test_rccl_capture_failure_falls_back_to_split_graphs():
     q = ctx.Queue()
     p = ctx.Process(target=_capture_fail_worker, args=(port, q))
     p.start()
-    refused, mode, info, err = q.get(timeout=300)
+    refused, mode, info, err = collect(q, [p], 1)[0]
     p.join(60)
     assert p.exitcode == 0
     assert refused and mode == "split" and info == "split (capture failed)"
@@ -125,7 +126,7 @@ def test_captured_rccl_allreduce_in_graph():
     q = ctx.Queue()
     p = ctx.Process(target=_captured_ddp_worker, args=(port, q))
     p.start()
-    err = q.get(timeout=300)
+    err = collect(q, [p], 1)[0]
     p.join(60)
     assert p.exitcode == 0
     assert err < 1e-5

@@ -8,6 +8,7 @@ import os
 import socket
 
 import pytest
+from mp_util import collect
 import torch
 import torch.multiprocessing as mp
 
@@ -103,7 +104,7 @@ def test_xgmi_allreduce_exact(world):
     ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = [q.get(timeout=240) for _ in range(world)]
+    res = collect(q, ps, world, timeout=110)
     for p in ps:
         p.join(60)
     for rank, worst, same, tune in res:
@@ -198,7 +199,7 @@ def test_xgmi_allreduce_sgd_epilogue(world):
     ps = [ctx.Process(target=_sgd_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = [q.get(timeout=240) for _ in range(world)]
+    res = collect(q, ps, world, timeout=110)
     for p in ps:
         p.join(60)
     for rank, worst, ok, cur in res:
@@ -284,7 +285,7 @@ def test_xgmi_timeout_fails_fast_without_updates():
     ps = [ctx.Process(target=_stall_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = sorted(q.get(timeout=240) for _ in range(2))
+    res = sorted(collect(q, ps, 2, timeout=110))
     for p in ps:
         p.join(60)
     for rank, elapsed, unchanged, raised, after, polls in res:

@@ -60,6 +60,9 @@ def main():
     torch.cuda.synchronize()
     counts = dict(C=13, F=17, A=352, B=640, D=400)
     bits = dict(C=1, F=2, A=4, B=8, D=16)
+    occ = ctypes.CDLL(SO).probe_bwd_all_occupancy
+    occ.restype = ctypes.c_int
+    print("resident k_bwd_all blocks per CU (occupancy API):", occ())
     report = {}
     for mask in a.mask:
         spans, per_role = [], {}
@@ -90,6 +93,7 @@ def main():
                 d["entry_max"].append(blk[:, 0].max())
                 d["exit"].append(blk[:, 7].mean())
                 d["exit_max"].append(blk[:, 7].max())
+                d.setdefault("entry_hist", []).append(np.histogram(blk[:, 0], bins=[0, 2, 4, 6, 8, 10, 12, 14, 99])[0])
                 if r in PHASES:
                     marks = MARKS[r]
                     durs = []
@@ -102,6 +106,7 @@ def main():
         for r, d in per_role.items():
             o = {"entry_mean": round(med(d["entry"]), 2), "entry_last": round(med(d["entry_max"]), 2),
                  "exit_mean": round(med(d["exit"]), 2), "exit_last": round(med(d["exit_max"]), 2)}
+            o["entry_hist_2us"] = [int(v) for v in np.median(np.array(d["entry_hist"]), axis=0)]
             if d["ph"]:
                 ph = np.median(np.array(d["ph"]), axis=0)
                 o["phases"] = {name: round(float(v), 2) for name, v in zip(PHASES[r], ph)}

@@ -42,3 +42,15 @@ extern "C" __attribute__((visibility("default"))) int probe_bwd_all(
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bwd_all<BWD_WCHUNK, BWD_WNTW>), dim3(nblk), dim3(256), lds, s, A);
   return (int)hipGetLastError();
 }
+
+// Resident k_bwd_all blocks per CU as the runtime computes it (registers,
+// LDS of the launch's dynamic size, waves).
+extern "C" __attribute__((visibility("default"))) int probe_bwd_all_occupancy() {
+  const size_t ldsA = wgrad_lds_floats<BWD_WCHUNK, BWD_WNTW>() * sizeof(float);
+  const size_t ldsB = B2_LDS_FLOATS * sizeof(float);
+  int n = -1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_bwd_all<BWD_WCHUNK, BWD_WNTW>, 256,
+                                                   ldsA > ldsB ? ldsA : ldsB) != hipSuccess)
+    return -1;
+  return n;
+}
