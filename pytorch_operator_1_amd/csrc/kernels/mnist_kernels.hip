@@ -309,6 +309,7 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
   __shared__ __attribute__((aligned(16))) float w1s[C1 * W1LD + 32];
   constexpr int NWV = NTH / 64, NPART = NTH / 256;  // waves; K parts of the conv2 GEMM
   __shared__ __attribute__((aligned(16))) float red[(NPART - 1) * 1024];
+  PTO_STAMP_SCOPE();
   const int b = blockIdx.x >> 2, nt = blockIdx.x & 3;
   const int tid = threadIdx.x;
   {
@@ -376,6 +377,7 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
     }
   }
   __syncthreads();
+  PTO_STAMP(1);
   const int wid = tid >> 6, lane = tid & 63;
   // conv1 + bias + ReLU + pool: 15 wave tasks = 5 channel groups x 3 pixel
   // chunks (64, 64, 16 pooled pixels)
@@ -490,6 +492,7 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
     }
   }
   __syncthreads();
+  PTO_STAMP(2);
   // conv2 implicit GEMM (k_conv2_fwd's lane maps), K (25 groups of 5 MFMAs)
   // split over NPART wave sets: 13+12 (512 threads) or 7+6+6+6 (1024)
   const int t = wid & 3, half = wid >> 2;
@@ -534,6 +537,7 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
     for (int rr = 0; rr < 4; ++rr) red[(half - 1) * 1024 + t * 256 + rr * 64 + lane] = acc[rr];
   }
   __syncthreads();
+  PTO_STAMP(3);
   if (half != 0) return;
 #pragma unroll
   for (int pp = 0; pp < NPART - 1; ++pp)
@@ -783,6 +787,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
   __shared__ __attribute__((aligned(16))) float dls[256];
   const int mtiles = (B + 15) >> 4, ntiles = (F1IN + 15) >> 4;
   const int t = threadIdx.x;
+  PTO_STAMP_SCOPE();
   if (blockIdx.x == (unsigned)(mtiles * ntiles)) {
     if (cm.pending && *cm.pending) {
       const float lr = *cm.a.lr;
@@ -833,6 +838,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
   if (t < W4) ws4[pad4(t)] = wv0;
   if (t + NT < W4) ws4[pad4(t + NT)] = wv1;
   __syncthreads();
+  PTO_STAMP(1);
   // ---- Z partial: rows r of the tile x classes r (<10), K slice of wave w
   {
     f32x4 acc0 = zero4(), acc1 = zero4();
@@ -852,6 +858,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     for (int rr = 0; rr < 4; ++rr) red[w * 256 + (gq * 4 + rr) * 16 + r] = acc[rr];
   }
   __syncthreads();
+  PTO_STAMP(2);
   // ---- log_softmax + NLL + dlogits: 16 lanes per row (waves 0..3)
   if (t < 256) {
     float z = bias;
@@ -875,6 +882,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     }
   }
   __syncthreads();
+  PTO_STAMP(3);
   // ---- dh1 = (dL W2) * [h1 > 0], column tiles w and w + 16, in place
   {
     const float4 a = *reinterpret_cast<const float4*>(dls + r * 16 + 4 * gq);
@@ -905,6 +913,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     }
   }
   __syncthreads();
+  PTO_STAMP(4);
   // ---- d(a2p) tile [16 rows, 16 cols] = dh1 W1, split-K over the waves
   {
     f32x4 acc0 = zero4(), acc1 = zero4();
@@ -922,6 +931,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     for (int rr = 0; rr < 4; ++rr) red[w * 256 + (gq * 4 + rr) * 16 + r] = acc[rr];
   }
   __syncthreads();
+  PTO_STAMP(5);
   if (t < 256) {
     float v = 0.f;
 #pragma unroll

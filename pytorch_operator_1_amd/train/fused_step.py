@@ -224,7 +224,12 @@ class FusedMnistTrainer:
         """(lr device ptr, momentum, weight decay, grad scale, nesterov)."""
         return (self.lr_dev.data_ptr(), self.momentum, self.weight_decay, 1.0 / self.world, int(self.nesterov))
 
-    def _forward(self):
+    def _forward_part(self, which: int):
+        """One launch of :meth:`_forward` (0 = F12, 1 = F3, 2 = F4dx), for the
+        timing probes under tools/."""
+        self._forward(only=which)
+
+    def _forward(self, only: int | None = None):
         """F12, F3, F4dx.  Fused-opt: F12 applies conv1's owed update on the
         fly (lazy) and F4dx commits it; F4dx's d(a2p) feeds the backward."""
         L, s, B, P = self.L, self._s(), self.B, self._p
@@ -241,16 +246,19 @@ class FusedMnistTrainer:
             rep = (None, 1, 0)
             lazy = (None, None, 0, None, None, 0.0, 0.0, 1.0, 0)
             w2out, pending = None, None
-        c(L.pto_conv12_fwd_lazy_x(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
-                                  P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
-                                  self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi, *lazy,
-                                  self.xcur.data_ptr(), w2out, *rep, s), "conv12_fwd")
-        c(L.pto_linear_fwd(self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
-                           self.h1.data_ptr(), B, 500, 800, 1, s), "fc1_fwd")
-        c(L.pto_fc2_ce_dx(self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
-                          self.target.data_ptr(), P["fc1.weight"].data_ptr(), self.loss_rows.data_ptr(),
-                          self.dlogits.data_ptr(), self.dh1.data_ptr(), self.da2p.data_ptr(), B, 1.0 / B, bi,
-                          *conv1, pending, *o, *rep, s), "fc2_ce_dx")
+        if only in (None, 0):
+            c(L.pto_conv12_fwd_lazy_x(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
+                                      P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
+                                      self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi, *lazy,
+                                      self.xcur.data_ptr(), w2out, *rep, s), "conv12_fwd")
+        if only in (None, 1):
+            c(L.pto_linear_fwd(self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
+                               self.h1.data_ptr(), B, 500, 800, 1, s), "fc1_fwd")
+        if only in (None, 2):
+            c(L.pto_fc2_ce_dx(self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
+                              self.target.data_ptr(), P["fc1.weight"].data_ptr(), self.loss_rows.data_ptr(),
+                              self.dlogits.data_ptr(), self.dh1.data_ptr(), self.da2p.data_ptr(), B, 1.0 / B, bi,
+                              *conv1, pending, *o, *rep, s), "fc2_ce_dx")
 
     def _backward(self):
         """``k_bwd_all``: the whole backward in one launch.  Fused-opt: every

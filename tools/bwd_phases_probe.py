@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--mask", type=int, nargs="*", default=[31, 8, 4])
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--fwd", action="store_true", help="time F12 and F4dx phases instead")
     a = ap.parse_args()
     if a.build:
         build()
@@ -58,6 +59,8 @@ def main():
     for _ in range(3):
         tr.step()
     torch.cuda.synchronize()
+    if a.fwd:
+        return fwd_phases(lib, rd, tr, dev, a.reps)
     counts = dict(C=13, F=17, A=352, B=640, D=400)
     bits = dict(C=1, F=2, A=4, B=8, D=16)
     occ = ctypes.CDLL(SO).probe_bwd_all_occupancy
@@ -114,6 +117,49 @@ def main():
         report[mask] = out
         print(f"mask {mask}: {json.dumps(out)}")
     print(json.dumps(report))
+
+
+def fwd_phases(lib, rd, tr, dev, reps):
+    """F12 (k_conv12_fwd2_t) and F4dx (k_fc2_ce_dx_mf) with their stamps:
+    the probe .so's own copies of the shipped launchers, fused-opt args."""
+    import numpy as np
+    import torch
+
+    from pytorch_operator_1_amd.ops import _lib
+
+    for name, sig in _lib._SIGS.items():
+        if hasattr(lib, name):
+            getattr(lib, name).argtypes = sig
+            getattr(lib, name).restype = ctypes.c_int
+    real = tr.L
+    tr.L = lib  # trainer launches through the probe library
+
+    kernels = {"F12": (lambda: tr._forward_part(0), 256, ["staged", "conv1", "conv2+reduce", "exit"], [0, 1, 2, 3, 7]),
+               "F4dx": (lambda: tr._forward_part(2), 201 + 0, ["staged", "Z gemm", "softmax", "dh1", "da2p", "exit"],
+                        [0, 1, 2, 3, 4, 5, 7])}
+    out = {}
+    for k, (fn, nblk, names, marks) in kernels.items():
+        ph, spans = [], []
+        for _ in range(reps):
+            fn()
+            torch.cuda.synchronize()
+            buf = (ctypes.c_ulonglong * (nblk * SLOTS))()
+            assert rd(buf, nblk * SLOTS) == 0
+            st = np.frombuffer(buf, dtype=np.uint64).reshape(nblk, SLOTS).astype(np.int64)
+            rel = (st - st[:, 0].min()) * 10.0 / 1000.0
+            if k == "F4dx":
+                rel = rel[:200]  # tile blocks (the commit block has no phases)
+            spans.append(float(rel[:, 7].max()))
+            ph.append([float((rel[:, k1] - rel[:, k0]).mean()) for k0, k1 in zip(marks, marks[1:])] +
+                      [float(rel[:, 0].mean()), float(rel[:, 0].max()), float(rel[:, 7].mean())])
+        m = np.median(np.array(ph), axis=0)
+        out[k] = {"span_us": round(float(np.median(spans)), 2),
+                  "phases": {n: round(float(v), 2) for n, v in zip(names, m)},
+                  "entry_mean": round(float(m[-3]), 2), "entry_last": round(float(m[-2]), 2),
+                  "exit_mean": round(float(m[-1]), 2)}
+        print(k, json.dumps(out[k]))
+    tr.L = real
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":
