@@ -833,15 +833,10 @@ static AttnShape make_shape(int B, int S, int H, int Hkv, long long q_rs, long l
 // caller's contract).
 // Waves per forward / dQ block: 8 (two 32-row query tiles x the 4 heads of
 // a GQA group share each K/V tile: 4 waves per SIMD at the same 64 KB of
-// LDS) unless PTO_ATTN_WAVES=4 or the shape does not split into 8.
+// LDS) unless the shape does not split into 8.
 static int attn_waves(const AttnShape& sh) {
-  static int env = -1;
-  if (env < 0) {
-    const char* e = getenv("PTO_ATTN_WAVES");
-    env = (e && atoi(e) == 4) ? 4 : 8;
-  }
   const int G = sh.H / sh.Hkv;
-  return (env == 8 && ((sh.S / QT) * G) % 8 == 0) ? 8 : 4;
+  return (((sh.S / QT) * G) % 8 == 0) ? 8 : 4;
 }
 
 template <int NWV>

@@ -343,14 +343,8 @@ bool bn_shape_ok(long long M, int C) {
 // the grid at 512 blocks (256 at C = 2048: one 4-wave block per CU) and ran
 // at ~40 % of HBM bandwidth; the default now allows 1024 blocks (4 per CU)
 // with >= 8 row iterations each, partials bounded to 4 M floats (16 MB).
-// PTO_BN_MAXBLK / PTO_BN_MINITERS override (A/B).
-int bn_env(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
 void bn_grid(long long M, int C, int* nblk, int* iters) {
-  static const int maxblk = bn_env("PTO_BN_MAXBLK", 1024);
-  static const int minit = bn_env("PTO_BN_MINITERS", 8);
+  constexpr int maxblk = 1024, minit = 8;
   const int rpi = BN_T / (C >> 3);
   const long long rows_iters = (M + rpi - 1) / rpi;
   long long nb = (rows_iters + minit - 1) / minit;

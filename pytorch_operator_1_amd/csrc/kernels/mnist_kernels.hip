@@ -1234,13 +1234,15 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
     if (tid < 72) c1v = reinterpret_cast<const uint32_t*>(code1 + (b * C1 + icg * 2) * 144)[tid];
   }
   {
-    constexpr int NW = (C2 * 50 + 255) / 256;  // 10
-    float wv_[NW];
-    const float* wb = w2 + icg * 50;
+    // the W2 slice as float2 (rows of 50 floats at a 2000-B stride, slice
+    // start 200*icg B: 8-byte aligned; launchers check w2)
+    constexpr int NW = (C2 * 25 + 255) / 256;  // 5
+    float2 wv_[NW];
+    const float2* wb = reinterpret_cast<const float2*>(w2 + icg * 50);
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
-      const int e = tid + 256 * q, k = e / 50, n = e - k * 50;
-      wv_[q] = e < C2 * 50 ? wb[k * 500 + n] : 0.f;
+      const int e = tid + 256 * q, k = e / 25, n2 = e - k * 25;
+      wv_[q] = e < C2 * 25 ? wb[k * 250 + n2] : float2{0.f, 0.f};
     }
     float4 gv4 = float4{0.f, 0.f, 0.f, 0.f};
     uint32_t cv = 0;
@@ -1250,8 +1252,8 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
     }
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
-      const int e = tid + 256 * q, k = e / 50, n = e - k * 50;
-      if (e < C2 * 50) ws[k * WLD + n] = wv_[q];
+      const int e = tid + 256 * q, k = e / 25, n2 = e - k * 25;
+      if (e < C2 * 25) *reinterpret_cast<float2*>(ws + k * WLD + 2 * n2) = wv_[q];
     }
     // dY^T [oc][pos] expanded straight from the registers: thread t < 200
     // holds pooled row ph = t & 3 of channel oc = t >> 2 (4 grads + 4 codes)
@@ -2002,6 +2004,7 @@ PTO_API int pto_mnist_ddp_sgd(float* p, float* g, float* m, int n, int c1, int z
 PTO_API int pto_conv2_bwd(const float* g2, const uint8_t* code2, const float* a1p, const float* w2, float* gw2,
                           float* gb2, float* da1p, int B, int parts, const float* x, const long long* bidx,
                           const uint8_t* code1, float* gw1, float* gb1, hipStream_t s) {
+  if ((parts & 2) && (((uintptr_t)w2) & 7)) return -1;  // float2 staging of the W2 slice
   const int nA = (parts & 1) ? ((B + B2_CHUNK - 1) / B2_CHUNK) * 32 : 0;
   const int nB = (parts & 2) ? B * B2_ICG : 0;
   const int nC = (parts & 4) ? (C2 + 3) / 4 : 0;
@@ -2070,6 +2073,7 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
                         const float* lr, float mom, float wd, float gscale, int nesterov, float* c1rep, int nrep,
                         int rep_stride, int grads_only, float* wpart, hipStream_t s) {
   if (!ctr) return -1;
+  if (((uintptr_t)(grads_only ? p + off_c2w : w2f)) & 7) return -1;  // float2 staging of the W2 slice
   if (!grads_only && (!bidx || !pending || !w2f || nbatches < 1)) return -1;
   if (B < 1 || nrep < 1 || nrep > C1_MAXREP || (nrep > 1 && !c1rep)) return -1;
   if (wpart && nrep != B) return -1;  // deterministic mode: one conv1 replica per sample

@@ -4,7 +4,7 @@ shape (B x 4096 tokens, 32 query / 8 KV heads, head dim 128) and report
 TF/s (causal FLOPs: 4 B H S^2 D / 2 forward, 2.5x that backward).
 
 Kernel variants are chosen by env vars read once per process
-(PTO_ATTN_DKDV, PTO_ATTN_WAVES), so A/B runs are separate processes:
+(PTO_ATTN_DKDV_PC), so A/B runs are separate processes:
     for v in 0 2 4; do PTO_ATTN_DKDV=$v python tools/attn_ab.py; done
 """
 import json
