@@ -168,9 +168,33 @@ __global__ __launch_bounds__(1024) void k_gridbar(unsigned* ctr, int rounds, int
   }
 }
 
+// Self-test of the cross-lane helpers of mfma_f32.h (DPP / permlane swaps):
+// one wave, inputs a[64], b[64] -> out[11][64] (tests/test_kernels_gpu.py).
+__global__ __launch_bounds__(64) void k_lane_ops_selftest(const float* __restrict__ a, const float* __restrict__ b,
+                                                          float* __restrict__ out) {
+  const int l = threadIdx.x;
+  const float x = a[l], y = b[l];
+  out[0 * 64 + l] = lane_xor1(x);
+  out[1 * 64 + l] = lane_xor2(x);
+  out[2 * 64 + l] = lane_mirror8(x);
+  out[3 * 64 + l] = lane_xor8(x);
+  out[4 * 64 + l] = lane_sum32(x);
+  out[5 * 64 + l] = halve32(x, y);
+  out[6 * 64 + l] = halve16(x, y);
+  out[7 * 64 + l] = row16_sum(x);
+  out[8 * 64 + l] = row16_max(x);
+  out[9 * 64 + l] = wave_sum(x);
+  out[10 * 64 + l] = wave_max(x);
+}
+
 }  // namespace
 
 #define PTO_API extern "C" __attribute__((visibility("default")))
+
+PTO_API int pto_lane_ops_selftest(const float* a, const float* b, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_lane_ops_selftest, dim3(1), dim3(64), 0, s, a, b, out);
+  return (int)hipGetLastError();
+}
 
 PTO_API int pto_probe_kernel(int blocks, int threads, float* out, int nstore, int lds_rounds, hipStream_t s) {
   if (threads == 64)

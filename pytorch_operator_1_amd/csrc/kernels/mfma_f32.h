@@ -194,14 +194,58 @@ PTO_DEV void block_colsum64_epi(const float* __restrict__ x, int ld, int M, int 
   if (t < 64 && c < N) epi(0, c, red[t] + red[t + 64] + red[t + 128] + red[t + 192]);
 }
 
+// Cross-lane exchanges on the VALU (DPP) and the gfx950 permlane swaps,
+// instead of __shfl_xor's ds_bpermute (an LDS-crossbar round trip per step:
+// a dependent reduction of 6 steps waits ~6 of them).
+//   lane_xor1 / lane_xor2: quad_perm;  lane_xor8: row_ror:8 (= xor 8 in a
+//   16-lane row);  lane_mirror8: row_half_mirror (lane i <- i ^ 7 in a group
+//   of 8) -- a valid partner for a reduction step on bit 2, since i ^ 7
+//   differs from i in that bit and the sets being merged stay disjoint.
+#define PTO_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), (ctrl), 0xF, 0xF, false))
+PTO_DEV float lane_xor1(float v) { return PTO_DPP(v, 0xB1); }     // quad_perm [1,0,3,2]
+PTO_DEV float lane_xor2(float v) { return PTO_DPP(v, 0x4E); }     // quad_perm [2,3,0,1]
+PTO_DEV float lane_mirror8(float v) { return PTO_DPP(v, 0x141); } // row_half_mirror
+PTO_DEV float lane_xor8(float v) { return PTO_DPP(v, 0x128); }    // row_ror:8
+// x + (x of lane ^ 32), in every lane (v_permlane32_swap)
+PTO_DEV float lane_sum32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// One halving step across lane bit 5 (or, with permlane16, bit 4): lanes
+// with the bit clear keep slot a, the others slot b, and each adds its
+// partner's copy of the slot it keeps: x keeps a's, y b's
+// (v_permlane32_swap / v_permlane16_swap exchange exactly those halves).
+PTO_DEV float halve32(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+PTO_DEV float halve16(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// all-reduce (sum / max) over the 16-lane rows
+PTO_DEV float row16_sum(float v) {
+  v += lane_xor8(v);
+  v += lane_mirror8(v);
+  v += lane_xor2(v);
+  return v + lane_xor1(v);
+}
+PTO_DEV float row16_max(float v) {
+  v = fmaxf(v, lane_xor8(v));
+  v = fmaxf(v, lane_mirror8(v));
+  v = fmaxf(v, lane_xor2(v));
+  return fmaxf(v, lane_xor1(v));
+}
+
 PTO_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v = lane_sum32(v);
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return row16_sum(__uint_as_float(r[0]) + __uint_as_float(r[1]));
 }
 
 PTO_DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return row16_max(fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1])));
 }

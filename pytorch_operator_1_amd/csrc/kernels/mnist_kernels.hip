@@ -844,10 +844,13 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     f32x4 acc0 = zero4(), acc1 = zero4();
 #pragma unroll
     for (int q = 0; q < NGK; ++q) {
-      const int k0 = kb + 16 * q + 4 * gq;
-      const bool ok = k0 < F1OUT;
-      const float4 a = ok ? *reinterpret_cast<const float4*>(hs + r * HLD + k0) : float4(z4);
-      const float4 b = (ok && r < NCLS) ? *reinterpret_cast<const float4*>(w2s + r * HLD + k0) : float4(z4);
+      // branch-free: reads clamped into the staged rows, the A value of a
+      // k past the end zeroed after the read (class rows >= 10 only feed
+      // unused output columns)
+      const int k0 = kb + 16 * q + 4 * gq, kc = min(k0, F1OUT - 4);
+      const float4 at = *reinterpret_cast<const float4*>(hs + r * HLD + kc);
+      const float4 a = k0 < F1OUT ? at : float4(z4);
+      const float4 b = *reinterpret_cast<const float4*>(w2s + min(r, NCLS - 1) * HLD + kc);
       acc0 = mfma16x16x4(a.x, b.x, acc0);
       acc1 = mfma16x16x4(a.y, b.y, acc1);
       acc0 = mfma16x16x4(a.z, b.z, acc0);
@@ -866,11 +869,9 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     for (int q = 0; q < FDX_WAVES; ++q) z += red[q * 256 + t];
     const bool cls = hn < NCLS;
     float mx = cls ? z : -INFINITY;
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    mx = row16_max(mx);
     float se = cls ? __expf(z - mx) : 0.f;
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) se += __shfl_xor(se, o, 64);
+    se = row16_sum(se);
     const float lse = mx + __logf(se);
     const bool live = grow < B;
     const float dl = (cls && live) ? (__expf(z - lse) - (hn == y ? 1.f : 0.f)) * inv_b : 0.f;
@@ -883,32 +884,40 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
   }
   __syncthreads();
   PTO_STAMP(3);
-  // ---- dh1 = (dL W2) * [h1 > 0], column tiles w and w + 16, in place
+  // ---- dh1 = (dL W2) * [h1 > 0], column tiles w and w + 16, in place.
+  // Branch-free operand reads (classes >= 10 have dL = 0 exactly, so their
+  // W2 row is clamped to a valid one; columns >= 500 read column 499 and are
+  // not written), all issued before the two interleaved 4-MFMA chains
   {
     const float4 a = *reinterpret_cast<const float4*>(dls + r * 16 + 4 * gq);
+    float bb[2][4], hv[2][4];
+    bool cok[2];
+    int cc[2];
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       const int col = (w + FDX_WAVES * hh) * 16 + r;
-      const bool cok = col < F1OUT;
-      float b[4];
+      cok[hh] = col < F1OUT;
+      cc[hh] = cok[hh] ? col : F1OUT - 1;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = 4 * gq + j;
-        b[j] = (cok && k < NCLS) ? w2s[k * HLD + col] : 0.f;
-      }
-      f32x4 acc = zero4();
-      acc = mfma16x16x4(a.x, b[0], acc);
-      acc = mfma16x16x4(a.y, b[1], acc);
-      acc = mfma16x16x4(a.z, b[2], acc);
-      acc = mfma16x16x4(a.w, b[3], acc);
-      if (cok) {
+      for (int j = 0; j < 4; ++j) bb[hh][j] = w2s[min(4 * gq + j, NCLS - 1) * HLD + cc[hh]];
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int row = gq * 4 + rr;
-          const float v = hs[row * HLD + col] > 0.f ? acc[rr] : 0.f;
-          hs[row * HLD + col] = v;
-          if (nt == 0 && mt * 16 + row < B) dh1[(mt * 16 + row) * F1OUT + col] = v;
-        }
+      for (int rr = 0; rr < 4; ++rr) hv[hh][rr] = hs[(gq * 4 + rr) * HLD + cc[hh]];
+    }
+    f32x4 acc[2] = {zero4(), zero4()};
+    const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) acc[hh] = mfma16x16x4(av[j], bb[hh][j], acc[hh]);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      if (!cok[hh]) continue;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = gq * 4 + rr;
+        const float v = hv[hh][rr] > 0.f ? acc[hh][rr] : 0.f;
+        hs[row * HLD + cc[hh]] = v;
+        if (nt == 0 && mt * 16 + row < B) dh1[(mt * 16 + row) * F1OUT + cc[hh]] = v;
       }
     }
   }
@@ -919,12 +928,13 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     f32x4 acc0 = zero4(), acc1 = zero4();
 #pragma unroll
     for (int q = 0; q < NGK; ++q) {
-      float av[4];
-      load4<LAY_ROWK>(hs, HLD, r, 16, kb + 16 * q + 4 * gq, kend, av);
-      acc0 = mfma16x16x4(av[0], bw[q][0], acc0);
-      acc1 = mfma16x16x4(av[1], bw[q][1], acc1);
-      acc0 = mfma16x16x4(av[2], bw[q][2], acc0);
-      acc1 = mfma16x16x4(av[3], bw[q][3], acc1);
+      // unconditional float4 read: a k past the row's end is clamped into
+      // the row (finite values that meet bw = 0 there)
+      const float4 av = *reinterpret_cast<const float4*>(hs + r * HLD + min(kb + 16 * q + 4 * gq, F1OUT - 4));
+      acc0 = mfma16x16x4(av.x, bw[q][0], acc0);
+      acc1 = mfma16x16x4(av.y, bw[q][1], acc1);
+      acc0 = mfma16x16x4(av.z, bw[q][2], acc0);
+      acc1 = mfma16x16x4(av.w, bw[q][3], acc1);
     }
     const f32x4 acc = acc0 + acc1;
 #pragma unroll
@@ -963,36 +973,32 @@ constexpr int B2_LDS_FLOATS = 64 * 65 + C2 * B2_DLD;
 
 // Recursive-halving wave reduction of 26 (padded to 32) per-lane sums: at
 // each step a lane keeps half of its live accumulators (chosen by its lane
-// bit) and receives its partner's copy of them: 16+8+4+2+1+1 = 32 shuffles
-// instead of 6 x 26.  The 26 wave totals are written to out[0..25].
+// bit) and receives its partner's copy of them: 16+8+4+2+1+1 = 32 exchanges
+// instead of 6 x 26.  Bits 5 and 4 by v_permlane32/16_swap (which move
+// exactly the halves each side keeps), bits 3..0 by DPP (bit 2's partner is
+// lane ^ 7, see lane_mirror8) -- no LDS-crossbar round trips.  The 26 wave
+// totals are written to out[0..25].
 PTO_DEV void wave_halving26(const float acc[26], int lane, float* out) {
   float h16[16], h8[8], h4[4], h2[2], h1;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const bool up = lane & 32;
-    const float a0 = acc[k], a1 = k + 16 < 26 ? acc[k + 16] : 0.f;
-    h16[k] = (up ? a1 : a0) + __shfl_xor(up ? a0 : a1, 32, 64);
-  }
+  for (int k = 0; k < 16; ++k) h16[k] = halve32(acc[k], k + 16 < 26 ? acc[k + 16] : 0.f);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const bool up = lane & 16;
-    h8[k] = (up ? h16[k + 8] : h16[k]) + __shfl_xor(up ? h16[k] : h16[k + 8], 16, 64);
-  }
+  for (int k = 0; k < 8; ++k) h8[k] = halve16(h16[k], h16[k + 8]);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const bool up = lane & 8;
-    h4[k] = (up ? h8[k + 4] : h8[k]) + __shfl_xor(up ? h8[k] : h8[k + 4], 8, 64);
+    h4[k] = (up ? h8[k + 4] : h8[k]) + lane_xor8(up ? h8[k] : h8[k + 4]);
   }
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const bool up = lane & 4;
-    h2[k] = (up ? h4[k + 2] : h4[k]) + __shfl_xor(up ? h4[k] : h4[k + 2], 4, 64);
+    h2[k] = (up ? h4[k + 2] : h4[k]) + lane_mirror8(up ? h4[k] : h4[k + 2]);
   }
   {
     const bool up = lane & 2;
-    h1 = (up ? h2[1] : h2[0]) + __shfl_xor(up ? h2[0] : h2[1], 2, 64);
+    h1 = (up ? h2[1] : h2[0]) + lane_xor2(up ? h2[0] : h2[1]);
   }
-  h1 += __shfl_xor(h1, 1, 64);
+  h1 += lane_xor1(h1);
   const int idx = ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 + ((lane >> 2) & 1) * 2 +
                   ((lane >> 1) & 1);
   if (!(lane & 1) && idx < 26) out[idx] = h1;
@@ -1126,7 +1132,7 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
     PTO_STAMP(2);
 #pragma unroll
     for (int u = 0; u < NTW; ++u) {
-      const float v = sum[u] + __shfl_xor(sum[u], 32, 64);
+      const float v = lane_sum32(sum[u]);
       const int n = col0 + 16 * u + c;
       if (h == 0 && n < 500) {
         if (part)
@@ -1319,7 +1325,7 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
       float tv = 0.f;
 #pragma unroll
       for (int k = 0; k < 25; ++k) tv = fmaf(dys[(k0 + k) * B2_DLD + pos], ws[(k0 + k) * WLD + cc], tv);
-      tail = tv + __shfl_xor(tv, 32, 64);
+      tail = lane_sum32(tv);
     }
     __syncthreads();  // ts aliases ws, xs aliases dys: every wave's GEMM reads are done
 #pragma unroll
@@ -1376,9 +1382,9 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
       sacc += tv[1];
       sacc += tv[2];
       sacc += tv[3];
-      sacc += __shfl_xor(sacc, 4, 64);
-      sacc += __shfl_xor(sacc, 2, 64);
-      sacc += __shfl_xor(sacc, 1, 64);
+      sacc += lane_mirror8(sacc);  // sum over the 8 lanes of the output
+      sacc += lane_xor2(sacc);
+      sacc += lane_xor1(sacc);
       if (part == 0) {
         if (da1p) da1p[b * A1P + (icg * 2 + 1) * 144 + pix] = sacc;
         dsum[o] = sacc;

@@ -129,8 +129,8 @@ def test_clean_pod_policy_running_and_delete_cascade(cluster):
     job = new_job("cleanup", image="pto/python:rocm", master_args=["-c", "print('done')"], workers=1,
                   worker_args=["-c", "import time; time.sleep(600)"], clean_pod_policy="Running")
     cluster.submit(job)
-    cluster.wait_for_condition("cleanup", timeout=60)
-    end = time.time() + 30
+    cluster.wait_for_condition("cleanup", timeout=120)
+    end = time.time() + 90  # generous: the suite also runs under pytest-xdist on a loaded host
     while time.time() < end:
         names = [p["metadata"]["name"] for p in cluster.store.list("pods")["items"]
                  if p["metadata"]["labels"].get("job-name") == "cleanup"]

@@ -213,3 +213,37 @@ def test_fused_trainer_converges():
         if i == 0:
             first = tr.last_loss()
     assert tr.last_loss() < 0.5 * first
+
+
+def test_cross_lane_helpers():
+    """The DPP / v_permlane{16,32}_swap exchanges the reductions use
+    (mfma_f32.h) against their definitions on one wave."""
+    import numpy as np
+
+    from pytorch_operator_1_amd.ops import _lib
+
+    g = torch.Generator().manual_seed(7)
+    a = torch.randn(64, generator=g)
+    b = torch.randn(64, generator=g)
+    out = torch.empty(11 * 64, device=DEV)
+    ad, bd = a.to(DEV), b.to(DEV)  # keep the device copies alive until the launch has run
+    _lib.check(_lib.lib().pto_lane_ops_selftest(ad.data_ptr(), bd.data_ptr(), out.data_ptr(), _lib.stream_ptr()),
+               "lane_ops")
+    torch.cuda.synchronize()
+    o = out.view(11, 64).cpu().numpy().astype(np.float64)
+    x, y, lane = a.numpy().astype(np.float64), b.numpy().astype(np.float64), np.arange(64)
+    np.testing.assert_array_equal(o[0], x[lane ^ 1])
+    np.testing.assert_array_equal(o[1], x[lane ^ 2])
+    np.testing.assert_array_equal(o[2], x[lane ^ 7])
+    np.testing.assert_array_equal(o[3], x[lane ^ 8])
+    f32 = lambda v: v.astype(np.float32).astype(np.float64)
+    np.testing.assert_array_equal(o[4], f32(x + x[lane ^ 32]))
+    # halving step: a lane with the bit clear keeps slot a and adds its
+    # partner's a; with the bit set, slot b plus the partner's b
+    np.testing.assert_array_equal(o[5], f32(np.where(lane & 32, y + y[lane ^ 32], x + x[lane ^ 32])))
+    np.testing.assert_array_equal(o[6], f32(np.where(lane & 16, y + y[lane ^ 16], x + x[lane ^ 16])))
+    rows = x.reshape(4, 16)
+    np.testing.assert_allclose(o[7], np.repeat(rows.sum(1), 16), rtol=1e-6)
+    np.testing.assert_array_equal(o[8], np.repeat(rows.max(1), 16))
+    np.testing.assert_allclose(o[9], np.full(64, x.sum()), rtol=1e-5)
+    np.testing.assert_array_equal(o[10], np.full(64, x.max()))
