@@ -1074,16 +1074,21 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
     for (int q = 0; q < NVG; ++q) {
       const int e = tid + 256 * q;
       if (e < CH * (F1IN / 4)) {
-        // XOR-swizzled slots.  Grads: row oc's quad G lives at G ^ ((oc >> 1) & 3)
-        // and, for oc bit 3 set, its two halves are swapped, so the 32 lanes
-        // of a read group (16 channels x 2 k-slots) hit 32 distinct banks.
-        // Codes: the dword of (oc, G) lives at G ^ ((oc >> 3) & 1), so
-        // channels oc and oc + 8 land in different banks.
-        const int smp = e / (F1IN / 4), r = e - smp * (F1IN / 4), oc_ = r >> 2;
-        const float4 v = vg[q];
-        reinterpret_cast<float4*>(gs)[smp * (F1IN / 4) + (oc_ << 2) + ((r & 3) ^ ((oc_ >> 1) & 3))] =
-            ((oc_ >> 3) & 1) ? float4{v.z, v.w, v.x, v.y} : v;
-        reinterpret_cast<uint32_t*>(cs)[smp * (F1IN / 4) + (oc_ << 2) + ((r & 3) ^ ((oc_ >> 3) & 1))] = vc[q];
+        // Transposed + swizzled: the loaded quad holds pooled pixels (G, g =
+        // 0..3) of channel oc; slot (oc, g) holds the 4 G values of pooled
+        // column g contiguously (one ds_read_b128 / one ds_read_b32 per
+        // sample in the MFMA loop instead of 4 + 4), at quad g ^ ((oc >> 2) &
+        // 3) of the channel's 16 floats: the 16 channels of a b128 read
+        // group then cover all 64 banks once, and the 64 code dwords too
+        const int smp = e / (F1IN / 4), r = e - smp * (F1IN / 4), oc_ = r >> 2, G = r & 3;
+        const int sw = (oc_ >> 2) & 3;
+        const float vv[4] = {vg[q].x, vg[q].y, vg[q].z, vg[q].w};
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          const int o = smp * F1IN + oc_ * 16 + 4 * (gg ^ sw) + G;
+          gs[o] = vv[gg];
+          cs[o] = (uint8_t)(vc[q] >> (8 * gg));
+        }
       }
     }
   }
@@ -1107,7 +1112,7 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
     static_assert(C2 % 16 == 2, "VALU tail covers exactly 2 rows");
     const int c = lane & 15, rr = (lane >> 4) & 1, h = lane >> 5;
     const int ocx = C2 - 2 + rr;
-    const int xg = ocx * 16, xgsw = (ocx >> 1) & 3, xghs = ((ocx >> 3) & 1) << 1, xcsw = (ocx >> 3) & 1;
+    const int xsw = (ocx >> 2) & 3;
     float sum[NTW];
 #pragma unroll
     for (int u = 0; u < NTW; ++u) sum[u] = 0.f;
@@ -1118,8 +1123,9 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
 #pragma unroll
       for (int pp = 0; pp < 16; ++pp) {
         const int G = pp >> 2, gq = pp & 3;
-        const float gv = gs[smp * F1IN + xg + ((G ^ xgsw) << 2) + (gq ^ xghs)];
-        const int cd = cs[smp * F1IN + xg + ((G ^ xcsw) << 2) + gq];
+        const int o = smp * F1IN + ocx * 16 + 4 * (gq ^ xsw) + G;
+        const float gv = gs[o];
+        const int cd = cs[o];
         const int po = (cd >> 1) * 12 + (cd & 1);  // window position of the code (cd 4: masked)
 #pragma unroll
         for (int u = 0; u < NTW; ++u) {
@@ -1146,16 +1152,17 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
   f32x4 acc0[NTW], acc1[NTW];
 #pragma unroll
   for (int u = 0; u < NTW; ++u) acc0[u] = acc1[u] = zero4();
-  const int ocr = oc;
-  const int goff = ocr * 16, gsw = (ocr >> 1) & 3, ghs = ((ocr >> 3) & 1) << 1, csw = (ocr >> 3) & 1;
+  const int goff = oc * 16 + 4 * (g ^ ((oc >> 2) & 3));
 #pragma unroll
   for (int smp = 0; smp < CH; ++smp) {
     float gv[4], bv[NTW][4][4];
     int cd[4];
+    const float4 g4 = *reinterpret_cast<const float4*>(gs + smp * F1IN + goff);
+    const uint32_t c4 = *reinterpret_cast<const uint32_t*>(cs + smp * F1IN + goff);
+    gv[0] = g4.x; gv[1] = g4.y; gv[2] = g4.z; gv[3] = g4.w;
 #pragma unroll
     for (int G = 0; G < 4; ++G) {
-      gv[G] = gs[smp * F1IN + goff + ((G ^ gsw) << 2) + (g ^ ghs)];
-      cd[G] = cs[smp * F1IN + goff + ((G ^ csw) << 2) + g];
+      cd[G] = (c4 >> (8 * G)) & 0xff;
 #pragma unroll
       for (int u = 0; u < NTW; ++u) {
         const float* ap = as + smp * (NCH * 144) + koff[u] + 24 * G + 2 * g;
@@ -2063,7 +2070,10 @@ PTO_API int pto_eval_head(const float* logp, const int64_t* labels, float* stats
 // Samples per conv2-wgrad block of k_bwd_all: 6 -> 30.2 KB of LDS, 5 blocks
 // per CU next to the 31.5 KB dgrad blocks (sweep 4..8: 21.7, 20.8, 17.6,
 // 18.1, 23.4 us, profiles/bwd_all_r2.md).
-constexpr int BWD_WCHUNK = 6;
+#ifndef PTO_BWD_WCHUNK  // probe builds (tools/bwd_roles_probe.py --chunk) sweep it
+#define PTO_BWD_WCHUNK 6
+#endif
+constexpr int BWD_WCHUNK = PTO_BWD_WCHUNK;
 // 16-column tiles per conv2-wgrad block of k_bwd_all.  2 shares the staged
 // grads/codes (and the A-operand reads) between two tiles but halves the
 // wgrad blocks: k_bwd_all 16.5 -> 18.4 us (r3), so 1

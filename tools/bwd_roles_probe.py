@@ -20,28 +20,46 @@ SO = os.path.join(ROOT, "tools", "probes", "libbwd_roles.so")
 ROLES = {1: "C conv2-bias", 2: "F fc2/bias", 4: "A conv2-wgrad", 8: "B dgrad+conv1-wgrad", 16: "D dW1"}
 
 
-def build():
+def so_path(chunk):
+    return SO if chunk is None else SO.replace(".so", f"_c{chunk}.so")
+
+
+def build(chunk=None):
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "kernels"), "-o", SO, SRC]
+           "-I", os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "kernels"), "-o", so_path(chunk), SRC]
+    if chunk is not None:
+        cmd.insert(1, f"-DPTO_BWD_WCHUNK={chunk}")
     subprocess.check_call(cmd)
-    print("built", SO)
+    print("built", so_path(chunk))
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--reps", type=int, default=15)
+    ap.add_argument("--chunk", type=int, nargs="*", default=None,
+                    help="conv2-wgrad samples per block to sweep (each its own probe build)")
     a = ap.parse_args()
     if a.build:
-        build()
+        for c in (a.chunk or [None]):
+            build(c)
         return
+    if a.chunk:
+        for c in a.chunk:
+            print(f"== wgrad chunk {c}")
+            run_one(so_path(c), a.reps, masks=[31, 4, 8])
+        return
+    run_one(SO, a.reps)
+
+
+def run_one(so, reps, masks=None):
     import torch
 
     from pytorch_operator_1_amd.ops import _lib
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
 
     P_, I_, L_ = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong
-    lib = ctypes.CDLL(SO)
+    lib = ctypes.CDLL(so)
     fn = lib.probe_bwd_all
     fn.argtypes = [P_] * 13 + [L_] * 8 + [P_, P_, L_, P_, I_, P_, P_, I_, I_, I_, P_]
     fn.restype = ctypes.c_int
@@ -59,7 +77,7 @@ def main():
                 tr.c1rep.data_ptr(), tr.c1_nrep, tr.c1_stride, mask, _lib.stream_ptr(dev))
         assert rc == 0, rc
 
-    masks = [31, 1 | 2, 4, 8, 16, 31 & ~4, 31 & ~8, 31 & ~16, 4 | 8]
+    masks = masks or [31, 1 | 2, 4, 8, 16, 31 & ~4, 31 & ~8, 31 & ~16, 4 | 8]
     graphs = {}
     s = torch.cuda.Stream(dev)
     with torch.cuda.stream(s):
@@ -73,7 +91,7 @@ def main():
                 launch(mk)
         graphs[mk] = g
     res = {mk: [] for mk in masks}
-    for _ in range(a.reps):
+    for _ in range(reps):
         for mk in masks:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
