@@ -587,6 +587,14 @@ __global__ __launch_bounds__(256) void k_linear_fwd(const float* __restrict__ x,
 // (i % 8) * (T / 8) + i / 8 puts T/8 consecutive tiles -- the m-tiles that
 // share one weight tile -- on one XCD, and each weight tile is fetched into
 // one L2 instead of up to four.  Identity unless T % 8 == 0.
+// Split-K partial tiles through LDS: wave w's accumulator element rr of
+// lane l (row (l >> 4)*4 + rr, column l & 15) goes to red[w*256 + rr*64 + l]
+// -- consecutive lanes, consecutive banks (the row-major [row][16] slot put
+// the four 16-lane groups of a write on the same 16 banks: 4-way conflicts);
+// red_slot(t) is where the reducing thread t (row t >> 4, column t & 15)
+// finds it.
+PTO_DEV int red_slot(int t) { return ((t >> 4) & 3) * 64 + (t >> 6) * 16 + (t & 15); }
+
 PTO_DEV int xcd_tile(int i, int T, bool on) { return (on && !(T & 7)) ? (i & 7) * (T >> 3) + (i >> 3) : i; }
 
 __global__ __launch_bounds__(1024) void k_linear_fwd_vec16(const float* __restrict__ x, const float* __restrict__ w,
@@ -601,13 +609,13 @@ __global__ __launch_bounds__(1024) void k_linear_fwd_vec16(const float* __restri
   const f32x4 acc = wave_tile_16x16<LAY_ROWK, LAY_ROWK, 4, true, true>(x, K, w, K, M, N, K, mt * 16, nt * 16,
                                                                        wv * kc, (wv + 1) * kc);
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) red[wv * 256 + ((lane >> 4) * 4 + rr) * 16 + (lane & 15)] = acc[rr];
+  for (int rr = 0; rr < 4; ++rr) red[wv * 256 + rr * 64 + lane] = acc[rr];
   __syncthreads();
   const int t = threadIdx.x;
   if (t < 256) {
     float v = 0.f;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v += red[q * 256 + t];
+    for (int q = 0; q < 16; ++q) v += red[q * 256 + red_slot(t)];
     const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
     if (m < M && n < N) EpiBiasRelu{bias, y, N, relu != 0}(m, n, v);
   }
@@ -858,7 +866,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     }
     const f32x4 acc = acc0 + acc1;
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) red[w * 256 + (gq * 4 + rr) * 16 + r] = acc[rr];
+    for (int rr = 0; rr < 4; ++rr) red[w * 256 + rr * 64 + lane] = acc[rr];
   }
   __syncthreads();
   PTO_STAMP(2);
@@ -866,7 +874,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
   if (t < 256) {
     float z = bias;
 #pragma unroll
-    for (int q = 0; q < FDX_WAVES; ++q) z += red[q * 256 + t];
+    for (int q = 0; q < FDX_WAVES; ++q) z += red[q * 256 + red_slot(t)];
     const bool cls = hn < NCLS;
     float mx = cls ? z : -INFINITY;
     mx = row16_max(mx);
@@ -938,14 +946,14 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     }
     const f32x4 acc = acc0 + acc1;
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) red[w * 256 + (gq * 4 + rr) * 16 + r] = acc[rr];
+    for (int rr = 0; rr < 4; ++rr) red[w * 256 + rr * 64 + lane] = acc[rr];
   }
   __syncthreads();
   PTO_STAMP(5);
   if (t < 256) {
     float v = 0.f;
 #pragma unroll
-    for (int q = 0; q < FDX_WAVES; ++q) v += red[q * 256 + t];
+    for (int q = 0; q < FDX_WAVES; ++q) v += red[q * 256 + red_slot(t)];
     const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
     if (m < B && n < F1IN) da2p[m * F1IN + n] = v;
   }
