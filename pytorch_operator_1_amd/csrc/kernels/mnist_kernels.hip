@@ -588,19 +588,23 @@ __global__ __launch_bounds__(256) void k_linear_fwd(const float* __restrict__ x,
 // share one weight tile -- on one XCD, and each weight tile is fetched into
 // one L2 instead of up to four.  Identity unless T % 8 == 0.
 // Split-K partial tiles through LDS: wave w's accumulator element rr of
-// lane l (row (l >> 4)*4 + rr, column l & 15) goes to red[w*256 + rr*64 + l]
-// -- consecutive lanes, consecutive banks (the row-major [row][16] slot put
-// the four 16-lane groups of a write on the same 16 banks: 4-way conflicts);
+// lane l (row (l >> 4)*4 + rr, column l & 15) goes to
+// red[w*RED_W + rr*RED_RR + l] -- consecutive lanes, consecutive banks on the
+// write (a row-major [row][16] slot put a write's four 16-lane groups on the
+// same 16 banks), and the RED_RR = 64 + 16 skew puts the reducing threads'
+// four rr values on four different 16-bank groups on the read (with 64 they
+// all land on one: 4-way conflicts moved from the write to the read).
 // red_slot(t) is where the reducing thread t (row t >> 4, column t & 15)
 // finds it.
-PTO_DEV int red_slot(int t) { return ((t >> 4) & 3) * 64 + (t >> 6) * 16 + (t & 15); }
+constexpr int RED_RR = 80, RED_W = 4 * RED_RR;
+PTO_DEV int red_slot(int t) { return ((t >> 4) & 3) * RED_RR + (t >> 6) * 16 + (t & 15); }
 
 PTO_DEV int xcd_tile(int i, int T, bool on) { return (on && !(T & 7)) ? (i & 7) * (T >> 3) + (i >> 3) : i; }
 
 __global__ __launch_bounds__(1024) void k_linear_fwd_vec16(const float* __restrict__ x, const float* __restrict__ w,
                                                            const float* __restrict__ bias, float* __restrict__ y,
                                                            int M, int N, int K, int relu) {
-  __shared__ float red[16 * 256];
+  __shared__ float red[16 * RED_W];
   const int mtiles = (M + 15) >> 4;
   const int tile = xcd_tile(blockIdx.x, gridDim.x, true);
   const int mt = tile % mtiles, nt = tile / mtiles;
@@ -609,13 +613,13 @@ __global__ __launch_bounds__(1024) void k_linear_fwd_vec16(const float* __restri
   const f32x4 acc = wave_tile_16x16<LAY_ROWK, LAY_ROWK, 4, true, true>(x, K, w, K, M, N, K, mt * 16, nt * 16,
                                                                        wv * kc, (wv + 1) * kc);
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) red[wv * 256 + rr * 64 + lane] = acc[rr];
+  for (int rr = 0; rr < 4; ++rr) red[wv * RED_W + rr * RED_RR + lane] = acc[rr];
   __syncthreads();
   const int t = threadIdx.x;
   if (t < 256) {
     float v = 0.f;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v += red[q * 256 + red_slot(t)];
+    for (int q = 0; q < 16; ++q) v += red[q * RED_W + red_slot(t)];
     const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
     if (m < M && n < N) EpiBiasRelu{bias, y, N, relu != 0}(m, n, v);
   }
@@ -763,6 +767,9 @@ __global__ __launch_bounds__(256) void k_fc2_ce(const float* __restrict__ h1, co
 }
 
 constexpr int FDX_WAVES = 16;
+// dL tile row stride: rows r*20 floats apart put the dh1 phase's float4 A
+// reads (16 rows per 16-lane group) on 16 distinct 4-bank groups (16: 4-way)
+constexpr int DLS_LD = 20;
 
 // F4dx: F4 + d(a2p) in one launch.  Block (mt, nt) = 16 waves: the fc2 +
 // log_softmax + NLL + dlogits + dh1 head of its 16 rows (recomputed per
@@ -791,8 +798,8 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
   constexpr int HLD = F1OUT;
   __shared__ __attribute__((aligned(16))) float hs[16 * HLD];
   __shared__ __attribute__((aligned(16))) float w2s[NCLS * HLD];
-  __shared__ float red[FDX_WAVES * 256];
-  __shared__ __attribute__((aligned(16))) float dls[256];
+  __shared__ float red[FDX_WAVES * RED_W];
+  __shared__ __attribute__((aligned(16))) float dls[16 * DLS_LD];
   const int mtiles = (B + 15) >> 4, ntiles = (F1IN + 15) >> 4;
   const int t = threadIdx.x;
   PTO_STAMP_SCOPE();
@@ -866,7 +873,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     }
     const f32x4 acc = acc0 + acc1;
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) red[w * 256 + rr * 64 + lane] = acc[rr];
+    for (int rr = 0; rr < 4; ++rr) red[w * RED_W + rr * RED_RR + lane] = acc[rr];
   }
   __syncthreads();
   PTO_STAMP(2);
@@ -874,7 +881,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
   if (t < 256) {
     float z = bias;
 #pragma unroll
-    for (int q = 0; q < FDX_WAVES; ++q) z += red[q * 256 + red_slot(t)];
+    for (int q = 0; q < FDX_WAVES; ++q) z += red[q * RED_W + red_slot(t)];
     const bool cls = hn < NCLS;
     float mx = cls ? z : -INFINITY;
     mx = row16_max(mx);
@@ -883,7 +890,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     const float lse = mx + __logf(se);
     const bool live = grow < B;
     const float dl = (cls && live) ? (__expf(z - lse) - (hn == y ? 1.f : 0.f)) * inv_b : 0.f;
-    dls[t] = dl;
+    dls[hm * DLS_LD + hn] = dl;
     const float zy = __shfl(z, (lane & 48) | (y & 15), 64);
     if (nt == 0 && live) {
       if (cls) dlogits[grow * NCLS + hn] = dl;
@@ -897,7 +904,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
   // W2 row is clamped to a valid one; columns >= 500 read column 499 and are
   // not written), all issued before the two interleaved 4-MFMA chains
   {
-    const float4 a = *reinterpret_cast<const float4*>(dls + r * 16 + 4 * gq);
+    const float4 a = *reinterpret_cast<const float4*>(dls + r * DLS_LD + 4 * gq);
     float bb[2][4], hv[2][4];
     bool cok[2];
     int cc[2];
@@ -907,7 +914,13 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
       cok[hh] = col < F1OUT;
       cc[hh] = cok[hh] ? col : F1OUT - 1;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bb[hh][j] = w2s[min(4 * gq + j, NCLS - 1) * HLD + cc[hh]];
+      for (int j = 0; j < 4; ++j) {
+        // classes 10..15 read rows 2..7 (the rows lane group gq - 2 reads for
+        // the same j: same address, a broadcast) rather than all row 9,
+        // whose banks overlap rows 0, 2, 3 and 6
+        const int c = 4 * gq + j;
+        bb[hh][j] = w2s[(c < NCLS ? c : c - 8) * HLD + cc[hh]];
+      }
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) hv[hh][rr] = hs[(gq * 4 + rr) * HLD + cc[hh]];
     }
@@ -946,14 +959,14 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     }
     const f32x4 acc = acc0 + acc1;
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) red[w * 256 + rr * 64 + lane] = acc[rr];
+    for (int rr = 0; rr < 4; ++rr) red[w * RED_W + rr * RED_RR + lane] = acc[rr];
   }
   __syncthreads();
   PTO_STAMP(5);
   if (t < 256) {
     float v = 0.f;
 #pragma unroll
-    for (int q = 0; q < FDX_WAVES; ++q) v += red[q * 256 + red_slot(t)];
+    for (int q = 0; q < FDX_WAVES; ++q) v += red[q * RED_W + red_slot(t)];
     const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
     if (m < B && n < F1IN) da2p[m * F1IN + n] = v;
   }
@@ -1226,18 +1239,23 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
   // sample's pooled grads and codes.
   const int b = bid / B2_ICG, icg = bid - b * B2_ICG;
   constexpr int WLD = 68;   // 64 + 4: the 4 k-rows of a wave hit disjoint banks
-  constexpr int TLD = 65;
+  // T is kept transposed, T^T [col][pos] at row stride 68: the GEMM's
+  // accumulator rows (4 column rows per lane group, 4*68 = 16 mod 64 banks
+  // apart) store conflict-free, and col2im's reads of one tap column at 64
+  // distinct positions are one contiguous row.  ([pos][col] at stride 65
+  // stored with 4-way conflicts: 4 position rows 4 banks apart.)
+  constexpr int TLD = 68;
   // Two LDS regions, each reused once the phase that reads it is over
   // (30 KB in all):
-  //   R1: W2 slice [50][68]                     -> after the GEMM: T [64][65]
+  //   R1: W2 slice [50][68]                     -> after the GEMM: T^T [50][68]
   //       -> after col2im: the conv1 wave partials
   //   R2: expanded dY2^T [50][68]               -> after the GEMM: input
   //       image [784] + conv1 codes [2][144] (held in registers until then)
   //       + d(a1p) of the two channels [288]
   // The W2 slice's pad columns 50..63 are never written: they only feed T
   // columns col2im does not read; the K rows past 50 are masked at the read.
-  constexpr int R1 = 64 * TLD;
-  static_assert(50 * WLD <= R1, "W2 slice fits R1");
+  constexpr int R1 = 64 * 65;
+  static_assert(50 * WLD <= R1 && 50 * TLD <= R1, "W2 slice and T^T fit R1");
   float* ws = smem;                      // R1
   float* ts = smem;                      // R1 after the GEMM
   float* dys = smem + R1;                // R2
@@ -1301,7 +1319,8 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
   __syncthreads();
   PTO_STAMP(1);
   {
-    // T columns 0..47 on the matrix cores (3 column tiles); the 2 valid
+    // T^T = W2slice^T dY^T: rows = T columns, columns = positions.
+    // T columns 0..47 on the matrix cores (3 row tiles); the 2 valid
     // columns of the 4th tile (48, 49) on the VALU: lane = position (16) x
     // column (2) x K half (2), 25 FMAs, one shuffle -- a 13-MFMA tile that
     // was 7/8 padding
@@ -1318,7 +1337,7 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
         const int k = 48 + gg;
         const float a = k < C2 ? dys[k * B2_DLD + wv * 16 + r] : 0.f;
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) acc[q] = mfma16x16x4(a, k < C2 ? ws[k * WLD + q * 16 + r] : 0.f, acc[q]);
+        for (int q = 0; q < NQ; ++q) acc[q] = mfma16x16x4(k < C2 ? ws[k * WLD + q * 16 + r] : 0.f, a, acc[q]);
         break;
       }
       float av[4], bv[NQ][4];
@@ -1332,7 +1351,7 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
 #pragma unroll
       for (int q = 0; q < NQ; ++q)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[q] = mfma16x16x4(av[j], bv[q][j], acc[q]);
+        for (int j = 0; j < 4; ++j) acc[q] = mfma16x16x4(bv[q][j], av[j], acc[q]);
     }
     float tail;
     {
@@ -1347,8 +1366,8 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
     for (int q = 0; q < NQ; ++q)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
-        ts[(wv * 16 + gg * 4 + rr) * TLD + q * 16 + r] = acc[q][rr];
-    if (gg < 2) ts[(wv * 16 + r) * TLD + 48 + gg] = tail;
+        ts[(q * 16 + gg * 4 + rr) * TLD + wv * 16 + r] = acc[q][rr];
+    if (gg < 2) ts[(48 + gg) * TLD + wv * 16 + r] = tail;
     if (fuse1) {
       if (tid < 196) reinterpret_cast<float4*>(xs)[tid] = xv;
       if (tid < 72) reinterpret_cast<uint32_t*>(c1s)[tid] = c1v;
@@ -1360,8 +1379,9 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
     // 288 outputs on 256 threads: one full output per thread, then the last
     // 32 outputs split 8 ways over all threads (<= 4 taps each, 3-step
     // shuffle sum) instead of a second full round on half a wave.  Taps
-    // outside the 8x8 map read T[0][0] and are dropped by a select, so all
-    // of a thread's reads issue back to back (no exec-masked branches)
+    // outside the 8x8 map read position 0 of the same T column (same
+    // address as any lane reading it: a broadcast) and are dropped by a
+    // select, so all of a thread's reads issue back to back
     {
       const int o = tid, icl = o / 144, pix = o - icl * 144;
       const int y = pix / 12, xx = pix - y * 12;
@@ -1372,7 +1392,7 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
         for (int kw = 0; kw < 5; ++kw) {
           const int sy = y - kh, sx = xx - kw;
           const bool ok = (unsigned)sy < 8u && (unsigned)sx < 8u;
-          tv[kh * 5 + kw] = ts[ok ? (sy * 8 + sx) * TLD + icl * 25 + kh * 5 + kw : 0];
+          tv[kh * 5 + kw] = ts[(icl * 25 + kh * 5 + kw) * TLD + (ok ? sy * 8 + sx : 0)];
           tv[kh * 5 + kw] = ok ? tv[kh * 5 + kw] : 0.f;
         }
       float sacc = 0.f;
@@ -1390,7 +1410,7 @@ PTO_DEV void c2_dgrad_block(int bid, float* smem, const float* __restrict__ g2, 
         const int tt = part + 8 * i;
         const int kh = tt / 5, kw = tt - kh * 5, sy = y - kh, sx = xx - kw;
         const bool ok = tt < 25 && (unsigned)sy < 8u && (unsigned)sx < 8u;
-        tv[i] = ts[ok ? (sy * 8 + sx) * TLD + 25 + tt : 0];
+        tv[i] = ts[(25 + (tt < 25 ? tt : 0)) * TLD + (ok ? sy * 8 + sx : 0)];
         tv[i] = ok ? tv[i] : 0.f;
       }
       float sacc = tv[0];  // tap order, as the sequential sum over valid taps

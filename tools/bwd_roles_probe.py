@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 SRC = os.path.join(ROOT, "tools", "probes", "bwd_roles.hip")
 SO = os.path.join(ROOT, "tools", "probes", "libbwd_roles.so")
-ROLES = {1: "C conv2-bias", 2: "F fc2/bias", 4: "A conv2-wgrad", 8: "B dgrad+conv1-wgrad", 16: "D dW1"}
+ROLES = {1: "C conv2-bias", 2: "F fc2/bias", 4: "A conv2-wgrad", 8: "B dgrad+conv1-wgrad", 16: "D dW1", 32: "-c1 (B without its conv1 wgrad)"}
 
 
 def so_path(chunk):
@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--chunk", type=int, nargs="*", default=None,
                     help="conv2-wgrad samples per block to sweep (each its own probe build)")
+    ap.add_argument("--pmc-mask", type=int, default=None,
+                    help="no timing: 30 eager launches of this role mask, for a rocprofv3 --pmc run "
+                         "(pmc_summary.py --skip 3 drops the trainer's own 3 warm-up dispatches)")
     a = ap.parse_args()
     if a.build:
         for c in (a.chunk or [None]):
@@ -49,10 +52,10 @@ def main():
             print(f"== wgrad chunk {c}")
             run_one(so_path(c), a.reps, masks=[31, 4, 8])
         return
-    run_one(SO, a.reps)
+    run_one(SO, a.reps, pmc_mask=a.pmc_mask)
 
 
-def run_one(so, reps, masks=None):
+def run_one(so, reps, masks=None, pmc_mask=None):
     import torch
 
     from pytorch_operator_1_amd.ops import _lib
@@ -77,6 +80,11 @@ def run_one(so, reps, masks=None):
                 tr.c1rep.data_ptr(), tr.c1_nrep, tr.c1_stride, mask, _lib.stream_ptr(dev))
         assert rc == 0, rc
 
+    if pmc_mask is not None:
+        for _ in range(30):
+            launch(pmc_mask)
+        torch.cuda.synchronize()
+        return
     masks = masks or [31, 1 | 2, 4, 8, 16, 31 & ~4, 31 & ~8, 31 & ~16, 4 | 8]
     graphs = {}
     s = torch.cuda.Stream(dev)

@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("paths", nargs="+")
     ap.add_argument("--filter", default="")
+    ap.add_argument("--skip", type=int, default=0, help="drop each kernel's first N dispatches")
     a = ap.parse_args()
     # kernel -> counter -> list of per-dispatch totals
     acc = defaultdict(lambda: defaultdict(list))
@@ -34,8 +35,13 @@ def main():
                 if a.filter and a.filter not in name:
                     continue
                 per[(short(name), disp, ctr)] += val
+            first = defaultdict(list)
+            for (k, d, ctr) in per:
+                first[k].append(d)
+            keep = {k: set(sorted(set(ds))[a.skip:]) for k, ds in first.items()}
             for (k, d, ctr), v in per.items():
-                acc[k][ctr].append(v)
+                if d in keep[k]:
+                    acc[k][ctr].append(v)
     for k, ctrs in acc.items():
         print(f"## {k}")
         for ctr, vals in sorted(ctrs.items()):

@@ -6,7 +6,8 @@
 #include "../../pytorch_operator_1_amd/csrc/kernels/mnist_kernels.hip"
 
 // mask bits: 1 conv2 bias (C), 2 fc2/bias reductions (F), 4 conv2 wgrad (A),
-// 8 conv2 dgrad + conv1 wgrad (B), 16 dW1 (D)
+// 8 conv2 dgrad + conv1 wgrad (B), 16 dW1 (D); 32 (with 8): B without the
+// fused conv1 wgrad
 extern "C" __attribute__((visibility("default"))) int probe_bwd_all(
     const float* g2, const uint8_t* code2, const float* a1p, const float* w2f, const float* x, const uint8_t* code1,
     const float* dh1, const float* a2p, const float* h1, const float* dl, float* p, float* g, float* m,
@@ -32,6 +33,10 @@ extern "C" __attribute__((visibility("default"))) int probe_bwd_all(
   A.nF = (mask & 2) ? (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9 : 0;
   A.nA = (mask & 4) ? ((B + BWD_WCHUNK - 1) / BWD_WCHUNK) * (32 / BWD_WNTW) : 0;
   A.nB = (mask & 8) ? B * B2_ICG : 0;
+  if (mask & 32) {  // dgrad blocks without the fused conv1 wgrad
+    A.gw1 = nullptr;
+    A.nrep = 1;
+  }
   A.nD = (mask & 16) ? (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4 : 0;
   A.wpart = nullptr;
   const size_t ldsA = wgrad_lds_floats<BWD_WCHUNK, BWD_WNTW>() * sizeof(float);
