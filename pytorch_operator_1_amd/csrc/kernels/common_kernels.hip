@@ -261,3 +261,9 @@ PTO_API int pto_noop(int blocks, hipStream_t s) {
   hipLaunchKernelGGL(k_noop, dim3(blocks), dim3(64), 0, s, nullptr);
   return (int)hipGetLastError();
 }
+
+// Upload an instantiated graph's launch resources ahead of its first timed
+// replay (the handle from torch.cuda.CUDAGraph.raw_cuda_graph_exec()).
+PTO_API int pto_graph_upload(void* exec, hipStream_t s) {
+  return (int)hipGraphUpload(reinterpret_cast<hipGraphExec_t>(exec), s);
+}

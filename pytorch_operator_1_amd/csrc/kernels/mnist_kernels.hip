@@ -1033,10 +1033,18 @@ PTO_DEV void wave_halving26(const float acc[26], int lane, float* out) {
 // pooled conv1 values + the 800 pooled grads + 800 codes with coalesced
 // 16-byte loads, then runs its MFMAs from LDS.  NTW = 2 shares that staging
 // (and every A-operand read) between two column tiles.
+// Staged a1p planes of the wgrad blocks: 12 rows at stride WG_RS, channel
+// planes WG_PS apart (dwords).  The MFMA loop's patch reads are ds_read2_b32
+// (banks = dword mod 32 per 32-lane half): with the dense 12 / 144 layout
+// the lanes' (tap, pooled column) addresses wrapped onto each other (+4
+// conflict cycles per read2, ~2e5 per launch); 20 / 260 is the layout
+// tools/lds_bank_model.py finds conflict-free for all 32 column tiles.
+constexpr int WG_RS = 20, WG_PS = 260;
+static_assert(WG_RS % 4 == 0 && WG_PS % 4 == 0 && WG_PS >= 12 * WG_RS, "float4-staged planes");
 template <int NTW>
 constexpr int wgrad_nch() { return NTW == 1 ? 2 : 3; }  // 16 cols span <= 2 channels, 32 cols <= 3
 template <int CH, int NTW>
-constexpr int wgrad_lds_floats() { return CH * (wgrad_nch<NTW>() * 144 + F1IN + F1IN / 4); }
+constexpr int wgrad_lds_floats() { return CH * (wgrad_nch<NTW>() * WG_PS + F1IN + F1IN / 4); }
 template <int CH, int NTW = 1>
 PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, const uint8_t* __restrict__ code2,
                             const float* __restrict__ a1p, float* __restrict__ gw2, int B,
@@ -1058,12 +1066,12 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
     kvalid[u] = kk < 500;
     const int ic = kvalid[u] ? kk / 25 : ic0, r25 = kvalid[u] ? kk - ic * 25 : 0;
     const int kh = r25 / 5, kw = r25 - kh * 5;
-    koff[u] = (ic - ic0) * 144 + kh * 12 + kw;
+    koff[u] = (ic - ic0) * WG_PS + kh * WG_RS + kw;
   }
   const bool ocvalid = oc < C2;
   const int b0 = chunk * CH, nb = min(B, b0 + CH) - b0;
-  float* as = smem;                                           // [CH][NCH][144]
-  float* gs = smem + CH * NCH * 144;                          // [CH][800]
+  float* as = smem;                                           // [CH][NCH][12 x WG_RS, WG_PS]
+  float* gs = smem + CH * NCH * WG_PS;                        // [CH][800]
   uint8_t* cs = reinterpret_cast<uint8_t*>(gs + CH * F1IN);  // [CH][800] bytes
   const int tid = threadIdx.x;
   {
@@ -1089,7 +1097,10 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
 #pragma unroll
     for (int q = 0; q < NVA; ++q) {
       const int e = tid + 256 * q;
-      if (e < CH * A4) reinterpret_cast<float4*>(as)[e] = va[q];
+      if (e < CH * A4) {
+        const int sc = e / 36, f4 = e - sc * 36, row = f4 / 3;  // (sample, channel) plane, row of 3 float4
+        *reinterpret_cast<float4*>(as + sc * WG_PS + row * WG_RS + 4 * (f4 - row * 3)) = va[q];
+      }
     }
 #pragma unroll
     for (int q = 0; q < NVG; ++q) {
@@ -1147,10 +1158,10 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
         const int o = smp * F1IN + ocx * 16 + 4 * (gq ^ xsw) + G;
         const float gv = gs[o];
         const int cd = cs[o];
-        const int po = (cd >> 1) * 12 + (cd & 1);  // window position of the code (cd 4: masked)
+        const int po = (cd >> 1) * WG_RS + (cd & 1);  // window position of the code (cd 4: masked)
 #pragma unroll
         for (int u = 0; u < NTW; ++u) {
-          const float* ap = as + smp * (NCH * 144) + koff[u] + 24 * G + 2 * gq;
+          const float* ap = as + smp * (NCH * WG_PS) + koff[u] + 2 * WG_RS * G + 2 * gq;
           const float bvx = ap[cd < 4 ? po : 0];
           sum[u] = fmaf(cd < 4 ? gv : 0.f, bvx, sum[u]);
         }
@@ -1186,11 +1197,11 @@ PTO_DEV void c2_wgrad_block(int bid, float* smem, const float* __restrict__ g2, 
       cd[G] = (c4 >> (8 * G)) & 0xff;
 #pragma unroll
       for (int u = 0; u < NTW; ++u) {
-        const float* ap = as + smp * (NCH * 144) + koff[u] + 24 * G + 2 * g;
+        const float* ap = as + smp * (NCH * WG_PS) + koff[u] + 2 * WG_RS * G + 2 * g;
         bv[u][G][0] = ap[0];
         bv[u][G][1] = ap[1];
-        bv[u][G][2] = ap[12];
-        bv[u][G][3] = ap[13];
+        bv[u][G][2] = ap[WG_RS];
+        bv[u][G][3] = ap[WG_RS + 1];
       }
     }
 #pragma unroll
@@ -2049,7 +2060,7 @@ PTO_API int pto_conv2_bwd(const float* g2, const uint8_t* code2, const float* a1
   const int nA = (parts & 1) ? ((B + B2_CHUNK - 1) / B2_CHUNK) * 32 : 0;
   const int nB = (parts & 2) ? B * B2_ICG : 0;
   const int nC = (parts & 4) ? (C2 + 3) / 4 : 0;
-  const size_t ldsA = (parts & 1) ? B2_CHUNK * (288 + F1IN + F1IN / 4) * sizeof(float) : 0;
+  const size_t ldsA = (parts & 1) ? wgrad_lds_floats<B2_CHUNK, 1>() * sizeof(float) : 0;
   const size_t ldsB = (parts & 2) ? B2_LDS_FLOATS * sizeof(float) : 0;
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;
   if (nA + nB + nC == 0) return 0;
@@ -2095,11 +2106,13 @@ PTO_API int pto_eval_head(const float* logp, const int64_t* labels, float* stats
   LAUNCH_CHECK();
 }
 
-// Samples per conv2-wgrad block of k_bwd_all: 6 -> 30.2 KB of LDS, 5 blocks
-// per CU next to the 31.5 KB dgrad blocks (sweep 4..8: 21.7, 20.8, 17.6,
-// 18.1, 23.4 us, profiles/bwd_all_r2.md).
+// Samples per conv2-wgrad block of k_bwd_all: 5 -> 29.7 KB of LDS with the
+// padded 20/260 a1p planes, 5 blocks per CU next to the 29.5 KB dgrad blocks
+// (6 needs 35.6 KB: 4 blocks per CU; role probe, all roles: 13.99 vs 14.63 us,
+// profiles/lds_conflicts_r3.md; the round-2 sweep over 4..8 with the dense
+// planes picked 6, profiles/bwd_all_r2.md).
 #ifndef PTO_BWD_WCHUNK  // probe builds (tools/bwd_roles_probe.py --chunk) sweep it
-#define PTO_BWD_WCHUNK 6
+#define PTO_BWD_WCHUNK 5
 #endif
 constexpr int BWD_WCHUNK = PTO_BWD_WCHUNK;
 // 16-column tiles per conv2-wgrad block of k_bwd_all.  2 shares the staged

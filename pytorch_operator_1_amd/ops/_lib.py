@@ -123,6 +123,7 @@ _SIGS = {
     "pto_ce_bwd": [_P, _P, _P, _P, _L, _I, _L, _P],
     "pto_transpose_bf16": [_P, _P, _L, _L, _L, _L, _P],
     "pto_noop": [_I, _P],
+    "pto_graph_upload": [_P, _P],
     "pto_lane_ops_selftest": [_P, _P, _P, _P],
     "pto_probe_kernel": [_I, _I, _P, _I, _I, _P],
     "pto_gridbar_probe": [_I, _I, _P, _I, _I, _P],

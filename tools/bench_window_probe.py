@@ -6,7 +6,8 @@ then after idle gaps.  Usage: python tools/bench_window_probe.py
 [--mode first|rewarm|rewarm_last] (first: only the first window after a
 bench-like warmup; rewarm: every captured graph replayed twice more, state
 rolled back, before the warmup steps; rewarm_last: the timed graph replayed
-once more (rolled back) right before the window)."""
+once more (rolled back) right before the window; upload_last: hipGraphUpload of the
+timed graph right before the window)."""
 from __future__ import annotations
 
 import json
@@ -23,7 +24,7 @@ def main():
     import argparse
 
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", default="all", choices=["all", "first", "rewarm", "rewarm_last"])
+    ap.add_argument("--mode", default="all", choices=["all", "first", "rewarm", "rewarm_last", "upload_last"])
     a = ap.parse_args()
     from pytorch_operator_1_amd.train.runner import build_trainer
 
@@ -59,6 +60,11 @@ def main():
     tr.run(5)
     if a.mode == "rewarm_last":
         replay_rollback([tr._graph_close[20]], 1)
+    if a.mode == "upload_last":
+        from pytorch_operator_1_amd.ops import _lib
+
+        _lib.check(_lib.lib().pto_graph_upload(tr._graph_close[20].raw_cuda_graph_exec(), _lib.stream_ptr(dev)),
+                   "hipGraphUpload")
     torch.cuda.synchronize(dev)
     out = {"mode": a.mode, "warmup_s": round(time.perf_counter() - t0, 2)}
     if a.mode != "all":

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("paths", nargs="+")
     ap.add_argument("--filter", default="")
     ap.add_argument("--skip", type=int, default=0, help="drop each kernel's first N dispatches")
+    ap.add_argument("--per-dispatch", action="store_true", help="one line per dispatch instead of averages")
     a = ap.parse_args()
     # kernel -> counter -> list of per-dispatch totals
     acc = defaultdict(lambda: defaultdict(list))
@@ -35,6 +36,13 @@ def main():
                 if a.filter and a.filter not in name:
                     continue
                 per[(short(name), disp, ctr)] += val
+            if a.per_dispatch:
+                rows = defaultdict(dict)
+                for (k, d, ctr), v in per.items():
+                    rows[(d, k)][ctr] = v
+                for (d, k), cv in sorted(rows.items()):
+                    print(f"{d:6d} {k[:40]:40s} " + "  ".join(f"{c}={v:.4g}" for c, v in sorted(cv.items())))
+                continue
             first = defaultdict(list)
             for (k, d, ctr) in per:
                 first[k].append(d)
