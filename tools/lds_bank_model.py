@@ -163,3 +163,32 @@ def search_wgrad():
     best.sort()
     print("wgrad patch conflicts per sample (all 32 tiles), current rs=12 ps=144:", wgrad_patch())
     print("  best (conflicts, row stride, plane stride):", best[:6])
+
+
+# ---------------------------------------------------------------- conv1 wgrad gather (dgrad blocks)
+def conv1_gather(xld=28, seed=0, trials=8):
+    """c2_dgrad_block's conv1 weight grad: lane = pooled pixel (72 per wave),
+    25 code-dependent b32 reads xs[(2py+dy+kh)*xld + 2px+dx+kw]; mean conflict
+    cycles per wave over random argmax codes."""
+    import random
+
+    rnd = random.Random(seed)
+    tot = 0
+    for _ in range(trials):
+        for p0 in (0, 72):
+            codes = [rnd.randrange(4) for _ in range(72)]
+            for it in (0, 1):
+                for kh in range(5):
+                    for kw in range(5):
+                        addrs = []
+                        for l in range(64):
+                            pl = l + 64 * it
+                            if pl >= 72:
+                                addrs.append(None)
+                                continue
+                            pix = p0 + pl
+                            py, px = divmod(pix, 12)
+                            cd = codes[pl]
+                            addrs.append(f((2 * py + (cd >> 1) + kh) * xld + 2 * px + (cd & 1) + kw))
+                        tot += extra("read_b32", addrs)
+    return tot / (trials * 2)
