@@ -296,6 +296,7 @@ __global__ __launch_bounds__(256) void k_conv2_fwd(const float* __restrict__ a1p
 //  * lazy conv1 update (one-process schedule, LazyConv1), the image copy
 //    for the backward (xout) and the conv2.weight snapshot (w2out).
 constexpr int W1LD = 28;
+constexpr int W1PLD = 52;  // a channel pair's 25 interleaved taps, padded to whole float4
 template <int NTH>
 __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__ x, const float* __restrict__ w1,
                                                      const float* __restrict__ b1, const float* __restrict__ w2,
@@ -307,6 +308,10 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
   __shared__ __attribute__((aligned(16))) float in_s[A1P];
   __shared__ __attribute__((aligned(16))) float xs[784];
   __shared__ __attribute__((aligned(16))) float w1s[C1 * W1LD + 32];
+  // the full tasks' channel pairs interleaved, (w[2p][k], w[2p+1][k]) per
+  // tap: the b128 loads land as the packed FMA's weight pairs directly
+  // (from per-channel rows the compiler spent ~43 v_mov per task pairing them)
+  __shared__ __attribute__((aligned(16))) float w1p[(C1 / 2) * W1PLD];
   constexpr int NWV = NTH / 64, NPART = NTH / 256;  // waves; K parts of the conv2 GEMM
   __shared__ __attribute__((aligned(16))) float red[(NPART - 1) * 1024];
   PTO_STAMP_SCOPE();
@@ -372,8 +377,13 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
 #pragma unroll
     for (int q = 0; q < QW1; ++q) {
       const int e = tid + NTH * q;
-      if (e < C1 * 25) w1s[(e / 25) * W1LD + e % 25] = wq[q];
-      else if (e < C1 * 26) w1s[C1 * W1LD + e - C1 * 25] = wq[q];
+      if (e < C1 * 25) {
+        const int oc = e / 25, k = e - oc * 25;
+        w1s[oc * W1LD + k] = wq[q];
+        w1p[(oc >> 1) * W1PLD + 2 * k + (oc & 1)] = wq[q];
+      } else if (e < C1 * 26) {
+        w1s[C1 * W1LD + e - C1 * 25] = wq[q];
+      }
     }
   }
   __syncthreads();
@@ -435,16 +445,15 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
     }
     const int cg = task >> 1;
     const int pix = (task & 1) * 64 + lane;
-    float wr[CPT][W1LD], bz[CPT];
+    static_assert(CPT == 2, "w1p interleaves channel pairs");
+    float wp[W1PLD], bz[CPT];
 #pragma unroll
-    for (int cc = 0; cc < CPT; ++cc) {
-#pragma unroll
-      for (int j = 0; j < W1LD / 4; ++j) {
-        const float4 v = *reinterpret_cast<const float4*>(w1s + (cg * CPT + cc) * W1LD + 4 * j);
-        wr[cc][4 * j] = v.x; wr[cc][4 * j + 1] = v.y; wr[cc][4 * j + 2] = v.z; wr[cc][4 * j + 3] = v.w;
-      }
-      bz[cc] = w1s[C1 * W1LD + cg * CPT + cc];
+    for (int j = 0; j < W1PLD / 4; ++j) {
+      const float4 v = *reinterpret_cast<const float4*>(w1p + cg * W1PLD + 4 * j);
+      wp[4 * j] = v.x; wp[4 * j + 1] = v.y; wp[4 * j + 2] = v.z; wp[4 * j + 3] = v.w;
     }
+#pragma unroll
+    for (int cc = 0; cc < CPT; ++cc) bz[cc] = w1s[C1 * W1LD + cg * CPT + cc];
     if (pix >= 144) continue;
     const int ph = pix / 12, pw = pix - ph * 12;
     float p[6][6];
@@ -471,7 +480,8 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
 #pragma unroll
         for (int kw = 0; kw < 5; ++kw) {
           const float pv = p[dy + kh][dx + kw];
-          acc2 = __builtin_elementwise_fma(f32x2{pv, pv}, f32x2{wr[0][kh * 5 + kw], wr[1][kh * 5 + kw]}, acc2);
+          acc2 = __builtin_elementwise_fma(f32x2{pv, pv}, f32x2{wp[2 * (kh * 5 + kw)], wp[2 * (kh * 5 + kw) + 1]},
+                                           acc2);
         }
       s2[q] = acc2;
     }
