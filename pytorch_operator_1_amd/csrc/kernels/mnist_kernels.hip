@@ -285,17 +285,16 @@ __global__ __launch_bounds__(256) void k_conv2_fwd(const float* __restrict__ a1p
 // map straight into LDS (2880 outputs x 100 FMAs: cheaper than a kernel
 // boundary) and the nt == 0 block also writes it (+ argmax codes) to HBM for
 // the backward pass.
-//  * conv1: a wave owns (2-channel pair, 64 pooled pixels), so its weights
-//    are wave-uniform: read ONCE per task from LDS as broadcast ds_read_b128
-//    into VGPRs (channel rows padded to 28 floats); the 6x6 input patch is 18
-//    ds_read_b64.  The last 16 pixels of each 4-channel group run as quarter
-//    tasks (lane = channel*16 + pixel): 20 full + 5 quarter tasks.
+//  * conv1: a lane task is (channel pair, pooled pixel): 100 packed FMAs
+//    (v_pk_fma_f32, the pair's weights interleaved in LDS), the 6x6 input
+//    patch read as float2 pairs.  20 full wave tasks (pair x 64-pixel chunk,
+//    wave-uniform weights, broadcast b128 reads) + 3 tail tasks (4 pairs x
+//    the last 16 pixels).
 //  * conv2 implicit GEMM (k_conv2_fwd's lane maps): K split over the four
 //    wave sets (7+6+6+6 groups of 5 MFMAs), partial tiles combined through
 //    LDS, so each SIMD interleaves independent MFMA chains.
 //  * lazy conv1 update (one-process schedule, LazyConv1), the image copy
 //    for the backward (xout) and the conv2.weight snapshot (w2out).
-constexpr int W1LD = 28;
 constexpr int W1PLD = 52;  // a channel pair's 25 interleaved taps, padded to whole float4
 template <int NTH>
 __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__ x, const float* __restrict__ w1,
@@ -307,7 +306,7 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
   __shared__ float ws[16 * WS_LD];
   __shared__ __attribute__((aligned(16))) float in_s[A1P];
   __shared__ __attribute__((aligned(16))) float xs[784];
-  __shared__ __attribute__((aligned(16))) float w1s[C1 * W1LD + 32];
+  __shared__ float b1s[C1];
   // the full tasks' channel pairs interleaved, (w[2p][k], w[2p+1][k]) per
   // tap: the b128 loads land as the packed FMA's weight pairs directly
   // (from per-channel rows the compiler spent ~43 v_mov per task pairing them)
@@ -379,72 +378,38 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
       const int e = tid + NTH * q;
       if (e < C1 * 25) {
         const int oc = e / 25, k = e - oc * 25;
-        w1s[oc * W1LD + k] = wq[q];
         w1p[(oc >> 1) * W1PLD + 2 * k + (oc & 1)] = wq[q];
       } else if (e < C1 * 26) {
-        w1s[C1 * W1LD + e - C1 * 25] = wq[q];
+        b1s[e - C1 * 25] = wq[q];
       }
     }
   }
   __syncthreads();
   PTO_STAMP(1);
   const int wid = tid >> 6, lane = tid & 63;
-  // conv1 + bias + ReLU + pool: 15 wave tasks = 5 channel groups x 3 pixel
-  // chunks (64, 64, 16 pooled pixels)
-  // balanced layout (default): tasks 0-9 = 5 channel groups x the two 64-pixel
-  // chunks; tasks 10-14 = the last 16 pixels of one channel group with the
-  // group's 4 channels spread over the lanes (lane = channel*16 + pixel), a
-  // quarter of a full task's FMAs instead of a full task's lockstep cost.
-  // full tasks hold 2 channels' weights (VGPR budget of 4 waves/SIMD): 20
-  // full tasks (10 channel pairs x 2 chunks) + 5 quarter tasks over 16 waves
+  // conv1 + bias + ReLU + pool as (channel pair, pooled pixel) lane tasks,
+  // every one the same 100 packed FMAs: 20 full wave tasks (10 pairs x the
+  // two 64-pixel chunks, weights wave-uniform) + 3 tail tasks for pixels
+  // 128..143 (lane = 4 pairs x 16 pixels, per-lane weight rows).  23 tasks
+  // on 16 waves: at most 6 per SIMD (the per-channel tail tasks of unpacked
+  // FMAs made it 25 tasks, up to 7 per SIMD).
   static_assert(NTH == 1024, "F12 is laid out for 16 waves");
   constexpr int CPT = 2;
-  constexpr int NFULL = 2 * C1 / CPT, NTASK = NFULL + 5;
+  constexpr int NPAIR = C1 / CPT, NFULL = 2 * NPAIR, NTASK = NFULL + (NPAIR + 3) / 4;
   for (int si = 0; si < 2; ++si) {
     const int task = wid + NWV * si;
     if (task >= NTASK) break;
-    if (task >= NFULL) {
-      const int oc = (task - NFULL) * 4 + (lane >> 4), pix = 128 + (lane & 15);
-      float wr1[W1LD];
-#pragma unroll
-      for (int j = 0; j < W1LD / 4; ++j) {
-        const float4 v = *reinterpret_cast<const float4*>(w1s + oc * W1LD + 4 * j);
-        wr1[4 * j] = v.x; wr1[4 * j + 1] = v.y; wr1[4 * j + 2] = v.z; wr1[4 * j + 3] = v.w;
-      }
-      const float bz1 = w1s[C1 * W1LD + oc];
-      const int ph = pix / 12, pw = pix - ph * 12;
-      float p[6][6];
-#pragma unroll
-      for (int r = 0; r < 6; ++r)
-#pragma unroll
-        for (int c = 0; c < 6; c += 2) {
-          const float2 v = *reinterpret_cast<const float2*>(xs + (2 * ph + r) * 28 + 2 * pw + c);
-          p[r][c] = v.x;
-          p[r][c + 1] = v.y;
-        }
-      float v[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int dy = q >> 1, dx = q & 1;
-        float sacc = bz1;
-#pragma unroll
-        for (int kh = 0; kh < 5; ++kh)
-#pragma unroll
-          for (int kw = 0; kw < 5; ++kw) sacc = fmaf(p[dy + kh][dx + kw], wr1[kh * 5 + kw], sacc);
-        v[q] = sacc;
-      }
-      float o;
-      uint8_t cd;
-      relu_pool4(v, o, cd);
-      in_s[oc * 144 + pix] = o;
-      if (nt == 0) {
-        a1p[b * A1P + oc * 144 + pix] = o;
-        code1[b * A1P + oc * 144 + pix] = cd;
-      }
-      continue;
+    int cg, pix;
+    bool live = true;
+    if (task < NFULL) {
+      cg = task >> 1;
+      pix = (task & 1) * 64 + lane;
+    } else {
+      cg = (task - NFULL) * 4 + (lane >> 4);
+      pix = 128 + (lane & 15);
+      live = cg < NPAIR;
+      cg = min(cg, NPAIR - 1);
     }
-    const int cg = task >> 1;
-    const int pix = (task & 1) * 64 + lane;
     static_assert(CPT == 2, "w1p interleaves channel pairs");
     float wp[W1PLD], bz[CPT];
 #pragma unroll
@@ -453,8 +418,8 @@ __global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__
       wp[4 * j] = v.x; wp[4 * j + 1] = v.y; wp[4 * j + 2] = v.z; wp[4 * j + 3] = v.w;
     }
 #pragma unroll
-    for (int cc = 0; cc < CPT; ++cc) bz[cc] = w1s[C1 * W1LD + cg * CPT + cc];
-    if (pix >= 144) continue;
+    for (int cc = 0; cc < CPT; ++cc) bz[cc] = b1s[cg * CPT + cc];
+    if (!live) continue;
     const int ph = pix / 12, pw = pix - ph * 12;
     float p[6][6];
 #pragma unroll
