@@ -874,7 +874,10 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
   }
   __syncthreads();
   PTO_STAMP(3);
-  // ---- dh1 = (dL W2) * [h1 > 0], column tiles w and w + 16, in place.
+  // ---- dh1 = (dL W2) * [h1 > 0], column tiles 2w and 2w + 1, in place:
+  // exactly the K slice [KC*w, KC*w + 32) this wave reads in the d(a2p)
+  // phase (and read in the Z phase), so no block barrier between the two --
+  // the wave's own LDS stores precede its reads.
   // Branch-free operand reads (classes >= 10 have dL = 0 exactly, so their
   // W2 row is clamped to a valid one; columns >= 500 read column 499 and are
   // not written), all issued before the two interleaved 4-MFMA chains
@@ -885,7 +888,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     int cc[2];
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      const int col = (w + FDX_WAVES * hh) * 16 + r;
+      const int col = (2 * w + hh) * 16 + r;
       cok[hh] = col < F1OUT;
       cc[hh] = cok[hh] ? col : F1OUT - 1;
 #pragma unroll
@@ -917,7 +920,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
       }
     }
   }
-  __syncthreads();
+  static_assert(KC == 32 && 2 * 16 * FDX_WAVES >= F1OUT, "wave w's dh1 tiles are its d(a2p) K slice");
   PTO_STAMP(4);
   // ---- d(a2p) tile [16 rows, 16 cols] = dh1 W1, split-K over the waves
   {
