@@ -61,8 +61,49 @@ def parse_args(argv=None):
     return p.parse_args(argv)
 
 
+def _launch_ranks(args, argv) -> int | None:
+    """``--gpus N`` (N > 1) without a launcher: start N fresh rank processes
+    under ``torch.distributed.run`` (127.0.0.1 rendezvous) as CHILDREN of
+    this one, before anything here touches the GPU, and return their exit
+    code.  Never measures fewer ranks than asked for: a world size that
+    disagrees with ``--gpus`` is an error.  Returns None when this process
+    is itself a rank (or N == 1)."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr, flush=True)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    host_ranks = args.cpu or os.environ.get("PTO_BACKEND") == "gloo"
+    if not host_ranks:
+        # device_count() does not initialise HIP on this image (a child must
+        # not be started from a process that already did)
+        n_dev = torch.cuda.device_count()
+        if n_dev < args.gpus:
+            print(f"[bench] error: --gpus {args.gpus} but only {n_dev} GPU(s) visible; refusing to measure fewer "
+                  f"ranks (PTO_BACKEND=gloo rehearses several ranks on one GPU)", file=sys.stderr, flush=True)
+            return 2
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + argv
+    print(f"[bench] starting {args.gpus} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
 def main(argv=None):
     args = parse_args(argv)
+    rc = _launch_ranks(args, argv)
+    if rc is not None:
+        return rc
     mnist = args.model == "mnist"
     if args.steps is None:
         args.steps = 2000 if mnist else 20
@@ -75,12 +116,14 @@ def main(argv=None):
     use_gpu = torch.cuda.is_available() and not args.cpu
     # PTO_BACKEND=gloo: rehearse the multi-rank path with several ranks on
     # one GPU (RCCL refuses duplicate devices); default nccl (= RCCL) on GPU
+    rccl_log = pdist.rccl_log_setup() if (use_gpu and args.gpus > 1 and
+                                          os.environ.get("PTO_BACKEND", "nccl") in ("nccl", "rccl")) else None
     env, device = pdist.init_distributed(os.environ.get("PTO_BACKEND"), use_gpu=use_gpu)
-    if env.world_size != args.gpus and env.rank == 0:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
+    if env.world_size != args.gpus:  # unreachable after _launch_ranks; never report a mislabelled world
+        raise SystemExit(f"[bench] --gpus {args.gpus} but the process group has {env.world_size} ranks")
 
     if not mnist:
-        return run_model_bench(args, env, device, pdist)
+        return run_model_bench(args, env, device, pdist, rccl_log)
 
     from pytorch_operator_1_amd.train.runner import build_trainer
 
@@ -115,6 +158,10 @@ def main(argv=None):
     elapsed = time.perf_counter() - t0
     elapsed = pdist.all_reduce_max(elapsed, device)
     loss = trainer.last_loss()
+    # evidence of the world that was measured (outside the timed region)
+    world = pdist.describe_world(device, rccl_log)
+    comm = dict(getattr(trainer, "comm_info", None) or {})
+    comm.update(world)
 
     n = env.world_size
     ms_per_step = elapsed / args.steps * 1e3
@@ -148,7 +195,7 @@ def main(argv=None):
                 "backend": (torch.distributed.get_backend() if n > 1 else "none"),
                 "baseline": "210 samples/s/rank (BASELINE.md, derived lower bound); vs_baseline = value/(210*n_gpus)",
                 "final_loss": round(loss, 4) if loss is not None else None,
-                "grad_allreduce": getattr(trainer, "comm_info", None),
+                "grad_allreduce": comm,
             },
         }
     pdist.cleanup()
@@ -214,7 +261,7 @@ def measure_submit_to_first_step(gpu: bool, timeout: float = 240.0) -> dict:
 MI355X_BF16_DENSE_FLOPS = 2.5e15
 
 
-def run_model_bench(args, env, device, pdist):
+def run_model_bench(args, env, device, pdist, rccl_log=None):
     """BASELINE configs 3/4: ResNet-50 / Llama-3 DDP, full optimizer steps."""
     from pytorch_operator_1_amd.train.bench_models import LlamaTrainer, ResNetTrainer
 
@@ -245,6 +292,7 @@ def run_model_bench(args, env, device, pdist):
     n = env.world_size
     per_step = trainer.samples_per_step()
     value = per_step * n * args.steps / elapsed
+    world = pdist.describe_world(device, rccl_log)
     if env.rank == 0:
         cfg = {"model": args.model, "global_batch": args.batch_size * n, "per_rank_batch": args.batch_size,
                "seq_len": args.seq_len if args.model.startswith("llama") else None,
@@ -255,6 +303,7 @@ def run_model_bench(args, env, device, pdist):
                "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 1),
                "final_loss": trainer.last_loss()}
         cfg.update(trainer.describe())
+        cfg["world"] = world
         if breakdown:
             cfg["phase_ms"] = breakdown
         if hasattr(trainer, "flops_per_step"):
@@ -271,4 +320,4 @@ def run_model_bench(args, env, device, pdist):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

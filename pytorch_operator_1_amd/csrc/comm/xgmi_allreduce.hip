@@ -21,11 +21,32 @@
 // that call, which peers only reach once their previous launch, including
 // its stage-2 reads of this tmp, has completed).
 //
-// Visibility (MI355X_MICROARCH.md "inter-workgroup visibility", applied at
-// system scope because readers are other devices): producer = stores ->
-// s_waitcnt vmcnt(0) -> barrier -> release fence (system: L2 write-back) ->
-// s_waitcnt vmcnt(0) -> relaxed system flag store; consumer = relaxed poll ->
-// system acquire (L1/L2 invalidate) -> s_waitcnt -> barrier -> loads.
+// Visibility: two protocols (pto_ar_set_protocol, chosen at setup; the
+// trainer's autotune verifies the one it keeps against RCCL on the real
+// links, falling back from 0 to 1 to RCCL).
+//
+//   0 "coherent" (default): NO cache-maintenance fences.  Every byte a peer
+//     reads that this launch writes (the folded gradient, the stage-1 partial
+//     sums in tmp) is stored WRITE-THROUGH at system scope (buffer stores
+//     with sc0 sc1); every storing wave drains (s_waitcnt vmcnt(0): the
+//     stores are acknowledged at system scope) and the workgroup barrier
+//     orders that before the one-lane flag store (system-scope relaxed store
+//     into the peer's uncached flag page).  Every load of peer-written bytes
+//     is a system-coherent buffer load (sc0 sc1: misses in this CU's L1 and
+//     this XCD's L2), so no acquire is needed (the system-scope analogue of
+//     MI355X_MICROARCH.md "Valid forms": sc1 payload + drained flag, sc1
+//     loads).  The gradient bytes written by the PREVIOUS kernel on the
+//     stream (k_bwd_all) are in HBM once that kernel has ended: the end-of-
+//     kernel release writes every XCD's dirty L2 lines back (at least agent
+//     scope, which on the 8-XCD part is an L2 write-back, or the next kernel
+//     on another XCD could not read them), and a peer's sc0 sc1 loads read
+//     HBM.  Cost per barrier: one flag round trip, no L2 walk.
+//   1 "fenced": plain stores and loads; producer = stores -> s_waitcnt
+//     vmcnt(0) -> barrier -> release fence (system: L2 write-back) ->
+//     s_waitcnt vmcnt(0) -> relaxed system flag store; consumer = relaxed poll
+//     -> system acquire (L1/L2 invalidate) -> s_waitcnt -> barrier -> loads.
+//     One write-back + one invalidate per workgroup per barrier (18.8 us per
+//     call at world 1, profiles/ddp_step_r3.md).
 // Flags live in uncached memory; every spin is bounded (pto_ar_set_timeout_ms,
 // default 500 ms) and reports a timeout through *err instead of hanging the
 // device.
@@ -71,15 +92,34 @@ namespace {
 constexpr int AR_MAX_RANKS = 8;
 // workgroups per launch: ceil(chunk / AR_THREADS) up to this cap, so every
 // thread handles ONE float4 per stage down to world 1-2 on MNIST's 1.7 MB
-// (64 left a 3-round dependent chain per stage at world 1: 18.8 us)
 constexpr int AR_MAX_BLOCKS = 256;
 constexpr int AR_CHANNELS = 2;
 constexpr int AR_THREADS = 512;
 constexpr int AR_MAX_REP = 256;  // gradient replicas folded before barrier 1 (launcher check)
 constexpr int AR_REP_CHUNK = 16;  // replica loads in flight at once
+// stage-1 sums of this rank's own chunk kept in registers for stage 2 (the
+// same thread handles element j of the chunk in both stages): iterations
+// beyond this re-read them from tmp
+constexpr int AR_CARRY = 4;
 constexpr long long AR_ONESHOT_MAX = 65536;  // floats (256 KB): one-shot path
 constexpr long long AR_TICKS_PER_MS = 100000LL;  // wall_clock64 runs at 100 MHz
 long long g_timeout_ticks = 500 * AR_TICKS_PER_MS;  // pto_ar_set_timeout_ms
+int g_protocol = 0;  // pto_ar_set_protocol: 0 coherent (write-through + sc0 sc1 loads), 1 fenced
+
+// buffer-instruction cache bits (aux operand): sc0 | sc1 = system scope
+constexpr int AUX_SYS = 1 | 16;
+
+// global (not flat) views of generic pointers: flag words and the local
+// parameter/momentum/gradient float4 groups
+using gu32 = __attribute__((address_space(1))) uint32_t;
+using v4f = __attribute__((ext_vector_type(4))) float;
+using gv4f = __attribute__((address_space(1))) v4f;
+__device__ __forceinline__ gu32* G(uint32_t* p) { return (gu32*)p; }
+__device__ __forceinline__ float4 gld4(const float* p) {
+  const v4f v = *(const gv4f*)p;
+  return float4{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ void gst4(float* p, float4 a) { *(gv4f*)p = v4f{a.x, a.y, a.z, a.w}; }
 
 struct ArPeers {
   float* in[AR_MAX_RANKS];
@@ -92,25 +132,62 @@ __host__ __device__ constexpr int flag_index(int chan, int phase, int block, int
 }
 constexpr int AR_FLAG_WORDS = AR_CHANNELS * 2 * AR_MAX_BLOCKS * AR_MAX_RANKS;
 
+// float4 access to a buffer that peers read or write.  COHERENT: system-
+// scope buffer loads/stores (sc0 sc1), i.e. write-through stores and loads
+// that miss in L1/L2; otherwise plain accesses (the fenced protocol's
+// release/acquire provide visibility).  The descriptor covers `bytes` from
+// `base` (the launcher keeps every range below 2 GB).
+struct Buf {
+  __amdgpu_buffer_rsrc_t r;
+  float* p;
+};
+__device__ __forceinline__ Buf mkbuf(float* base, long long bytes) {
+  return Buf{__builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000), base};
+}
+template <bool COHERENT>
+__device__ __forceinline__ float4 ld4(const Buf& b, long long i4) {
+  if constexpr (COHERENT) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b128(b.r, (int)(i4 * 16), 0, AUX_SYS);
+    return __builtin_bit_cast(float4, v);
+  } else {
+    return reinterpret_cast<const float4*>(b.p)[i4];
+  }
+}
+template <bool COHERENT>
+__device__ __forceinline__ void st4(const Buf& b, long long i4, float4 v) {
+  if constexpr (COHERENT) {
+    using u4 = __attribute__((ext_vector_type(4))) unsigned int;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), b.r, (int)(i4 * 16), 0, AUX_SYS);
+  } else {
+    reinterpret_cast<float4*>(b.p)[i4] = v;
+  }
+}
+
 // Returns false (for every thread of the block) if the barrier failed: a
 // peer did not arrive within `timeout` ticks, or an earlier barrier of this
 // rank already failed (*err != 0).  s_fail is per phase, so a fast thread
 // resetting phase 1's word cannot race a slow thread still reading phase 0's.
-__device__ __forceinline__ bool block_barrier(const ArPeers& P, int chan, int phase, int rank, int world, uint32_t e,
+// FENCED: system release before the flag store, system acquire after the
+// wait; otherwise the drained write-through stores need no release and the
+// consumer's sc0 sc1 loads no acquire.
+template <bool FENCED>
+__device__ __forceinline__ bool block_barrier(const ArPeers* __restrict__ P, int chan, int phase, int rank, int world, uint32_t e,
                                               long long timeout, int* err) {
   __shared__ int s_fail[2];
   const int t = threadIdx.x, b = blockIdx.x;
   if (t == 0) s_fail[phase] = 0;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave: its stores acknowledged
   __syncthreads();
   if (t < world) {
     bool dead = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
     if (!dead) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back this XCD's L2
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(P.flags[t] + flag_index(chan, phase, b, rank), e, __ATOMIC_RELAXED,
+      if constexpr (FENCED) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back this XCD's L2
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __hip_atomic_store(G(P->flags[t] + flag_index(chan, phase, b, rank)), e, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
-      uint32_t* f = P.flags[rank] + flag_index(chan, phase, b, t);
+      gu32* f = G(P->flags[rank] + flag_index(chan, phase, b, t));
       const long long t0 = wall_clock64();
       while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
         if (wall_clock64() - t0 > timeout) {
@@ -123,10 +200,14 @@ __device__ __forceinline__ bool block_barrier(const ArPeers& P, int chan, int ph
           dead = true;
           break;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(1);
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // invalidate L1/L2 before reading peer data
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (FENCED) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // invalidate L1/L2 before reading peer data
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler order only: no loads above the poll
+      }
     }
     if (dead) s_fail[phase] = 1;
   }
@@ -154,94 +235,120 @@ struct ArSgd {
   long long rep_from;
 };
 
-// Fold the local replicas into float4 element (float offset fi) of the local
-// gradient g, if fi lies in the replicated range.  Every replica load is
-// issued before the first add.
-__device__ __forceinline__ void fold_rep(const ArSgd& f, float* g, long long fi) {
+// Fold the local replicas into float4 element i4 (float offset 4*i4 from the
+// buffer base) of the local gradient, if it lies in the replicated range.
+// Every replica load is issued before the first add; the folded value is
+// stored through `g` (write-through under the coherent protocol: peers read
+// it).
+template <bool COHERENT>
+__device__ __forceinline__ void fold_rep(const ArSgd& f, const Buf& g, long long off, long long i4) {
+  const long long fi = off + 4 * i4;  // float index in the whole buffer (rep_from's frame)
   if (!f.rep || f.nrep <= 1 || fi < f.rep_from || fi >= f.rep_from + f.rep_stride) return;
   const long long k = fi - f.rep_from;
-  float4 a = *reinterpret_cast<const float4*>(g + fi);
+  float4 a = gld4(g.p + 4 * i4);
   for (int r0 = 0; r0 < f.nrep - 1; r0 += AR_REP_CHUNK) {  // replica order
     float4 v[AR_REP_CHUNK];
 #pragma unroll
     for (int r = 0; r < AR_REP_CHUNK; ++r)
-      v[r] = *reinterpret_cast<const float4*>(f.rep + (long long)min(r0 + r, f.nrep - 2) * f.rep_stride + k);
+      v[r] = gld4(f.rep + (long long)min(r0 + r, f.nrep - 2) * f.rep_stride + k);
 #pragma unroll
     for (int r = 0; r < AR_REP_CHUNK; ++r) {
       if (r0 + r >= f.nrep - 1) break;
       a.x += v[r].x; a.y += v[r].y; a.z += v[r].z; a.w += v[r].w;
-      *reinterpret_cast<float4*>(f.rep + (long long)(r0 + r) * f.rep_stride + k) = float4{0.f, 0.f, 0.f, 0.f};
+      gst4(f.rep + (long long)(r0 + r) * f.rep_stride + k, float4{0.f, 0.f, 0.f, 0.f});
     }
   }
-  *reinterpret_cast<float4*>(g + fi) = a;
+  st4<COHERENT>(g, i4, a);
 }
 
+// SGD on float4 group i (float index) of the local parameters/momentum.
+__device__ __forceinline__ void sgd4(const ArSgd& f, long long i, float4 g, float4& pv, float4& mv, float lr) {
+  sgd_elem(pv.x, g.x, mv.x, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+  sgd_elem(pv.y, g.y, mv.y, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+  sgd_elem(pv.z, g.z, mv.z, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+  sgd_elem(pv.w, g.w, mv.w, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+  gst4(f.p + i, pv);
+  gst4(f.m + i, mv);
+}
+
+__device__ __forceinline__ float4 add4(float4 a, float4 b) { return float4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
+
 // n4 float4 elements starting at float offset `off` of every rank's buffers.
-template <bool SGD>
+template <bool SGD, bool FENCED>
 __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce(const ArPeers* __restrict__ peers, long long off,
                                                                long long n4, int rank, int world, int chan,
                                                                uint32_t* __restrict__ epochs, int* err, long long timeout,
                                                                ArSgd f) {
+  constexpr bool CO = !FENCED;
   __shared__ uint32_t s_epoch;
-  const ArPeers P = *peers;
+  const ArPeers* __restrict__ P = peers;
   if (threadIdx.x == 0) s_epoch = epochs[chan * AR_MAX_BLOCKS + blockIdx.x] + 1;
   __syncthreads();
   const uint32_t e = s_epoch;
   if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blockIdx.x] = e;
   const long long cs = (n4 + world - 1) / world;  // chunk length (float4)
   const long long stride = (long long)gridDim.x * AR_THREADS;
+  const long long j0 = (long long)blockIdx.x * AR_THREADS + threadIdx.x;
+  const long long bytes = n4 * 16;
+  float* const my_in = P->in[rank];
   if (f.rep && f.nrep > 1 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
     // the elements this workgroup's peers will read: the same sub-range of every chunk
+    const Buf g = mkbuf(my_in + off, bytes);
     for (int q = 0; q < world; ++q)
-      for (long long j = (long long)blockIdx.x * AR_THREADS + threadIdx.x; j < cs && q * cs + j < n4; j += stride)
-        fold_rep(f, P.in[rank], off + 4 * (q * cs + j));
+      for (long long j = j0; j < cs && q * cs + j < n4; j += stride) fold_rep<CO>(f, g, off, q * cs + j);
   }
 
-  if (!block_barrier(P, chan, 0, rank, world, e, timeout, err)) return;
-  // stage 1: reduce my chunk over all ranks (rank order 0..W-1 everywhere)
+  if (!block_barrier<FENCED>(P, chan, 0, rank, world, e, timeout, err)) return;
+  // stage 1: reduce my chunk over all ranks (rank order 0..W-1 everywhere);
+  // the first AR_CARRY iterations' sums stay in registers for stage 2, tmp
+  // gets them only if a peer (or a later iteration) reads them
+  float4 own[AR_CARRY];
   {
     const long long c0 = (long long)rank * cs, c1 = min(n4, c0 + cs);
-    for (long long i = c0 + (long long)blockIdx.x * AR_THREADS + threadIdx.x; i < c1; i += stride) {
+    int it = 0;
+    for (long long i = c0 + j0; i < c1; i += stride, ++it) {
       float4 v[AR_MAX_RANKS];
 #pragma unroll
       for (int q = 0; q < AR_MAX_RANKS; ++q)
-        if (q < world) v[q] = reinterpret_cast<const float4*>(P.in[q] + off)[i];
+        if (q < world) v[q] = ld4<CO>(mkbuf(P->in[q] + off, bytes), i);
       float4 a = v[0];
 #pragma unroll
       for (int q = 1; q < AR_MAX_RANKS; ++q)
-        if (q < world) {
-          a.x += v[q].x;
-          a.y += v[q].y;
-          a.z += v[q].z;
-          a.w += v[q].w;
-        }
-      reinterpret_cast<float4*>(P.tmp[rank] + off)[i] = a;
+        if (q < world) a = add4(a, v[q]);
+#pragma unroll
+      for (int c = 0; c < AR_CARRY; ++c)
+        if (c == it) own[c] = a;
+      if (world > 1 || it >= AR_CARRY) st4<CO>(mkbuf(P->tmp[rank] + off, bytes), i, a);
     }
   }
-  if (!block_barrier(P, chan, 1, rank, world, e, timeout, err)) return;
-  // stage 2: gather every chunk into my input (or: update my parameters)
   const float lr = SGD ? *f.a.lr : 0.f;
-  for (long long j = (long long)blockIdx.x * AR_THREADS + threadIdx.x; j < cs; j += stride) {
+  if (!block_barrier<FENCED>(P, chan, 1, rank, world, e, timeout, err)) return;
+  // stage 2: gather every chunk into my input (or: update my parameters)
+  int it = 0;
+  for (long long j = j0; j < cs; j += stride, ++it) {
     float4 v[AR_MAX_RANKS];
 #pragma unroll
     for (int q = 0; q < AR_MAX_RANKS; ++q)
-      if (q < world && (long long)q * cs + j < n4) v[q] = reinterpret_cast<const float4*>(P.tmp[q] + off)[q * cs + j];
+      if (q < world && (long long)q * cs + j < n4) {
+        if (q == rank && it < AR_CARRY) {
+#pragma unroll
+          for (int c = 0; c < AR_CARRY; ++c)
+            if (c == it) v[q] = own[c];
+        } else {
+          v[q] = ld4<CO>(mkbuf(P->tmp[q] + off, bytes), q * cs + j);
+        }
+      }
 #pragma unroll
     for (int q = 0; q < AR_MAX_RANKS; ++q)
       if (q < world && (long long)q * cs + j < n4) {
         if constexpr (SGD) {
           const long long i = off + 4 * (q * cs + j);
-          float4 pv = *reinterpret_cast<float4*>(f.p + i);
-          float4 mv = *reinterpret_cast<float4*>(f.m + i);
-          sgd_elem(pv.x, v[q].x, mv.x, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
-          sgd_elem(pv.y, v[q].y, mv.y, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
-          sgd_elem(pv.z, v[q].z, mv.z, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
-          sgd_elem(pv.w, v[q].w, mv.w, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
-          *reinterpret_cast<float4*>(f.p + i) = pv;
-          *reinterpret_cast<float4*>(f.m + i) = mv;
-          if (i >= f.zero_from) *reinterpret_cast<float4*>(P.in[rank] + i) = float4{0.f, 0.f, 0.f, 0.f};
+          float4 pv = gld4(f.p + i);
+          float4 mv = gld4(f.m + i);
+          sgd4(f, i, v[q], pv, mv, lr);
+          if (i >= f.zero_from) gst4(my_in + i, float4{0.f, 0.f, 0.f, 0.f});
         } else {
-          reinterpret_cast<float4*>(P.in[rank] + off)[q * cs + j] = v[q];
+          gst4(my_in + off + 4 * (q * cs + j), v[q]);
         }
       }
   }
@@ -249,61 +356,90 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce(const ArPeers* __
 }
 
 // One-shot variant: n4 <= gridDim.x * AR_THREADS (one float4 per thread).
-template <bool SGD>
+template <bool SGD, bool FENCED>
 __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_1shot(const ArPeers* __restrict__ peers,
                                                                      long long off, long long n4, int rank,
                                                                      int world, int chan,
                                                                      uint32_t* __restrict__ epochs, int* err,
                                                                      long long timeout, ArSgd f) {
+  constexpr bool CO = !FENCED;
   __shared__ uint32_t s_epoch;
-  const ArPeers P = *peers;
+  const ArPeers* __restrict__ P = peers;
   if (threadIdx.x == 0) s_epoch = epochs[chan * AR_MAX_BLOCKS + blockIdx.x] + 1;
   __syncthreads();
   const uint32_t e = s_epoch;
   if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blockIdx.x] = e;
   const long long i = (long long)blockIdx.x * AR_THREADS + threadIdx.x;
   const bool act = i < n4;
+  const long long bytes = n4 * 16;
+  float* const my_in = P->in[rank];
   if (act && f.rep && f.nrep > 1 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-    fold_rep(f, P.in[rank], off + 4 * i);
-  if (!block_barrier(P, chan, 0, rank, world, e, timeout, err)) return;
+    fold_rep<CO>(f, mkbuf(my_in + off, bytes), off, i);
+  if (!block_barrier<FENCED>(P, chan, 0, rank, world, e, timeout, err)) return;
   float4 a = {0.f, 0.f, 0.f, 0.f};
   if (act) {
     float4 v[AR_MAX_RANKS];
 #pragma unroll
     for (int q = 0; q < AR_MAX_RANKS; ++q)
-      if (q < world) v[q] = reinterpret_cast<const float4*>(P.in[q] + off)[i];
+      if (q < world) v[q] = ld4<CO>(mkbuf(P->in[q] + off, bytes), i);
     a = v[0];
 #pragma unroll
     for (int q = 1; q < AR_MAX_RANKS; ++q)
-      if (q < world) {
-        a.x += v[q].x;
-        a.y += v[q].y;
-        a.z += v[q].z;
-        a.w += v[q].w;
-      }
+      if (q < world) a = add4(a, v[q]);
   }
   // every peer is done reading my input (on failure: nothing is written)
-  if (!block_barrier(P, chan, 1, rank, world, e, timeout, err)) return;
+  if (!block_barrier<FENCED>(P, chan, 1, rank, world, e, timeout, err)) return;
   if (act) {
     if constexpr (SGD) {
       const float lr = *f.a.lr;
       const long long j = off + 4 * i;
-      float4 pv = *reinterpret_cast<float4*>(f.p + j);
-      float4 mv = *reinterpret_cast<float4*>(f.m + j);
-      sgd_elem(pv.x, a.x, mv.x, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
-      sgd_elem(pv.y, a.y, mv.y, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
-      sgd_elem(pv.z, a.z, mv.z, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
-      sgd_elem(pv.w, a.w, mv.w, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
-      *reinterpret_cast<float4*>(f.p + j) = pv;
-      *reinterpret_cast<float4*>(f.m + j) = mv;
-      if (j >= f.zero_from) *reinterpret_cast<float4*>(P.in[rank] + j) = float4{0.f, 0.f, 0.f, 0.f};
+      float4 pv = gld4(f.p + j);
+      float4 mv = gld4(f.m + j);
+      sgd4(f, j, a, pv, mv, lr);
+      if (j >= f.zero_from) gst4(my_in + j, float4{0.f, 0.f, 0.f, 0.f});
     } else {
-      reinterpret_cast<float4*>(P.in[rank] + off)[i] = a;
+      gst4(my_in + off + 4 * i, a);
     }
   }
   if (SGD && f.bidx && blockIdx.x == 0 && threadIdx.x == 0) *f.bidx = (*f.bidx + 1) % f.nbatches;
 }
 
+// Workgroups used for n floats (identical on every rank: derived from n, W).
+int blocks_for(long long n, int world) {
+  if (n <= AR_ONESHOT_MAX) return (int)((n / 4 + AR_THREADS - 1) / AR_THREADS);
+  const long long cs = ((n / 4) + world - 1) / world;
+  long long b = (cs + AR_THREADS - 1) / AR_THREADS;
+  if (b < 1) b = 1;
+  if (b > AR_MAX_BLOCKS) b = AR_MAX_BLOCKS;
+  return (int)b;
+}
+
+template <bool SGD>
+int launch(const void* peers, long long off, long long n, int rank, int world, int chan, void* epochs, void* err,
+           const ArSgd& f, hipStream_t s) {
+  const ArPeers* P = reinterpret_cast<const ArPeers*>(peers);
+  uint32_t* ep = reinterpret_cast<uint32_t*>(epochs);
+  int* er = reinterpret_cast<int*>(err);
+  const long long n4 = n / 4;
+  if (n <= AR_ONESHOT_MAX) {
+    const dim3 g((unsigned)((n4 + AR_THREADS - 1) / AR_THREADS));
+    if (g_protocol)
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce_1shot<SGD, true>), g, dim3(AR_THREADS), 0, s, P, off, n4,
+                         rank, world, chan, ep, er, g_timeout_ticks, f);
+    else
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce_1shot<SGD, false>), g, dim3(AR_THREADS), 0, s, P, off, n4,
+                         rank, world, chan, ep, er, g_timeout_ticks, f);
+    return (int)hipGetLastError();
+  }
+  const dim3 g((unsigned)blocks_for(n, world));
+  if (g_protocol)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce<SGD, true>), g, dim3(AR_THREADS), 0, s, P, off, n4, rank,
+                       world, chan, ep, er, g_timeout_ticks, f);
+  else
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce<SGD, false>), g, dim3(AR_THREADS), 0, s, P, off, n4, rank,
+                       world, chan, ep, er, g_timeout_ticks, f);
+  return (int)hipGetLastError();
+}
 
 }  // namespace
 
@@ -319,6 +455,15 @@ PTO_API int pto_ar_set_timeout_ms(int ms) {
   g_timeout_ticks = (long long)ms * AR_TICKS_PER_MS;
   return 0;
 }
+// Visibility protocol for launches issued (or graph-captured) from now on:
+// 0 coherent (default), 1 fenced (see the file header).  Every rank of a
+// group must use the same one.
+PTO_API int pto_ar_set_protocol(int p) {
+  if (p < 0 || p > 1) return -1;
+  g_protocol = p;
+  return 0;
+}
+PTO_API int pto_ar_get_protocol() { return g_protocol; }
 
 // Flags: uncached device memory, zeroed.
 PTO_API int pto_ar_alloc_flags(void** out) {
@@ -344,15 +489,11 @@ PTO_API int pto_ar_open_ipc_handle(const void* handle, void** ptr_out) {
 }
 PTO_API int pto_ar_close_ipc_handle(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
 
-// Workgroups used for n floats (identical on every rank: derived from n, W).
-PTO_API int pto_ar_blocks(long long n, int world) {
-  if (n <= AR_ONESHOT_MAX) return (int)((n / 4 + AR_THREADS - 1) / AR_THREADS);
-  const long long cs = ((n / 4) + world - 1) / world;
-  long long b = (cs + AR_THREADS - 1) / AR_THREADS;
-  if (b < 1) b = 1;
-  if (b > AR_MAX_BLOCKS) b = AR_MAX_BLOCKS;
-  return (int)b;
-}
+PTO_API int pto_ar_blocks(long long n, int world) { return blocks_for(n, world); }
+
+// Largest range (floats) one call may cover: the buffer descriptors of the
+// coherent protocol address it with 32-bit byte offsets.
+constexpr long long AR_MAX_FLOATS = (1LL << 29) - 4;
 
 // In-place SUM all-reduce of n floats at float offset `off` of the registered
 // input buffers.  peers: device copy of ArPeers.  Requires n % 4 == 0,
@@ -360,20 +501,11 @@ PTO_API int pto_ar_blocks(long long n, int world) {
 // multi-GPU step, no peers), chan < 2.
 PTO_API int pto_ar_allreduce(const void* peers, long long off, long long n, int rank, int world, int chan,
                              void* epochs, void* err, hipStream_t s) {
-  if (n % 4 || off % 4 || world < 1 || world > AR_MAX_RANKS || chan < 0 || chan >= AR_CHANNELS || rank < 0 ||
-      rank >= world)
+  if (n % 4 || off % 4 || n > AR_MAX_FLOATS || world < 1 || world > AR_MAX_RANKS || chan < 0 ||
+      chan >= AR_CHANNELS || rank < 0 || rank >= world)
     return -1;
   if (n == 0) return 0;
-  if (n <= AR_ONESHOT_MAX) {
-    hipLaunchKernelGGL(k_xgmi_allreduce_1shot<false>, dim3((unsigned)((n / 4 + AR_THREADS - 1) / AR_THREADS)),
-                       dim3(AR_THREADS), 0, s, reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,
-                       reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), g_timeout_ticks, ArSgd{});
-    return (int)hipGetLastError();
-  }
-  hipLaunchKernelGGL(k_xgmi_allreduce<false>, dim3(pto_ar_blocks(n, world)), dim3(AR_THREADS), 0, s,
-                     reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,
-                     reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), g_timeout_ticks, ArSgd{});
-  return (int)hipGetLastError();
+  return launch<false>(peers, off, n, rank, world, chan, epochs, err, ArSgd{}, s);
 }
 
 // All-reduce + SGD-momentum epilogue over the same range: p/m are this rank's
@@ -386,8 +518,9 @@ PTO_API int pto_ar_allreduce_sgd(const void* peers, long long off, long long n, 
                                  float gscale, int nesterov, long long zero_from, long long* bidx,
                                  long long nbatches, float* rep, int nrep, int rep_stride, long long rep_from,
                                  hipStream_t s) {
-  if (n % 4 || off % 4 || world < 1 || world > AR_MAX_RANKS || chan < 0 || chan >= AR_CHANNELS || rank < 0 ||
-      rank >= world || !p || !m || !lr || ((((uintptr_t)p) | ((uintptr_t)m)) & 15) || (bidx && nbatches < 1))
+  if (n % 4 || off % 4 || n > AR_MAX_FLOATS || world < 1 || world > AR_MAX_RANKS || chan < 0 ||
+      chan >= AR_CHANNELS || rank < 0 || rank >= world || !p || !m || !lr ||
+      ((((uintptr_t)p) | ((uintptr_t)m)) & 15) || (bidx && nbatches < 1))
     return -1;
   if (rep && (nrep < 1 || nrep > AR_MAX_REP || rep_stride % 4 || rep_from % 4 || (((uintptr_t)rep) & 15)))
     return -1;
@@ -407,14 +540,5 @@ PTO_API int pto_ar_allreduce_sgd(const void* peers, long long off, long long n, 
   f.nrep = rep ? nrep : 1;
   f.rep_stride = rep_stride;
   f.rep_from = rep_from;
-  if (n <= AR_ONESHOT_MAX) {
-    hipLaunchKernelGGL(k_xgmi_allreduce_1shot<true>, dim3((unsigned)((n / 4 + AR_THREADS - 1) / AR_THREADS)),
-                       dim3(AR_THREADS), 0, s, reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,
-                       reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), g_timeout_ticks, f);
-    return (int)hipGetLastError();
-  }
-  hipLaunchKernelGGL(k_xgmi_allreduce<true>, dim3(pto_ar_blocks(n, world)), dim3(AR_THREADS), 0, s,
-                     reinterpret_cast<const ArPeers*>(peers), off, n / 4, rank, world, chan,
-                     reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err), g_timeout_ticks, f);
-  return (int)hipGetLastError();
+  return launch<true>(peers, off, n, rank, world, chan, epochs, err, f, s);
 }

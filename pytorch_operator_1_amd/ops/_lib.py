@@ -141,6 +141,8 @@ _SIGS = {
     "pto_ar_peers_bytes": [],
     "pto_ar_epoch_words": [],
     "pto_ar_set_timeout_ms": [_I],
+    "pto_ar_set_protocol": [_I],
+    "pto_ar_get_protocol": [],
     "pto_ar_alloc_flags": [ctypes.POINTER(ctypes.c_void_p)],
     "pto_ar_free": [_P],
     "pto_ar_get_ipc_handle": [_P, _P, ctypes.POINTER(ctypes.c_longlong)],

@@ -39,6 +39,10 @@ from ..ops import _lib
 
 
 DEFAULT_TIMEOUT_MS = 500
+# visibility protocols of the kernel (csrc/comm/xgmi_allreduce.hip header):
+# "coherent" = write-through stores + system-coherent loads, no fences;
+# "fenced" = per-workgroup system release/acquire around every barrier
+PROTOCOLS = {"coherent": 0, "fenced": 1}
 
 
 class XgmiTimeout(RuntimeError):
@@ -46,9 +50,11 @@ class XgmiTimeout(RuntimeError):
 
 
 class XgmiAllReduce:
-    def __init__(self, buf: torch.Tensor, group=None, timeout_ms: int | None = None):
+    def __init__(self, buf: torch.Tensor, group=None, timeout_ms: int | None = None, protocol: str | None = None):
         """``buf``: this rank's fp32 gradient buffer (same numel on every
-        rank); all-reduces operate in place on ranges of it."""
+        rank); all-reduces operate in place on ranges of it.  ``protocol``:
+        "coherent" (default, ``PTO_XGMI_PROTOCOL``) or "fenced"; every rank
+        must pass the same."""
         if buf.dtype != torch.float32 or not buf.is_cuda or not buf.is_contiguous():
             raise ValueError("XgmiAllReduce: contiguous fp32 HIP buffer required")
         self.group = group
@@ -65,6 +71,9 @@ class XgmiAllReduce:
         self.timeout_ms = int(timeout_ms if timeout_ms is not None
                               else os.environ.get("PTO_XGMI_TIMEOUT_MS", DEFAULT_TIMEOUT_MS))
         _lib.check(L.pto_ar_set_timeout_ms(self.timeout_ms), "ar_set_timeout_ms")
+        self.protocol = protocol or os.environ.get("PTO_XGMI_PROTOCOL", "coherent")
+        if self.protocol not in PROTOCOLS:
+            raise ValueError(f"XgmiAllReduce: protocol must be one of {sorted(PROTOCOLS)}, not {self.protocol!r}")
         self.buf = buf
         self.device = buf.device
         self.tmp = torch.empty_like(buf)
@@ -127,6 +136,7 @@ class XgmiAllReduce:
         if offset + n > self.buf.numel():
             raise ValueError("XgmiAllReduce: range outside the registered buffer")
         s = (stream or torch.cuda.current_stream(self.device)).cuda_stream
+        _lib.check(_lib.lib().pto_ar_set_protocol(PROTOCOLS[self.protocol]), "ar_set_protocol")
         _lib.check(_lib.lib().pto_ar_allreduce(self.peers.data_ptr(), offset, n, self.rank, self.world, chan,
                                                self.epochs.data_ptr(), self.err.data_ptr(), s), "xgmi_allreduce")
 
@@ -157,6 +167,7 @@ class XgmiAllReduce:
             if replicas.numel() < (n_replicas - 1) * rep_stride or replicas.device != self.device:
                 raise ValueError("XgmiAllReduce: replica buffer too small for n_replicas")
             rep = replicas.data_ptr()
+        _lib.check(_lib.lib().pto_ar_set_protocol(PROTOCOLS[self.protocol]), "ar_set_protocol")
         _lib.check(_lib.lib().pto_ar_allreduce_sgd(self.peers.data_ptr(), offset, n, self.rank, self.world, chan,
                                                    self.epochs.data_ptr(), self.err.data_ptr(), params.data_ptr(),
                                                    mom.data_ptr(), lr_dev.data_ptr(), momentum, weight_decay, gscale,
@@ -199,40 +210,70 @@ class XgmiAllReduce:
             raise XgmiTimeout(f"xGMI all-reduce barrier timed out after {self.timeout_ms} ms "
                               f"(phase mask {e}): a peer rank died or stalled")
 
+    def verify(self, ranges, rounds: int = 8) -> dict:
+        """Check the kernel against RCCL/the group's all-reduce over
+        ``rounds`` back-to-back calls with fresh random data each (a stale
+        read shows as a wrong sum), and that every rank holds bit-identical
+        results.  Collective; the buffer is restored afterwards.  Returns
+        ``{"correct", "max_rel_err", "timed_out", "protocol"}`` agreed by
+        every rank."""
+        saved = self.buf.clone()
+        bad, identical = 0.0, True
+        for it in range(rounds):
+            g = torch.Generator(device=self.device).manual_seed(1234 + 7919 * it + self.rank)
+            self.buf.copy_(torch.randn(self.buf.shape, generator=g, device=self.device))
+            ref = self.buf.clone()
+            for off, n in ranges:
+                dist.all_reduce(ref[off:off + n], group=self.group)
+            for c, (off, n) in enumerate(ranges):
+                self.allreduce_(off, n, chan=c % 2)
+            torch.cuda.synchronize(self.device)
+            scale = max(1.0, ref.abs().max().item())
+            for off, n in ranges:
+                bad = max(bad, (self.buf[off:off + n] - ref[off:off + n]).abs().max().item() / scale)
+            # every rank must hold identical values (fixed summation order)
+            chk = self.buf.clone()
+            dist.all_reduce(chk, op=dist.ReduceOp.MAX, group=self.group)
+            identical &= float((chk - self.buf).abs().max().item()) == 0.0
+        timed_out = int(self.err.item()) != 0
+        self.buf.copy_(saved)
+        torch.cuda.synchronize(self.device)
+        ok = self._agree(bad <= 1e-5 and identical and not timed_out)
+        return {"correct": ok, "max_rel_err": bad, "identical": identical, "timed_out": timed_out,
+                "protocol": self.protocol, "verify_rounds": rounds}
+
+    def _agree(self, flag: bool) -> bool:
+        """True on every rank iff ``flag`` is true on every rank."""
+        t = torch.tensor([1.0 if flag else 0.0], device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return t.item() == 1.0
+
+    def verify_with_fallback(self, ranges) -> dict:
+        """:meth:`verify` with the current protocol; if the coherent protocol
+        gives wrong sums on these links, switch to the fenced one and verify
+        again.  Returns the last verify result plus ``use_xgmi`` (False
+        unless correct) and ``protocols_tried``."""
+        res = self.verify(ranges)
+        tried = [dict(res)]
+        if not res["correct"] and self.protocol == "coherent" and not res["timed_out"]:
+            self.protocol = "fenced"
+            res = self.verify(ranges)
+            tried.append(dict(res))
+        out = {"use_xgmi": bool(res["correct"]), **res, "protocols_tried": [t["protocol"] for t in tried]}
+        if not res["correct"]:
+            out["verify_log"] = tried
+        return out
+
     def autotune(self, ranges, iters: int = 30) -> dict:
-        """Verify against RCCL and time both over ``ranges`` [(offset, n)],
-        returning ``{"use_xgmi": bool, "xgmi_us": t, "rccl_us": t}`` — the
-        same decision on every rank (times are max over ranks)."""
+        """Verify against RCCL (:meth:`verify`; a failure of the coherent
+        protocol falls back to the fenced one) and time the kernel against
+        RCCL on ``ranges`` [(offset, n)], returning ``{"use_xgmi": bool,
+        "xgmi_us": t, "rccl_us": t, ...}`` -- the same decision on every rank
+        (times are max over ranks)."""
         if self.world == 1:
             return self._autotune_single(ranges, iters)
-        saved = self.buf.clone()
-        g = torch.Generator(device=self.device).manual_seed(1234 + self.rank)
-        self.buf.copy_(torch.randn(self.buf.shape, generator=g, device=self.device))
-        ref = self.buf.clone()
-        for off, n in ranges:
-            dist.all_reduce(ref[off:off + n], group=self.group)
-        for c, (off, n) in enumerate(ranges):
-            self.allreduce_(off, n, chan=c % 2)
-        torch.cuda.synchronize(self.device)
-        bad = 0.0
-        for off, n in ranges:
-            bad = max(bad, (self.buf[off:off + n] - ref[off:off + n]).abs().max().item())
-        # every rank must hold identical values (fixed summation order)
-        chk = self.buf.clone()
-        dist.all_reduce(chk, op=dist.ReduceOp.MAX, group=self.group)
-        identical = float((chk - self.buf).abs().max().item()) == 0.0
-        scale = max(1.0, ref.abs().max().item())
-        timed_out = int(self.err.item()) != 0
-
-        def agree(flag: bool) -> bool:  # every rank takes the same branch
-            t = torch.tensor([1.0 if flag else 0.0], device=self.device)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
-            return t.item() == 1.0
-
-        result = {"use_xgmi": False, "correct": False, "max_abs_err": bad, "timed_out": timed_out}
-        if not agree(bad <= 1e-5 * scale and identical and not timed_out):
-            self.buf.copy_(saved)
-            torch.cuda.synchronize(self.device)
+        result = self.verify_with_fallback(ranges)
+        if not result["correct"]:
             return result
 
         def timed(fn):
@@ -254,9 +295,10 @@ class XgmiAllReduce:
             for off, n in ranges:
                 dist.all_reduce(self.buf[off:off + n], group=self.group)
 
+        saved = self.buf.clone()
         run_xgmi(), run_rccl()  # warm
         tx, tr = timed(run_xgmi), timed(run_rccl)
-        ok_after = agree(int(self.err.item()) == 0)
+        ok_after = self._agree(int(self.err.item()) == 0)
         self.buf.copy_(saved)
         torch.cuda.synchronize(self.device)
         result.update(correct=ok_after, use_xgmi=bool(ok_after and tx < tr), xgmi_us=round(tx, 2),
@@ -280,8 +322,8 @@ class XgmiAllReduce:
         tx = (time.perf_counter() - t0) / iters * 1e6
         self.buf.copy_(saved)
         torch.cuda.synchronize(self.device)
-        return {"use_xgmi": ok, "correct": ok, "max_abs_err": 0.0 if ok else float("nan"), "timed_out": False,
-                "xgmi_us": round(tx, 2), "rccl_us": None}
+        return {"use_xgmi": ok, "correct": ok, "max_rel_err": 0.0 if ok else float("nan"), "timed_out": False,
+                "xgmi_us": round(tx, 2), "rccl_us": None, "protocol": self.protocol}
 
     def close(self):
         L = _lib.lib()

@@ -46,6 +46,7 @@ from __future__ import annotations
 
 import math
 import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -206,12 +207,17 @@ class FusedMnistTrainer:
                 raise
             self.comm_info = {"transport": "rccl", "xgmi_error": str(e)}
             return
-        tune = ar.autotune([(0, self.numel)])
+        # correctness only (multi-round check against the group's all-reduce,
+        # coherent -> fenced protocol fallback); whether the xGMI STEP beats
+        # the RCCL step is decided on the captured steps themselves
+        # (build_fused_trainer -> autotune_schedule)
+        ranges = [(0, self.numel)]
+        tune = ar.verify_with_fallback(ranges) if self.world > 1 else ar.autotune(ranges)
         if self.comm == "xgmi" and not tune["correct"]:
             raise RuntimeError(f"xGMI all-reduce failed verification: {tune}")
         if self.comm == "xgmi" or tune["use_xgmi"]:
             self._xgmi = ar
-            self.comm_info = dict(tune, transport="xgmi", optimizer="allreduce-epilogue")
+            self.comm_info = dict(tune, transport="xgmi", optimizer="allreduce-epilogue", protocol=ar.protocol)
         else:
             ar.close()
             self.comm_info = dict(tune, transport="rccl")
@@ -573,3 +579,97 @@ class FusedMnistTrainer:
         self.batch_idx.fill_(int(sd.get("batch_idx", 0)) % self.n_batches)
         self.steps_done = int(sd.get("steps_done", 0))
         self.set_lr(float(sd.get("lr", self.lr)))
+
+
+def autotune_schedule(xg: FusedMnistTrainer, rc: FusedMnistTrainer, verify_steps: int = 8, reps: int = 3) -> dict:
+    """Decide between the ``ddp-xgmi`` and ``ddp-rccl`` multi-GPU steps on
+    the steps themselves: both trainers (same init, same data) run
+    ``verify_steps`` captured steps -- the xGMI all-reduce with its SGD
+    epilogue and replica fold vs graph-captured RCCL + ``k_ddp_sgd`` -- and
+    their parameters must agree (max relative error per tensor <= 1e-4,
+    different summation orders) and the xGMI ranks must be bit-identical;
+    then each replays ``reps`` of its ``unroll``-step graph, timed on the
+    host (max over ranks).  Both trainers are rolled back to their initial
+    state.  Collective: every rank calls it with the same trainers."""
+    from ..utils import dist as pdist
+
+    dev = xg.device
+    snaps = [[t.clone() for t in tr._state()] for tr in (xg, rc)]
+
+    def restore():
+        torch.cuda.synchronize(dev)
+        for tr, snap in zip((xg, rc), snaps):
+            for d, s_ in zip(tr._state(), snap):
+                d.copy_(s_)
+            tr.steps_done, tr._owed = 0, False
+        torch.cuda.synchronize(dev)
+
+    def agree(flag: bool) -> bool:
+        t = torch.tensor([1.0 if flag else 0.0], device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return t.item() == 1.0
+
+    out: dict = {"verify_steps": verify_steps, "timed_steps": reps * xg.unroll}
+    try:
+        xg._align_ranks("tune-verify")
+        xg.run(verify_steps)
+        rc.run(verify_steps)
+        torch.cuda.synchronize(dev)
+        err = 0.0
+        for name, pv in xg.p.items():
+            ref = rc.p[name]
+            err = max(err, float((pv - ref).abs().max() / ref.abs().max().clamp_min(1e-12)))
+        mine = xg.params.detach().clone()
+        chk = mine.clone() if dist.get_backend() == "nccl" else mine.cpu()
+        dist.all_reduce(chk, op=dist.ReduceOp.MAX)
+        identical = bool(torch.equal(chk.to(mine.device), mine))
+        out.update(param_rel_err=err, identical=identical)
+        ok = agree(err <= 1e-4 and identical and xg._xgmi.error_word() == 0)
+        out["correct"] = ok
+
+        def timed(tr) -> float:
+            tr._align_ranks("tune-time")
+            tr.run(tr.unroll)  # warm
+            torch.cuda.synchronize(dev)
+            pdist.barrier(dev)
+            tr._align_ranks("tune-time2")
+            t0 = time.perf_counter()
+            tr.run(reps * tr.unroll)
+            torch.cuda.synchronize(dev)
+            return pdist.all_reduce_max((time.perf_counter() - t0) / (reps * tr.unroll) * 1e6, dev)
+
+        if ok:
+            out["xgmi_step_us"] = round(timed(xg), 2)
+            out["rccl_step_us"] = round(timed(rc), 2)
+            ok = agree(xg._xgmi.error_word() == 0)
+            out["correct"] = ok
+        out["kept"] = "ddp-xgmi" if ok and out["xgmi_step_us"] <= out["rccl_step_us"] else "ddp-rccl"
+    finally:
+        restore()
+    return out
+
+
+def build_fused_trainer(device, **kw) -> FusedMnistTrainer:
+    """The fused trainer, with the multi-GPU schedule chosen on the real
+    links: at world size > 1 and ``comm="auto"`` (``PTO_COMM``), a trainer
+    whose verified xGMI all-reduce was set up is raced against an RCCL-
+    schedule twin on the same data (:func:`autotune_schedule`); the faster
+    is returned (the other's peer mappings are closed) and the race is
+    recorded in ``comm_info["schedule_autotune"]``."""
+    comm = kw.get("comm") or os.environ.get("PTO_COMM", "auto")
+    tr = FusedMnistTrainer(device, **kw)
+    if tr.world == 1 or comm != "auto" or tr.schedule != "ddp-xgmi":
+        return tr
+    twin_kw = dict(kw, comm="rccl", data=tr.data.view(-1, 784), target=tr.target.view(-1))
+    twin = FusedMnistTrainer(device, **twin_kw)
+    res = autotune_schedule(tr, twin)
+    keep, drop = (tr, twin) if res["kept"] == "ddp-xgmi" else (twin, tr)
+    if drop._xgmi is not None:
+        torch.cuda.synchronize(device)
+        drop._graphs, drop._graph_pow, drop._graph_close = None, {}, {}
+        drop._xgmi.close()
+        drop._xgmi = None
+    keep.comm_info["schedule_autotune"] = res
+    if keep is twin:
+        keep.comm_info["xgmi_verify"] = {k: v for k, v in tr.comm_info.items() if k != "world_size"}
+    return keep

@@ -78,7 +78,7 @@ def build_trainer(impl: str, device, **kw):
         if device.type != "cuda":
             # The fused path is HIP-only; CPU runs (gloo tests) use eager.
             return EagerMnistTrainer(device, **kw)
-        from .fused_step import FusedMnistTrainer
+        from .fused_step import build_fused_trainer
 
-        return FusedMnistTrainer(device, **kw)
+        return build_fused_trainer(device, **kw)
     raise ValueError(f"unknown impl {impl!r}")

@@ -128,6 +128,11 @@ def generation_store(env: DistEnv, timeout_s: float):
     gen = os.environ.get("PTO_RESTART_GENERATION")
     if gen is None or not env.is_distributed:
         return None
+    if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") or os.environ.get("TORCHELASTIC_RUN_ID"):
+        # torchrun inside the pod: MASTER_PORT is the elastic agent's own
+        # TCPStore, and the agent already scopes every rendezvous to its run
+        # -- hosting a second store there would fail with EADDRINUSE
+        return None
     store = dist.TCPStore(env.master_addr, env.master_port, env.world_size, env.is_master,
                           timeout=datetime.timedelta(seconds=timeout_s), wait_for_workers=False,
                           use_libuv=os.environ.get("USE_LIBUV", "1") == "1")
@@ -186,6 +191,86 @@ def all_reduce_max(value: float, device: torch.device) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def rccl_log_setup() -> str | None:
+    """Route RCCL's INFO log (communicator init and transport selection
+    only: no per-collective lines) to a per-process file, so the transport
+    RCCL picked for each peer (P2P/IPC over xGMI, SHM, NET) can be reported.
+    Must run before the process group is created; a user-set NCCL_DEBUG is
+    left alone (returns None)."""
+    if os.environ.get("NCCL_DEBUG") or os.environ.get("NCCL_DEBUG_FILE"):
+        return None
+    import tempfile
+
+    path = os.path.join(tempfile.gettempdir(), f"pto-rccl-{os.getpid()}.log")
+    os.environ["NCCL_DEBUG"] = "INFO"
+    os.environ["NCCL_DEBUG_SUBSYS"] = "INIT,P2P,SHM,NET,GRAPH"
+    os.environ["NCCL_DEBUG_FILE"] = path
+    return path
+
+
+_CHANNEL_RE = None
+
+
+def parse_rccl_transports(text: str) -> dict:
+    """Transport summary from an RCCL/NCCL INFO log: how many ring/tree
+    channel connections use each transport (``via P2P/IPC``, ``via SHM``,
+    ``via NET/...``), plus the channel/ring counts RCCL reports."""
+    import re
+
+    global _CHANNEL_RE
+    if _CHANNEL_RE is None:
+        _CHANNEL_RE = re.compile(r"Channel \d+(?:/\d+)? ?: ?\d+\[[^\]]*\] -> \d+\[[^\]]*\] (?:\[\w+\] )?via (\S+)")
+    via: dict[str, int] = {}
+    for m in _CHANNEL_RE.finditer(text):
+        via[m.group(1)] = via.get(m.group(1), 0) + 1
+    out: dict = {"via": via}
+    m = re.search(r"(\d+) coll channels,[^\n]*?(\d+) p2p channels", text)
+    if m:
+        out["coll_channels"], out["p2p_channels"] = int(m.group(1)), int(m.group(2))
+    m = re.search(r"RCCL version\s*(\S+)|NCCL version\s*(\S+)", text)
+    if m:
+        out["version"] = m.group(1) or m.group(2)
+    return out
+
+
+def describe_world(device: torch.device, rccl_log: str | None = None) -> dict:
+    """What the measured world really was (bench.py evidence): the world
+    size the process group reports, every rank's device (PCI bus id / UUID),
+    and -- with an RCCL log from :func:`rccl_log_setup` -- the transports
+    RCCL chose.  Collective over the default group (call it on every rank,
+    outside timed regions); world size 1 returns the local entry."""
+    me: dict = {"device": str(device)}
+    if device.type == "cuda":
+        props = torch.cuda.get_device_properties(device)
+        me["name"] = props.name
+        bus = [getattr(props, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id")]
+        if None not in bus:
+            me["pci"] = "%04x:%02x:%02x" % tuple(bus)
+        uuid = getattr(props, "uuid", None)
+        if uuid is not None:
+            me["uuid"] = str(uuid)
+        me["visible"] = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+    if rccl_log and os.path.exists(rccl_log):
+        with open(rccl_log, errors="replace") as f:
+            me["rccl"] = parse_rccl_transports(f.read())
+    pg = dist.is_available() and dist.is_initialized()
+    ranks = [me]
+    if pg and dist.get_world_size() > 1:
+        ranks = [None] * dist.get_world_size()
+        dist.all_gather_object(ranks, me)
+    out = {"pg_world_size": dist.get_world_size() if pg else 1, "ranks": ranks}
+    devs = [r.get("pci") or r.get("uuid") for r in ranks]
+    if None not in devs:
+        out["distinct_devices"] = len(set(devs))
+    via: dict[str, int] = {}
+    for r in ranks:
+        for k, v in (r.get("rccl") or {}).get("via", {}).items():
+            via[k] = via.get(k, 0) + v
+    if via:
+        out["rccl_transport"] = via
+    return out
 
 
 def cleanup() -> None:

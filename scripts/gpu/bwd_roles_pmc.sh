@@ -1,7 +1,7 @@
 #!/bin/bash
 # LDS counters of k_bwd_all per role (tools/bwd_roles_probe.py --pmc-mask;
 # the probe .so is built on the CPU host beforehand), then of the whole step.
-set -e
+set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"

@@ -2,7 +2,7 @@
 # DDP-schedule step at world size 1 (grads-only backward + RCCL all-reduce of
 # a 1-rank group + SGD launch) under rocprofv3: per-kernel stats
 # (gpurun_out/ddp_kstats.txt), next to the one-process step's.
-set -e
+set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"

@@ -2,7 +2,7 @@
 # Per-kernel stats of the MNIST step under rocprofv3 for one or more env
 # settings: kstats.sh "PTO_DETERMINISTIC=0" "PTO_DETERMINISTIC=1" ...  Keeps only the
 # stats CSVs (the traces are large).
-set -e
+set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"

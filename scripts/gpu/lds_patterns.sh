@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ_LDS_BANK_CONFLICT per dispatch of the LDS access-pattern probe kernels
-set -e
+set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"

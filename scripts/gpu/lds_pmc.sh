@@ -1,7 +1,7 @@
 #!/bin/bash
 # LDS counters of the MNIST step kernels per env setting:
 #   lds_pmc.sh "PTO_DETERMINISTIC=0" "PTO_DETERMINISTIC=1" ...
-set -e
+set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Llama-3-8B step: phase breakdown + rocprofv3 kernel trace summary.
-set -e
+set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out

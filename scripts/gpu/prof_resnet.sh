@@ -1,6 +1,6 @@
 #!/bin/bash
 # ResNet-50 step: rocprofv3 kernel trace, steady-state window (last 3 steps).
-set -e
+set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out

@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 kernel stats + two SQ counter passes of the shipped MNIST step
 # (raw profiler output under /tmp: only the summary goes to gpurun_out)
-set -e
+set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"

@@ -5,7 +5,7 @@
 # the host all-reduce, schedule autotune, power-of-two step graphs, timing,
 # JSON).  Time-sliced processes on one GPU: NOT a scaling measurement, hence
 # the long barrier timeout.
-set -e
+set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out

@@ -2,7 +2,7 @@
 # Round validation: smoke, every gpu test (kernel numerics first, the
 # multi-process operator tests last -- tests/conftest.py), default bench.
 # Usage: round_check.sh [--no-x]
-set -e
+set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out

@@ -2,7 +2,7 @@
 # MNIST step check: kernel / graph / DDP / xGMI GPU tests, the default bench,
 # the DDP-schedule step time at world size 1, and rocprofv3 kernel stats of
 # the one-process step (summary -> gpurun_out/step_kstats.txt).
-set -e
+set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"

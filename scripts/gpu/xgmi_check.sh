@@ -1,7 +1,7 @@
 #!/bin/bash
 # xGMI peer all-reduce protocol tests (W ranks sharing the one GPU), then the
 # 2-rank fused DDP test that now runs over it.
-set -e
+set -eo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out

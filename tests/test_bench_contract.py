@@ -66,3 +66,31 @@ def test_pto_bench_scaling_sweep_cpu():
     lines = [json.loads(ln) for ln in out.stdout.splitlines() if ln.startswith('{"metric"')]
     assert [d["n_gpus"] for d in lines] == [1, 2]
     assert "efficiency" in out.stdout and "100.0%" in out.stdout
+
+
+def test_bench_gpus_n_without_launcher_starts_n_ranks():
+    """`bench.py --gpus 2` with no torchrun must not measure one rank and
+    call it two: it starts 2 child ranks itself and reports n_gpus 2 with
+    the process group's own world size as evidence."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                                                            "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "2"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--gpus", "2", "--steps", "4", "--warmup", "1",
+           "--dataset-size", "640", "--no-latency"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [line for line in out.stdout.splitlines() if line.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    world = d["config"]["grad_allreduce"]
+    assert world["pg_world_size"] == 2 and len(world["ranks"]) == 2
+
+
+def test_bench_world_size_mismatch_is_an_error():
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(WORLD_SIZE="3")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--gpus", "2", "--steps", "2", "--warmup", "1"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert out.returncode == 2 and "WORLD_SIZE=3" in out.stderr
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]

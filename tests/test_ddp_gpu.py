@@ -36,9 +36,13 @@ def _worker(rank, world, port, q, comm):
         os.environ["PTO_DETERMINISTIC"] = "1"
     if comm == "host-allreduce":
         comm = "rccl"  # "not xGMI": with a gloo group the collective is gloo's host all-reduce
+    if comm.startswith("xgmi-fenced"):
+        os.environ["PTO_XGMI_PROTOCOL"] = "fenced"
+        comm = "xgmi"
+    race = comm == "auto-race"
     import torch.distributed as dist
 
-    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer, build_fused_trainer
 
     verify_fail = comm == "xgmi-verify-fail"
     if verify_fail:
@@ -54,8 +58,19 @@ def _worker(rank, world, port, q, comm):
     dist.init_process_group("gloo")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=N, seed=1, rank=rank, comm=comm)
-    if comm == "xgmi":
+    if race:
+        # the schedule race of build_fused_trainer: the verified xGMI step vs
+        # the collective step on the same data, both rolled back afterwards
+        tr = build_fused_trainer(dev, batch_size=64, dataset_size=N, seed=1, rank=rank, comm="auto")
+        res = tr.comm_info["schedule_autotune"]
+        assert res["correct"] and res["identical"] and res["param_rel_err"] < 1e-4, res
+        assert res["kept"] == tr.schedule and res["xgmi_step_us"] > 0 and res["rccl_step_us"] > 0, res
+        assert tr.steps_done == 0 and int(tr.batch_idx.item()) == 0
+    else:
+        tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=N, seed=1, rank=rank, comm=comm)
+    if race:
+        pass
+    elif comm == "xgmi":
         assert tr.comm_info["transport"] == "xgmi" and tr.graph_mode == "full" and tr.schedule == "ddp-xgmi"
     else:
         assert tr.comm_info["transport"] == "host-allreduce (gloo)" and tr.graph_mode == "split"
@@ -78,14 +93,16 @@ def _worker(rank, world, port, q, comm):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("comm", ["host-allreduce", "xgmi", "xgmi-det", "xgmi-verify-fail"])
+@pytest.mark.parametrize("comm", ["host-allreduce", "xgmi", "xgmi-fenced", "xgmi-det", "xgmi-verify-fail",
+                                  "auto-race"])
 def test_fused_ddp_two_ranks_matches_reference(comm):
     """host-allreduce: grads-only step, gloo all-reduce between split graphs,
     SGD launch; xgmi: one peer-memory all-reduce of the whole buffer with the
     SGD epilogue inside the whole-step graph (no optimizer launch); xgmi-det:
     the same with the deterministic backward; xgmi-verify-fail: the kernel
     fails autotune's verification and every rank falls back to the host
-    all-reduce."""
+    all-reduce; xgmi-fenced: the kernel's fenced visibility protocol;
+    auto-race: build_fused_trainer races the two schedules first."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

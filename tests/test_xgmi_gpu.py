@@ -36,7 +36,7 @@ def _fill(buf, rank, it):
     buf.copy_(torch.randn(buf.shape, generator=g, device=buf.device))
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, protocol="coherent"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         import torch.distributed as dist
@@ -49,7 +49,7 @@ def _worker(rank, world, port, q):
         n = 431_296  # MNIST flat gradient size (param_offsets, 64-aligned)
         split = 405_632  # fc bucket | conv bucket boundary
         buf = torch.zeros(n, device=dev)
-        ar = XgmiAllReduce(buf)
+        ar = XgmiAllReduce(buf, protocol=protocol)
         worst = 0.0
         side = torch.cuda.Stream(dev)
         for it in range(12):
@@ -96,12 +96,12 @@ def _worker(rank, world, port, q):
         raise
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_xgmi_allreduce_exact(world):
+@pytest.mark.parametrize("world,protocol", [(2, "coherent"), (4, "coherent"), (2, "fenced")])
+def test_xgmi_allreduce_exact(world, protocol):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, protocol)) for r in range(world)]
     for p in ps:
         p.start()
     res = collect(q, ps, world, timeout=110)
@@ -111,7 +111,7 @@ def test_xgmi_allreduce_exact(world):
         assert not isinstance(worst, str), worst
         assert worst < 1e-4, (rank, worst)
         assert same
-        assert tune["correct"], tune
+        assert tune["correct"] and tune["protocol"] == protocol, tune
     print("autotune", res[0][3])
     for p in ps:
         assert p.exitcode == 0
