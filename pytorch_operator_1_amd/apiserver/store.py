@@ -361,6 +361,7 @@ class Store:
             cur = self._objs.pop(key, None)
             if cur is None:
                 raise NotFound(resource, name)
+            self._created_unix.pop(cur["metadata"].get("uid"), None)
             cur["metadata"]["deletionTimestamp"] = now_rfc3339()
             rv = self._bump(cur)
             self._log("del", key, None, rv)

@@ -105,6 +105,7 @@ struct Proc {
   std::string gen_base;    // PTO_RESTART_GENERATION given at spawn
   bool held = false;       // restart owed, waiting for its group to drain
   double held_delay = 0;   // its own CrashLoopBackOff delay
+  bool wave_killed = false;  // stopped by a group wave it did not cause: not its own restart
 };
 
 // One restart wave at a time per group: `draining` from the first failing
@@ -473,11 +474,16 @@ struct Agent {
       // leader was reaped (its pid, hence the group id, was still reserved)
       bool restart = !p.stopping && (p.restart_policy == "Always" ||
                                      (p.restart_policy == "OnFailure" && p.exit_code != 0));
+      const bool innocent = p.wave_killed;  // killed by its group's wave, did not fail itself
+      p.wave_killed = false;
       if (restart) {
         p.last_exit_code = p.exit_code;
         p.last_finished_at = p.finished_at;
-        double delay = std::min(backoff_max, backoff_base * (double)(1 << std::min(p.restart_count, 16)));
-        p.restart_count += 1;
+        // one restart per wave, charged to the member that failed: the
+        // controller's backoffLimit sums restartCount over the job's pods
+        // (pastBackoffLimit), so a wave must not count once per member
+        double delay = innocent ? 0.0 : std::min(backoff_max, backoff_base * (double)(1 << std::min(p.restart_count, 16)));
+        if (!innocent) p.restart_count += 1;
         p.state = "waiting";
         p.reason = "CrashLoopBackOff";
         p.restart_at = mono_s() + delay;
@@ -510,11 +516,19 @@ struct Agent {
       Proc& q = kv.second;
       if (q.group != name || q.id == culprit || q.stopping) continue;
       if (q.state == "running" && q.pid > 0) {
+        q.wave_killed = true;
         ::kill(-q.pid, SIGKILL);
         ++killed;
       } else if (q.state == "waiting" && q.reason == "CrashLoopBackOff") {
         q.held = true;  // already owed a restart: it joins this wave
         q.held_delay = std::max(0.0, q.restart_at - mono_s());
+      } else if (q.state == "terminated" && q.exit_code == 0 && q.restart_policy == "OnFailure") {
+        // finished cleanly before a peer failed: the new wave needs every
+        // rank (WORLD_SIZE), so it rejoins -- without a restart of its own
+        q.state = "waiting";
+        q.reason = "CrashLoopBackOff";
+        q.held = true;
+        q.held_delay = 0;
       }
     }
     fprintf(stderr, "pto-node-agent: group %s: %s failed, restart wave %d (%d member(s) stopped)\n",

@@ -606,9 +606,13 @@ class Kubelet:
 
     def _start_containers(self, pod, rt):
         policy = pod.get("spec", {}).get("restartPolicy") or "Always"
+        # only replicas the node restarts in place form the restart group: a
+        # Never pod (ExitCode jobs: the controller recreates it under a new
+        # generation) must not be killed by an in-place wave, nor be waited for
+        in_place = policy in ("OnFailure", "Always")
         for c in pod["spec"].get("containers") or []:
             self._spawn(pod, rt, c, f"{rt.owner}/{c.get('name')}", restart_policy=policy,
-                        group=rt.job_key if self.group_restarts else "")
+                        group=rt.job_key if (self.group_restarts and in_place) else "")
 
     def _report(self, pod, rt, procs):
         statuses = []
