@@ -83,335 +83,33 @@
 #include <stdint.h>
 #include <string.h>
 
-#include "sgd_f32.h"
+#include "xgmi_ar.h"
 
 #define PTO_API extern "C" __attribute__((visibility("default")))
 
 namespace {
 
-constexpr int AR_MAX_RANKS = 8;
-// workgroups per launch: ceil(chunk / AR_THREADS) up to this cap, so every
-// thread handles ONE float4 per stage down to world 1-2 on MNIST's 1.7 MB
-constexpr int AR_MAX_BLOCKS = 256;
-constexpr int AR_CHANNELS = 2;
-constexpr int AR_THREADS = 512;
-constexpr int AR_MAX_REP = 256;  // gradient replicas folded before barrier 1 (launcher check)
-constexpr int AR_REP_CHUNK = 16;  // replica loads in flight at once
-// stage-1 sums of this rank's own chunk kept in registers for stage 2 (the
-// same thread handles element j of the chunk in both stages): iterations
-// beyond this re-read them from tmp
-constexpr int AR_CARRY = 4;
-constexpr long long AR_ONESHOT_MAX = 65536;  // floats (256 KB): one-shot path
-constexpr long long AR_TICKS_PER_MS = 100000LL;  // wall_clock64 runs at 100 MHz
+using namespace pto_ar;
+
 long long g_timeout_ticks = 500 * AR_TICKS_PER_MS;  // pto_ar_set_timeout_ms
 int g_protocol = 0;  // pto_ar_set_protocol: 0 coherent (write-through + sc0 sc1 loads), 1 fenced
 
-// buffer-instruction cache bits (aux operand): sc0 | sc1 = system scope
-constexpr int AUX_SYS = 1 | 16;
-
-// global (not flat) views of generic pointers: flag words and the local
-// parameter/momentum/gradient float4 groups
-using gu32 = __attribute__((address_space(1))) uint32_t;
-using v4f = __attribute__((ext_vector_type(4))) float;
-using gv4f = __attribute__((address_space(1))) v4f;
-__device__ __forceinline__ gu32* G(uint32_t* p) { return (gu32*)p; }
-__device__ __forceinline__ float4 gld4(const float* p) {
-  const v4f v = *(const gv4f*)p;
-  return float4{v.x, v.y, v.z, v.w};
-}
-__device__ __forceinline__ void gst4(float* p, float4 a) { *(gv4f*)p = v4f{a.x, a.y, a.z, a.w}; }
-
-struct ArPeers {
-  float* in[AR_MAX_RANKS];
-  float* tmp[AR_MAX_RANKS];
-  uint32_t* flags[AR_MAX_RANKS];
-};
-
-__host__ __device__ constexpr int flag_index(int chan, int phase, int block, int src) {
-  return ((chan * 2 + phase) * AR_MAX_BLOCKS + block) * AR_MAX_RANKS + src;
-}
-constexpr int AR_FLAG_WORDS = AR_CHANNELS * 2 * AR_MAX_BLOCKS * AR_MAX_RANKS;
-
-// float4 access to a buffer that peers read or write.  COHERENT: system-
-// scope buffer loads/stores (sc0 sc1), i.e. write-through stores and loads
-// that miss in L1/L2; otherwise plain accesses (the fenced protocol's
-// release/acquire provide visibility).  The descriptor covers `bytes` from
-// `base` (the launcher keeps every range below 2 GB).
-struct Buf {
-  __amdgpu_buffer_rsrc_t r;
-  float* p;
-};
-__device__ __forceinline__ Buf mkbuf(float* base, long long bytes) {
-  return Buf{__builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000), base};
-}
-template <bool COHERENT>
-__device__ __forceinline__ float4 ld4(const Buf& b, long long i4) {
-  if constexpr (COHERENT) {
-    auto v = __builtin_amdgcn_raw_buffer_load_b128(b.r, (int)(i4 * 16), 0, AUX_SYS);
-    return __builtin_bit_cast(float4, v);
-  } else {
-    return reinterpret_cast<const float4*>(b.p)[i4];
-  }
-}
-template <bool COHERENT>
-__device__ __forceinline__ void st4(const Buf& b, long long i4, float4 v) {
-  if constexpr (COHERENT) {
-    using u4 = __attribute__((ext_vector_type(4))) unsigned int;
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), b.r, (int)(i4 * 16), 0, AUX_SYS);
-  } else {
-    reinterpret_cast<float4*>(b.p)[i4] = v;
-  }
-}
-
-// Returns false (for every thread of the block) if the barrier failed: a
-// peer did not arrive within `timeout` ticks, or an earlier barrier of this
-// rank already failed (*err != 0).  s_fail is per phase, so a fast thread
-// resetting phase 1's word cannot race a slow thread still reading phase 0's.
-// FENCED: system release before the flag store, system acquire after the
-// wait; otherwise the drained write-through stores need no release and the
-// consumer's sc0 sc1 loads no acquire.
-template <bool FENCED>
-__device__ __forceinline__ bool block_barrier(const ArPeers* __restrict__ P, int chan, int phase, int rank, int world, uint32_t e,
-                                              long long timeout, int* err) {
-  __shared__ int s_fail[2];
-  const int t = threadIdx.x, b = blockIdx.x;
-  if (t == 0) s_fail[phase] = 0;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave: its stores acknowledged
-  __syncthreads();
-  if (t < world) {
-    bool dead = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-    if (!dead) {
-      if constexpr (FENCED) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back this XCD's L2
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __hip_atomic_store(G(P->flags[t] + flag_index(chan, phase, b, rank)), e, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-      gu32* f = G(P->flags[rank] + flag_index(chan, phase, b, t));
-      const long long t0 = wall_clock64();
-      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
-        if (wall_clock64() - t0 > timeout) {
-          atomicOr(err, 1 << phase);
-          dead = true;
-          break;
-        }
-        // another block (or an earlier launch) already gave up: stop now
-        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-          dead = true;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if constexpr (FENCED) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // invalidate L1/L2 before reading peer data
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler order only: no loads above the poll
-      }
-    }
-    if (dead) s_fail[phase] = 1;
-  }
-  __syncthreads();
-  return s_fail[phase] == 0;
-}
-
-// Fused optimizer epilogue of the all-reduce: own parameters/momentum (same
-// flat layout as the gradient buffer), hyper-parameters, zero range, and an
-// optional batch cursor advanced once the update is done.
-struct ArSgd {
-  float* p;
-  float* m;
-  SgdArgs a;
-  long long zero_from;  // float index: own gradient zeroed from here on
-  long long* bidx;      // nullptr: no cursor
-  long long nbatches;
-  // optional gradient replicas of the float range [rep_from, rep_from +
-  // rep_stride) (k_bwd_all's conv1 replicas, multi-GPU step): replica r >= 1
-  // at rep + (r-1)*rep_stride.  Folded into the local gradient (and zeroed)
-  // by the workgroup that owns the element, BEFORE barrier 1, so every peer
-  // reads folded values.
-  float* rep;
-  int nrep, rep_stride;
-  long long rep_from;
-};
-
-// Fold the local replicas into float4 element i4 (float offset 4*i4 from the
-// buffer base) of the local gradient, if it lies in the replicated range.
-// Every replica load is issued before the first add; the folded value is
-// stored through `g` (write-through under the coherent protocol: peers read
-// it).
-template <bool COHERENT>
-__device__ __forceinline__ void fold_rep(const ArSgd& f, const Buf& g, long long off, long long i4) {
-  const long long fi = off + 4 * i4;  // float index in the whole buffer (rep_from's frame)
-  if (!f.rep || f.nrep <= 1 || fi < f.rep_from || fi >= f.rep_from + f.rep_stride) return;
-  const long long k = fi - f.rep_from;
-  float4 a = gld4(g.p + 4 * i4);
-  for (int r0 = 0; r0 < f.nrep - 1; r0 += AR_REP_CHUNK) {  // replica order
-    float4 v[AR_REP_CHUNK];
-#pragma unroll
-    for (int r = 0; r < AR_REP_CHUNK; ++r)
-      v[r] = gld4(f.rep + (long long)min(r0 + r, f.nrep - 2) * f.rep_stride + k);
-#pragma unroll
-    for (int r = 0; r < AR_REP_CHUNK; ++r) {
-      if (r0 + r >= f.nrep - 1) break;
-      a.x += v[r].x; a.y += v[r].y; a.z += v[r].z; a.w += v[r].w;
-      gst4(f.rep + (long long)(r0 + r) * f.rep_stride + k, float4{0.f, 0.f, 0.f, 0.f});
-    }
-  }
-  st4<COHERENT>(g, i4, a);
-}
-
-// SGD on float4 group i (float index) of the local parameters/momentum.
-__device__ __forceinline__ void sgd4(const ArSgd& f, long long i, float4 g, float4& pv, float4& mv, float lr) {
-  sgd_elem(pv.x, g.x, mv.x, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
-  sgd_elem(pv.y, g.y, mv.y, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
-  sgd_elem(pv.z, g.z, mv.z, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
-  sgd_elem(pv.w, g.w, mv.w, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
-  gst4(f.p + i, pv);
-  gst4(f.m + i, mv);
-}
-
-__device__ __forceinline__ float4 add4(float4 a, float4 b) { return float4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
-
-// n4 float4 elements starting at float offset `off` of every rank's buffers.
 template <bool SGD, bool FENCED>
 __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce(const ArPeers* __restrict__ peers, long long off,
                                                                long long n4, int rank, int world, int chan,
                                                                uint32_t* __restrict__ epochs, int* err, long long timeout,
                                                                ArSgd f) {
-  constexpr bool CO = !FENCED;
-  __shared__ uint32_t s_epoch;
-  const ArPeers* __restrict__ P = peers;
-  if (threadIdx.x == 0) s_epoch = epochs[chan * AR_MAX_BLOCKS + blockIdx.x] + 1;
-  __syncthreads();
-  const uint32_t e = s_epoch;
-  if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blockIdx.x] = e;
-  const long long cs = (n4 + world - 1) / world;  // chunk length (float4)
-  const long long stride = (long long)gridDim.x * AR_THREADS;
-  const long long j0 = (long long)blockIdx.x * AR_THREADS + threadIdx.x;
-  const long long bytes = n4 * 16;
-  float* const my_in = P->in[rank];
-  if (f.rep && f.nrep > 1 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-    // the elements this workgroup's peers will read: the same sub-range of every chunk
-    const Buf g = mkbuf(my_in + off, bytes);
-    for (int q = 0; q < world; ++q)
-      for (long long j = j0; j < cs && q * cs + j < n4; j += stride) fold_rep<CO>(f, g, off, q * cs + j);
-  }
-
-  if (!block_barrier<FENCED>(P, chan, 0, rank, world, e, timeout, err)) return;
-  // stage 1: reduce my chunk over all ranks (rank order 0..W-1 everywhere);
-  // the first AR_CARRY iterations' sums stay in registers for stage 2, tmp
-  // gets them only if a peer (or a later iteration) reads them
-  float4 own[AR_CARRY];
-  {
-    const long long c0 = (long long)rank * cs, c1 = min(n4, c0 + cs);
-    int it = 0;
-    for (long long i = c0 + j0; i < c1; i += stride, ++it) {
-      float4 v[AR_MAX_RANKS];
-#pragma unroll
-      for (int q = 0; q < AR_MAX_RANKS; ++q)
-        if (q < world) v[q] = ld4<CO>(mkbuf(P->in[q] + off, bytes), i);
-      float4 a = v[0];
-#pragma unroll
-      for (int q = 1; q < AR_MAX_RANKS; ++q)
-        if (q < world) a = add4(a, v[q]);
-#pragma unroll
-      for (int c = 0; c < AR_CARRY; ++c)
-        if (c == it) own[c] = a;
-      if (world > 1 || it >= AR_CARRY) st4<CO>(mkbuf(P->tmp[rank] + off, bytes), i, a);
-    }
-  }
-  const float lr = SGD ? *f.a.lr : 0.f;
-  if (!block_barrier<FENCED>(P, chan, 1, rank, world, e, timeout, err)) return;
-  // stage 2: gather every chunk into my input (or: update my parameters)
-  int it = 0;
-  for (long long j = j0; j < cs; j += stride, ++it) {
-    float4 v[AR_MAX_RANKS];
-#pragma unroll
-    for (int q = 0; q < AR_MAX_RANKS; ++q)
-      if (q < world && (long long)q * cs + j < n4) {
-        if (q == rank && it < AR_CARRY) {
-#pragma unroll
-          for (int c = 0; c < AR_CARRY; ++c)
-            if (c == it) v[q] = own[c];
-        } else {
-          v[q] = ld4<CO>(mkbuf(P->tmp[q] + off, bytes), q * cs + j);
-        }
-      }
-#pragma unroll
-    for (int q = 0; q < AR_MAX_RANKS; ++q)
-      if (q < world && (long long)q * cs + j < n4) {
-        if constexpr (SGD) {
-          const long long i = off + 4 * (q * cs + j);
-          float4 pv = gld4(f.p + i);
-          float4 mv = gld4(f.m + i);
-          sgd4(f, i, v[q], pv, mv, lr);
-          if (i >= f.zero_from) gst4(my_in + i, float4{0.f, 0.f, 0.f, 0.f});
-        } else {
-          gst4(my_in + off + 4 * (q * cs + j), v[q]);
-        }
-      }
-  }
-  if (SGD && f.bidx && blockIdx.x == 0 && threadIdx.x == 0) *f.bidx = (*f.bidx + 1) % f.nbatches;
+  ar_twostage<SGD, FENCED, AR_THREADS>(peers, off, n4, rank, world, chan, epochs, err, timeout, f, blockIdx.x,
+                                       gridDim.x);
 }
 
-// One-shot variant: n4 <= gridDim.x * AR_THREADS (one float4 per thread).
 template <bool SGD, bool FENCED>
 __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_1shot(const ArPeers* __restrict__ peers,
                                                                      long long off, long long n4, int rank,
                                                                      int world, int chan,
                                                                      uint32_t* __restrict__ epochs, int* err,
                                                                      long long timeout, ArSgd f) {
-  constexpr bool CO = !FENCED;
-  __shared__ uint32_t s_epoch;
-  const ArPeers* __restrict__ P = peers;
-  if (threadIdx.x == 0) s_epoch = epochs[chan * AR_MAX_BLOCKS + blockIdx.x] + 1;
-  __syncthreads();
-  const uint32_t e = s_epoch;
-  if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blockIdx.x] = e;
-  const long long i = (long long)blockIdx.x * AR_THREADS + threadIdx.x;
-  const bool act = i < n4;
-  const long long bytes = n4 * 16;
-  float* const my_in = P->in[rank];
-  if (act && f.rep && f.nrep > 1 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-    fold_rep<CO>(f, mkbuf(my_in + off, bytes), off, i);
-  if (!block_barrier<FENCED>(P, chan, 0, rank, world, e, timeout, err)) return;
-  float4 a = {0.f, 0.f, 0.f, 0.f};
-  if (act) {
-    float4 v[AR_MAX_RANKS];
-#pragma unroll
-    for (int q = 0; q < AR_MAX_RANKS; ++q)
-      if (q < world) v[q] = ld4<CO>(mkbuf(P->in[q] + off, bytes), i);
-    a = v[0];
-#pragma unroll
-    for (int q = 1; q < AR_MAX_RANKS; ++q)
-      if (q < world) a = add4(a, v[q]);
-  }
-  // every peer is done reading my input (on failure: nothing is written)
-  if (!block_barrier<FENCED>(P, chan, 1, rank, world, e, timeout, err)) return;
-  if (act) {
-    if constexpr (SGD) {
-      const float lr = *f.a.lr;
-      const long long j = off + 4 * i;
-      float4 pv = gld4(f.p + j);
-      float4 mv = gld4(f.m + j);
-      sgd4(f, j, a, pv, mv, lr);
-      if (j >= f.zero_from) gst4(my_in + j, float4{0.f, 0.f, 0.f, 0.f});
-    } else {
-      gst4(my_in + off + 4 * i, a);
-    }
-  }
-  if (SGD && f.bidx && blockIdx.x == 0 && threadIdx.x == 0) *f.bidx = (*f.bidx + 1) % f.nbatches;
-}
-
-// Workgroups used for n floats (identical on every rank: derived from n, W).
-int blocks_for(long long n, int world) {
-  if (n <= AR_ONESHOT_MAX) return (int)((n / 4 + AR_THREADS - 1) / AR_THREADS);
-  const long long cs = ((n / 4) + world - 1) / world;
-  long long b = (cs + AR_THREADS - 1) / AR_THREADS;
-  if (b < 1) b = 1;
-  if (b > AR_MAX_BLOCKS) b = AR_MAX_BLOCKS;
-  return (int)b;
+  ar_oneshot<SGD, FENCED, AR_THREADS>(peers, off, n4, rank, world, chan, epochs, err, timeout, f, blockIdx.x);
 }
 
 template <bool SGD>
@@ -464,6 +162,7 @@ PTO_API int pto_ar_set_protocol(int p) {
   return 0;
 }
 PTO_API int pto_ar_get_protocol() { return g_protocol; }
+PTO_API long long pto_ar_timeout_ticks() { return g_timeout_ticks; }
 
 // Flags: uncached device memory, zeroed.
 PTO_API int pto_ar_alloc_flags(void** out) {

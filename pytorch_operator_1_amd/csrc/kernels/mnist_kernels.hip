@@ -33,6 +33,7 @@
 // the dataset without any copy kernels.
 #include "mfma_f32.h"
 #include "sgd_f32.h"
+#include "xgmi_ar.h"
 
 // Phase timestamps for the timing probes under tools/probes (which define
 // PTO_STAMP before including this file); nothing in the shipped library.
@@ -295,14 +296,35 @@ __global__ __launch_bounds__(256) void k_conv2_fwd(const float* __restrict__ a1p
 //    LDS, so each SIMD interleaves independent MFMA chains.
 //  * lazy conv1 update (one-process schedule, LazyConv1), the image copy
 //    for the backward (xout) and the conv2.weight snapshot (w2out).
+//  * ARM != 0 (overlapped multi-GPU step, fused_step.py "ddp-xgmi"): blocks
+//    >= 4B are the PREVIOUS step's fc-gradient all-reduce + SGD epilogue
+//    (xgmi_ar.h two-stage, protocol ARM-1), which nothing here reads.  The
+//    kernel is capped at 64 VGPRs (8 waves per SIMD) so an all-reduce block
+//    fits on a CU next to a conv block (61 KB of LDS each) and the exchange
+//    runs concurrently with the convolutions instead of after them.
+struct ArRole {
+  const pto_ar::ArPeers* peers;
+  long long off, n4;
+  int rank, world, chan, nblk;
+  uint32_t* epochs;
+  int* err;
+  long long timeout;
+  pto_ar::ArSgd f;
+};
 constexpr int W1PLD = 52;  // a channel pair's 25 interleaved taps, padded to whole float4
-template <int NTH>
-__global__ __launch_bounds__(NTH) void k_conv12_fwd2_t(const float* __restrict__ x, const float* __restrict__ w1,
-                                                     const float* __restrict__ b1, const float* __restrict__ w2,
-                                                     const float* __restrict__ b2, float* __restrict__ a1p,
-                                                     uint8_t* __restrict__ code1, float* __restrict__ a2p,
-                                                     uint8_t* __restrict__ code2, int B,
-                                                     const long long* __restrict__ bidx, LazyConv1 lz) {
+template <int NTH, int ARM = 0>
+__global__ __launch_bounds__(NTH, ARM ? 2 * NTH / 256 : 1) void k_conv12_fwd2_t(
+    const float* __restrict__ x, const float* __restrict__ w1, const float* __restrict__ b1,
+    const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ a1p, uint8_t* __restrict__ code1,
+    float* __restrict__ a2p, uint8_t* __restrict__ code2, int B, const long long* __restrict__ bidx, LazyConv1 lz,
+    ArRole ar) {
+  if constexpr (ARM != 0) {
+    if ((int)blockIdx.x >= 4 * B) {
+      pto_ar::ar_twostage<true, ARM == 2, NTH, true>(ar.peers, ar.off, ar.n4, ar.rank, ar.world, ar.chan, ar.epochs,
+                                                  ar.err, ar.timeout, ar.f, (int)blockIdx.x - 4 * B, ar.nblk);
+      return;
+    }
+  }
   __shared__ float ws[16 * WS_LD];
   __shared__ __attribute__((aligned(16))) float in_s[A1P];
   __shared__ __attribute__((aligned(16))) float xs[784];
@@ -1960,8 +1982,56 @@ PTO_API int pto_conv12_fwd_lazy_x(const float* x, const float* w1, const float* 
   if (nrep < 1 || nrep > C1_MAXREP || (nrep > 1 && !rep) || (pending && (!g1f || !m1f || !lr))) return -1;
   LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off, xout, w2out, rep, nrep,
                rep_stride};
-  hipLaunchKernelGGL(k_conv12_fwd2_t<1024>, dim3(B * 4), dim3(1024), 0, s, x, w1, b1, w2, b2, a1p, code1, a2p, code2,
-                     B, bidx, lz);
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv12_fwd2_t<1024, 0>), dim3(B * 4), dim3(1024), 0, s, x, w1, b1, w2, b2, a1p,
+                     code1, a2p, code2, B, bidx, lz, ArRole{});
+  LAUNCH_CHECK();
+}
+
+extern "C" long long pto_ar_timeout_ticks();
+
+// F12 (plain forward: no lazy conv1 update) + the all-reduce of float range
+// [off, off + n) of the registered gradient buffers with the SGD epilogue on
+// p/m (zero_from: local gradient zeroed from there on), as extra workgroups
+// of the same launch (ArRole).  protocol: 0 coherent, 1 fenced -- the one
+// the XgmiAllReduce instance of `peers` uses.
+PTO_API int pto_conv12_fwd_ar(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
+                              float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B, const long long* bidx,
+                              float* xout, const void* peers, long long off, long long n, int rank, int world,
+                              int chan, void* epochs, void* err, int protocol, float* p, float* m, const float* lr,
+                              float mom, float wd, float gscale, int nesterov, long long zero_from, hipStream_t s) {
+  using namespace pto_ar;
+  if (n <= AR_ONESHOT_MAX || n % 4 || off % 4 || n > (1LL << 29) || world < 1 || world > AR_MAX_RANKS || chan < 0 ||
+      chan >= AR_CHANNELS || rank < 0 || rank >= world || !p || !m || !lr || !peers || protocol < 0 || protocol > 1 ||
+      ((((uintptr_t)p) | ((uintptr_t)m)) & 15))
+    return -1;
+  LazyConv1 lz{nullptr, nullptr, nullptr, sgd_args(lr, mom, wd, gscale, nesterov), 0, xout, nullptr, nullptr, 1, 0};
+  ArRole ar;
+  ar.peers = reinterpret_cast<const ArPeers*>(peers);
+  ar.off = off;
+  ar.n4 = n / 4;
+  ar.rank = rank;
+  ar.world = world;
+  ar.chan = chan;
+  ar.nblk = blocks_for(n, world, 1024);
+  ar.epochs = reinterpret_cast<uint32_t*>(epochs);
+  ar.err = reinterpret_cast<int*>(err);
+  ar.timeout = pto_ar_timeout_ticks();
+  ar.f = ArSgd{};
+  ar.f.p = p;
+  ar.f.m = m;
+  ar.f.a = sgd_args(lr, mom, wd, gscale, nesterov);
+  ar.f.zero_from = zero_from;
+  ar.f.bidx = nullptr;
+  ar.f.nbatches = 1;
+  ar.f.rep = nullptr;
+  ar.f.nrep = 1;
+  const dim3 g((unsigned)(B * 4 + ar.nblk));
+  if (protocol)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv12_fwd2_t<1024, 2>), g, dim3(1024), 0, s, x, w1, b1, w2, b2, a1p, code1,
+                       a2p, code2, B, bidx, lz, ar);
+  else
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv12_fwd2_t<1024, 1>), g, dim3(1024), 0, s, x, w1, b1, w2, b2, a1p, code1,
+                       a2p, code2, B, bidx, lz, ar);
   LAUNCH_CHECK();
 }
 

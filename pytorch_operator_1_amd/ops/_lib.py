@@ -33,6 +33,8 @@ HIP_SOURCES = ("kernels/mnist_kernels.hip", "kernels/common_kernels.hip", "kerne
                "comm/xgmi_allreduce.hip")
 
 _lock = threading.Lock()
+# launchers return an int hipError; these few return something else
+_RESTYPES = {"pto_ar_timeout_ticks": ctypes.c_longlong}
 _lib = None
 
 
@@ -70,7 +72,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
                 return LIB_PATH
     tmp = LIB_PATH + f".tmp{os.getpid()}"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(CSRC, "kernels"), "-o", tmp] + _sources()
+           "-I", os.path.join(CSRC, "kernels"), "-I", os.path.join(CSRC, "comm"), "-o", tmp] + _sources()
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -97,6 +99,8 @@ _SIGS = {
     "pto_conv1_bwd_data": [_P, _P, _P, _P, _I, _P],
     # fused-optimizer schedule of the single-process MNIST step
     "pto_conv12_fwd_lazy_x": [_P] * 9 + [_I, _P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _P, _P, _P, _I, _I, _P],
+    "pto_conv12_fwd_ar": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _L, _L, _I, _I, _I, _P, _P, _I, _P, _P,
+                          _P, _F, _F, _F, _I, _L, _P],
     "pto_bwd_all": [_P] * 13 + [_L] * 8 + [_P, _P, _L, _P, _I, _P, _F, _F, _F, _I, _P, _I, _I, _I, _P, _P],
     "pto_conv1_commit": [_P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _P, _I, _I, _P],
     "pto_mnist_ddp_sgd": [_P, _P, _P, _I, _I, _I, _P, _I, _P, _F, _F, _F, _I, _P, _L, _P],
@@ -150,6 +154,7 @@ _SIGS = {
     "pto_ar_close_ipc_handle": [_P],
     "pto_ar_blocks": [_L, _I],
     "pto_ar_allreduce": [_P, _L, _L, _I, _I, _I, _P, _P, _P],
+    "pto_ar_timeout_ticks": [],
     "pto_ar_allreduce_sgd": [_P, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _F, _I, _L, _P, _L, _P, _I, _I, _L,
                              _P],
 }
@@ -180,7 +185,7 @@ def lib():
             if fn is None:
                 continue
             fn.argtypes = args
-            fn.restype = ctypes.c_int
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
         _lib = L
         return _lib
 

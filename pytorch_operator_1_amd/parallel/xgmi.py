@@ -175,6 +175,22 @@ class XgmiAllReduce:
                                                    n_replicas if rep else 1, rep_stride, rep_from, s),
                    "xgmi_allreduce_sgd")
 
+    def role_args(self, offset: int, n: int, chan: int, params: torch.Tensor, mom: torch.Tensor,
+                  lr_dev: torch.Tensor, momentum: float, weight_decay: float, gscale: float, nesterov: bool,
+                  zero_from: int) -> tuple:
+        """Arguments of an all-reduce-with-SGD run as extra workgroups of
+        another launch (``pto_conv12_fwd_ar``): peers table, range, rank,
+        world, channel, epochs, error word, protocol, the update's buffers
+        and hyper-parameters."""
+        if n % 4 or offset % 4 or offset + n > self.buf.numel():
+            raise ValueError("XgmiAllReduce: bad range for an all-reduce role")
+        for t in (params, mom):
+            if t.dtype != torch.float32 or t.numel() != self.buf.numel() or t.device != self.device:
+                raise ValueError("XgmiAllReduce: params/momentum must match the gradient buffer")
+        return (self.peers.data_ptr(), offset, n, self.rank, self.world, chan, self.epochs.data_ptr(),
+                self.err.data_ptr(), PROTOCOLS[self.protocol], params.data_ptr(), mom.data_ptr(), lr_dev.data_ptr(),
+                momentum, weight_decay, gscale, int(nesterov), zero_from)
+
     def error_word(self) -> int:
         """Device error word (synchronises with the current stream)."""
         return int(self.err.item())

@@ -76,11 +76,14 @@ def _pg_ready() -> bool:
 class FusedMnistTrainer:
     def __init__(self, device, batch_size=64, lr=0.01, momentum=0.5, dataset_size=60000, seed=1, rank=0,
                  weight_decay=0.0, nesterov=False, graph: str | None = None, comm: str | None = None,
-                 data=None, target=None, unroll: int | None = None, force_ddp: bool = False):
+                 data=None, target=None, unroll: int | None = None, force_ddp: bool = False,
+                 overlap: bool | None = None):
         """``graph``: "full" (whole steps in graphs; default), "split"
         (collectives between graphs) or "none" (eager launches).
         ``force_ddp``: the grads-only + all-reduce + SGD-launch schedule at
-        world size 1 (the DDP code path in one process)."""
+        world size 1 (the DDP code path in one process).  ``overlap``
+        (ddp-xgmi; default on): the fc part of the exchange runs as extra
+        workgroups of the next step's F12 launch."""
         assert device.type == "cuda", "FusedMnistTrainer runs on a HIP device"
         self.L = _lib.lib()
         self.device = device
@@ -168,6 +171,18 @@ class FusedMnistTrainer:
         self.c1_nrep = B if self.deterministic else C1_REPLICAS
         self.c1_stride = self.numel - self._c1
         self.schedule = "fused-opt" if not self.ddp else ("ddp-xgmi" if self._xgmi is not None else "ddp-rccl")
+        # ddp-xgmi overlap: step k's all-reduce is split at the fc | conv
+        # boundary.  The conv part (100 KB, conv1 replicas folded, cursor
+        # advance) runs right after the backward (one-shot kernel, channel
+        # 0): the next F12 reads those weights.  The fc part (1.6 MB, 94% of
+        # the bytes) runs as extra workgroups of step k+1's F12 launch
+        # (channel 1), which reads no fc parameter, so the exchange overlaps
+        # the convolutions; F3 of step k+1 is its first reader.  The last
+        # step of every graph / eager step closes with a stand-alone fc
+        # all-reduce, so every run() leaves complete updates.
+        self.overlap = self._xgmi is not None and (True if overlap is None else bool(overlap))
+        if self.overlap:
+            self.comm_info["overlap"] = "fc all-reduce under the next step's F12 (same launch)"
         nrep_tail = max(1, self.c1_nrep - 1) * self.c1_stride
         if self.schedule == "ddp-rccl":
             self._ar_buf = torch.zeros(total + nrep_tail, **f32)
@@ -235,9 +250,11 @@ class FusedMnistTrainer:
         timing probes under tools/."""
         self._forward(only=which)
 
-    def _forward(self, only: int | None = None):
+    def _forward(self, only: int | None = None, fc_owed: bool = False):
         """F12, F3, F4dx.  Fused-opt: F12 applies conv1's owed update on the
-        fly (lazy) and F4dx commits it; F4dx's d(a2p) feeds the backward."""
+        fly (lazy) and F4dx commits it; F4dx's d(a2p) feeds the backward.
+        ``fc_owed`` (ddp-xgmi overlap): F12 also runs the previous step's fc
+        all-reduce + SGD as extra workgroups."""
         L, s, B, P = self.L, self._s(), self.B, self._p
         c = _lib.check
         bi = self.batch_idx.data_ptr()
@@ -252,7 +269,12 @@ class FusedMnistTrainer:
             rep = (None, 1, 0)
             lazy = (None, None, 0, None, None, 0.0, 0.0, 1.0, 0)
             w2out, pending = None, None
-        if only in (None, 0):
+        if only in (None, 0) and fc_owed:
+            c(L.pto_conv12_fwd_ar(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
+                                  P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
+                                  self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi,
+                                  self.xcur.data_ptr(), *self._fc_role_args(), s), "conv12_fwd_ar")
+        elif only in (None, 0):
             c(L.pto_conv12_fwd_lazy_x(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
                                       P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
                                       self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi, *lazy,
@@ -281,9 +303,30 @@ class FusedMnistTrainer:
             self.c1rep.data_ptr(), self.c1_nrep, self.c1_stride, int(go), _lib.ptr(self.wpart), self._s()),
             "bwd_all")
 
+    def _fc_role_args(self):
+        lr, mom, wd, gs, nes = self._opt_args()
+        return self._xgmi.role_args(0, self._split, 1, self._params, self.mom, self.lr_dev, mom, wd, gs, bool(nes),
+                                    self.numel)
+
+    def _close_fc(self):
+        """ddp-xgmi overlap: the owed fc all-reduce + SGD as a launch of its
+        own (end of a graph / eager step)."""
+        lr, mom, wd, gs, nes = self._opt_args()
+        self._xgmi.allreduce_sgd_(0, self._split, params=self._params, mom=self.mom, lr_dev=self.lr_dev, momentum=mom,
+                                  weight_decay=wd, gscale=gs, nesterov=bool(nes), zero_from=self.numel, chan=1)
+
     def _allreduce_update(self):
         """DDP: gradient all-reduce + SGD (+ zeroing of the accumulated conv
-        grads and the cursor advance)."""
+        grads and the cursor advance).  ddp-xgmi overlap: the conv range
+        only (the fc range is owed to the next F12 / the closing launch)."""
+        if self._xgmi is not None and self.overlap:
+            lr, mom, wd, gs, nes = self._opt_args()
+            self._xgmi.allreduce_sgd_(self._split, self.numel - self._split, params=self._params, mom=self.mom,
+                                      lr_dev=self.lr_dev, momentum=mom, weight_decay=wd, gscale=gs,
+                                      nesterov=bool(nes), zero_from=self._split, cursor=self.batch_idx,
+                                      n_batches=self.n_batches, replicas=self.c1rep, n_replicas=self.c1_nrep,
+                                      rep_from=self._c1, chan=0)
+            return
         if self._xgmi is not None:
             lr, mom, wd, gs, nes = self._opt_args()
             self._xgmi.allreduce_sgd_(0, self.numel, params=self._params, mom=self.mom, lr_dev=self.lr_dev,
@@ -301,11 +344,16 @@ class FusedMnistTrainer:
                                             *self._opt_args(), self.batch_idx.data_ptr(), self.n_batches, self._s()),
                    "ddp_sgd")
 
-    def _eager_step(self):
-        self._forward()
+    def _eager_step(self, first: bool = True, last: bool = True):
+        """One step's launches.  ``first``/``last``: its place in a captured
+        run (ddp-xgmi overlap: only a non-first step's F12 carries the
+        previous step's fc all-reduce; the last step closes it)."""
+        self._forward(fc_owed=self.overlap and not first)
         self._backward()
         if self.ddp:
             self._allreduce_update()
+            if self.overlap and last:
+                self._close_fc()
 
     def _commit_launch(self):
         _lib.check(self.L.pto_conv1_commit(self._params[self._c1:].data_ptr(), self.grads[self._c1:].data_ptr(),
@@ -390,8 +438,8 @@ class FusedMnistTrainer:
         for k in self._graph_sizes():
             gk = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gk, capture_error_mode=_CAPTURE_MODE):
-                for _ in range(k):
-                    self._eager_step()
+                for i in range(k):
+                    self._eager_step(first=i == 0, last=i == k - 1)
             self._graph_pow[k] = gk
         # fused-opt: a "closing" graph per run length 1..unroll whose last
         # node commits the owed conv1 update, so run(n) needs no flush after

@@ -1,0 +1,70 @@
+"""Long-horizon parity of the SHIPPED configuration:
+one epoch -- 937 steps of batch 64 -- of the fused trainer exactly as
+bench.py runs it (HIP graphs of 32 steps, closing graphs, conv1's lazy
+update) against the stock-PyTorch trainer (``EagerMnistTrainer``: nn.Module
++ autograd + torch.optim.SGD, the behavioural twin of the reference's
+``examples/mnist/mnist.py:35-65``) from the same initialisation on the same
+batches.  Compared: the loss every 100 steps, and loss/accuracy of the
+reference's test pass on a held-out set.
+
+The synthetic set here is made harder than ``synthetic_mnist`` (a faint
+class blob under strong noise) so the epoch ends short of 100% accuracy and
+the accuracy comparison means something.  Parity with the reference's
+published 0.9664 on real MNIST stays unpinned: no dataset exists here."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def hard_mnist(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    labels = torch.randint(0, 10, (n,), generator=g)
+    imgs = torch.rand((n, 1, 28, 28), generator=g)
+    ys = torch.tensor([2, 2, 2, 11, 11, 11, 20, 20, 20, 11])
+    xs = torch.tensor([2, 11, 20, 2, 11, 20, 2, 11, 20, 8])
+    r = torch.arange(28)
+    y0, x0 = ys[labels][:, None], xs[labels][:, None]
+    rows = (r >= y0) & (r < y0 + 6)
+    cols = (r >= x0) & (r < x0 + 6)
+    imgs[:, 0].add_((rows[:, :, None] & cols[:, None, :]).float(), alpha=0.12)
+    imgs = (imgs.clamp_(0, 1) - 0.1307) / 0.3081
+    return imgs.to(DEV), labels.to(DEV)
+
+
+def test_one_epoch_fused_matches_stock_pytorch():
+    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+    from pytorch_operator_1_amd.train.runner import EagerMnistTrainer
+
+    dev = torch.device(DEV)
+    x, y = hard_mnist(60000, seed=11)
+    xt, yt = hard_mnist(10000, seed=12)
+    fused = FusedMnistTrainer(dev, batch_size=64, data=x, target=y, seed=1)
+    assert fused.schedule == "fused-opt" and fused.unroll == 32 and fused.graph_mode == "full"
+    eager = EagerMnistTrainer(dev, batch_size=64, data=x, target=y, seed=1)
+    assert fused.n_batches == eager.n_batches == 937
+    rows = []
+    for chunk in [100] * 9 + [37]:
+        fused.run(chunk)
+        for _ in range(chunk):
+            le = eager.step()
+        rows.append((fused.last_loss(), float(le)))
+    assert fused.steps_done == 937 and int(fused.batch_idx.item()) == 0  # one full epoch, cursor wrapped
+    for i, (lf, le) in enumerate(rows):
+        assert abs(lf - le) <= 0.02 * le + 2e-3, (i, lf, le, rows)
+    assert rows[-1][1] < 0.7 * rows[0][1], rows  # the epoch did learn
+
+    loss_f, acc_f = fused.evaluate(xt, yt)
+    m = eager.module.eval()
+    with torch.no_grad():
+        out = torch.cat([m(xt[i:i + 1000]) for i in range(0, 10000, 1000)])
+        loss_e = F.nll_loss(out, yt, reduction="sum").item() / 10000
+        acc_e = (out.argmax(1) == yt).float().mean().item()
+    print(f"per-100-step loss (fused, stock): {rows}; test loss {loss_f:.4f}/{loss_e:.4f} "
+          f"accuracy {acc_f:.4f}/{acc_e:.4f}")
+    assert 0.3 < acc_e < 0.9999, acc_e  # short of perfect: the comparison is informative
+    assert abs(acc_f - acc_e) <= 0.01, (acc_f, acc_e)
+    assert abs(loss_f - loss_e) <= 0.02 * loss_e + 1e-3, (loss_f, loss_e)

@@ -27,7 +27,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--only", choices=["ddp", "xgmi", "single"], default=None, help="time one schedule (for rocprof)")
+    ap.add_argument("--only", choices=["ddp", "xgmi", "xgmi_noov", "single"], default=None,
+                    help="time one schedule (for rocprof)")
     a = ap.parse_args()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -43,8 +44,11 @@ def main():
     # ddp: grads-only step + RCCL all-reduce of the 1-rank group + SGD launch;
     # xgmi: grads-only step + the xGMI all-reduce kernel with its SGD
     # epilogue over one rank (the N>1 step's launches minus the peer reads)
+    # xgmi: the fc part of the exchange inside the next step's F12 launch
+    # (overlap, the default); xgmi_noov: one whole-buffer all-reduce per step
     runs = (("ddp_step_us", "ddp", dict(force_ddp=True, comm="rccl")),
             ("ddp_xgmi_step_us", "xgmi", dict(force_ddp=True, comm="xgmi")),
+            ("ddp_xgmi_noov_step_us", "xgmi_noov", dict(force_ddp=True, comm="xgmi", overlap=False)),
             ("single_gpu_step_us", "single", {}))
     for key, tag, kw in runs:
         if a.only and a.only != tag:
