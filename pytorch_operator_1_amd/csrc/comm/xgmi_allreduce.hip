@@ -112,6 +112,24 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_1shot(const ArPee
   ar_oneshot<SGD, FENCED, AR_THREADS>(peers, off, n4, rank, world, chan, epochs, err, timeout, f, blockIdx.x);
 }
 
+template <bool FENCED>
+__global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_bf16(const ArPeers* __restrict__ peers, long long off,
+                                                                    long long nv, int rank, int world, int chan,
+                                                                    uint32_t* __restrict__ epochs, int* err,
+                                                                    long long timeout) {
+  ar_twostage_bf16<FENCED, AR_THREADS>(peers, off, nv, rank, world, chan, epochs, err, timeout, blockIdx.x,
+                                       gridDim.x);
+}
+
+template <bool FENCED>
+__global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_bf16_1shot(const ArPeers* __restrict__ peers,
+                                                                          long long off, long long nv, int rank,
+                                                                          int world, int chan,
+                                                                          uint32_t* __restrict__ epochs, int* err,
+                                                                          long long timeout) {
+  ar_oneshot_bf16<FENCED, AR_THREADS>(peers, off, nv, rank, world, chan, epochs, err, timeout, blockIdx.x);
+}
+
 template <bool SGD>
 int launch(const void* peers, long long off, long long n, int rank, int world, int chan, void* epochs, void* err,
            const ArSgd& f, hipStream_t s) {
@@ -240,4 +258,38 @@ PTO_API int pto_ar_allreduce_sgd(const void* peers, long long off, long long n, 
   f.rep_stride = rep_stride;
   f.rep_from = rep_from;
   return launch<true>(peers, off, n, rank, world, chan, epochs, err, f, s);
+}
+
+// In-place SUM all-reduce of n bf16 values at element offset `off` of the
+// registered (bf16) input buffers: n % 8 == 0, off % 8 == 0.  A range of at
+// most AR_ONESHOT_MAX * 2 bf16 (the same 256 KB) takes the one-shot path.
+PTO_API int pto_ar_allreduce_bf16(const void* peers, long long off, long long n, int rank, int world, int chan,
+                                  void* epochs, void* err, hipStream_t s) {
+  if (n % 8 || off % 8 || n > 2 * AR_MAX_FLOATS || world < 1 || world > AR_MAX_RANKS || chan < 0 ||
+      chan >= AR_CHANNELS || rank < 0 || rank >= world)
+    return -1;
+  if (n == 0) return 0;
+  const ArPeers* P = reinterpret_cast<const ArPeers*>(peers);
+  uint32_t* ep = reinterpret_cast<uint32_t*>(epochs);
+  int* er = reinterpret_cast<int*>(err);
+  const long long nv = n / 8;
+  if (n <= 2 * AR_ONESHOT_MAX) {
+    const dim3 g((unsigned)((nv + AR_THREADS - 1) / AR_THREADS));
+    if (g_protocol)
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce_bf16_1shot<true>), g, dim3(AR_THREADS), 0, s, P, off, nv,
+                         rank, world, chan, ep, er, g_timeout_ticks);
+    else
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce_bf16_1shot<false>), g, dim3(AR_THREADS), 0, s, P, off, nv,
+                         rank, world, chan, ep, er, g_timeout_ticks);
+    return (int)hipGetLastError();
+  }
+  // as many workgroups as the fp32 path uses for the same bytes
+  const dim3 g((unsigned)blocks_for(n / 2, world));
+  if (g_protocol)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce_bf16<true>), g, dim3(AR_THREADS), 0, s, P, off, nv, rank,
+                       world, chan, ep, er, g_timeout_ticks);
+  else
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce_bf16<false>), g, dim3(AR_THREADS), 0, s, P, off, nv, rank,
+                       world, chan, ep, er, g_timeout_ticks);
+  return (int)hipGetLastError();
 }

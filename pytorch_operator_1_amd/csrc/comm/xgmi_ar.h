@@ -38,6 +38,7 @@ constexpr int AUX_SYS = 1 | 16;
 using gu32 = __attribute__((address_space(1))) uint32_t;
 using v4f = __attribute__((ext_vector_type(4))) float;
 using gv4f = __attribute__((address_space(1))) v4f;
+using v4u = __attribute__((ext_vector_type(4))) unsigned int;
 __device__ __forceinline__ gu32* G(uint32_t* p) { return (gu32*)p; }
 __device__ __forceinline__ float4 gld4(const float* p) {
   const v4f v = *(const gv4f*)p;
@@ -80,8 +81,7 @@ __device__ __forceinline__ float4 ld4(const Buf& b, long long i4) {
 template <bool COHERENT>
 __device__ __forceinline__ void st4(const Buf& b, long long i4, float4 v) {
   if constexpr (COHERENT) {
-    using u4 = __attribute__((ext_vector_type(4))) unsigned int;
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), b.r, (int)(i4 * 16), 0, AUX_SYS);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), b.r, (int)(i4 * 16), 0, AUX_SYS);
   } else {
     reinterpret_cast<float4*>(b.p)[i4] = v;
   }
@@ -355,6 +355,130 @@ __device__ __forceinline__ void ar_oneshot(const ArPeers* __restrict__ peers, lo
     }
   }
   if (SGD && f.bidx && blk == 0 && threadIdx.x == 0) *f.bidx = (*f.bidx + 1) % f.nbatches;
+}
+
+// ---------------------------------------------------------------- bf16 --
+// Plain SUM all-reduce of bf16 gradient buckets (the large-model DDP comm
+// hook, parallel/ddp.py): 16-byte vectors of 8 bf16, summed in fp32 in rank
+// order and rounded to bf16 once (stage 1 / the one-shot sum), so every rank
+// ends with bit-identical values.  Same barriers, protocols and failure
+// semantics as the fp32 path; no optimizer epilogue.
+struct F8 {
+  float v[8];
+};
+__device__ __forceinline__ F8 bf16x8_to_f32(v4u x) {
+  F8 r;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    r.v[2 * k] = __uint_as_float(x[k] << 16);
+    r.v[2 * k + 1] = __uint_as_float(x[k] & 0xffff0000u);
+  }
+  return r;
+}
+__device__ __forceinline__ uint32_t f32_to_bf16_rne(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if (f != f) return 0x7fc0u;  // NaN stays a quiet NaN
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ v4u f32_to_bf16x8(const F8& a) {
+  v4u r;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r[k] = f32_to_bf16_rne(a.v[2 * k]) | (f32_to_bf16_rne(a.v[2 * k + 1]) << 16);
+  return r;
+}
+template <bool COHERENT>
+__device__ __forceinline__ v4u ldv(const Buf& b, long long i) {
+  if constexpr (COHERENT) return __builtin_amdgcn_raw_buffer_load_b128(b.r, (int)(i * 16), 0, AUX_SYS);
+  else return reinterpret_cast<const v4u*>(b.p)[i];
+}
+template <bool COHERENT>
+__device__ __forceinline__ void stv(const Buf& b, long long i, v4u v) {
+  if constexpr (COHERENT) __builtin_amdgcn_raw_buffer_store_b128(v, b.r, (int)(i * 16), 0, AUX_SYS);
+  else reinterpret_cast<v4u*>(b.p)[i] = v;
+}
+// byte-offset view of a registered buffer (`off` in elements of `esize` bytes)
+__device__ __forceinline__ float* at(float* base, long long off, int esize) {
+  return reinterpret_cast<float*>(reinterpret_cast<char*>(base) + off * esize);
+}
+// nv vectors of 8 bf16 starting at element `off` of every rank's buffers.
+template <bool FENCED, int NT>
+__device__ __forceinline__ void ar_twostage_bf16(const ArPeers* __restrict__ P, long long off, long long nv, int rank,
+                                                 int world, int chan, uint32_t* __restrict__ epochs, int* err,
+                                                 long long timeout, int blk, int nblk) {
+  constexpr bool CO = !FENCED;
+  __shared__ uint32_t s_epoch;
+  if (threadIdx.x == 0) s_epoch = epochs[chan * AR_MAX_BLOCKS + blk] + 1;
+  __syncthreads();
+  const uint32_t e = s_epoch;
+  if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blk] = e;
+  const long long cs = (nv + world - 1) / world;
+  const long long stride = (long long)nblk * NT;
+  const long long j0 = (long long)blk * NT + threadIdx.x;
+  const long long bytes = nv * 16;
+  if (!block_barrier<FENCED>(P, chan, 0, blk, rank, world, e, timeout, err)) return;
+  {
+    const long long c0 = (long long)rank * cs, c1 = min(nv, c0 + cs);
+    for (long long i = c0 + j0; i < c1; i += stride) {
+      v4u raw[AR_MAX_RANKS];
+#pragma unroll
+      for (int q = 0; q < AR_MAX_RANKS; ++q)
+        if (q < world) raw[q] = ldv<CO>(mkbuf(at(P->in[q], off, 2), bytes), i);
+      F8 a = bf16x8_to_f32(raw[0]);
+#pragma unroll
+      for (int q = 1; q < AR_MAX_RANKS; ++q)
+        if (q < world) {
+          const F8 b = bf16x8_to_f32(raw[q]);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) a.v[k] += b.v[k];
+        }
+      stv<CO>(mkbuf(at(P->tmp[rank], off, 2), bytes), i, f32_to_bf16x8(a));
+    }
+  }
+  if (!block_barrier<FENCED>(P, chan, 1, blk, rank, world, e, timeout, err)) return;
+  float* const my_in = at(P->in[rank], off, 2);
+  for (long long j = j0; j < cs; j += stride) {
+    v4u v[AR_MAX_RANKS];
+#pragma unroll
+    for (int q = 0; q < AR_MAX_RANKS; ++q)
+      if (q < world && (long long)q * cs + j < nv) v[q] = ldv<CO>(mkbuf(at(P->tmp[q], off, 2), bytes), q * cs + j);
+#pragma unroll
+    for (int q = 0; q < AR_MAX_RANKS; ++q)
+      if (q < world && (long long)q * cs + j < nv) reinterpret_cast<v4u*>(my_in)[q * cs + j] = v[q];
+  }
+}
+
+// One-shot variant: nv <= nblk * NT (one vector per thread).
+template <bool FENCED, int NT>
+__device__ __forceinline__ void ar_oneshot_bf16(const ArPeers* __restrict__ P, long long off, long long nv, int rank,
+                                                int world, int chan, uint32_t* __restrict__ epochs, int* err,
+                                                long long timeout, int blk) {
+  constexpr bool CO = !FENCED;
+  __shared__ uint32_t s_epoch;
+  if (threadIdx.x == 0) s_epoch = epochs[chan * AR_MAX_BLOCKS + blk] + 1;
+  __syncthreads();
+  const uint32_t e = s_epoch;
+  if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blk] = e;
+  const long long i = (long long)blk * NT + threadIdx.x;
+  const bool act = i < nv;
+  const long long bytes = nv * 16;
+  if (!block_barrier<FENCED>(P, chan, 0, blk, rank, world, e, timeout, err)) return;
+  F8 a{};
+  if (act) {
+    v4u raw[AR_MAX_RANKS];
+#pragma unroll
+    for (int q = 0; q < AR_MAX_RANKS; ++q)
+      if (q < world) raw[q] = ldv<CO>(mkbuf(at(P->in[q], off, 2), bytes), i);
+    a = bf16x8_to_f32(raw[0]);
+#pragma unroll
+    for (int q = 1; q < AR_MAX_RANKS; ++q)
+      if (q < world) {
+        const F8 b = bf16x8_to_f32(raw[q]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a.v[k] += b.v[k];
+      }
+  }
+  if (!block_barrier<FENCED>(P, chan, 1, blk, rank, world, e, timeout, err)) return;
+  if (act) reinterpret_cast<v4u*>(at(P->in[rank], off, 2))[i] = f32_to_bf16x8(a);
 }
 
 // Workgroups of NT threads an all-reduce of n floats uses (identical on every

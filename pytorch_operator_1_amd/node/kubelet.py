@@ -25,7 +25,15 @@ Per pod:
 
 GPU pinning (``gpu_visibility``, per pod: the ``pto.amd.com/gpu-visibility``
 annotation):
-  * ``isolated`` (default) — the process sees only its own GPUs
+  * ``job`` (default) — the process's own GPU is device 0 (``LOCAL_RANK=0``,
+    so an image that just uses ``cuda:0`` lands on it, as under a device
+    plugin), followed by the GPUs allocated to the OTHER replicas of the
+    same job on this node (known at start: all of them with gang
+    admission).  No other job's GPU is visible, but the job's own peers stay
+    enumerable, so RCCL can pick its P2P/IPC transport over xGMI instead of
+    staging through host memory, and the xGMI all-reduce can map the
+    peers' buffers.
+  * ``isolated`` — the process sees only its own GPUs
     (``HIP_VISIBLE_DEVICES`` = its allocation, ``LOCAL_RANK=0``), the
     Kubernetes device-plugin model: any image that just uses ``cuda:0``
     lands on its own GPU.
@@ -101,7 +109,7 @@ EFFECTIVE_ENV_ANNOTATION = "pto.amd.com/effective-env"
 # env keys whose effective value is recorded on the pod
 _EFFECTIVE_KEYS = ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
                    "HIP_VISIBLE_DEVICES", "PTO_MASTER_SERVICE", "PTO_MASTER_PORT_REQUESTED")
-GPU_VISIBILITY_MODES = ("node", "isolated")
+GPU_VISIBILITY_MODES = ("job", "node", "isolated")
 # per-pod choice of the visibility model (pod template annotation); the
 # node-wide default is --gpu-visibility / PTO_GPU_VISIBILITY
 GPU_VISIBILITY_ANNOTATION = "pto.amd.com/gpu-visibility"
@@ -174,7 +182,7 @@ class Kubelet:
                  hbm_per_gpu: float = C.HBM_PER_GPU_BYTES, gpu_visibility: str | None = None, metrics=None,
                  sysfs_root: str | None = None, gpu_share: int | None = None, group_restarts: bool = True):
         self.client = client
-        self.gpu_visibility = gpu_visibility or os.environ.get("PTO_GPU_VISIBILITY", "isolated")
+        self.gpu_visibility = gpu_visibility or os.environ.get("PTO_GPU_VISIBILITY", "job")
         if self.gpu_visibility not in GPU_VISIBILITY_MODES:
             raise ValueError(f"gpu_visibility must be one of {GPU_VISIBILITY_MODES}")
         # in-place restarts (OnFailure/Always) of a multi-replica job's
@@ -211,6 +219,7 @@ class Kubelet:
         self._drained: set[str] = set()
         self.job_gen: dict[str, int] = {}
         self.job_ports: dict[str, int] = {}
+        self._gang_gpus: dict[str, dict] = {}  # job -> {owner: allocator slots} of its last gang admission
         self._port_locks: dict[int, int] = {}  # port -> flock fd of its host-wide reservation
         self.pod_informer = Informer(client, "pods")
         self.svc_informer = Informer(client, "services")
@@ -399,7 +408,21 @@ class Kubelet:
             self._set_unschedulable(pod, rt, r.get("error", "insufficient amd.com/gpu"))
             return False
         rt.gpus = list(r["assigned"].get(rt.owner, []))
+        if group:  # the whole gang's GPUs: "job" visibility shows them to every member
+            self._gang_gpus[rt.job_key] = {o: list(g) for o, g in r["assigned"].items()}
         return True
+
+    def _job_peer_devices(self, rt) -> list[int]:
+        """Devices of the other replicas of rt's job on this node (live
+        runtimes, plus the job's gang assignment for members not started)."""
+        slots = set()
+        for r in self.pods.values():
+            if r is not rt and r.job_key == rt.job_key and r.gpus:
+                slots.update(r.gpus)
+        for owner, gs in self._gang_gpus.get(rt.job_key, {}).items():
+            if owner != rt.owner:
+                slots.update(gs)
+        return sorted({g // self.gpu_share for g in slots})
 
     def _set_unschedulable(self, pod, rt, msg):
         st = {"phase": "Pending", "conditions": [{"type": "PodScheduled", "status": "False",
@@ -490,6 +513,8 @@ class Kubelet:
         live = {self._job_key(p) for p in pods}
         for jk in [jk for jk in self.job_ports if jk not in live and jk not in self.retired]:
             self._drop_job_port(jk)
+        for jk in [jk for jk in self._gang_gpus if jk not in live]:
+            del self._gang_gpus[jk]
 
     def _drop_job_port(self, jk):
         port = self.job_ports.pop(jk)
@@ -534,6 +559,11 @@ class Kubelet:
                 env["HIP_VISIBLE_DEVICES"] = _physical_ids(list(range(n)))
                 env["LOCAL_RANK"] = str(mine[0] if mine else 0)
                 env["LOCAL_WORLD_SIZE"] = env.get("WORLD_SIZE", "1")  # single node: every replica is local
+            elif mode == "job":
+                peers = [d for d in self._job_peer_devices(rt) if d not in mine]
+                env["HIP_VISIBLE_DEVICES"] = _physical_ids(mine + peers)
+                env["LOCAL_RANK"] = "0"
+                env["LOCAL_WORLD_SIZE"] = "1"
             else:
                 env["HIP_VISIBLE_DEVICES"] = _physical_ids(mine)
                 env["LOCAL_RANK"] = "0"

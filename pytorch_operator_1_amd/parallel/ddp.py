@@ -16,11 +16,19 @@ and relies on its bucketing.  This is the MI355X-first replacement:
 * The 1/world average is NOT a separate pass: the fused optimizers take
   ``grad_scale`` and fold it into their single read of the gradient
   (:meth:`grad_scale`), and zero the buffer in the same pass.
-* Bucket size defaults to 256 MB: xGMI is point-to-point (7 links x
-  ~150 GB/s per GPU), a ring all-reduce on 8 GPUs moves 2*(7/8)*size per
-  GPU, so large buckets amortise the per-collective latency
-  (~30-50 us) while still leaving >60 buckets to overlap with Llama-8B's
-  16 GB of bf16 gradients.
+* Bucket size: at most 256 MB (xGMI is point-to-point, 7 links x ~150
+  GB/s per GPU; a ring all-reduce on 8 GPUs moves 2*(7/8)*size per GPU, so
+  large buckets amortise the per-collective latency of ~30-50 us and still
+  leave >60 buckets to overlap with Llama-8B's 16 GB of bf16 gradients),
+  and at most a quarter of the model (>= 4 buckets, so a small model such
+  as ResNet-50 -- 51 MB of bf16 gradients -- overlaps too), never below
+  4 MB.
+* Comm hook: when the whole gradient buffer is small
+  (<= ``PTO_XGMI_MAX_MB``, 512 MB), it is registered with the xGMI peer
+  all-reduce kernel (:mod:`.xgmi`, fp32 or bf16), verified against the
+  group's all-reduce, and every bucket is timed both ways at startup; a
+  bucket goes to the kernel if it was faster there (the decision is
+  recorded in :attr:`GradBucketer.comm_info`).
 """
 from __future__ import annotations
 
@@ -46,7 +54,10 @@ class GradBucketer:
     """
 
     def __init__(self, module: torch.nn.Module, bucket_mb: float | None = None, process_group=None,
-                 overlap: bool = True, mode: str | None = None):
+                 overlap: bool = True, mode: str | None = None, comm: str | None = None):
+        """``comm``: "auto" (default, ``PTO_COMM``): per-bucket xGMI kernel
+        vs RCCL by measurement; "xgmi": every bucket on the kernel; "rccl":
+        never the kernel."""
         self.module = module
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
@@ -54,11 +65,16 @@ class GradBucketer:
         self.mode = mode or os.environ.get("PTO_GRAD_MODE") or ("copy" if self.world > 1 else "none")
         if self.mode not in ("view", "copy", "none"):
             raise ValueError(f"GradBucketer: unknown mode {self.mode}")
-        bucket_mb = bucket_mb if bucket_mb is not None else float(os.environ.get("PTO_BUCKET_MB", "256"))
-        cap = int(bucket_mb * 1024 * 1024)
         params = [p for p in module.parameters() if p.requires_grad]
         if not params:
             raise ValueError("GradBucketer: module has no trainable parameters")
+        if bucket_mb is None and "PTO_BUCKET_MB" in os.environ:
+            bucket_mb = float(os.environ["PTO_BUCKET_MB"])
+        if bucket_mb is None:
+            total_bytes = sum(p.numel() * p.element_size() for p in params)
+            cap = int(min(256 * 2**20, max(4 * 2**20, total_bytes / 4)))
+        else:
+            cap = int(bucket_mb * 1024 * 1024)
         self.params = params
         dev = params[0].device
         self._views: dict = {}
@@ -99,7 +115,52 @@ class GradBucketer:
         if self.mode == "copy" or (self.overlap and self.mode == "view"):
             for p in params:
                 self._handles.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        self._xgmi: dict = {}
+        self.comm_info: dict = {"buckets": len(self.buckets), "bucket_bytes": cap, "transport": "rccl"}
+        comm = comm or os.environ.get("PTO_COMM", "auto")
+        if comm not in ("auto", "xgmi", "rccl"):
+            raise ValueError(f"GradBucketer: comm must be auto, xgmi or rccl, not {comm!r}")
+        if self.world > 1 and comm != "rccl" and dev.type == "cuda":
+            self._setup_xgmi(comm)
         self.reset()
+
+    def _setup_xgmi(self, comm: str):
+        """Register each flat buffer with the xGMI kernel (if small enough),
+        verify it, and route the buckets it runs faster."""
+        from .xgmi import XgmiAllReduce
+
+        limit = float(os.environ.get("PTO_XGMI_MAX_MB", "512")) * 2**20
+        if self.grad_bytes() > limit or any(dt not in (torch.float32, torch.bfloat16) for dt in self.flat):
+            self.comm_info["xgmi"] = "not used (gradients above PTO_XGMI_MAX_MB or not fp32/bf16)"
+            return
+        decisions = []
+        for dt, buf in self.flat.items():
+            try:
+                ar = XgmiAllReduce(buf, group=self.pg, timeout_ms=int(os.environ.get("PTO_XGMI_TIMEOUT_MS", "10000")))
+            except (RuntimeError, ValueError) as e:  # every rank raises together
+                self.comm_info["xgmi"] = f"setup failed: {e}"[:300]
+                return
+            mine = [(i, b) for i, b in enumerate(self.buckets) if b["dtype"] == dt]
+            ranges = [(b["lo"], b["hi"] - b["lo"]) for _, b in mine]
+            res = ar.verify_with_fallback(ranges)
+            if not res["correct"]:
+                ar.close()
+                self.comm_info["xgmi"] = {k: v for k, v in res.items() if k != "verify_log"}
+                return
+            used = False
+            for (i, b), rng in zip(mine, ranges):
+                tx, tr, ok = ar.time_vs_collective([rng], iters=10, stream=self.comm_stream)
+                take = ok and (comm == "xgmi" or tx < tr)
+                b["transport"] = "xgmi" if take else "rccl"
+                b["chan"] = i % 2
+                used |= take
+                decisions.append({"bucket": i, "mb": round((b["hi"] - b["lo"]) * buf.element_size() / 2**20, 2),
+                                  "xgmi_us": round(tx, 1), "rccl_us": round(tr, 1), "use": b["transport"]})
+            if used:
+                self._xgmi[dt] = ar
+            else:
+                ar.close()
+        self.comm_info.update(transport="xgmi+rccl" if self._xgmi else "rccl", xgmi_buckets=decisions)
 
     # ------------------------------------------------------------------
     def reset(self):
@@ -112,6 +173,12 @@ class GradBucketer:
     def _launch(self, i):
         b = self.buckets[i]
         t = self._bucket_view(b)
+        if b.get("transport") == "xgmi":  # the peer-memory kernel on the comm stream (no work handle)
+            ar = self._xgmi[b["dtype"]]
+            if self.comm_stream is not None:
+                self.comm_stream.wait_event(torch.cuda.current_stream(t.device).record_event())
+            ar.allreduce_(b["lo"], b["hi"] - b["lo"], chan=b["chan"], stream=self.comm_stream)
+            return
         if self.comm_stream is not None:
             ev = torch.cuda.current_stream(t.device).record_event()
             self.comm_stream.wait_event(ev)
@@ -155,6 +222,8 @@ class GradBucketer:
                 w.wait()
             if self.comm_stream is not None:
                 torch.cuda.current_stream(self.comm_stream.device).wait_stream(self.comm_stream)
+            for ar in self._xgmi.values():
+                ar.poll()  # a stalled/dead peer raises XgmiTimeout (one step late, never blocking)
         self.reset()
 
     @property
@@ -182,6 +251,9 @@ class GradBucketer:
         for h in self._handles:
             h.remove()
         self._handles = []
+        for ar in self._xgmi.values():
+            ar.close()
+        self._xgmi = {}
 
     def grad_bytes(self) -> int:
         return sum(b.numel() * b.element_size() for b in self.flat.values())

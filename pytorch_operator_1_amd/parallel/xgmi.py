@@ -51,12 +51,14 @@ class XgmiTimeout(RuntimeError):
 
 class XgmiAllReduce:
     def __init__(self, buf: torch.Tensor, group=None, timeout_ms: int | None = None, protocol: str | None = None):
-        """``buf``: this rank's fp32 gradient buffer (same numel on every
-        rank); all-reduces operate in place on ranges of it.  ``protocol``:
+        """``buf``: this rank's fp32 or bf16 gradient buffer (same numel on
+        every rank); all-reduces operate in place on ranges of it (bf16:
+        summed in fp32, rounded once; no SGD epilogue).  ``protocol``:
         "coherent" (default, ``PTO_XGMI_PROTOCOL``) or "fenced"; every rank
         must pass the same."""
-        if buf.dtype != torch.float32 or not buf.is_cuda or not buf.is_contiguous():
-            raise ValueError("XgmiAllReduce: contiguous fp32 HIP buffer required")
+        if buf.dtype not in (torch.float32, torch.bfloat16) or not buf.is_cuda or not buf.is_contiguous():
+            raise ValueError("XgmiAllReduce: contiguous fp32/bf16 HIP buffer required")
+        self.align = 4 if buf.dtype == torch.float32 else 8  # elements per 16-byte vector
         self.group = group
         pg = dist.is_available() and dist.is_initialized()
         # world size 1 (no process group needed): the multi-GPU step's
@@ -131,13 +133,14 @@ class XgmiAllReduce:
 
     def allreduce_(self, offset: int, n: int, chan: int = 0, stream=None):
         """SUM in place over ``buf[offset:offset+n]`` on every rank."""
-        if n % 4 or offset % 4:
-            raise ValueError("XgmiAllReduce: offset and length must be multiples of 4 floats")
+        if n % self.align or offset % self.align:
+            raise ValueError(f"XgmiAllReduce: offset and length must be multiples of {self.align} elements")
         if offset + n > self.buf.numel():
             raise ValueError("XgmiAllReduce: range outside the registered buffer")
         s = (stream or torch.cuda.current_stream(self.device)).cuda_stream
         _lib.check(_lib.lib().pto_ar_set_protocol(PROTOCOLS[self.protocol]), "ar_set_protocol")
-        _lib.check(_lib.lib().pto_ar_allreduce(self.peers.data_ptr(), offset, n, self.rank, self.world, chan,
+        fn = _lib.lib().pto_ar_allreduce if self.align == 4 else _lib.lib().pto_ar_allreduce_bf16
+        _lib.check(fn(self.peers.data_ptr(), offset, n, self.rank, self.world, chan,
                                                self.epochs.data_ptr(), self.err.data_ptr(), s), "xgmi_allreduce")
 
     def allreduce_sgd_(self, offset: int, n: int, params: torch.Tensor, mom: torch.Tensor, lr_dev: torch.Tensor,
@@ -152,6 +155,8 @@ class XgmiAllReduce:
         local copies of the gradient range ``[rep_from, numel)`` (replica r
         >= 1 at ``replicas[(r-1)*(numel-rep_from):]``), folded into the
         gradient and zeroed before the exchange."""
+        if self.align != 4:
+            raise ValueError("XgmiAllReduce: the SGD epilogue needs an fp32 buffer")
         if n % 4 or offset % 4:
             raise ValueError("XgmiAllReduce: offset and length must be multiples of 4 floats")
         if offset + n > self.buf.numel():
@@ -238,23 +243,26 @@ class XgmiAllReduce:
         for it in range(rounds):
             g = torch.Generator(device=self.device).manual_seed(1234 + 7919 * it + self.rank)
             self.buf.copy_(torch.randn(self.buf.shape, generator=g, device=self.device))
-            ref = self.buf.clone()
+            ref = self.buf.float()  # the reference sum in fp32 (bf16 buffers: exact up to fp32)
             for off, n in ranges:
                 dist.all_reduce(ref[off:off + n], group=self.group)
+            scale = max(1.0, ref.abs().max().item())
             for c, (off, n) in enumerate(ranges):
                 self.allreduce_(off, n, chan=c % 2)
             torch.cuda.synchronize(self.device)
-            scale = max(1.0, ref.abs().max().item())
             for off, n in ranges:
-                bad = max(bad, (self.buf[off:off + n] - ref[off:off + n]).abs().max().item() / scale)
+                bad = max(bad, (self.buf[off:off + n].float() - ref[off:off + n]).abs().max().item() / scale)
             # every rank must hold identical values (fixed summation order)
-            chk = self.buf.clone()
+            mine = self.buf.float()
+            chk = mine.clone()
             dist.all_reduce(chk, op=dist.ReduceOp.MAX, group=self.group)
-            identical &= float((chk - self.buf).abs().max().item()) == 0.0
+            identical &= float((chk - mine).abs().max().item()) == 0.0
         timed_out = int(self.err.item()) != 0
         self.buf.copy_(saved)
         torch.cuda.synchronize(self.device)
-        ok = self._agree(bad <= 1e-5 and identical and not timed_out)
+        # bf16: one rounding of the fp32 sum (<= 2^-9 relative)
+        tol = 1e-5 if self.align == 4 else 1e-2
+        ok = self._agree(bad <= tol and identical and not timed_out)
         return {"correct": ok, "max_rel_err": bad, "identical": identical, "timed_out": timed_out,
                 "protocol": self.protocol, "verify_rounds": rounds}
 
@@ -291,7 +299,16 @@ class XgmiAllReduce:
         result = self.verify_with_fallback(ranges)
         if not result["correct"]:
             return result
+        tx, tr, ok_after = self.time_vs_collective(ranges, iters)
+        result.update(correct=ok_after, use_xgmi=bool(ok_after and tx < tr), xgmi_us=round(tx, 2),
+                      rccl_us=round(tr, 2), timed_out=not ok_after)
+        return result
 
+    def time_vs_collective(self, ranges, iters: int = 30, stream=None) -> tuple[float, float, bool]:
+        """Host-timed mean of ``iters`` calls over ``ranges`` (max over
+        ranks) for this kernel and for the group's all-reduce (RCCL), and
+        whether the kernel's error word stayed clean on every rank.  The
+        buffer is restored afterwards.  Collective."""
         def timed(fn):
             torch.cuda.synchronize(self.device)
             dist.barrier(group=self.group)
@@ -305,7 +322,7 @@ class XgmiAllReduce:
 
         def run_xgmi():
             for c, (off, n) in enumerate(ranges):
-                self.allreduce_(off, n, chan=c % 2)
+                self.allreduce_(off, n, chan=c % 2, stream=stream)
 
         def run_rccl():
             for off, n in ranges:
@@ -314,12 +331,10 @@ class XgmiAllReduce:
         saved = self.buf.clone()
         run_xgmi(), run_rccl()  # warm
         tx, tr = timed(run_xgmi), timed(run_rccl)
-        ok_after = self._agree(int(self.err.item()) == 0)
+        ok = self._agree(int(self.err.item()) == 0)
         self.buf.copy_(saved)
         torch.cuda.synchronize(self.device)
-        result.update(correct=ok_after, use_xgmi=bool(ok_after and tx < tr), xgmi_us=round(tx, 2),
-                      rccl_us=round(tr, 2), timed_out=not ok_after)
-        return result
+        return tx, tr, ok
 
     def _autotune_single(self, ranges, iters: int) -> dict:
         """World size 1: the sum over one rank is the input itself."""

@@ -205,6 +205,9 @@ def _main(argv=None):
     if use_cuda:
         print("Using CUDA (HIP) on", torch.cuda.get_device_name(0))
     torch.manual_seed(args.seed)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    rccl_log = (pdist.rccl_log_setup() if use_cuda and world_env > 1 and
+                pdist.resolve_backend(args.backend, True) == "nccl" else None)
     env, device = pdist.init_distributed(args.backend, use_gpu=use_cuda)
     if env.is_distributed:
         print(f"Using distributed PyTorch with {dist.get_backend()} backend")
@@ -232,6 +235,15 @@ def _main(argv=None):
     if comm_info and world > 1:
         print(f"[pto] gradient all-reduce: {comm_info}", flush=True)
         metrics.emit(event="comm", rank=rank, **{k: v for k, v in comm_info.items() if not isinstance(v, dict)})
+    if world > 1:
+        # which devices the world spans and the transport RCCL picked per
+        # peer (P2P/IPC over xGMI vs SHM): the trainer's constructor ran the
+        # first collective, so the connections exist
+        w = pdist.describe_world(device, rccl_log)
+        if rank == 0:
+            print(f"[pto] world: {json.dumps(w)}", flush=True)
+        metrics.emit(event="world", rank=rank, pg_world_size=w["pg_world_size"],
+                     rccl_transport=json.dumps(w.get("rccl_transport", {})))
     start_step = 0
     path, st = resume_state(args.checkpoint_dir, rank, world)
     if st is not None:

@@ -45,7 +45,7 @@ def _envs(c, job, n):
     return out
 
 
-@pytest.mark.parametrize("mode", ["node", "isolated"])
+@pytest.mark.parametrize("mode", ["job", "node", "isolated"])
 def test_master1_worker7_gpu_env(tmp_path, mode):
     # gang admission: all 8 GPUs are assigned at once (a replica that finished
     # early would otherwise hand its GPU to one admitted after it)
@@ -63,7 +63,13 @@ def test_master1_worker7_gpu_env(tmp_path, mode):
     assert {e["PTO_MASTER_SERVICE"] for n, e in envs.items() if "worker" in n} == {f"pin-{mode}-master-0"}
     gpu_ids = sorted(int(e["PTO_GPU_IDS"]) for e in envs.values())
     assert gpu_ids == list(range(8))  # every GPU handed to exactly one replica
-    if mode == "node":
+    if mode == "job":
+        # own GPU first (cuda:0), then the job's 7 other GPUs: peers enumerable for RCCL P2P / xGMI IPC
+        for e in envs.values():
+            vis = e["HIP_VISIBLE_DEVICES"].split(",")
+            assert vis[0] == e["PTO_GPU_IDS"] and sorted(map(int, vis)) == list(range(8)), e
+        assert {e["LOCAL_RANK"] for e in envs.values()} == {"0"}
+    elif mode == "node":
         assert {e["HIP_VISIBLE_DEVICES"] for e in envs.values()} == {"0,1,2,3,4,5,6,7"}
         assert all(e["LOCAL_RANK"] == e["PTO_GPU_IDS"] for e in envs.values())
         assert {e["LOCAL_WORLD_SIZE"] for e in envs.values()} == {"8"}
