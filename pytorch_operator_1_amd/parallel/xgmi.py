@@ -243,7 +243,7 @@ class XgmiAllReduce:
         for it in range(rounds):
             g = torch.Generator(device=self.device).manual_seed(1234 + 7919 * it + self.rank)
             self.buf.copy_(torch.randn(self.buf.shape, generator=g, device=self.device))
-            ref = self.buf.float()  # the reference sum in fp32 (bf16 buffers: exact up to fp32)
+            ref = self.buf.to(torch.float32, copy=True)  # the reference sum in fp32 (never an alias of buf)
             for off, n in ranges:
                 dist.all_reduce(ref[off:off + n], group=self.group)
             scale = max(1.0, ref.abs().max().item())
