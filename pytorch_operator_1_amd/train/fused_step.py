@@ -77,13 +77,15 @@ class FusedMnistTrainer:
     def __init__(self, device, batch_size=64, lr=0.01, momentum=0.5, dataset_size=60000, seed=1, rank=0,
                  weight_decay=0.0, nesterov=False, graph: str | None = None, comm: str | None = None,
                  data=None, target=None, unroll: int | None = None, force_ddp: bool = False,
-                 overlap: bool | None = None):
+                 overlap: bool | None = None, plan_steps: int | None = None):
         """``graph``: "full" (whole steps in graphs; default), "split"
         (collectives between graphs) or "none" (eager launches).
         ``force_ddp``: the grads-only + all-reduce + SGD-launch schedule at
         world size 1 (the DDP code path in one process).  ``overlap``
         (ddp-xgmi; default on): the fc part of the exchange runs as extra
-        workgroups of the next step's F12 launch."""
+        workgroups of the next step's F12 launch.  ``plan_steps``
+        (fused-opt): run() of at most this many steps replays a native
+        launch plan instead of graphs (0: always graphs)."""
         assert device.type == "cuda", "FusedMnistTrainer runs on a HIP device"
         self.L = _lib.lib()
         self.device = device
@@ -96,6 +98,7 @@ class FusedMnistTrainer:
         self.ddp = self.world > 1 or force_ddp
         self.fused_opt = not self.ddp
         self.unroll = max(1, int(unroll if unroll is not None else os.environ.get("PTO_GRAPH_UNROLL", "32")))
+        self.plan_steps = int(plan_steps if plan_steps is not None else 0)
         self.comm = comm or os.environ.get("PTO_COMM", "auto")
         if self.comm not in ("auto", "xgmi", "rccl"):
             raise ValueError(f"comm must be auto, xgmi or rccl, not {self.comm!r}")
@@ -209,6 +212,8 @@ class FusedMnistTrainer:
             self.comm_info.update(schedule=self.schedule, world_size=self.world, backend=backend,
                                   graph_mode=self.graph_mode)
         self._graphs = None  # [one step] (full) or [forward+backward, optimizer] (split)
+        self._recording = None  # launch plan being recorded (_call)
+        self._plan = None  # fused-opt: the step's launches as a native plan (run() of short runs)
         self._graph_pow: dict[int, torch.cuda.CUDAGraph] = {}
         self._graph_close: dict[int, torch.cuda.CUDAGraph] = {}
 
@@ -241,6 +246,14 @@ class FusedMnistTrainer:
     def _s(self):
         return _lib.stream_ptr(self.device)
 
+    def _call(self, name: str, *args):
+        """Launch ``pto_<name>(*args, stream)``, or -- while a launch plan is
+        being recorded -- append it to the plan (``pto_plan_<name>``)."""
+        if self._recording is not None:
+            _lib.check(getattr(self.L, "pto_plan_" + name)(self._recording, *args), "plan_" + name)
+        else:
+            _lib.check(getattr(self.L, "pto_" + name)(*args, self._s()), name)
+
     def _opt_args(self):
         """(lr device ptr, momentum, weight decay, grad scale, nesterov)."""
         return (self.lr_dev.data_ptr(), self.momentum, self.weight_decay, 1.0 / self.world, int(self.nesterov))
@@ -259,6 +272,8 @@ class FusedMnistTrainer:
         c = _lib.check
         bi = self.batch_idx.data_ptr()
         o = self._opt_args()
+        if fc_owed and self._recording is not None:
+            raise RuntimeError("launch plans record the one-process step only")
         conv1 = (self._params[self._c1:].data_ptr(), self.grads[self._c1:].data_ptr(),
                  self.mom[self._c1:].data_ptr(), self.numel - self._c1)
         if self.fused_opt:
@@ -275,18 +290,18 @@ class FusedMnistTrainer:
                                   self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi,
                                   self.xcur.data_ptr(), *self._fc_role_args(), s), "conv12_fwd_ar")
         elif only in (None, 0):
-            c(L.pto_conv12_fwd_lazy_x(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
-                                      P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
-                                      self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi, *lazy,
-                                      self.xcur.data_ptr(), w2out, *rep, s), "conv12_fwd")
+            self._call("conv12_fwd_lazy_x", self.data.data_ptr(), P["conv1.weight"].data_ptr(),
+                       P["conv1.bias"].data_ptr(), P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(),
+                       self.a1p.data_ptr(), self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi,
+                       *lazy, self.xcur.data_ptr(), w2out, *rep)
         if only in (None, 1):
-            c(L.pto_linear_fwd(self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
-                               self.h1.data_ptr(), B, 500, 800, 1, s), "fc1_fwd")
+            self._call("linear_fwd", self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
+                       self.h1.data_ptr(), B, 500, 800, 1)
         if only in (None, 2):
-            c(L.pto_fc2_ce_dx(self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
-                              self.target.data_ptr(), P["fc1.weight"].data_ptr(), self.loss_rows.data_ptr(),
-                              self.dlogits.data_ptr(), self.dh1.data_ptr(), self.da2p.data_ptr(), B, 1.0 / B, bi,
-                              *conv1, pending, *o, *rep, s), "fc2_ce_dx")
+            self._call("fc2_ce_dx", self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
+                       self.target.data_ptr(), P["fc1.weight"].data_ptr(), self.loss_rows.data_ptr(),
+                       self.dlogits.data_ptr(), self.dh1.data_ptr(), self.da2p.data_ptr(), B, 1.0 / B, bi, *conv1,
+                       pending, *o, *rep)
 
     def _backward(self):
         """``k_bwd_all``: the whole backward in one launch.  Fused-opt: every
@@ -294,14 +309,13 @@ class FusedMnistTrainer:
         conv1's update becomes owed.  DDP (grads-only): every gradient lands
         in the flat buffer and nothing else changes."""
         go = self.ddp
-        _lib.check(self.L.pto_bwd_all(
-            self.da2p.data_ptr(), self.code2.data_ptr(), self.a1p.data_ptr(), _lib.ptr(self.w2f),
-            self.xcur.data_ptr(), self.code1.data_ptr(), self.dh1.data_ptr(), self.a2p.data_ptr(),
-            self.h1.data_ptr(), self.dlogits.data_ptr(), self._params.data_ptr(), self.grads.data_ptr(),
-            self.mom.data_ptr(), *self._offs, self.c2_ctr.data_ptr(), None if go else self.batch_idx.data_ptr(),
-            self.n_batches, None if go else self.pending.data_ptr(), self.B, *self._opt_args(),
-            self.c1rep.data_ptr(), self.c1_nrep, self.c1_stride, int(go), _lib.ptr(self.wpart), self._s()),
-            "bwd_all")
+        self._call("bwd_all", self.da2p.data_ptr(), self.code2.data_ptr(), self.a1p.data_ptr(), _lib.ptr(self.w2f),
+                   self.xcur.data_ptr(), self.code1.data_ptr(), self.dh1.data_ptr(), self.a2p.data_ptr(),
+                   self.h1.data_ptr(), self.dlogits.data_ptr(), self._params.data_ptr(), self.grads.data_ptr(),
+                   self.mom.data_ptr(), *self._offs, self.c2_ctr.data_ptr(),
+                   None if go else self.batch_idx.data_ptr(), self.n_batches,
+                   None if go else self.pending.data_ptr(), self.B, *self._opt_args(), self.c1rep.data_ptr(),
+                   self.c1_nrep, self.c1_stride, int(go), _lib.ptr(self.wpart))
 
     def _fc_role_args(self):
         lr, mom, wd, gs, nes = self._opt_args()
@@ -356,10 +370,9 @@ class FusedMnistTrainer:
                 self._close_fc()
 
     def _commit_launch(self):
-        _lib.check(self.L.pto_conv1_commit(self._params[self._c1:].data_ptr(), self.grads[self._c1:].data_ptr(),
-                                           self.mom[self._c1:].data_ptr(), self.numel - self._c1,
-                                           self.pending.data_ptr(), *self._opt_args(), self.c1rep.data_ptr(),
-                                           self.c1_nrep, self.c1_stride, self._s()), "conv1_commit")
+        self._call("conv1_commit", self._params[self._c1:].data_ptr(), self.grads[self._c1:].data_ptr(),
+                   self.mom[self._c1:].data_ptr(), self.numel - self._c1, self.pending.data_ptr(),
+                   *self._opt_args(), self.c1rep.data_ptr(), self.c1_nrep, self.c1_stride)
 
     def flush(self):
         """Commit an owed conv1 update (fused-opt) so the flat buffers hold
@@ -483,6 +496,30 @@ class FusedMnistTrainer:
             self.comm_info["graph_mode"] = "split (capture failed)"
             self._capture()
 
+    def _build_plan(self):
+        """fused-opt: the step's four launches + the closing conv1 commit,
+        recorded once as a native launch plan (``pto_plan_*``)."""
+        plan = self.L.pto_plan_create()
+        if not plan:
+            raise RuntimeError("pto_plan_create failed")
+        self._recording = plan
+        try:
+            self._forward()
+            self._backward()
+            _lib.check(self.L.pto_plan_mark_body(plan), "plan_mark_body")
+            self._commit_launch()
+        finally:
+            self._recording = None
+        self._plan = plan
+
+    def __del__(self):
+        plan, self._plan = getattr(self, "_plan", None), None
+        if plan:
+            try:
+                self.L.pto_plan_free(plan)
+            except Exception:  # noqa: BLE001 - interpreter shutdown
+                pass
+
     def run(self, n: int, blocking_check: bool = True):
         """Run exactly ``n`` training steps, then check the gradient
         transport's error word (a dead or stalled xGMI peer raises
@@ -491,6 +528,16 @@ class FusedMnistTrainer:
         of waiting for this chunk, so a training loop keeps the device busy
         while it logs."""
         if n <= 0:
+            return
+        if self.fused_opt and self.graph_mode == "full" and n <= self.plan_steps:
+            # a short run: the launches straight from one native call -- the
+            # GPU starts within microseconds instead of after a graph
+            # launch's setup (profiles/bench_window_r4.md)
+            if self._plan is None:
+                self._build_plan()
+            _lib.check(self.L.pto_plan_run(self._plan, n, 1, self._s()), "plan_run")
+            self.steps_done += n
+            self._owed = False
             return
         if self.graph_mode == "full":
             self._ensure_captured()
