@@ -40,7 +40,8 @@ knobs):
       conv1 gradient replica per sample); bitwise reproducible runs.
 
 Env knobs: ``PTO_COMM`` (auto|xgmi|rccl), ``PTO_GRAPH_UNROLL``,
-``PTO_DETERMINISTIC``, ``PTO_CAPTURE_COMM`` (0: collectives between graphs).
+``PTO_DETERMINISTIC``, ``PTO_CAPTURE_COMM`` (0: collectives between graphs),
+``PTO_XGMI_OVERLAP`` (0: one whole-buffer xGMI all-reduce per step).
 """
 from __future__ import annotations
 
@@ -183,7 +184,9 @@ class FusedMnistTrainer:
         # the convolutions; F3 of step k+1 is its first reader.  The last
         # step of every graph / eager step closes with a stand-alone fc
         # all-reduce, so every run() leaves complete updates.
-        self.overlap = self._xgmi is not None and (True if overlap is None else bool(overlap))
+        if overlap is None:
+            overlap = os.environ.get("PTO_XGMI_OVERLAP", "1") == "1"
+        self.overlap = self._xgmi is not None and bool(overlap)
         if self.overlap:
             self.comm_info["overlap"] = "fc all-reduce under the next step's F12 (same launch)"
         nrep_tail = max(1, self.c1_nrep - 1) * self.c1_stride

@@ -332,7 +332,7 @@ def test_trainer_exits_retryable_when_xgmi_peer_killed(tmp_path):
             p.wait()
     log0 = (tmp_path / "r0.log").read_text()
     log1 = (tmp_path / "r1.log").read_text()
-    assert procs[1].returncode == -9, log1[-2000:]
+    assert procs[1].returncode == -9, "rank 1:\n" + log1[-2000:] + "\nrank 0:\n" + log0[-2000:]
     assert procs[0].returncode == 138, log0[-3000:]
     assert "timed out" in log0
     assert t_kill is not None and t_exit - t_kill < 5.0, (t_exit - t_kill, log0[-2000:])
