@@ -297,13 +297,14 @@ def run_model_bench(args, env, device, pdist, rccl_log=None):
         cfg = {"model": args.model, "global_batch": args.batch_size * n, "per_rank_batch": args.batch_size,
                "seq_len": args.seq_len if args.model.startswith("llama") else None,
                "parallelism": f"dp{n}", "backend": (torch.distributed.get_backend() if n > 1 else "none"),
-               "bucket_mb": trainer.bucketer.buckets and round(
-                   max((b["hi"] - b["lo"]) for b in trainer.bucketer.buckets)
-                   * next(iter(trainer.bucketer.flat.values())).element_size() / 2**20, 1),
+               "bucket_mb": round(max((b["hi"] - b["lo"]) * trainer.bucketer.flat[b["dtype"]].element_size()
+                                      for b in trainer.bucketer.buckets) / 2**20, 1)
+               if trainer.bucketer.buckets else None,
                "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 1),
                "final_loss": trainer.last_loss()}
         cfg.update(trainer.describe())
         cfg["world"] = world
+        cfg["grad_allreduce"] = dict(getattr(trainer.bucketer, "comm_info", {}) or {})
         if breakdown:
             cfg["phase_ms"] = breakdown
         if hasattr(trainer, "flops_per_step"):
