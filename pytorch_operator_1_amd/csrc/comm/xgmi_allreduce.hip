@@ -112,6 +112,22 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_1shot(const ArPee
   ar_oneshot<SGD, FENCED, AR_THREADS>(peers, off, n4, rank, world, chan, epochs, err, timeout, f, blockIdx.x);
 }
 
+// The fc all-reduce of the overlapped MNIST step as a launch of its own:
+// EXACTLY the decomposition of the all-reduce role inside the F12 launch
+// (1024-thread workgroups, lean stages, blocks_for(n, world, 1024)), so a
+// rank that runs a step's fc exchange stand-alone interoperates with a peer
+// that ran the same exchange inside its F12 (block b covers the same
+// elements and advances the same epoch either way).
+constexpr int AR_ROLE_THREADS = 1024;
+template <bool FENCED>
+__global__ __launch_bounds__(AR_ROLE_THREADS) void k_xgmi_allreduce_role(const ArPeers* __restrict__ peers, long long off,
+                                                                          long long n4, int rank, int world, int chan,
+                                                                          uint32_t* __restrict__ epochs, int* err,
+                                                                          long long timeout, ArSgd f) {
+  ar_twostage<true, FENCED, AR_ROLE_THREADS, true>(peers, off, n4, rank, world, chan, epochs, err, timeout, f,
+                                                    blockIdx.x, gridDim.x);
+}
+
 template <bool FENCED>
 __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_bf16(const ArPeers* __restrict__ peers, long long off,
                                                                     long long nv, int rank, int world, int chan,
@@ -291,5 +307,38 @@ PTO_API int pto_ar_allreduce_bf16(const void* peers, long long off, long long n,
   else
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce_bf16<false>), g, dim3(AR_THREADS), 0, s, P, off, nv, rank,
                        world, chan, ep, er, g_timeout_ticks);
+  return (int)hipGetLastError();
+}
+
+// Stand-alone launch of the all-reduce-with-SGD ROLE (same arguments as
+// pto_conv12_fwd_ar's role part, same workgroup decomposition).
+PTO_API int pto_ar_role_sgd(const void* peers, long long off, long long n, int rank, int world, int chan, void* epochs,
+                            void* err, int protocol, float* p, float* m, const float* lr, float mom, float wd,
+                            float gscale, int nesterov, long long zero_from, hipStream_t s) {
+  if (n <= AR_ONESHOT_MAX || n % 4 || off % 4 || n > AR_MAX_FLOATS || world < 1 || world > AR_MAX_RANKS ||
+      chan < 0 || chan >= AR_CHANNELS || rank < 0 || rank >= world || !p || !m || !lr || !peers || protocol < 0 ||
+      protocol > 1 || ((((uintptr_t)p) | ((uintptr_t)m)) & 15))
+    return -1;
+  ArSgd f{};
+  f.p = p;
+  f.m = m;
+  f.a.lr = lr;
+  f.a.mom = mom;
+  f.a.wd = wd;
+  f.a.gscale = gscale;
+  f.a.nesterov = nesterov;
+  f.zero_from = zero_from;
+  f.nbatches = 1;
+  f.nrep = 1;
+  const ArPeers* P = reinterpret_cast<const ArPeers*>(peers);
+  const dim3 g((unsigned)blocks_for(n, world, AR_ROLE_THREADS));
+  if (protocol)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce_role<true>), g, dim3(AR_ROLE_THREADS), 0, s, P, off, n / 4,
+                       rank, world, chan, reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err),
+                       g_timeout_ticks, f);
+  else
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce_role<false>), g, dim3(AR_ROLE_THREADS), 0, s, P, off, n / 4,
+                       rank, world, chan, reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err),
+                       g_timeout_ticks, f);
   return (int)hipGetLastError();
 }

@@ -318,12 +318,17 @@ __global__ __launch_bounds__(NTH, ARM ? 2 * NTH / 256 : 1) void k_conv12_fwd2_t(
     const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ a1p, uint8_t* __restrict__ code1,
     float* __restrict__ a2p, uint8_t* __restrict__ code2, int B, const long long* __restrict__ bidx, LazyConv1 lz,
     ArRole ar) {
+  // all-reduce blocks FIRST in the grid: they are dispatched before the conv
+  // blocks, so their latency chain (two barriers, three memory rounds)
+  // starts at once and runs under the convolutions
+  int bx = (int)blockIdx.x;
   if constexpr (ARM != 0) {
-    if ((int)blockIdx.x >= 4 * B) {
+    if (bx < ar.nblk) {
       pto_ar::ar_twostage<true, ARM == 2, NTH, true>(ar.peers, ar.off, ar.n4, ar.rank, ar.world, ar.chan, ar.epochs,
-                                                  ar.err, ar.timeout, ar.f, (int)blockIdx.x - 4 * B, ar.nblk);
+                                                  ar.err, ar.timeout, ar.f, bx, ar.nblk);
       return;
     }
+    bx -= ar.nblk;
   }
   __shared__ float ws[16 * WS_LD];
   __shared__ __attribute__((aligned(16))) float in_s[A1P];
@@ -336,7 +341,7 @@ __global__ __launch_bounds__(NTH, ARM ? 2 * NTH / 256 : 1) void k_conv12_fwd2_t(
   constexpr int NWV = NTH / 64, NPART = NTH / 256;  // waves; K parts of the conv2 GEMM
   __shared__ __attribute__((aligned(16))) float red[(NPART - 1) * 1024];
   PTO_STAMP_SCOPE();
-  const int b = blockIdx.x >> 2, nt = blockIdx.x & 3;
+  const int b = bx >> 2, nt = bx & 3;
   const int tid = threadIdx.x;
   {
     x = batch_ptr(x, bidx, B * 784);

@@ -327,10 +327,11 @@ class FusedMnistTrainer:
 
     def _close_fc(self):
         """ddp-xgmi overlap: the owed fc all-reduce + SGD as a launch of its
-        own (end of a graph / eager step)."""
-        lr, mom, wd, gs, nes = self._opt_args()
-        self._xgmi.allreduce_sgd_(0, self._split, params=self._params, mom=self.mom, lr_dev=self.lr_dev, momentum=mom,
-                                  weight_decay=wd, gscale=gs, nesterov=bool(nes), zero_from=self.numel, chan=1)
+        own (end of a graph / eager step), with the F12 role's exact
+        workgroup decomposition -- ranks whose run() chunks differ (one
+        closes a step's exchange, its peer runs it inside F12) still pair up
+        block by block."""
+        _lib.check(self.L.pto_ar_role_sgd(*self._fc_role_args(), self._s()), "ar_role_sgd")
 
     def _allreduce_update(self):
         """DDP: gradient all-reduce + SGD (+ zeroing of the accumulated conv

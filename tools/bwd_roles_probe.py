@@ -26,7 +26,7 @@ def so_path(chunk):
 
 def build(chunk=None):
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "kernels"), "-o", so_path(chunk), SRC]
+           "-I", os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "kernels"), "-I", os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "comm"), "-o", so_path(chunk), SRC]
     if chunk is not None:
         cmd.insert(1, f"-DPTO_BWD_WCHUNK={chunk}")
     subprocess.check_call(cmd)
