@@ -2218,89 +2218,3 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bwd_all<BWD_WCHUNK, BWD_WNTW>), dim3(A.nA + A.nB + A.nC + A.nD + A.nF), dim3(256), lds, s, A);
   LAUNCH_CHECK();
 }
-
-// ---------------------------------------------------------- launch plans --
-// A recorded list of the step's launcher calls (every argument bound at
-// record time), replayed by ONE host call: `pto_plan_run` issues the body
-// `reps` times then the tail once, straight into the stream.  The fused
-// trainer uses it for short runs: the first kernel starts a few us after the
-// call instead of after a graph launch's fixed setup (profiles/
-// bench_window_r4.md), and 4 launches per step submit far faster than the
-// GPU executes them.
-#include <functional>
-#include <vector>
-
-namespace {
-struct LaunchPlan {
-  std::vector<std::function<int(hipStream_t)>> ops;
-  size_t body = 0;  // ops[0, body) = one step; ops[body, end) = the tail
-};
-template <class F, class... A>
-int plan_push(void* plan, F fn, A... a) {
-  if (!plan) return -1;
-  static_cast<LaunchPlan*>(plan)->ops.emplace_back([=](hipStream_t s) { return fn(a..., s); });
-  return 0;
-}
-}  // namespace
-
-PTO_API void* pto_plan_create() { return new LaunchPlan; }
-PTO_API int pto_plan_free(void* plan) {
-  delete static_cast<LaunchPlan*>(plan);
-  return 0;
-}
-// Everything recorded so far is the body; what follows is the tail.
-PTO_API int pto_plan_mark_body(void* plan) {
-  if (!plan) return -1;
-  static_cast<LaunchPlan*>(plan)->body = static_cast<LaunchPlan*>(plan)->ops.size();
-  return 0;
-}
-PTO_API int pto_plan_run(void* plan, int reps, int tail, hipStream_t s) {
-  if (!plan || reps < 0) return -1;
-  const LaunchPlan& P = *static_cast<LaunchPlan*>(plan);
-  for (int r = 0; r < reps; ++r)
-    for (size_t i = 0; i < P.body; ++i)
-      if (int rc = P.ops[i](s)) return rc;
-  if (tail)
-    for (size_t i = P.body; i < P.ops.size(); ++i)
-      if (int rc = P.ops[i](s)) return rc;
-  return 0;
-}
-
-PTO_API int pto_plan_conv12_fwd_lazy_x(void* plan, const float* x, const float* w1, const float* b1, const float* w2,
-                                       const float* b2, float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B,
-                                       const long long* bidx, const float* g1f, const float* m1f, int bias_off,
-                                       const int* pending, const float* lr, float mom, float wd, float gscale,
-                                       int nesterov, float* xout, float* w2out, const float* rep, int nrep,
-                                       int rep_stride) {
-  return plan_push(plan, pto_conv12_fwd_lazy_x, x, w1, b1, w2, b2, a1p, code1, a2p, code2, B, bidx, g1f, m1f,
-                   bias_off, pending, lr, mom, wd, gscale, nesterov, xout, w2out, rep, nrep, rep_stride);
-}
-PTO_API int pto_plan_linear_fwd(void* plan, const float* x, const float* w, const float* b, float* y, int M, int N,
-                                int K, int relu) {
-  return plan_push(plan, pto_linear_fwd, x, w, b, y, M, N, K, relu);
-}
-PTO_API int pto_plan_fc2_ce_dx(void* plan, const float* h1, const float* w2, const float* b2, const int64_t* labels,
-                               const float* w1, float* loss_rows, float* dlogits, float* dh1, float* da2p, int B,
-                               float inv_b, const long long* bidx, float* p1, float* g1, float* m1, int n1,
-                               const int* pending, const float* lr, float mom, float wd, float gscale, int nesterov,
-                               float* rep, int nrep, int rep_stride) {
-  return plan_push(plan, pto_fc2_ce_dx, h1, w2, b2, labels, w1, loss_rows, dlogits, dh1, da2p, B, inv_b, bidx, p1, g1,
-                   m1, n1, pending, lr, mom, wd, gscale, nesterov, rep, nrep, rep_stride);
-}
-PTO_API int pto_plan_bwd_all(void* plan, const float* g2, const uint8_t* code2, const float* a1p, const float* w2f,
-                             const float* x, const uint8_t* code1, const float* dh1, const float* a2p, const float* h1,
-                             const float* dl, float* p, float* g, float* m, long long off_fc2w, long long off_fc2b,
-                             long long off_fc1w, long long off_fc1b, long long off_c2w, long long off_c2b,
-                             long long off_c1w, long long off_c1b, int* ctr, long long* bidx, long long nbatches,
-                             int* pending, int B, const float* lr, float mom, float wd, float gscale, int nesterov,
-                             float* c1rep, int nrep, int rep_stride, int grads_only, float* wpart) {
-  return plan_push(plan, pto_bwd_all, g2, code2, a1p, w2f, x, code1, dh1, a2p, h1, dl, p, g, m, off_fc2w, off_fc2b,
-                   off_fc1w, off_fc1b, off_c2w, off_c2b, off_c1w, off_c1b, ctr, bidx, nbatches, pending, B, lr, mom,
-                   wd, gscale, nesterov, c1rep, nrep, rep_stride, grads_only, wpart);
-}
-PTO_API int pto_plan_conv1_commit(void* plan, float* p1, float* g1, float* m1, int n1, int* pending, const float* lr,
-                                  float mom, float wd, float gscale, int nesterov, float* rep, int nrep,
-                                  int rep_stride) {
-  return plan_push(plan, pto_conv1_commit, p1, g1, m1, n1, pending, lr, mom, wd, gscale, nesterov, rep, nrep,
-                   rep_stride);
-}

@@ -34,7 +34,7 @@ HIP_SOURCES = ("kernels/mnist_kernels.hip", "kernels/common_kernels.hip", "kerne
 
 _lock = threading.Lock()
 # launchers return an int hipError; these few return something else
-_RESTYPES = {"pto_ar_timeout_ticks": ctypes.c_longlong, "pto_plan_create": ctypes.c_void_p}
+_RESTYPES = {"pto_ar_timeout_ticks": ctypes.c_longlong}
 _lib = None
 
 
@@ -138,11 +138,6 @@ _SIGS = {
     # causal GQA flash attention, head_dim 128 (csrc/kernels/attention.hip)
     "pto_attn_fwd": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _L, _L, _L, _L, _F, _P],
     "pto_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _L, _L, _L, _L, _F, _P],
-    # launch plans (mnist_kernels.hip): recorded launcher calls replayed by one host call
-    "pto_plan_create": [],
-    "pto_plan_free": [_P],
-    "pto_plan_mark_body": [_P],
-    "pto_plan_run": [_P, _I, _I, _P],
     # xGMI peer all-reduce (csrc/comm/xgmi_allreduce.hip)
     "pto_ar_ipc_handle_size": [],
     "pto_ar_flag_bytes": [_I],
@@ -165,10 +160,6 @@ _SIGS = {
     "pto_ar_allreduce_sgd": [_P, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _F, _I, _L, _P, _L, _P, _I, _I, _L,
                              _P],
 }
-
-
-for _name in ("conv12_fwd_lazy_x", "linear_fwd", "fc2_ce_dx", "bwd_all", "conv1_commit"):
-    _SIGS["pto_plan_" + _name] = [_P] + _SIGS["pto_" + _name][:-1]
 
 
 def lib():

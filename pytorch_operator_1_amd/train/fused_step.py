@@ -78,15 +78,13 @@ class FusedMnistTrainer:
     def __init__(self, device, batch_size=64, lr=0.01, momentum=0.5, dataset_size=60000, seed=1, rank=0,
                  weight_decay=0.0, nesterov=False, graph: str | None = None, comm: str | None = None,
                  data=None, target=None, unroll: int | None = None, force_ddp: bool = False,
-                 overlap: bool | None = None, plan_steps: int | None = None):
+                 overlap: bool | None = None):
         """``graph``: "full" (whole steps in graphs; default), "split"
         (collectives between graphs) or "none" (eager launches).
         ``force_ddp``: the grads-only + all-reduce + SGD-launch schedule at
         world size 1 (the DDP code path in one process).  ``overlap``
         (ddp-xgmi; default on): the fc part of the exchange runs as extra
-        workgroups of the next step's F12 launch.  ``plan_steps``
-        (fused-opt): run() of at most this many steps replays a native
-        launch plan instead of graphs (0: always graphs)."""
+        workgroups of the next step's F12 launch."""
         assert device.type == "cuda", "FusedMnistTrainer runs on a HIP device"
         self.L = _lib.lib()
         self.device = device
@@ -99,7 +97,6 @@ class FusedMnistTrainer:
         self.ddp = self.world > 1 or force_ddp
         self.fused_opt = not self.ddp
         self.unroll = max(1, int(unroll if unroll is not None else os.environ.get("PTO_GRAPH_UNROLL", "32")))
-        self.plan_steps = int(plan_steps if plan_steps is not None else 0)
         self.comm = comm or os.environ.get("PTO_COMM", "auto")
         if self.comm not in ("auto", "xgmi", "rccl"):
             raise ValueError(f"comm must be auto, xgmi or rccl, not {self.comm!r}")
@@ -215,8 +212,6 @@ class FusedMnistTrainer:
             self.comm_info.update(schedule=self.schedule, world_size=self.world, backend=backend,
                                   graph_mode=self.graph_mode)
         self._graphs = None  # [one step] (full) or [forward+backward, optimizer] (split)
-        self._recording = None  # launch plan being recorded (_call)
-        self._plan = None  # fused-opt: the step's launches as a native plan (run() of short runs)
         self._graph_pow: dict[int, torch.cuda.CUDAGraph] = {}
         self._graph_close: dict[int, torch.cuda.CUDAGraph] = {}
 
@@ -250,12 +245,8 @@ class FusedMnistTrainer:
         return _lib.stream_ptr(self.device)
 
     def _call(self, name: str, *args):
-        """Launch ``pto_<name>(*args, stream)``, or -- while a launch plan is
-        being recorded -- append it to the plan (``pto_plan_<name>``)."""
-        if self._recording is not None:
-            _lib.check(getattr(self.L, "pto_plan_" + name)(self._recording, *args), "plan_" + name)
-        else:
-            _lib.check(getattr(self.L, "pto_" + name)(*args, self._s()), name)
+        """Launch ``pto_<name>(*args, stream)`` on the current stream."""
+        _lib.check(getattr(self.L, "pto_" + name)(*args, self._s()), name)
 
     def _opt_args(self):
         """(lr device ptr, momentum, weight decay, grad scale, nesterov)."""
@@ -275,8 +266,6 @@ class FusedMnistTrainer:
         c = _lib.check
         bi = self.batch_idx.data_ptr()
         o = self._opt_args()
-        if fc_owed and self._recording is not None:
-            raise RuntimeError("launch plans record the one-process step only")
         conv1 = (self._params[self._c1:].data_ptr(), self.grads[self._c1:].data_ptr(),
                  self.mom[self._c1:].data_ptr(), self.numel - self._c1)
         if self.fused_opt:
@@ -500,30 +489,6 @@ class FusedMnistTrainer:
             self.comm_info["graph_mode"] = "split (capture failed)"
             self._capture()
 
-    def _build_plan(self):
-        """fused-opt: the step's four launches + the closing conv1 commit,
-        recorded once as a native launch plan (``pto_plan_*``)."""
-        plan = self.L.pto_plan_create()
-        if not plan:
-            raise RuntimeError("pto_plan_create failed")
-        self._recording = plan
-        try:
-            self._forward()
-            self._backward()
-            _lib.check(self.L.pto_plan_mark_body(plan), "plan_mark_body")
-            self._commit_launch()
-        finally:
-            self._recording = None
-        self._plan = plan
-
-    def __del__(self):
-        plan, self._plan = getattr(self, "_plan", None), None
-        if plan:
-            try:
-                self.L.pto_plan_free(plan)
-            except Exception:  # noqa: BLE001 - interpreter shutdown
-                pass
-
     def run(self, n: int, blocking_check: bool = True):
         """Run exactly ``n`` training steps, then check the gradient
         transport's error word (a dead or stalled xGMI peer raises
@@ -532,16 +497,6 @@ class FusedMnistTrainer:
         of waiting for this chunk, so a training loop keeps the device busy
         while it logs."""
         if n <= 0:
-            return
-        if self.fused_opt and self.graph_mode == "full" and n <= self.plan_steps:
-            # a short run: the launches straight from one native call -- the
-            # GPU starts within microseconds instead of after a graph
-            # launch's setup (profiles/bench_window_r4.md)
-            if self._plan is None:
-                self._build_plan()
-            _lib.check(self.L.pto_plan_run(self._plan, n, 1, self._s()), "plan_run")
-            self.steps_done += n
-            self._owed = False
             return
         if self.graph_mode == "full":
             self._ensure_captured()

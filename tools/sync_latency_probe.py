@@ -49,12 +49,6 @@ def main():
         return f
 
     out = {}
-    # short runs: native launch plan vs the closing graph (same steps)
-    tr._build_plan()
-    for n in (1, 5, 20, 64, 200):
-        out[f"plan{n}"] = timed(lambda: tr.L.pto_plan_run(tr._plan, n, 1, tr._s()), reps=20)
-        out[f"graph{n}"] = timed(lambda: tr.run(n), reps=20)
-    print(json.dumps(out), flush=True)
     for name, fl in FLAGS.items():
         rc = hip.hipSetDeviceFlags(ctypes.c_uint(fl))
         cur = ctypes.c_uint(0)
