@@ -112,6 +112,15 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_1shot(const ArPee
   ar_oneshot<SGD, FENCED, AR_THREADS>(peers, off, n4, rank, world, chan, epochs, err, timeout, f, blockIdx.x);
 }
 
+template <bool FENCED>
+__global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_1shot_1bar(const ArPeers* __restrict__ peers,
+                                                                          long long off, long long n4, int rank,
+                                                                          int world, int chan,
+                                                                          uint32_t* __restrict__ epochs, int* err,
+                                                                          long long timeout, ArSgd f) {
+  ar_oneshot<true, FENCED, AR_THREADS, false>(peers, off, n4, rank, world, chan, epochs, err, timeout, f, blockIdx.x);
+}
+
 // The fc all-reduce of the overlapped MNIST step as a launch of its own:
 // EXACTLY the decomposition of the all-reduce role inside the F12 launch
 // (1024-thread workgroups, lean stages, blocks_for(n, world, 1024)), so a
@@ -307,6 +316,50 @@ PTO_API int pto_ar_allreduce_bf16(const void* peers, long long off, long long n,
   else
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce_bf16<false>), g, dim3(AR_THREADS), 0, s, P, off, nv, rank,
                        world, chan, ep, er, g_timeout_ticks);
+  return (int)hipGetLastError();
+}
+
+// One-shot all-reduce + SGD with ONE barrier (ar_oneshot BAR2 = false): the
+// conv part of the overlapped MNIST step.  Same arguments as
+// pto_ar_allreduce_sgd; n <= AR_ONESHOT_MAX and zero_from >= off + n (the
+// call writes nothing into the input range).
+PTO_API int pto_ar_allreduce_sgd_1bar(const void* peers, long long off, long long n, int rank, int world, int chan,
+                                      void* epochs, void* err, float* p, float* m, const float* lr, float mom,
+                                      float wd, float gscale, int nesterov, long long zero_from, long long* bidx,
+                                      long long nbatches, float* rep, int nrep, int rep_stride, long long rep_from,
+                                      hipStream_t s) {
+  if (n % 4 || off % 4 || n > AR_ONESHOT_MAX || world < 1 || world > AR_MAX_RANKS || chan < 0 ||
+      chan >= AR_CHANNELS || rank < 0 || rank >= world || !p || !m || !lr ||
+      ((((uintptr_t)p) | ((uintptr_t)m)) & 15) || (bidx && nbatches < 1) || zero_from < off + n)
+    return -1;
+  if (rep && (nrep < 1 || nrep > AR_MAX_REP || rep_stride % 4 || rep_from % 4 || (((uintptr_t)rep) & 15)))
+    return -1;
+  if (n == 0) return 0;
+  ArSgd f{};
+  f.p = p;
+  f.m = m;
+  f.a.lr = lr;
+  f.a.mom = mom;
+  f.a.wd = wd;
+  f.a.gscale = gscale;
+  f.a.nesterov = nesterov;
+  f.zero_from = zero_from;
+  f.bidx = bidx;
+  f.nbatches = nbatches;
+  f.rep = rep;
+  f.nrep = rep ? nrep : 1;
+  f.rep_stride = rep_stride;
+  f.rep_from = rep_from;
+  const dim3 g((unsigned)((n / 4 + AR_THREADS - 1) / AR_THREADS));
+  const ArPeers* P = reinterpret_cast<const ArPeers*>(peers);
+  if (g_protocol)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce_1shot_1bar<true>), g, dim3(AR_THREADS), 0, s, P, off, n / 4,
+                       rank, world, chan, reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err),
+                       g_timeout_ticks, f);
+  else
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce_1shot_1bar<false>), g, dim3(AR_THREADS), 0, s, P, off, n / 4,
+                       rank, world, chan, reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err),
+                       g_timeout_ticks, f);
   return (int)hipGetLastError();
 }
 

@@ -310,8 +310,13 @@ __device__ __forceinline__ void ar_twostage(const ArPeers* __restrict__ peers, l
   if (SGD && f.bidx && blk == 0 && threadIdx.x == 0) *f.bidx = (*f.bidx + 1) % f.nbatches;
 }
 
-// One-shot variant: n4 <= nblk * NT (one float4 per thread).
-template <bool SGD, bool FENCED, int NT>
+// One-shot variant: n4 <= nblk * NT (one float4 per thread).  BAR2 = false
+// drops the second barrier ("nobody reads my input any more"): only for a
+// caller whose NEXT cross-rank barrier on another channel orders every
+// peer's reads of this call before any write of this rank's input range,
+// and which writes nothing into that range here (zero_from past the range;
+// the MNIST overlap schedule, fused_step.py).
+template <bool SGD, bool FENCED, int NT, bool BAR2 = true>
 __device__ __forceinline__ void ar_oneshot(const ArPeers* __restrict__ peers, long long off, long long n4, int rank,
                                            int world, int chan, uint32_t* __restrict__ epochs, int* err,
                                            long long timeout, const ArSgd& f, int blk) {
@@ -341,7 +346,11 @@ __device__ __forceinline__ void ar_oneshot(const ArPeers* __restrict__ peers, lo
       if (q < world) a = add4(a, v[q]);
   }
   // every peer is done reading my input (on failure: nothing is written)
-  if (!block_barrier<FENCED>(P, chan, 1, blk, rank, world, e, timeout, err)) return;
+  if constexpr (BAR2) {
+    if (!block_barrier<FENCED>(P, chan, 1, blk, rank, world, e, timeout, err)) return;
+  } else {
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  }
   if (act) {
     if constexpr (SGD) {
       const float lr = *f.a.lr;

@@ -806,9 +806,17 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
   const int t = threadIdx.x;
   PTO_STAMP_SCOPE();
   if (blockIdx.x == (unsigned)(mtiles * ntiles)) {
-    if (cm.pending && *cm.pending) {
-      const float lr = *cm.a.lr;
-      for (int i = 4 * t; i < cm.n; i += 4 * FDX_WAVES * 64) commit4(cm, i, lr);
+    if (cm.pending) {
+      if (*cm.pending) {
+        const float lr = *cm.a.lr;
+        for (int i = 4 * t; i < cm.n; i += 4 * FDX_WAVES * 64) commit4(cm, i, lr);
+      }
+    } else if (cm.g) {
+      // overlapped multi-GPU step: zero the atomically accumulated conv
+      // grads for this step's backward (the one-barrier conv all-reduce of
+      // the previous step cannot: peers may still be reading them then)
+      for (int i = 4 * t; i < cm.n; i += 4 * FDX_WAVES * 64)
+        *reinterpret_cast<float4*>(cm.g + i) = float4{0.f, 0.f, 0.f, 0.f};
     }
     return;
   }

@@ -156,6 +156,8 @@ _SIGS = {
     "pto_ar_allreduce": [_P, _L, _L, _I, _I, _I, _P, _P, _P],
     "pto_ar_timeout_ticks": [],
     "pto_ar_allreduce_bf16": [_P, _L, _L, _I, _I, _I, _P, _P, _P],
+    "pto_ar_allreduce_sgd_1bar": [_P, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _F, _I, _L, _P, _L, _P, _I, _I,
+                                  _L, _P],
     "pto_ar_role_sgd": [_P, _L, _L, _I, _I, _I, _P, _P, _I, _P, _P, _P, _F, _F, _F, _I, _L, _P],
     "pto_ar_allreduce_sgd": [_P, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _F, _I, _L, _P, _L, _P, _I, _I, _L,
                              _P],

@@ -146,7 +146,8 @@ class XgmiAllReduce:
     def allreduce_sgd_(self, offset: int, n: int, params: torch.Tensor, mom: torch.Tensor, lr_dev: torch.Tensor,
                        momentum: float, weight_decay: float, gscale: float, nesterov: bool, zero_from: int,
                        cursor: torch.Tensor | None = None, n_batches: int = 1, chan: int = 0, stream=None,
-                       replicas: torch.Tensor | None = None, n_replicas: int = 1, rep_from: int = 0):
+                       replicas: torch.Tensor | None = None, n_replicas: int = 1, rep_from: int = 0,
+                       single_barrier: bool = False):
         """All-reduce ``buf[offset:offset+n]`` and apply SGD-momentum with
         the (``gscale``-scaled) result to ``params``/``mom`` (flat buffers in
         the gradient layout) inside the same launch; the local gradient is
@@ -154,7 +155,11 @@ class XgmiAllReduce:
         advanced mod ``n_batches`` after the update.  ``replicas``: extra
         local copies of the gradient range ``[rep_from, numel)`` (replica r
         >= 1 at ``replicas[(r-1)*(numel-rep_from):]``), folded into the
-        gradient and zeroed before the exchange."""
+        gradient and zeroed before the exchange.  ``single_barrier``: the
+        one-shot form without its second barrier (``pto_ar_allreduce_sgd_1bar``;
+        range <= 65536 floats, nothing zeroed) -- only when the caller's next
+        barrier on another channel already orders the peers' reads of this
+        call before its next write of the range (fused_step.py overlap)."""
         if self.align != 4:
             raise ValueError("XgmiAllReduce: the SGD epilogue needs an fp32 buffer")
         if n % 4 or offset % 4:
@@ -173,7 +178,8 @@ class XgmiAllReduce:
                 raise ValueError("XgmiAllReduce: replica buffer too small for n_replicas")
             rep = replicas.data_ptr()
         _lib.check(_lib.lib().pto_ar_set_protocol(PROTOCOLS[self.protocol]), "ar_set_protocol")
-        _lib.check(_lib.lib().pto_ar_allreduce_sgd(self.peers.data_ptr(), offset, n, self.rank, self.world, chan,
+        fn = _lib.lib().pto_ar_allreduce_sgd_1bar if single_barrier else _lib.lib().pto_ar_allreduce_sgd
+        _lib.check(fn(self.peers.data_ptr(), offset, n, self.rank, self.world, chan,
                                                    self.epochs.data_ptr(), self.err.data_ptr(), params.data_ptr(),
                                                    mom.data_ptr(), lr_dev.data_ptr(), momentum, weight_decay, gscale,
                                                    int(nesterov), zero_from, cur, n_batches, rep,

@@ -276,6 +276,11 @@ class FusedMnistTrainer:
             rep = (None, 1, 0)
             lazy = (None, None, 0, None, None, 0.0, 0.0, 1.0, 0)
             w2out, pending = None, None
+            # F4dx's spare block: with the overlap, it zeroes the conv grads
+            # (whole conv range) for this step's backward; otherwise idle
+            conv1 = ((self._params[self._split:].data_ptr(), self.grads[self._split:].data_ptr(),
+                      self.mom[self._split:].data_ptr(), self.numel - self._split) if self.overlap
+                     else (conv1[0], None, conv1[2], conv1[3]))
         if only in (None, 0) and fc_owed:
             c(L.pto_conv12_fwd_ar(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
                                   P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
@@ -327,12 +332,16 @@ class FusedMnistTrainer:
         grads and the cursor advance).  ddp-xgmi overlap: the conv range
         only (the fc range is owed to the next F12 / the closing launch)."""
         if self._xgmi is not None and self.overlap:
+            # one barrier: the fc exchange that follows (channel 1, in the
+            # next F12 or the closing launch) orders every peer's reads of
+            # these conv grads before this rank's next write of them -- the
+            # zeroing in the next F4dx and the next backward's atomics
             lr, mom, wd, gs, nes = self._opt_args()
             self._xgmi.allreduce_sgd_(self._split, self.numel - self._split, params=self._params, mom=self.mom,
                                       lr_dev=self.lr_dev, momentum=mom, weight_decay=wd, gscale=gs,
-                                      nesterov=bool(nes), zero_from=self._split, cursor=self.batch_idx,
+                                      nesterov=bool(nes), zero_from=self.numel, cursor=self.batch_idx,
                                       n_batches=self.n_batches, replicas=self.c1rep, n_replicas=self.c1_nrep,
-                                      rep_from=self._c1, chan=0)
+                                      rep_from=self._c1, chan=0, single_barrier=True)
             return
         if self._xgmi is not None:
             lr, mom, wd, gs, nes = self._opt_args()
