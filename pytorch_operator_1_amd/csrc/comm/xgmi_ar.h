@@ -239,8 +239,19 @@ __device__ __forceinline__ void ar_twostage(const ArPeers* __restrict__ peers, l
     for (long long i = c0 + j0; i < c1; i += stride, ++it) {
       float4 a;
       if constexpr (LEAN) {
+        // up to 4 ranks' loads in flight at once (a rank-by-rank chain would
+        // pay one cross-GPU round trip per rank), summed in rank order
         a = ld4<CO>(mkbuf(P->in[0] + off, bytes), i);
-        for (int q = 1; q < world; ++q) a = add4(a, ld4<CO>(mkbuf(P->in[q] + off, bytes), i));
+#pragma unroll
+        for (int q0 = 1; q0 < AR_MAX_RANKS; q0 += 2) {
+          float4 v[2];
+#pragma unroll
+          for (int k = 0; k < 2; ++k)
+            if (q0 + k < world) v[k] = ld4<CO>(mkbuf(P->in[q0 + k] + off, bytes), i);
+#pragma unroll
+          for (int k = 0; k < 2; ++k)
+            if (q0 + k < world) a = add4(a, v[k]);
+        }
       } else {
         float4 v[AR_MAX_RANKS];
 #pragma unroll
@@ -261,6 +272,8 @@ __device__ __forceinline__ void ar_twostage(const ArPeers* __restrict__ peers, l
   if (!block_barrier<FENCED>(P, chan, 1, blk, rank, world, e, timeout, err)) return;
   // stage 2: gather every chunk into my input (or: update my parameters)
   if constexpr (LEAN) {
+    // one rank's chunk element per round (the register cap of the host
+    // kernel); its peer load and the local p/m loads go out together
     for (long long j = j0; j < cs; j += stride)
       for (int q = 0; q < world; ++q) {
         const long long k = q * cs + j;

@@ -644,24 +644,30 @@ class FusedMnistTrainer:
         self.set_lr(float(sd.get("lr", self.lr)))
 
 
-def autotune_schedule(xg: FusedMnistTrainer, rc: FusedMnistTrainer, verify_steps: int = 8, reps: int = 3) -> dict:
-    """Decide between the ``ddp-xgmi`` and ``ddp-rccl`` multi-GPU steps on
-    the steps themselves: both trainers (same init, same data) run
-    ``verify_steps`` captured steps -- the xGMI all-reduce with its SGD
-    epilogue and replica fold vs graph-captured RCCL + ``k_ddp_sgd`` -- and
-    their parameters must agree (max relative error per tensor <= 1e-4,
-    different summation orders) and the xGMI ranks must be bit-identical;
-    then each replays ``reps`` of its ``unroll``-step graph, timed on the
-    host (max over ranks).  Both trainers are rolled back to their initial
-    state.  Collective: every rank calls it with the same trainers."""
+def _variant(tr: FusedMnistTrainer) -> str:
+    return tr.schedule + ("+overlap" if tr.overlap else "")
+
+
+def autotune_schedule(cands: list, rc: FusedMnistTrainer, verify_steps: int = 8, reps: int = 3) -> dict:
+    """Decide between multi-GPU step variants on the steps themselves: the
+    xGMI candidates (``ddp-xgmi`` with and without the F12 overlap) and the
+    ``ddp-rccl`` reference trainer ``rc`` (same init, same data) each run
+    ``verify_steps`` captured steps; every candidate's parameters must agree
+    with the RCCL step's (max relative error per tensor <= 1e-4: different
+    summation orders) and be bit-identical on every rank.  Then each
+    replays ``reps`` of its ``unroll``-step graph, timed on the host (max
+    over ranks), and the fastest correct one is kept.  Every trainer is
+    rolled back to its initial state.  Collective: every rank calls it with
+    the same trainers in the same order."""
     from ..utils import dist as pdist
 
-    dev = xg.device
-    snaps = [[t.clone() for t in tr._state()] for tr in (xg, rc)]
+    dev = rc.device
+    everyone = list(cands) + [rc]
+    snaps = [[t.clone() for t in tr._state()] for tr in everyone]
 
     def restore():
         torch.cuda.synchronize(dev)
-        for tr, snap in zip((xg, rc), snaps):
+        for tr, snap in zip(everyone, snaps):
             for d, s_ in zip(tr._state(), snap):
                 d.copy_(s_)
             tr.steps_done, tr._owed = 0, False
@@ -672,41 +678,49 @@ def autotune_schedule(xg: FusedMnistTrainer, rc: FusedMnistTrainer, verify_steps
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return t.item() == 1.0
 
-    out: dict = {"verify_steps": verify_steps, "timed_steps": reps * xg.unroll}
+    def timed(tr) -> float:
+        tr._align_ranks("tune-time")
+        tr.run(tr.unroll)  # warm
+        torch.cuda.synchronize(dev)
+        pdist.barrier(dev)
+        tr._align_ranks("tune-time2")
+        t0 = time.perf_counter()
+        tr.run(reps * tr.unroll)
+        torch.cuda.synchronize(dev)
+        return pdist.all_reduce_max((time.perf_counter() - t0) / (reps * tr.unroll) * 1e6, dev)
+
+    out: dict = {"verify_steps": verify_steps, "timed_steps": reps * rc.unroll, "candidates": {}}
     try:
-        xg._align_ranks("tune-verify")
-        xg.run(verify_steps)
         rc.run(verify_steps)
         torch.cuda.synchronize(dev)
-        err = 0.0
-        for name, pv in xg.p.items():
-            ref = rc.p[name]
-            err = max(err, float((pv - ref).abs().max() / ref.abs().max().clamp_min(1e-12)))
-        mine = xg.params.detach().clone()
-        chk = mine.clone() if dist.get_backend() == "nccl" else mine.cpu()
-        dist.all_reduce(chk, op=dist.ReduceOp.MAX)
-        identical = bool(torch.equal(chk.to(mine.device), mine))
-        out.update(param_rel_err=err, identical=identical)
-        ok = agree(err <= 1e-4 and identical and xg._xgmi.error_word() == 0)
-        out["correct"] = ok
-
-        def timed(tr) -> float:
-            tr._align_ranks("tune-time")
-            tr.run(tr.unroll)  # warm
+        ok_c = []
+        for xg in cands:
+            xg._align_ranks("tune-verify")
+            xg.run(verify_steps)
             torch.cuda.synchronize(dev)
-            pdist.barrier(dev)
-            tr._align_ranks("tune-time2")
-            t0 = time.perf_counter()
-            tr.run(reps * tr.unroll)
-            torch.cuda.synchronize(dev)
-            return pdist.all_reduce_max((time.perf_counter() - t0) / (reps * tr.unroll) * 1e6, dev)
-
-        if ok:
-            out["xgmi_step_us"] = round(timed(xg), 2)
-            out["rccl_step_us"] = round(timed(rc), 2)
-            ok = agree(xg._xgmi.error_word() == 0)
-            out["correct"] = ok
-        out["kept"] = "ddp-xgmi" if ok and out["xgmi_step_us"] <= out["rccl_step_us"] else "ddp-rccl"
+            err = 0.0
+            for name, pv in xg.p.items():
+                ref = rc.p[name]
+                err = max(err, float((pv - ref).abs().max() / ref.abs().max().clamp_min(1e-12)))
+            mine = xg.params.detach().clone()
+            chk = mine.clone() if dist.get_backend() == "nccl" else mine.cpu()
+            dist.all_reduce(chk, op=dist.ReduceOp.MAX)
+            identical = bool(torch.equal(chk.to(mine.device), mine))
+            ok = agree(err <= 1e-4 and identical and xg._xgmi.error_word() == 0)
+            out["candidates"][_variant(xg)] = {"param_rel_err": err, "identical": identical, "correct": ok}
+            ok_c.append(ok)
+        times = {}
+        for xg, ok in zip(cands, ok_c):
+            if ok:
+                t = timed(xg)
+                ok = agree(xg._xgmi.error_word() == 0)
+                out["candidates"][_variant(xg)].update(step_us=round(t, 2), correct=ok)
+                if ok:
+                    times[_variant(xg)] = t
+        times[_variant(rc)] = timed(rc)
+        out["candidates"][_variant(rc)] = {"step_us": round(times[_variant(rc)], 2)}
+        out["kept"] = min(times, key=times.get)
+        out["correct"] = all(ok_c)
     finally:
         restore()
     return out
@@ -715,24 +729,34 @@ def autotune_schedule(xg: FusedMnistTrainer, rc: FusedMnistTrainer, verify_steps
 def build_fused_trainer(device, **kw) -> FusedMnistTrainer:
     """The fused trainer, with the multi-GPU schedule chosen on the real
     links: at world size > 1 and ``comm="auto"`` (``PTO_COMM``), a trainer
-    whose verified xGMI all-reduce was set up is raced against an RCCL-
-    schedule twin on the same data (:func:`autotune_schedule`); the faster
-    is returned (the other's peer mappings are closed) and the race is
-    recorded in ``comm_info["schedule_autotune"]``."""
+    whose verified xGMI all-reduce was set up (F12-overlapped) is raced
+    against a whole-buffer xGMI twin and an RCCL-schedule twin on the same
+    data (:func:`autotune_schedule`); the fastest is returned (the others'
+    peer mappings are closed) and the race is recorded in
+    ``comm_info["schedule_autotune"]``."""
     comm = kw.get("comm") or os.environ.get("PTO_COMM", "auto")
     tr = FusedMnistTrainer(device, **kw)
     if tr.world == 1 or comm != "auto" or tr.schedule != "ddp-xgmi":
         return tr
-    twin_kw = dict(kw, comm="rccl", data=tr.data.view(-1, 784), target=tr.target.view(-1))
-    twin = FusedMnistTrainer(device, **twin_kw)
-    res = autotune_schedule(tr, twin)
-    keep, drop = (tr, twin) if res["kept"] == "ddp-xgmi" else (twin, tr)
-    if drop._xgmi is not None:
-        torch.cuda.synchronize(device)
-        drop._graphs, drop._graph_pow, drop._graph_close = None, {}, {}
-        drop._xgmi.close()
-        drop._xgmi = None
+    data = dict(data=tr.data.view(-1, 784), target=tr.target.view(-1))
+    cands = [tr]
+    if tr.overlap:
+        plain = FusedMnistTrainer(device, **dict(kw, comm="xgmi", overlap=False, **data))
+        if plain.schedule == "ddp-xgmi":
+            cands.append(plain)
+    twin = FusedMnistTrainer(device, **dict(kw, comm="rccl", **data))
+    res = autotune_schedule(cands, twin)
+    everyone = cands + [twin]
+    keep = next(t for t in everyone if _variant(t) == res["kept"])
+    for drop in everyone:
+        if drop is keep:
+            continue
+        if drop._xgmi is not None:
+            torch.cuda.synchronize(device)
+            drop._graphs, drop._graph_pow, drop._graph_close = None, {}, {}
+            drop._xgmi.close()
+            drop._xgmi = None
     keep.comm_info["schedule_autotune"] = res
-    if keep is twin:
+    if keep._xgmi is None:
         keep.comm_info["xgmi_verify"] = {k: v for k, v in tr.comm_info.items() if k != "world_size"}
     return keep

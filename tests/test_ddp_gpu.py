@@ -63,8 +63,12 @@ def _worker(rank, world, port, q, comm, steps=STEPS):
         # the collective step on the same data, both rolled back afterwards
         tr = build_fused_trainer(dev, batch_size=64, dataset_size=N, seed=1, rank=rank, comm="auto")
         res = tr.comm_info["schedule_autotune"]
-        assert res["correct"] and res["identical"] and res["param_rel_err"] < 1e-4, res
-        assert res["kept"] == tr.schedule and res["xgmi_step_us"] > 0 and res["rccl_step_us"] > 0, res
+        cands = res["candidates"]
+        assert res["correct"] and set(cands) == {"ddp-xgmi+overlap", "ddp-xgmi", "ddp-rccl"}, res
+        for name in ("ddp-xgmi+overlap", "ddp-xgmi"):
+            assert cands[name]["identical"] and cands[name]["param_rel_err"] < 1e-4, res
+        assert all(c["step_us"] > 0 for c in cands.values()), res
+        assert res["kept"] == tr.schedule + ("+overlap" if tr.overlap else ""), res
         assert tr.steps_done == 0 and int(tr.batch_idx.item()) == 0
     else:
         tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=N, seed=1, rank=rank, comm=comm)
