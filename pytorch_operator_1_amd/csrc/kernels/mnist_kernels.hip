@@ -31,6 +31,8 @@
 // kernels that read x / labels take a device pointer to the current batch
 // index (`bidx`, advanced by the SGD launch), so a captured HIP graph walks
 // the dataset without any copy kernels.
+#include <stdlib.h>
+
 #include "mfma_f32.h"
 #include "sgd_f32.h"
 #include "xgmi_ar.h"
@@ -1721,7 +1723,30 @@ struct BwdAllArgs {
   // the cursor is left alone
   int grads_only;
   float* g2b; float* g1w; float* g1b; float* gfw; float* gfb;  // grad slots of conv2.bias, fc1.w/b, fc2.w/b
+  // dW1 tiles done by the dgrad blocks after their own work (one wave per
+  // tile, no LDS) instead of by nD blocks of their own that queue behind
+  // the LDS-heavy roles (nD = 0 then)
+  int d_in_b;
 };
+
+// One dW1 tile (16x16 of fc1.weight's gradient, K = batch) by one wave:
+// SGD epilogue (one process) or a store into the flat grad buffer.
+PTO_DEV void dw1_wave_tile(const BwdAllArgs& A, int tile) {
+  if (A.grads_only) {
+    constexpr int MT = (F1OUT + 15) / 16;
+    if (tile >= MT * ((F1IN + 15) / 16)) return;
+    const int mt = tile % MT, nt = tile / MT, lane = threadIdx.x & 63;
+    const f32x4 acc = wave_tile_16x16<LAY_KROW, LAY_KROW, 4>(A.dh1, F1OUT, A.a2p, F1IN, F1OUT, F1IN, A.B, mt * 16,
+                                                             nt * 16, 0, A.B);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int m = mt * 16 + (lane >> 4) * 4 + rr, n = nt * 16 + (lane & 15);
+      if (m < F1OUT && n < F1IN) A.g1w[m * F1IN + n] = acc[rr];
+    }
+  } else {
+    dw1_sgd_tile(tile, A.dh1, A.a2p, A.p1w, A.m1w, A.B, A.a);
+  }
+}
 
 struct EpiSgd {
   float* p; float* m; int ld; float lr; const SgdArgs* a;
@@ -1857,6 +1882,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
     float* gb1 = r == 0 ? A.gb1 : A.c1rep + (r - 1) * A.rep_stride + A.bias_off;
     c2_dgrad_block(bid, smem, A.g2, A.code2, A.w2f, nullptr, A.B, A.x, nullptr, A.code1, gw1, gb1,
                    A.wpart != nullptr);
+    if (A.d_in_b) dw1_wave_tile(A, wv * A.nB + bid);  // waves 0, 1 of every block, wave 2 of the first ones
     return;
   }
   bid -= A.nB;
@@ -2217,7 +2243,9 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   A.nA = ((B + BWD_WCHUNK - 1) / BWD_WCHUNK) * (32 / BWD_WNTW);
   A.nB = B * B2_ICG;
   A.nC = (C2 + 3) / 4;
-  A.nD = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
+  static const int d_in_b = getenv("PTO_BWD_D_IN_B") ? atoi(getenv("PTO_BWD_D_IN_B")) : 0;  // A/B probe
+  A.d_in_b = d_in_b && 4 * A.nB >= ((F1OUT + 15) / 16) * ((F1IN + 15) / 16);
+  A.nD = A.d_in_b ? 0 : (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
   A.nF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9;
   A.wpart = wpart;
   const size_t ldsA = wgrad_lds_floats<BWD_WCHUNK, BWD_WNTW>() * sizeof(float);
