@@ -123,7 +123,7 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_1shot_1bar(const 
 
 // The fc all-reduce of the overlapped MNIST step as a launch of its own:
 // EXACTLY the decomposition of the all-reduce role inside the F12 launch
-// (1024-thread workgroups, lean stages, blocks_for(n, world, 1024)), so a
+// (1024-thread workgroups, ar_role_sgd, role_blocks(n, world, 1024)), so a
 // rank that runs a step's fc exchange stand-alone interoperates with a peer
 // that ran the same exchange inside its F12 (block b covers the same
 // elements and advances the same epoch either way).
@@ -133,8 +133,8 @@ __global__ __launch_bounds__(AR_ROLE_THREADS) void k_xgmi_allreduce_role(const A
                                                                           long long n4, int rank, int world, int chan,
                                                                           uint32_t* __restrict__ epochs, int* err,
                                                                           long long timeout, ArSgd f) {
-  ar_twostage<true, FENCED, AR_ROLE_THREADS, true>(peers, off, n4, rank, world, chan, epochs, err, timeout, f,
-                                                    blockIdx.x, gridDim.x);
+  __shared__ float4 lds[AR_ROLE_THREADS];
+  ar_role_sgd<FENCED, AR_ROLE_THREADS>(peers, off, n4, rank, world, chan, epochs, err, timeout, f, blockIdx.x, lds);
 }
 
 template <bool FENCED>
@@ -384,7 +384,9 @@ PTO_API int pto_ar_role_sgd(const void* peers, long long off, long long n, int r
   f.nbatches = 1;
   f.nrep = 1;
   const ArPeers* P = reinterpret_cast<const ArPeers*>(peers);
-  const dim3 g((unsigned)blocks_for(n, world, AR_ROLE_THREADS));
+  const int nb = role_blocks(n, world, AR_ROLE_THREADS);
+  if (nb > AR_MAX_BLOCKS) return -1;
+  const dim3 g((unsigned)nb);
   if (protocol)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce_role<true>), g, dim3(AR_ROLE_THREADS), 0, s, P, off, n / 4,
                        rank, world, chan, reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err),

@@ -379,6 +379,66 @@ __device__ __forceinline__ void ar_oneshot(const ArPeers* __restrict__ peers, lo
   if (SGD && f.bidx && blk == 0 && threadIdx.x == 0) *f.bidx = (*f.bidx + 1) % f.nbatches;
 }
 
+// ------------------------------------------------------- rank-split role --
+// The all-reduce + SGD as a ROLE inside a register-capped kernel (the MNIST
+// forward launch, <= 64 VGPRs): every thread has exactly ONE float4 in
+// flight per stage, whatever the world size, because the block's NT threads
+// are split into W groups of S = NT / W, group q handling rank q:
+//   stage 1  thread (q, s) loads rank q's element s of this block's
+//            sub-range of MY chunk into LDS; the first S threads sum the W
+//            values in rank order (only this rank computes its chunk's sum,
+//            so the order is fixed) and store it write-through into tmp;
+//   stage 2  thread (q, s) loads element s of the sub-range of chunk q from
+//            rank q's tmp, applies SGD to the local parameter/momentum.
+// Block b covers sub-range [b*S, b*S + S) of every chunk on every rank (the
+// pairing the per-block barriers rely on), so nblk = ceil(chunk / S) ~ n4 /
+// NT blocks at any W -- more blocks, not more serial rounds, as W grows.
+// lds: NT float4 of scratch.  No replica fold, no cursor.
+__host__ __device__ inline int role_blocks(long long n, int world, int nt) {
+  const long long cs = ((n / 4) + world - 1) / world, S = nt / world;
+  return (int)((cs + S - 1) / S);
+}
+template <bool FENCED, int NT>
+__device__ __forceinline__ void ar_role_sgd(const ArPeers* __restrict__ P, long long off, long long n4, int rank,
+                                            int world, int chan, uint32_t* __restrict__ epochs, int* err,
+                                            long long timeout, const ArSgd& f, int blk, float4* lds) {
+  constexpr bool CO = !FENCED;
+  __shared__ uint32_t s_epoch;
+  if (threadIdx.x == 0) s_epoch = epochs[chan * AR_MAX_BLOCKS + blk] + 1;
+  __syncthreads();
+  const uint32_t e = s_epoch;
+  if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blk] = e;
+  const long long cs = (n4 + world - 1) / world;
+  const int S = NT / world;
+  const int q = threadIdx.x / S, sidx = threadIdx.x - q * S;
+  const bool in_group = q < world;
+  const long long j = (long long)blk * S + sidx;  // element of every chunk this thread covers
+  const long long bytes = n4 * 16;
+  if (!block_barrier<FENCED>(P, chan, 0, blk, rank, world, e, timeout, err)) return;
+  // stage 1: my chunk's element j from rank q -> LDS, then rank-order sums
+  const long long i1 = (long long)rank * cs + j;
+  const bool v1 = in_group && j < cs && i1 < n4;
+  if (v1) lds[q * S + sidx] = ld4<CO>(mkbuf(P->in[q] + off, bytes), i1);
+  __syncthreads();
+  if (q == 0 && v1) {
+    float4 a = lds[sidx];
+    for (int r = 1; r < world; ++r) a = add4(a, lds[r * S + sidx]);
+    st4<CO>(mkbuf(P->tmp[rank] + off, bytes), i1, a);
+  }
+  const float lr = *f.a.lr;
+  if (!block_barrier<FENCED>(P, chan, 1, blk, rank, world, e, timeout, err)) return;
+  // stage 2: element j of chunk q from rank q's partial sums
+  const long long k = (long long)q * cs + j;
+  if (in_group && j < cs && k < n4) {
+    const float4 v = ld4<CO>(mkbuf(P->tmp[q] + off, bytes), k);
+    const long long i = off + 4 * k;
+    float4 pv = gld4(f.p + i);
+    float4 mv = gld4(f.m + i);
+    sgd4(f, i, v, pv, mv, lr);
+    if (i >= f.zero_from) gst4(P->in[rank] + i, float4{0.f, 0.f, 0.f, 0.f});
+  }
+}
+
 // ---------------------------------------------------------------- bf16 --
 // Plain SUM all-reduce of bf16 gradient buckets (the large-model DDP comm
 // hook, parallel/ddp.py): 16-byte vectors of 8 bf16, summed in fp32 in rank

@@ -298,9 +298,10 @@ __global__ __launch_bounds__(256) void k_conv2_fwd(const float* __restrict__ a1p
 //    LDS, so each SIMD interleaves independent MFMA chains.
 //  * lazy conv1 update (one-process schedule, LazyConv1), the image copy
 //    for the backward (xout) and the conv2.weight snapshot (w2out).
-//  * ARM != 0 (overlapped multi-GPU step, fused_step.py "ddp-xgmi"): blocks
-//    >= 4B are the PREVIOUS step's fc-gradient all-reduce + SGD epilogue
-//    (xgmi_ar.h two-stage, protocol ARM-1), which nothing here reads.  The
+//  * ARM != 0 (overlapped multi-GPU step, fused_step.py "ddp-xgmi"): the
+//    first ar.nblk blocks are the PREVIOUS step's fc-gradient all-reduce +
+//    SGD epilogue (xgmi_ar.h ar_role_sgd, protocol ARM-1), which nothing
+//    here reads.  The
 //    kernel is capped at 64 VGPRs (8 waves per SIMD) so an all-reduce block
 //    fits on a CU next to a conv block (61 KB of LDS each) and the exchange
 //    runs concurrently with the convolutions instead of after them.
@@ -326,8 +327,9 @@ __global__ __launch_bounds__(NTH, ARM ? 2 * NTH / 256 : 1) void k_conv12_fwd2_t(
   int bx = (int)blockIdx.x;
   if constexpr (ARM != 0) {
     if (bx < ar.nblk) {
-      pto_ar::ar_twostage<true, ARM == 2, NTH, true>(ar.peers, ar.off, ar.n4, ar.rank, ar.world, ar.chan, ar.epochs,
-                                                  ar.err, ar.timeout, ar.f, bx, ar.nblk);
+      __shared__ float4 ar_lds[NTH];
+      pto_ar::ar_role_sgd<ARM == 2, NTH>(ar.peers, ar.off, ar.n4, ar.rank, ar.world, ar.chan, ar.epochs, ar.err,
+                                         ar.timeout, ar.f, bx, ar_lds);
       return;
     }
     bx -= ar.nblk;
@@ -2051,7 +2053,8 @@ PTO_API int pto_conv12_fwd_ar(const float* x, const float* w1, const float* b1, 
   ar.rank = rank;
   ar.world = world;
   ar.chan = chan;
-  ar.nblk = blocks_for(n, world, 1024);
+  ar.nblk = role_blocks(n, world, 1024);
+  if (ar.nblk > AR_MAX_BLOCKS) return -1;
   ar.epochs = reinterpret_cast<uint32_t*>(epochs);
   ar.err = reinterpret_cast<int*>(err);
   ar.timeout = pto_ar_timeout_ticks();
