@@ -364,10 +364,13 @@ PTO_API int pto_ar_allreduce_sgd_1bar(const void* peers, long long off, long lon
 }
 
 // Stand-alone launch of the all-reduce-with-SGD ROLE (same arguments as
-// pto_conv12_fwd_ar's role part, same workgroup decomposition).
+// pto_conv12_fwd_ar's role part, same workgroup decomposition), plus an
+// optional local range [ztail, ztail + ztail_n) zeroed after barrier 0.
 PTO_API int pto_ar_role_sgd(const void* peers, long long off, long long n, int rank, int world, int chan, void* epochs,
                             void* err, int protocol, float* p, float* m, const float* lr, float mom, float wd,
-                            float gscale, int nesterov, long long zero_from, hipStream_t s) {
+                            float gscale, int nesterov, long long zero_from, float* ztail, long long ztail_n,
+                            hipStream_t s) {
+  if (ztail_n % 4 || ztail_n < 0 || (ztail && (((uintptr_t)ztail) & 15))) return -1;
   if (n <= AR_ONESHOT_MAX || n % 4 || off % 4 || n > AR_MAX_FLOATS || world < 1 || world > AR_MAX_RANKS ||
       chan < 0 || chan >= AR_CHANNELS || rank < 0 || rank >= world || !p || !m || !lr || !peers || protocol < 0 ||
       protocol > 1 || ((((uintptr_t)p) | ((uintptr_t)m)) & 15))
@@ -383,6 +386,8 @@ PTO_API int pto_ar_role_sgd(const void* peers, long long off, long long n, int r
   f.zero_from = zero_from;
   f.nbatches = 1;
   f.nrep = 1;
+  f.ztail = ztail_n ? ztail : nullptr;
+  f.ztail4 = ztail_n / 4;
   const ArPeers* P = reinterpret_cast<const ArPeers*>(peers);
   const int nb = role_blocks(n, world, AR_ROLE_THREADS);
   if (nb > AR_MAX_BLOCKS) return -1;

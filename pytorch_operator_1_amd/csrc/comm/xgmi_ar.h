@@ -157,6 +157,12 @@ struct ArSgd {
   float* rep;
   int nrep, rep_stride;
   long long rep_from;
+  // optional local float4 range zeroed once barrier 0 has passed (every peer
+  // has then finished the launches it queued before this one): the closing
+  // fc exchange of the overlapped MNIST step clears the conv gradients the
+  // one-shot conv exchange left behind, so a run() ends with zero gradients
+  float* ztail;
+  long long ztail4;
 };
 
 // Fold the local replicas into float4 element i4 (float offset 4*i4 from the
@@ -415,6 +421,11 @@ __device__ __forceinline__ void ar_role_sgd(const ArPeers* __restrict__ P, long 
   const long long j = (long long)blk * S + sidx;  // element of every chunk this thread covers
   const long long bytes = n4 * 16;
   if (!block_barrier<FENCED>(P, chan, 0, blk, rank, world, e, timeout, err)) return;
+  if (f.ztail) {
+    const long long nt = (long long)role_blocks(4 * n4, world, NT) * NT;
+    for (long long z = (long long)blk * NT + threadIdx.x; z < f.ztail4; z += nt)
+      gst4(f.ztail + 4 * z, float4{0.f, 0.f, 0.f, 0.f});
+  }
   // stage 1: my chunk's element j from rank q -> LDS, then rank-order sums
   const long long i1 = (long long)rank * cs + j;
   const bool v1 = in_group && j < cs && i1 < n4;

@@ -31,8 +31,6 @@
 // kernels that read x / labels take a device pointer to the current batch
 // index (`bidx`, advanced by the SGD launch), so a captured HIP graph walks
 // the dataset without any copy kernels.
-#include <stdlib.h>
-
 #include "mfma_f32.h"
 #include "sgd_f32.h"
 #include "xgmi_ar.h"
@@ -815,12 +813,6 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
         const float lr = *cm.a.lr;
         for (int i = 4 * t; i < cm.n; i += 4 * FDX_WAVES * 64) commit4(cm, i, lr);
       }
-    } else if (cm.g) {
-      // overlapped multi-GPU step: zero the atomically accumulated conv
-      // grads for this step's backward (the one-barrier conv all-reduce of
-      // the previous step cannot: peers may still be reading them then)
-      for (int i = 4 * t; i < cm.n; i += 4 * FDX_WAVES * 64)
-        *reinterpret_cast<float4*>(cm.g + i) = float4{0.f, 0.f, 0.f, 0.f};
     }
     return;
   }
@@ -1725,30 +1717,7 @@ struct BwdAllArgs {
   // the cursor is left alone
   int grads_only;
   float* g2b; float* g1w; float* g1b; float* gfw; float* gfb;  // grad slots of conv2.bias, fc1.w/b, fc2.w/b
-  // dW1 tiles done by the dgrad blocks after their own work (one wave per
-  // tile, no LDS) instead of by nD blocks of their own that queue behind
-  // the LDS-heavy roles (nD = 0 then)
-  int d_in_b;
 };
-
-// One dW1 tile (16x16 of fc1.weight's gradient, K = batch) by one wave:
-// SGD epilogue (one process) or a store into the flat grad buffer.
-PTO_DEV void dw1_wave_tile(const BwdAllArgs& A, int tile) {
-  if (A.grads_only) {
-    constexpr int MT = (F1OUT + 15) / 16;
-    if (tile >= MT * ((F1IN + 15) / 16)) return;
-    const int mt = tile % MT, nt = tile / MT, lane = threadIdx.x & 63;
-    const f32x4 acc = wave_tile_16x16<LAY_KROW, LAY_KROW, 4>(A.dh1, F1OUT, A.a2p, F1IN, F1OUT, F1IN, A.B, mt * 16,
-                                                             nt * 16, 0, A.B);
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int m = mt * 16 + (lane >> 4) * 4 + rr, n = nt * 16 + (lane & 15);
-      if (m < F1OUT && n < F1IN) A.g1w[m * F1IN + n] = acc[rr];
-    }
-  } else {
-    dw1_sgd_tile(tile, A.dh1, A.a2p, A.p1w, A.m1w, A.B, A.a);
-  }
-}
 
 struct EpiSgd {
   float* p; float* m; int ld; float lr; const SgdArgs* a;
@@ -1884,7 +1853,6 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
     float* gb1 = r == 0 ? A.gb1 : A.c1rep + (r - 1) * A.rep_stride + A.bias_off;
     c2_dgrad_block(bid, smem, A.g2, A.code2, A.w2f, nullptr, A.B, A.x, nullptr, A.code1, gw1, gb1,
                    A.wpart != nullptr);
-    if (A.d_in_b) dw1_wave_tile(A, wv * A.nB + bid);  // waves 0, 1 of every block, wave 2 of the first ones
     return;
   }
   bid -= A.nB;
@@ -2033,14 +2001,18 @@ extern "C" long long pto_ar_timeout_ticks();
 // F12 (plain forward: no lazy conv1 update) + the all-reduce of float range
 // [off, off + n) of the registered gradient buffers with the SGD epilogue on
 // p/m (zero_from: local gradient zeroed from there on), as extra workgroups
-// of the same launch (ArRole).  protocol: 0 coherent, 1 fenced -- the one
+// of the same launch (ArRole); [ztail, ztail + ztail_n) (the conv gradients
+// of the previous step, read by the peers' conv exchange) is zeroed by the
+// role's workgroups once their first barrier has passed.  protocol: 0 coherent, 1 fenced -- the one
 // the XgmiAllReduce instance of `peers` uses.
 PTO_API int pto_conv12_fwd_ar(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
                               float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B, const long long* bidx,
                               float* xout, const void* peers, long long off, long long n, int rank, int world,
                               int chan, void* epochs, void* err, int protocol, float* p, float* m, const float* lr,
-                              float mom, float wd, float gscale, int nesterov, long long zero_from, hipStream_t s) {
+                              float mom, float wd, float gscale, int nesterov, long long zero_from, float* ztail,
+                              long long ztail_n, hipStream_t s) {
   using namespace pto_ar;
+  if (ztail_n % 4 || ztail_n < 0 || (ztail && (((uintptr_t)ztail) & 15))) return -1;
   if (n <= AR_ONESHOT_MAX || n % 4 || off % 4 || n > (1LL << 29) || world < 1 || world > AR_MAX_RANKS || chan < 0 ||
       chan >= AR_CHANNELS || rank < 0 || rank >= world || !p || !m || !lr || !peers || protocol < 0 || protocol > 1 ||
       ((((uintptr_t)p) | ((uintptr_t)m)) & 15))
@@ -2067,6 +2039,8 @@ PTO_API int pto_conv12_fwd_ar(const float* x, const float* w1, const float* b1, 
   ar.f.nbatches = 1;
   ar.f.rep = nullptr;
   ar.f.nrep = 1;
+  ar.f.ztail = ztail_n ? ztail : nullptr;
+  ar.f.ztail4 = ztail_n / 4;
   const dim3 g((unsigned)(B * 4 + ar.nblk));
   if (protocol)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv12_fwd2_t<1024, 2>), g, dim3(1024), 0, s, x, w1, b1, w2, b2, a1p, code1,
@@ -2246,9 +2220,7 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   A.nA = ((B + BWD_WCHUNK - 1) / BWD_WCHUNK) * (32 / BWD_WNTW);
   A.nB = B * B2_ICG;
   A.nC = (C2 + 3) / 4;
-  static const int d_in_b = getenv("PTO_BWD_D_IN_B") ? atoi(getenv("PTO_BWD_D_IN_B")) : 0;  // A/B probe
-  A.d_in_b = d_in_b && 4 * A.nB >= ((F1OUT + 15) / 16) * ((F1IN + 15) / 16);
-  A.nD = A.d_in_b ? 0 : (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
+  A.nD = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
   A.nF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9;
   A.wpart = wpart;
   const size_t ldsA = wgrad_lds_floats<BWD_WCHUNK, BWD_WNTW>() * sizeof(float);

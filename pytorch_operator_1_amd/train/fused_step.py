@@ -276,16 +276,17 @@ class FusedMnistTrainer:
             rep = (None, 1, 0)
             lazy = (None, None, 0, None, None, 0.0, 0.0, 1.0, 0)
             w2out, pending = None, None
-            # F4dx's spare block: with the overlap, it zeroes the conv grads
-            # (whole conv range) for this step's backward; otherwise idle
-            conv1 = ((self._params[self._split:].data_ptr(), self.grads[self._split:].data_ptr(),
-                      self.mom[self._split:].data_ptr(), self.numel - self._split) if self.overlap
-                     else (conv1[0], None, conv1[2], conv1[3]))
+            conv1 = (conv1[0], None, conv1[2], conv1[3])  # F4dx's spare block idles
         if only in (None, 0) and fc_owed:
+            # the all-reduce role also zeroes the previous step's conv grads
+            # once its first barrier has passed (every peer's conv exchange,
+            # which read them, is complete), before this step's backward
+            zt = self.grads[self._split:]
             c(L.pto_conv12_fwd_ar(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
                                   P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
                                   self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi,
-                                  self.xcur.data_ptr(), *self._fc_role_args(), s), "conv12_fwd_ar")
+                                  self.xcur.data_ptr(), *self._fc_role_args(), zt.data_ptr(), zt.numel(), s),
+              "conv12_fwd_ar")
         elif only in (None, 0):
             self._call("conv12_fwd_lazy_x", self.data.data_ptr(), P["conv1.weight"].data_ptr(),
                        P["conv1.bias"].data_ptr(), P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(),
@@ -324,8 +325,13 @@ class FusedMnistTrainer:
         own (end of a graph / eager step), with the F12 role's exact
         workgroup decomposition -- ranks whose run() chunks differ (one
         closes a step's exchange, its peer runs it inside F12) still pair up
-        block by block."""
-        _lib.check(self.L.pto_ar_role_sgd(*self._fc_role_args(), self._s()), "ar_role_sgd")
+        block by block.  After its first barrier it also zeroes this rank's
+        conv gradients (every peer has finished the conv exchange that read
+        them), so a run() leaves all gradients zero; inside a graph the
+        next step's F12 all-reduce role does the same."""
+        zt = self.grads[self._split:]
+        _lib.check(self.L.pto_ar_role_sgd(*self._fc_role_args(), zt.data_ptr(), zt.numel(), self._s()),
+                   "ar_role_sgd")
 
     def _allreduce_update(self):
         """DDP: gradient all-reduce + SGD (+ zeroing of the accumulated conv
