@@ -385,76 +385,6 @@ __device__ __forceinline__ void ar_oneshot(const ArPeers* __restrict__ peers, lo
   if (SGD && f.bidx && blk == 0 && threadIdx.x == 0) *f.bidx = (*f.bidx + 1) % f.nbatches;
 }
 
-// ------------------------------------------------ in-launch one-shot role --
-// The one-barrier one-shot exchange + SGD (ar_oneshot<true, false, NT,
-// false>, coherent protocol) as a ROLE of the launch that PRODUCES the
-// gradients (k_bwd_all of the overlapped MNIST step): the caller has seen
-// every producer wave's arrival (agent-scope counter, after each producer
-// drained its atomics / sc1 stores), so the local gradient and replica bytes
-// are final at the memory side -- but possibly stale in this CU's L1 or this
-// XCD's L2, so EVERY load of them here is a system-coherent (sc0 sc1)
-// buffer load, and at most 8 replica float4 are in flight (the host kernel's
-// register budget).  Peer data: the same write-through + sc0 sc1 protocol as
-// ar_oneshot.
-template <int NT>
-__device__ __forceinline__ void ar_oneshot_fresh(const ArPeers* __restrict__ P, long long off, long long n4, int rank,
-                                                 int world, int chan, uint32_t* __restrict__ epochs, int* err,
-                                                 long long timeout, const ArSgd& f, int blk) {
-  __shared__ uint32_t s_epoch;
-  if (threadIdx.x == 0) s_epoch = epochs[chan * AR_MAX_BLOCKS + blk] + 1;
-  __syncthreads();
-  const uint32_t e = s_epoch;
-  if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blk] = e;
-  const long long i = (long long)blk * NT + threadIdx.x;
-  const bool act = i < n4;
-  const long long bytes = n4 * 16;
-  const Buf g = mkbuf(P->in[rank] + off, bytes);
-  if (act && f.rep && f.nrep > 1 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-    const long long fi = off + 4 * i;
-    if (fi >= f.rep_from && fi < f.rep_from + f.rep_stride) {
-      const long long k4 = (fi - f.rep_from) / 4, s4 = f.rep_stride / 4;
-      const Buf rb = mkbuf(f.rep, (long long)(f.nrep - 1) * f.rep_stride * 4);
-      float4 a = ld4<true>(g, i);
-      for (int r0 = 0; r0 < f.nrep - 1; r0 += 8) {  // replica order
-        float4 v[8];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = ld4<true>(rb, (long long)min(r0 + r, f.nrep - 2) * s4 + k4);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          if (r0 + r >= f.nrep - 1) break;
-          a = add4(a, v[r]);
-          gst4(f.rep + (long long)(r0 + r) * f.rep_stride + 4 * k4, float4{0.f, 0.f, 0.f, 0.f});
-        }
-      }
-      st4<true>(g, i, a);
-    }
-  }
-  if (!block_barrier<false>(P, chan, 0, blk, rank, world, e, timeout, err)) return;
-  float4 a = {0.f, 0.f, 0.f, 0.f};
-  if (act) {
-    float4 v[AR_MAX_RANKS];
-#pragma unroll
-    for (int q = 0; q < AR_MAX_RANKS; ++q)
-      if (q < world) v[q] = ld4<true>(mkbuf(P->in[q] + off, bytes), i);
-    a = v[0];
-#pragma unroll
-    for (int q = 1; q < AR_MAX_RANKS; ++q)
-      if (q < world) a = add4(a, v[q]);
-  }
-  // no second barrier (ar_oneshot BAR2 = false): the caller's next cross-rank
-  // barrier on another channel orders the peers' reads before any write of
-  // this input range
-  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
-  if (act) {
-    const float lr = *f.a.lr;
-    const long long j = off + 4 * i;
-    float4 pv = gld4(f.p + j);
-    float4 mv = gld4(f.m + j);
-    sgd4(f, j, a, pv, mv, lr);
-  }
-  if (f.bidx && blk == 0 && threadIdx.x == 0) *f.bidx = (*f.bidx + 1) % f.nbatches;
-}
-
 // ------------------------------------------------------- rank-split role --
 // The all-reduce + SGD as a ROLE inside a register-capped kernel (the MNIST
 // forward launch, <= 64 VGPRs): every thread has exactly ONE float4 in

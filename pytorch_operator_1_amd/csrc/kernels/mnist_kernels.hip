@@ -1677,22 +1677,6 @@ __global__ __launch_bounds__(256) void k_conv1_bwd(const float* __restrict__ g1,
 //   D  dW1 = dh1^T a2p tiles consumed by SGD on fc1.weight.
 //   F  dW2 (fc2) tiles, db1, db2 with SGD epilogues.
 // Block 0 advances the batch cursor and marks conv1's update as owed.
-// The conv-gradient exchange of the overlapped multi-GPU step folded into
-// k_bwd_all: the same one-barrier one-shot all-reduce + SGD as
-// pto_ar_allreduce_sgd_1bar (xgmi_ar.h ar_oneshot_fresh, 256-thread
-// workgroups), started by the last blocks of the grid once every wave that
-// writes a conv gradient (conv2 bias, conv2 wgrad, conv2 dgrad + conv1 wgrad
-// blocks) has drained its stores/atomics and counted itself in done[0].
-struct BwdXchg {
-  const pto_ar::ArPeers* peers;
-  long long off, n4;
-  int rank, world, chan;
-  uint32_t* epochs;
-  int* err;
-  long long timeout;
-  pto_ar::ArSgd f;
-};
-
 struct BwdAllArgs {
   const float* g2;         // d(a2p) [B][800]
   const uint8_t* code2;
@@ -1733,15 +1717,6 @@ struct BwdAllArgs {
   // the cursor is left alone
   int grads_only;
   float* g2b; float* g1w; float* g1b; float* gfw; float* gfb;  // grad slots of conv2.bias, fc1.w/b, fc2.w/b
-  // nX > 0 (overlapped multi-GPU step, grads-only, coherent xGMI protocol):
-  // the conv-range exchange + SGD runs as the LAST nX blocks of this launch
-  // instead of a launch of its own (BwdXchg, xchg_block)
-  int nX;
-  // XDONE_SHARDS arrival counters XDONE_STRIDE words apart (one 128-B line
-  // each), then the count of exchange blocks that saw them all
-  unsigned* xdone;
-  unsigned xtarget;      // producer workgroups of the launch
-  const BwdXchg* X;      // device copy (read by the exchange blocks only)
 };
 
 struct EpiSgd {
@@ -1754,59 +1729,6 @@ struct EpiSgd {
     m[i] = mv;
   }
 };
-
-// A producer workgroup of the folded conv exchange: every wave's conv-
-// gradient stores (sc1) and atomics are acknowledged, then one lane counts
-// the workgroup on its shard (agent scope).  One counter for all ~1070
-// producers serialised their adds at the memory side: +28 us per launch.
-constexpr int XDONE_SHARDS = 64, XDONE_STRIDE = 32;
-PTO_DEV unsigned wave_sum_u32(unsigned v) { return (unsigned)wave_sum((float)v); }  // exact below 2^24
-constexpr int XDONE_WORDS = XDONE_SHARDS * XDONE_STRIDE + 1;
-PTO_DEV void xchg_arrive(const BwdAllArgs& A) {
-  if (!A.nX) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_fetch_add(A.xdone + (blockIdx.x % XDONE_SHARDS) * XDONE_STRIDE, 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Exchange block `xb` of nX: wait (bounded) until every producer wave has
-// arrived -- all of them have lower block indices, so they are dispatched
-// before this block and never wait on it -- then the one-shot exchange.  The
-// last block to see the full count resets both words for the next launch.
-PTO_DEV void xchg_block(const BwdAllArgs& A, int xb) {
-  __shared__ int s_ok;
-  const BwdXchg& X = *A.X;
-  static_assert(XDONE_SHARDS == 64, "one shard per lane of the polling wave");
-  if (threadIdx.x < 64) {  // wave 0: lane l polls shard l (sc1 loads), wave-wide sum
-    unsigned* shard = A.xdone + threadIdx.x * XDONE_STRIDE;
-    unsigned* seen = A.xdone + XDONE_SHARDS * XDONE_STRIDE;
-    int ok = 1;
-    const long long t0 = wall_clock64();
-    while (wave_sum_u32(__hip_atomic_load(shard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < A.xtarget) {
-      if (__hip_atomic_load(X.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) { ok = 0; break; }
-      if (wall_clock64() - t0 > X.timeout) {
-        if (threadIdx.x == 0) atomicOr(X.err, 4);
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    // the last exchange block to see the full count re-arms the counters
-    unsigned last = 0;
-    if (ok && threadIdx.x == 0)
-      last = __hip_atomic_fetch_add(seen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)A.nX - 1;
-    if (__builtin_amdgcn_readfirstlane(last)) {
-      __hip_atomic_store(shard, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (threadIdx.x == 0) __hip_atomic_store(seen, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (threadIdx.x == 0) s_ok = ok;
-  }
-  __syncthreads();
-  if (!s_ok) return;
-  pto_ar::ar_oneshot_fresh<256>(X.peers, X.off, X.n4, X.rank, X.world, X.chan, X.epochs, X.err, X.timeout, X.f, xb);
-}
 
 template <int CH, int NTW>
 __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
@@ -1825,18 +1747,15 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   // 1.4 us slower, profiles/bwd_all_r2.md)
   if (bid < A.nC) {
     const int oc = bid * 4 + wv;
-    if (oc < C2) {
-      const float g = c2_bias_sum(oc, A.g2, A.code2, A.B);
-      if (lane == 0 && A.grads_only) {
-        __hip_atomic_store(A.g2b + oc, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1: read by xchg_block
-      } else if (lane == 0) {
-        float pv = A.p2b[oc], mv = A.m2b[oc];
-        sgd_elem(pv, g, mv, *A.a.lr, A.a.mom, A.a.wd, A.a.gscale, A.a.nesterov);
-        A.p2b[oc] = pv;
-        A.m2b[oc] = mv;
-      }
+    if (oc >= C2) return;
+    const float g = c2_bias_sum(oc, A.g2, A.code2, A.B);
+    if (lane == 0 && A.grads_only) A.g2b[oc] = g;
+    else if (lane == 0) {
+      float pv = A.p2b[oc], mv = A.m2b[oc];
+      sgd_elem(pv, g, mv, *A.a.lr, A.a.mom, A.a.wd, A.a.gscale, A.a.nesterov);
+      A.p2b[oc] = pv;
+      A.m2b[oc] = mv;
     }
-    xchg_arrive(A);
     return;
   }
   bid -= A.nC;
@@ -1867,10 +1786,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   if (bid < A.nA) {
     const bool det = A.wpart != nullptr;
     c2_wgrad_block<CH, NTW>(bid, smem, A.g2, A.code2, A.a1p, A.g2w, A.B, A.wpart);
-    if (A.grads_only && !det) {
-      xchg_arrive(A);
-      return;
-    }
+    if (A.grads_only && !det) return;
     // arrival: every lane's atomics have been performed at the memory side
     // (deterministic mode: the partial-tile stores are written back first)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1937,7 +1853,6 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
     float* gb1 = r == 0 ? A.gb1 : A.c1rep + (r - 1) * A.rep_stride + A.bias_off;
     c2_dgrad_block(bid, smem, A.g2, A.code2, A.w2f, nullptr, A.B, A.x, nullptr, A.code1, gw1, gb1,
                    A.wpart != nullptr);
-    xchg_arrive(A);
     return;
   }
   bid -= A.nB;
@@ -1949,8 +1864,6 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
       dw1_sgd_tile(bid * 4 + wv, A.dh1, A.a2p, A.p1w, A.m1w, A.B, A.a);
     return;
   }
-  bid -= A.nD;
-  if (bid < A.nX) xchg_block(A, bid);
 }
 
 // Host-side flush of an owed conv1 update (before the parameters are read
@@ -2279,10 +2192,8 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
                         long long off_fc1b, long long off_c2w, long long off_c2b, long long off_c1w,
                         long long off_c1b, int* ctr, long long* bidx, long long nbatches, int* pending, int B,
                         const float* lr, float mom, float wd, float gscale, int nesterov, float* c1rep, int nrep,
-                        int rep_stride, int grads_only, float* wpart, const void* xdesc, int nx, unsigned* xdone,
-                        hipStream_t s) {
+                        int rep_stride, int grads_only, float* wpart, hipStream_t s) {
   if (!ctr) return -1;
-  if (xdesc && (!grads_only || wpart || nx < 1 || nx > pto_ar::AR_MAX_BLOCKS || !xdone)) return -1;
   if (((uintptr_t)(grads_only ? p + off_c2w : w2f)) & 7) return -1;  // float2 staging of the W2 slice
   if (!grads_only && (!bidx || !pending || !w2f || nbatches < 1)) return -1;
   if (B < 1 || nrep < 1 || nrep > C1_MAXREP || (nrep > 1 && !c1rep)) return -1;
@@ -2312,57 +2223,9 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   A.nD = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
   A.nF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9;
   A.wpart = wpart;
-  // folded conv exchange: xdesc = DEVICE copy of pto_bwd_xchg_desc's
-  // descriptor, nx = its pto_bwd_xchg_blocks()
-  A.nX = xdesc ? nx : 0;
-  A.X = reinterpret_cast<const BwdXchg*>(xdesc);
-  A.xdone = xdone;
-  A.xtarget = (unsigned)(A.nA + A.nB + A.nC);  // producer workgroups
   const size_t ldsA = wgrad_lds_floats<BWD_WCHUNK, BWD_WNTW>() * sizeof(float);
   const size_t ldsB = B2_LDS_FLOATS * sizeof(float);
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bwd_all<BWD_WCHUNK, BWD_WNTW>), dim3(A.nA + A.nB + A.nC + A.nD + A.nF + A.nX), dim3(256), lds, s, A);
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_bwd_all<BWD_WCHUNK, BWD_WNTW>), dim3(A.nA + A.nB + A.nC + A.nD + A.nF), dim3(256), lds, s, A);
   LAUNCH_CHECK();
-}
-
-// Host-side descriptor of the conv exchange folded into k_bwd_all (BwdXchg;
-// pto_bwd_all's xdesc): the same arguments as pto_ar_allreduce_sgd_1bar
-// (to be copied to the device).  Coherent protocol only; the range is
-// one-shot sized and nothing in it is zeroed here.
-PTO_API int pto_bwd_xchg_desc_size() { return (int)sizeof(BwdXchg); }
-PTO_API int pto_bwd_xchg_blocks(long long n) { return (int)((n / 4 + 255) / 256); }
-PTO_API int pto_bwd_xchg_done_words() { return XDONE_WORDS; }
-PTO_API int pto_bwd_xchg_desc(void* out, const void* peers, long long off, long long n, int rank, int world,
-                              int chan, void* epochs, void* err, float* p, float* m, const float* lr, float mom,
-                              float wd, float gscale, int nesterov, long long* bidx, long long nbatches, float* rep,
-                              int nrep, int rep_stride, long long rep_from) {
-  using namespace pto_ar;
-  if (!out || !peers || n % 4 || off % 4 || n <= 0 || n > AR_ONESHOT_MAX || world < 1 ||
-      world > AR_MAX_RANKS || chan < 0 || chan >= AR_CHANNELS || rank < 0 || rank >= world || !p || !m || !lr ||
-      ((((uintptr_t)p) | ((uintptr_t)m)) & 15) || (bidx && nbatches < 1) || (n / 4 + 255) / 256 > AR_MAX_BLOCKS)
-    return -1;
-  if (rep && (nrep < 1 || nrep > AR_MAX_REP || rep_stride % 4 || rep_from % 4 || (((uintptr_t)rep) & 15)))
-    return -1;
-  BwdXchg X{};
-  X.peers = reinterpret_cast<const ArPeers*>(peers);
-  X.off = off;
-  X.n4 = n / 4;
-  X.rank = rank;
-  X.world = world;
-  X.chan = chan;
-  X.epochs = reinterpret_cast<uint32_t*>(epochs);
-  X.err = reinterpret_cast<int*>(err);
-  X.timeout = pto_ar_timeout_ticks();
-  X.f.p = p;
-  X.f.m = m;
-  X.f.a = sgd_args(lr, mom, wd, gscale, nesterov);
-  X.f.zero_from = off + n;
-  X.f.bidx = bidx;
-  X.f.nbatches = bidx ? nbatches : 1;
-  X.f.rep = rep;
-  X.f.nrep = rep ? nrep : 1;
-  X.f.rep_stride = rep_stride;
-  X.f.rep_from = rep_from;
-  *reinterpret_cast<BwdXchg*>(out) = X;
-  return 0;
 }

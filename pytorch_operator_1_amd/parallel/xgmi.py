@@ -186,40 +186,6 @@ class XgmiAllReduce:
                                                    n_replicas if rep else 1, rep_stride, rep_from, s),
                    "xgmi_allreduce_sgd")
 
-    def bwd_xchg_desc(self, offset: int, n: int, params: torch.Tensor, mom: torch.Tensor, lr_dev: torch.Tensor,
-                      momentum: float, weight_decay: float, gscale: float, nesterov: bool,
-                      cursor: torch.Tensor | None = None, n_batches: int = 1, replicas: torch.Tensor | None = None,
-                      n_replicas: int = 1, rep_from: int = 0, chan: int = 0):
-        """Host descriptor of the one-barrier one-shot all-reduce + SGD of
-        ``buf[offset:offset+n]`` run as the last workgroups of the launch that
-        produces the gradients (``pto_bwd_all``'s ``xdesc``; the MNIST
-        overlap schedule's conv exchange).  Same semantics as
-        ``allreduce_sgd_(..., single_barrier=True)``; coherent protocol only.
-        Returns (device copy of the descriptor, workgroups it needs)."""
-        if self.align != 4 or self.protocol != "coherent":
-            raise ValueError("XgmiAllReduce: the folded exchange needs an fp32 buffer and the coherent protocol")
-        if n % 4 or offset % 4 or offset + n > self.buf.numel():
-            raise ValueError("XgmiAllReduce: bad range for the folded exchange")
-        for t in (params, mom):
-            if t.dtype != torch.float32 or t.numel() != self.buf.numel() or t.device != self.device:
-                raise ValueError("XgmiAllReduce: params/momentum must match the gradient buffer")
-        rep_stride = self.buf.numel() - rep_from
-        rep = None
-        if replicas is not None and n_replicas > 1:
-            if replicas.numel() < (n_replicas - 1) * rep_stride or replicas.device != self.device:
-                raise ValueError("XgmiAllReduce: replica buffer too small for n_replicas")
-            rep = replicas.data_ptr()
-        L = _lib.lib()
-        desc = ctypes.create_string_buffer(L.pto_bwd_xchg_desc_size())
-        _lib.check(L.pto_bwd_xchg_desc(ctypes.addressof(desc), self.peers.data_ptr(), offset, n, self.rank, self.world, chan,
-                                       self.epochs.data_ptr(), self.err.data_ptr(), params.data_ptr(), mom.data_ptr(),
-                                       lr_dev.data_ptr(), momentum, weight_decay, gscale, int(nesterov),
-                                       cursor.data_ptr() if cursor is not None else None, n_batches, rep,
-                                       n_replicas if rep else 1, rep_stride, rep_from),
-                   "bwd_xchg_desc")
-        dev = torch.frombuffer(bytearray(desc.raw), dtype=torch.uint8).to(self.device)
-        return dev, int(L.pto_bwd_xchg_blocks(n))
-
     def role_args(self, offset: int, n: int, chan: int, params: torch.Tensor, mom: torch.Tensor,
                   lr_dev: torch.Tensor, momentum: float, weight_decay: float, gscale: float, nesterov: bool,
                   zero_from: int) -> tuple:

@@ -196,23 +196,6 @@ class FusedMnistTrainer:
         else:
             self._ar_buf = self.grads
             self.c1rep = torch.zeros(nrep_tail, **f32)
-        # ddp-xgmi overlap: the conv exchange runs as the last workgroups of
-        # k_bwd_all (they start once every conv-gradient producer wave has
-        # drained and counted itself), not as a launch of its own
-        # (PTO_XGMI_BWD_FOLD=0: the stand-alone one-shot launch; the fenced
-        # protocol and the deterministic mode always use it)
-        self._xdesc = None
-        if (self.overlap and self._xgmi.protocol == "coherent" and not self.deterministic
-                and os.environ.get("PTO_XGMI_BWD_FOLD", "1") == "1"):
-            self._xdone = torch.zeros(self.L.pto_bwd_xchg_done_words(), device=device, dtype=torch.int32)
-            lr, mom, wd, gs, nes = self._opt_args()
-            self._xdesc, self._xblocks = self._xgmi.bwd_xchg_desc(
-                self._split, self.numel - self._split, self._params, self.mom, self.lr_dev, mom, wd, gs, bool(nes),
-                cursor=self.batch_idx, n_batches=self.n_batches, replicas=self.c1rep, n_replicas=self.c1_nrep,
-                rep_from=self._c1)
-        if self.overlap:
-            self.comm_info["conv_exchange"] = ("last workgroups of k_bwd_all" if self._xdesc is not None
-                                               else "one-shot launch after k_bwd_all")
 
         # graph modes: "full" = whole steps (collectives included) in HIP
         # graphs; "split" = the collective issued between two graphs (a
@@ -330,9 +313,7 @@ class FusedMnistTrainer:
                    self.mom.data_ptr(), *self._offs, self.c2_ctr.data_ptr(),
                    None if go else self.batch_idx.data_ptr(), self.n_batches,
                    None if go else self.pending.data_ptr(), self.B, *self._opt_args(), self.c1rep.data_ptr(),
-                   self.c1_nrep, self.c1_stride, int(go), _lib.ptr(self.wpart),
-                   *((self._xdesc.data_ptr(), self._xblocks, self._xdone.data_ptr()) if self._xdesc is not None
-                     else (None, 0, None)))
+                   self.c1_nrep, self.c1_stride, int(go), _lib.ptr(self.wpart))
 
     def _fc_role_args(self):
         lr, mom, wd, gs, nes = self._opt_args()
@@ -356,8 +337,6 @@ class FusedMnistTrainer:
         """DDP: gradient all-reduce + SGD (+ zeroing of the accumulated conv
         grads and the cursor advance).  ddp-xgmi overlap: the conv range
         only (the fc range is owed to the next F12 / the closing launch)."""
-        if self._xgmi is not None and self.overlap and self._xdesc is not None:
-            return  # the conv exchange ran inside k_bwd_all
         if self._xgmi is not None and self.overlap:
             # one barrier: the fc exchange that follows (channel 1, in the
             # next F12 or the closing launch) orders every peer's reads of

@@ -39,7 +39,6 @@ extern "C" __attribute__((visibility("default"))) int probe_bwd_all(
   }
   A.nD = (mask & 16) ? (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4 : 0;
   A.wpart = nullptr;
-  A.nX = 0;  // no folded conv exchange
   const size_t ldsA = wgrad_lds_floats<BWD_WCHUNK, BWD_WNTW>() * sizeof(float);
   const size_t ldsB = B2_LDS_FLOATS * sizeof(float);
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;
