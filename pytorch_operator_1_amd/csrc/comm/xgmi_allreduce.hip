@@ -365,7 +365,7 @@ PTO_API int pto_ar_allreduce_sgd_1bar(const void* peers, long long off, long lon
 
 // Stand-alone launch of the all-reduce-with-SGD ROLE (same arguments as
 // pto_conv12_fwd_ar's role part, same workgroup decomposition), plus an
-// optional local range [ztail, ztail + ztail_n) zeroed after barrier 0.
+// optional local range [ztail, ztail + ztail_n) zeroed after the stage-1 barrier.
 PTO_API int pto_ar_role_sgd(const void* peers, long long off, long long n, int rank, int world, int chan, void* epochs,
                             void* err, int protocol, float* p, float* m, const float* lr, float mom, float wd,
                             float gscale, int nesterov, long long zero_from, float* ztail, long long ztail_n,

@@ -157,10 +157,11 @@ struct ArSgd {
   float* rep;
   int nrep, rep_stride;
   long long rep_from;
-  // optional local float4 range zeroed once barrier 0 has passed (every peer
-  // has then finished the launches it queued before this one): the closing
-  // fc exchange of the overlapped MNIST step clears the conv gradients the
-  // one-shot conv exchange left behind, so a run() ends with zero gradients
+  // optional local float4 range zeroed by ar_role_sgd once its stage-1
+  // barrier has passed (every peer has then finished the launches it queued
+  // before this one): the fc exchange of the overlapped MNIST step clears the
+  // conv gradients the one-shot conv exchange left behind, so the next
+  // backward accumulates from zero and a run() ends with zero gradients
   float* ztail;
   long long ztail4;
 };
@@ -420,11 +421,20 @@ __device__ __forceinline__ void ar_role_sgd(const ArPeers* __restrict__ P, long 
   const bool in_group = q < world;
   const long long j = (long long)blk * S + sidx;  // element of every chunk this thread covers
   const long long bytes = n4 * 16;
-  if (!block_barrier<FENCED>(P, chan, 0, blk, rank, world, e, timeout, err)) return;
-  if (f.ztail) {
-    const long long nt = (long long)role_blocks(4 * n4, world, NT) * NT;
-    for (long long z = (long long)blk * NT + threadIdx.x; z < f.ztail4; z += nt)
-      gst4(f.ztail + 4 * z, float4{0.f, 0.f, 0.f, 0.f});
+  // Barrier 0 ("every peer's input is complete") is NOT needed under the
+  // coherent protocol: this role always runs after the same step's conv
+  // exchange (ar_oneshot on the other channel, fused_step.py), and passing
+  // ITS barrier already means every peer finished the backward that wrote
+  // this range (end-of-kernel write-back before the peer's conv flag) and
+  // every peer finished its previous call of this role, including the
+  // stage-2 reads of tmp that stage 1 below overwrites (that call precedes
+  // the peer's conv exchange in stream order).  The sc0 sc1 loads below
+  // cannot hit stale cached copies.  The fenced protocol keeps barrier 0
+  // for its acquire (plain loads).
+  if constexpr (FENCED) {
+    if (!block_barrier<FENCED>(P, chan, 0, blk, rank, world, e, timeout, err)) return;
+  } else {
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   }
   // stage 1: my chunk's element j from rank q -> LDS, then rank-order sums
   const long long i1 = (long long)rank * cs + j;
@@ -438,6 +448,13 @@ __device__ __forceinline__ void ar_role_sgd(const ArPeers* __restrict__ P, long 
   }
   const float lr = *f.a.lr;
   if (!block_barrier<FENCED>(P, chan, 1, blk, rank, world, e, timeout, err)) return;
+  // every peer has passed its stage 1, so its conv exchange of the same step
+  // (which read the range zeroed here) is complete
+  if (f.ztail) {
+    const long long nt = (long long)role_blocks(4 * n4, world, NT) * NT;
+    for (long long z = (long long)blk * NT + threadIdx.x; z < f.ztail4; z += nt)
+      gst4(f.ztail + 4 * z, float4{0.f, 0.f, 0.f, 0.f});
+  }
   // stage 2: element j of chunk q from rank q's partial sums
   const long long k = (long long)q * cs + j;
   if (in_group && j < cs && k < n4) {

@@ -2003,7 +2003,7 @@ extern "C" long long pto_ar_timeout_ticks();
 // p/m (zero_from: local gradient zeroed from there on), as extra workgroups
 // of the same launch (ArRole); [ztail, ztail + ztail_n) (the conv gradients
 // of the previous step, read by the peers' conv exchange) is zeroed by the
-// role's workgroups once their first barrier has passed.  protocol: 0 coherent, 1 fenced -- the one
+// role's workgroups once their stage-1 barrier has passed.  protocol: 0 coherent, 1 fenced -- the one
 // the XgmiAllReduce instance of `peers` uses.
 PTO_API int pto_conv12_fwd_ar(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
                               float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B, const long long* bidx,

@@ -279,7 +279,7 @@ class FusedMnistTrainer:
             conv1 = (conv1[0], None, conv1[2], conv1[3])  # F4dx's spare block idles
         if only in (None, 0) and fc_owed:
             # the all-reduce role also zeroes the previous step's conv grads
-            # once its first barrier has passed (every peer's conv exchange,
+            # once its stage-1 barrier has passed (every peer's conv exchange,
             # which read them, is complete), before this step's backward
             zt = self.grads[self._split:]
             c(L.pto_conv12_fwd_ar(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
@@ -325,7 +325,7 @@ class FusedMnistTrainer:
         own (end of a graph / eager step), with the F12 role's exact
         workgroup decomposition -- ranks whose run() chunks differ (one
         closes a step's exchange, its peer runs it inside F12) still pair up
-        block by block.  After its first barrier it also zeroes this rank's
+        block by block.  After its stage-1 barrier it also zeroes this rank's
         conv gradients (every peer has finished the conv exchange that read
         them), so a run() leaves all gradients zero; inside a graph the
         next step's F12 all-reduce role does the same."""

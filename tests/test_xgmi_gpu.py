@@ -468,3 +468,81 @@ def test_xgmi_allreduce_uneven_load():
         assert bad == 0 and worst < 1e-4, (rank, worst, bad)
     for p in ps:
         assert p.exitcode == 0
+
+
+def _overlap_pair_worker(rank, world, port, q):
+    """The overlapped MNIST step's exchange pair at any world size: the
+    one-barrier one-shot all-reduce + SGD of a conv-sized range (chan 0,
+    NO second barrier), then the rank-split fc role (chan 1, 1024-thread
+    workgroups, S = 1024 / world threads per rank group) + SGD, which zeroes
+    the conv range after its first barrier -- the barrier that must order
+    every peer's one-shot reads before that zeroing.  Parameters and
+    momentum vs the same SGD in torch on the exact sum, every rank
+    bit-identical, the conv range zero after every pair."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch.distributed as dist
+
+        from pytorch_operator_1_amd.ops import _lib
+        from pytorch_operator_1_amd.parallel.xgmi import XgmiAllReduce
+
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        nfc, nconv = 81_920, 25_664  # fc range > the one-shot limit, conv range = MNIST's
+        n = nfc + nconv
+        lr, mom, wd = 0.05, 0.9, 1e-3
+        buf = torch.zeros(n, device=dev)
+        ar = XgmiAllReduce(buf, timeout_ms=20000)
+        p = torch.randn(n, generator=torch.Generator(device=dev).manual_seed(7), device=dev)
+        m = torch.zeros(n, device=dev)
+        pr, mr = p.clone(), m.clone()
+        lr_dev = torch.tensor([lr], device=dev)
+        L = _lib.lib()
+        s = torch.cuda.current_stream(dev).cuda_stream
+        worst, zero_ok = 0.0, True
+        for it in range(8):
+            _fill(buf, rank, 700 + it)
+            ar.allreduce_sgd_(nfc, nconv, params=p, mom=m, lr_dev=lr_dev, momentum=mom, weight_decay=wd,
+                              gscale=1.0 / world, nesterov=True, zero_from=n, chan=0, single_barrier=True)
+            zt = buf[nfc:]
+            _lib.check(L.pto_ar_role_sgd(*ar.role_args(0, nfc, 1, p, m, lr_dev, mom, wd, 1.0 / world, True, n),
+                                         zt.data_ptr(), zt.numel(), s), "ar_role_sgd")
+            torch.cuda.synchronize(dev)
+            d = _expected(n, world, 700 + it, dev) / world + wd * pr
+            mr.mul_(mom).add_(d)
+            pr.sub_(lr * (d + mom * mr))
+            worst = max(worst, (p - pr).abs().max().item(), (m - mr).abs().max().item())
+            zero_ok &= float(buf[nfc:].abs().max()) == 0.0
+        ar.check()
+        allv = [None] * world
+        dist.all_gather_object(allv, p.cpu())
+        same = all(torch.equal(allv[0], v) for v in allv)
+        ar.close()
+        dist.destroy_process_group()
+        q.put((rank, worst, same, zero_ok))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), False, False))
+        raise
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_xgmi_overlap_pair_any_world(world):
+    """World sizes the 2/4-rank tests do not reach: 3 (S = 341, idle
+    threads in every role workgroup) and 8 (the node's full world, 8 rank
+    groups of 128 threads)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_overlap_pair_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = collect(q, ps, world, timeout=110)
+    for p in ps:
+        p.join(60)
+    for rank, worst, same, zero_ok in res:
+        assert not isinstance(worst, str), worst
+        assert worst < 1e-4, (rank, worst)
+        assert same and zero_ok, (rank, same, zero_ok)
+    for p in ps:
+        assert p.exitcode == 0
