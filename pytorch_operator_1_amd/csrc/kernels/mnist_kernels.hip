@@ -86,12 +86,6 @@ struct LazyConv1 {
   float* w2out;         // nullptr, or [50][500]: conv2.weight as read here (k_bwd_all's dgrad reads it)
   const float* rep;     // extra gradient replicas (k_bwd_all): g + sum_r rep[r*rep_stride + i], r < nrep-1
   int nrep, rep_stride;
-  // lazy conv2.weight update (one-process schedule): conv2.weight's grads and
-  // momentum; an owed update is applied to each block's staged W2 tile on
-  // the fly (the b == 0 blocks' w2out snapshot then holds the updated rows)
-  // and committed by F4dx (Conv1Commit p2/g2/m2).  nullptr: not lazy
-  const float* g2;
-  const float* m2;
 };
 constexpr int C1_MAXREP = 256;  // max conv1 gradient replicas (launchers check)
 constexpr int REP_CHUNK = 16;   // replica loads the readers keep in flight at once
@@ -104,12 +98,7 @@ struct Conv1Commit {
   SgdArgs a;
   float* rep;           // extra gradient replicas, summed into the update and re-zeroed
   int nrep, rep_stride;
-  // lazy conv2.weight (C2 x 500 floats): committed alongside (nullptr: none)
-  float* p2;
-  float* g2;
-  float* m2;
 };
-constexpr int C2W = 50 * 500;  // conv2.weight floats
 
 // Conv1Commit's update of 4 elements at i: the gradient is the sum of the
 // primary slot and the replicas; all of them are zeroed.
@@ -366,20 +355,6 @@ __global__ __launch_bounds__(NTH, ARM ? 2 * NTH / 256 : 1) void k_conv12_fwd2_t(
       const int e = tid + NTH * q;
       wv[q] = (e < nrows * 125) ? wsrc[e] : float4{0.f, 0.f, 0.f, 0.f};
     }
-    // lazy conv2 (ARM == 0 only): grad / momentum tiles in the same memory
-    // round as the weights (applied below once `pending` is known)
-    float4 g4[2048 / NTH], m4[2048 / NTH];
-    if (ARM == 0 && lz.g2) {
-      const float4* gsrc = reinterpret_cast<const float4*>(lz.g2 + nt * 16 * 500);
-      const float4* msrc = reinterpret_cast<const float4*>(lz.m2 + nt * 16 * 500);
-#pragma unroll
-      for (int q = 0; q < 2048 / NTH; ++q) {
-        const int e = tid + NTH * q;
-        const bool ok = e < nrows * 125;
-        g4[q] = ok ? gsrc[e] : float4{0.f, 0.f, 0.f, 0.f};
-        m4[q] = ok ? msrc[e] : float4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
     const float4 xv = tid < 196 ? reinterpret_cast<const float4*>(x + b * 784)[tid] : float4{0.f, 0.f, 0.f, 0.f};
     constexpr int QW1 = (C1 * 26 + NTH - 1) / NTH;
     float wq[QW1], gq[QW1], mq[QW1];
@@ -406,20 +381,6 @@ __global__ __launch_bounds__(NTH, ARM ? 2 * NTH / 256 : 1) void k_conv12_fwd2_t(
     if (pend) {
 #pragma unroll
       for (int q = 0; q < QW1; ++q) sgd_elem(wq[q], gq[q], mq[q], lr, lz.a.mom, lz.a.wd, lz.a.gscale, lz.a.nesterov);
-    }
-    if constexpr (ARM == 0) {
-      // lazy conv2.weight: the owed update of this block's 16-row tile, from
-      // the same grad / momentum values and the same sgd_elem as F4dx's
-      // commit (bitwise equal); nothing is written here but the snapshot
-      if (lz.g2 && pend) {
-#pragma unroll
-        for (int q = 0; q < 2048 / NTH; ++q) {
-          sgd_elem(wv[q].x, g4[q].x, m4[q].x, lr, lz.a.mom, lz.a.wd, lz.a.gscale, lz.a.nesterov);
-          sgd_elem(wv[q].y, g4[q].y, m4[q].y, lr, lz.a.mom, lz.a.wd, lz.a.gscale, lz.a.nesterov);
-          sgd_elem(wv[q].z, g4[q].z, m4[q].z, lr, lz.a.mom, lz.a.wd, lz.a.gscale, lz.a.nesterov);
-          sgd_elem(wv[q].w, g4[q].w, m4[q].w, lr, lz.a.mom, lz.a.wd, lz.a.gscale, lz.a.nesterov);
-        }
-      }
     }
 #pragma unroll
     for (int q = 0; q < 2048 / NTH; ++q) {
@@ -854,16 +815,6 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
       }
     }
     return;
-  }
-  // lazy conv2.weight: every tile block commits an equal slice of the owed
-  // update (the one F12 applied on the fly; 32 float4 at B = 64) and zeroes
-  // its grads for this step's backward
-  if (cm.p2) {
-    const int nblk = mtiles * ntiles, per = (C2W / 4 + nblk - 1) / nblk;
-    for (int j = t; j < per; j += FDX_WAVES * 64) {
-      const int i = (blockIdx.x * per + j) * 4;
-      if (i < C2W && *cm.pending) sgd_flat4(cm.p2, cm.g2, cm.m2, i, *cm.a.lr, cm.a);
-    }
   }
   const int tile = xcd_tile(blockIdx.x, mtiles * ntiles, true);
   const int mt = tile % mtiles, nt = tile / mtiles;
@@ -1766,9 +1717,6 @@ struct BwdAllArgs {
   // the cursor is left alone
   int grads_only;
   float* g2b; float* g1w; float* g1b; float* gfw; float* gfb;  // grad slots of conv2.bias, fc1.w/b, fc2.w/b
-  // lazy conv2.weight (one-process schedule): the wgrad blocks only
-  // accumulate; the next F12 applies the update on the fly, F4dx commits it
-  int lazy_c2;
 };
 
 struct EpiSgd {
@@ -1838,7 +1786,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   if (bid < A.nA) {
     const bool det = A.wpart != nullptr;
     c2_wgrad_block<CH, NTW>(bid, smem, A.g2, A.code2, A.a1p, A.g2w, A.B, A.wpart);
-    if ((A.grads_only || A.lazy_c2) && !det) return;
+    if (A.grads_only && !det) return;
     // arrival: every lane's atomics have been performed at the memory side
     // (deterministic mode: the partial-tile stores are written back first)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1920,26 +1868,12 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
 
 // Host-side flush of an owed conv1 update (before the parameters are read
 // or replaced): commit it and clear `pending`.  One block.
-// Block 0 commits conv1; with lazy conv2 (cm.p2) blocks 1.. commit one
-// 256-float4 slice of conv2.weight each.  pending[1] counts the blocks that
-// have read pending[0]; the last one clears both, so no block can miss the
-// flag another block cleared.
 __global__ __launch_bounds__(256) void k_conv1_commit(Conv1Commit cm, int* __restrict__ pending) {
-  const bool owed = *cm.pending != 0;
-  if (owed) {
-    const float lr = *cm.a.lr;
-    if (blockIdx.x == 0) {
-      for (int i = 4 * threadIdx.x; i < cm.n; i += 1024) commit4(cm, i, lr);
-    } else {
-      const int i = ((blockIdx.x - 1) * 256 + threadIdx.x) * 4;
-      if (i < C2W) sgd_flat4(cm.p2, cm.g2, cm.m2, i, lr, cm.a);
-    }
-  }
+  if (!*cm.pending) return;
+  const float lr = *cm.a.lr;
+  for (int i = 4 * threadIdx.x; i < cm.n; i += 1024) commit4(cm, i, lr);
   __syncthreads();
-  if (threadIdx.x == 0 && atomicAdd(pending + 1, 1) == (int)gridDim.x - 1) {
-    pending[1] = 0;
-    pending[0] = 0;
-  }
+  if (threadIdx.x == 0) *pending = 0;
 }
 
 // The RCCL schedule's optimizer launch (ddp-rccl).  The all-reduce covers
@@ -2053,12 +1987,10 @@ PTO_API int pto_conv12_fwd_lazy_x(const float* x, const float* w1, const float* 
                                   const long long* bidx, const float* g1f, const float* m1f, int bias_off,
                                   const int* pending, const float* lr, float mom, float wd, float gscale, int nesterov,
                                   float* xout, float* w2out, const float* rep, int nrep, int rep_stride,
-                                  const float* g2w, const float* m2w, hipStream_t s) {
+                                  hipStream_t s) {
   if (nrep < 1 || nrep > C1_MAXREP || (nrep > 1 && !rep) || (pending && (!g1f || !m1f || !lr))) return -1;
-  // lazy conv2: needs the pending flag, 16-byte aligned tiles
-  if (g2w && (!pending || !m2w || ((((uintptr_t)g2w) | ((uintptr_t)m2w) | ((uintptr_t)w2)) & 15))) return -1;
   LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off, xout, w2out, rep, nrep,
-               rep_stride, g2w, m2w};
+               rep_stride};
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv12_fwd2_t<1024, 0>), dim3(B * 4), dim3(1024), 0, s, x, w1, b1, w2, b2, a1p,
                      code1, a2p, code2, B, bidx, lz, ArRole{});
   LAUNCH_CHECK();
@@ -2085,8 +2017,7 @@ PTO_API int pto_conv12_fwd_ar(const float* x, const float* w1, const float* b1, 
       chan >= AR_CHANNELS || rank < 0 || rank >= world || !p || !m || !lr || !peers || protocol < 0 || protocol > 1 ||
       ((((uintptr_t)p) | ((uintptr_t)m)) & 15))
     return -1;
-  LazyConv1 lz{nullptr, nullptr, nullptr, sgd_args(lr, mom, wd, gscale, nesterov), 0, xout, nullptr, nullptr, 1, 0,
-               nullptr, nullptr};
+  LazyConv1 lz{nullptr, nullptr, nullptr, sgd_args(lr, mom, wd, gscale, nesterov), 0, xout, nullptr, nullptr, 1, 0};
   ArRole ar;
   ar.peers = reinterpret_cast<const ArPeers*>(peers);
   ar.off = off;
@@ -2158,18 +2089,13 @@ PTO_API int pto_fc2_ce(const float* h1, const float* w, const float* b, const in
   LAUNCH_CHECK();
 }
 
-// pending: 2 ints (flag, arrival counter); p2w/g2w/m2w: lazy conv2.weight
-// (nullptr: conv1 only).
 PTO_API int pto_conv1_commit(float* p1, float* g1, float* m1, int n1, int* pending, const float* lr, float mom,
-                             float wd, float gscale, int nesterov, float* rep, int nrep, int rep_stride, float* p2w,
-                             float* g2w, float* m2w, hipStream_t s) {
+                             float wd, float gscale, int nesterov, float* rep, int nrep, int rep_stride,
+                             hipStream_t s) {
   if (n1 % 4 || rep_stride % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1) | ((uintptr_t)rep)) & 15))
     return -1;
-  if (p2w && (!g2w || !m2w || ((((uintptr_t)p2w) | ((uintptr_t)g2w) | ((uintptr_t)m2w)) & 15))) return -1;
-  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), rep, nrep, rep_stride,
-                 p2w, g2w, m2w};
-  const int nblk = 1 + (p2w ? (C2W / 4 + 255) / 256 : 0);
-  hipLaunchKernelGGL(k_conv1_commit, dim3(nblk), dim3(256), 0, s, cm, pending);
+  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), rep, nrep, rep_stride};
+  hipLaunchKernelGGL(k_conv1_commit, dim3(1), dim3(256), 0, s, cm, pending);
   LAUNCH_CHECK();
 }
 
@@ -2213,16 +2139,13 @@ PTO_API int pto_fc2_ce_dx(const float* h1, const float* w2, const float* b2, con
                           float* loss_rows, float* dlogits, float* dh1, float* da2p, int B, float inv_b,
                           const long long* bidx, float* p1, float* g1, float* m1, int n1, const int* pending,
                           const float* lr, float mom, float wd, float gscale, int nesterov, float* rep, int nrep,
-                          int rep_stride, float* p2w, float* g2w, float* m2w, hipStream_t s) {
+                          int rep_stride, hipStream_t s) {
   if (n1 % 4 || rep_stride % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1) | ((uintptr_t)rep)) & 15))
     return -1;
   if ((((uintptr_t)h1) | ((uintptr_t)w2)) & 15) return -1;  // float4 staging of the h1 tile and W2
   if (nrep < 1 || nrep > C1_MAXREP || (nrep > 1 && !rep)) return -1;
+  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), rep, nrep, rep_stride};
   const int nblk = ((B + 15) / 16) * ((F1IN + 15) / 16);
-  if (p2w && (!pending || !g2w || !m2w || ((((uintptr_t)p2w) | ((uintptr_t)g2w) | ((uintptr_t)m2w)) & 15)))
-    return -1;  // lazy conv2: the tile blocks commit conv2.weight in equal slices
-  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), rep, nrep, rep_stride,
-                 p2w, g2w, m2w};
   hipLaunchKernelGGL(k_fc2_ce_dx_mf, dim3(nblk + 1), dim3(FDX_WAVES * 64), 0, s, h1, w2, b2, labels, w1, loss_rows,
                      dlogits, dh1, da2p, B, inv_b, bidx, cm);
   LAUNCH_CHECK();
@@ -2269,9 +2192,8 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
                         long long off_fc1b, long long off_c2w, long long off_c2b, long long off_c1w,
                         long long off_c1b, int* ctr, long long* bidx, long long nbatches, int* pending, int B,
                         const float* lr, float mom, float wd, float gscale, int nesterov, float* c1rep, int nrep,
-                        int rep_stride, int grads_only, float* wpart, int lazy_c2, hipStream_t s) {
+                        int rep_stride, int grads_only, float* wpart, hipStream_t s) {
   if (!ctr) return -1;
-  if (lazy_c2 && (grads_only || wpart)) return -1;  // lazy conv2: one-process, atomics mode
   if (((uintptr_t)(grads_only ? p + off_c2w : w2f)) & 7) return -1;  // float2 staging of the W2 slice
   if (!grads_only && (!bidx || !pending || !w2f || nbatches < 1)) return -1;
   if (B < 1 || nrep < 1 || nrep > C1_MAXREP || (nrep > 1 && !c1rep)) return -1;
@@ -2301,7 +2223,6 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   A.nD = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
   A.nF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9;
   A.wpart = wpart;
-  A.lazy_c2 = lazy_c2;
   const size_t ldsA = wgrad_lds_floats<BWD_WCHUNK, BWD_WNTW>() * sizeof(float);
   const size_t ldsB = B2_LDS_FLOATS * sizeof(float);
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;

@@ -144,9 +144,7 @@ class FusedMnistTrainer:
         # snapshot while its wgrad blocks update the parameter (fused-opt)
         self.w2f = torch.empty(50 * 500, **f32) if self.fused_opt else None
         self.c2_ctr = torch.zeros(32, device=device, dtype=torch.int32)  # wgrad tile arrival counters
-        # [0]: conv1 (and lazy conv2) update owed (fused-opt); [1]: arrival
-        # counter of the multi-block commit launch
-        self.pending = torch.zeros(2, device=device, dtype=torch.int32)
+        self.pending = torch.zeros(1, device=device, dtype=torch.int32)  # conv1 update owed (fused-opt)
         self.wpart = torch.empty(((B + 3) // 4) * 50 * 500, **f32) if self.deterministic else None
 
         if data is None:
@@ -173,15 +171,6 @@ class FusedMnistTrainer:
         # optimizer launch (k_ddp_sgd)
         self.c1_nrep = B if self.deterministic else C1_REPLICAS
         self.c1_stride = self.numel - self._c1
-        # lazy conv2.weight update (fused-opt): k_bwd_all's wgrad blocks only
-        # accumulate, the next F12 applies the owed update to its staged
-        # tiles on the fly and F4dx's tile blocks commit it (PTO_LAZY_C2=0:
-        # the wgrad tile's last-arriving block updates it inside k_bwd_all)
-        self.lazy_c2 = (self.fused_opt and not self.deterministic
-                        and os.environ.get("PTO_LAZY_C2", "1") == "1")
-        c2 = offs["conv2.weight"][0]
-        self._c2 = ((self._params[c2:].data_ptr(), self.grads[c2:].data_ptr(), self.mom[c2:].data_ptr())
-                    if self.lazy_c2 else (None, None, None))
         self.schedule = "fused-opt" if not self.ddp else ("ddp-xgmi" if self._xgmi is not None else "ddp-rccl")
         # ddp-xgmi overlap: step k's all-reduce is split at the fc | conv
         # boundary.  The conv part (100 KB, conv1 replicas folded, cursor
@@ -302,7 +291,7 @@ class FusedMnistTrainer:
             self._call("conv12_fwd_lazy_x", self.data.data_ptr(), P["conv1.weight"].data_ptr(),
                        P["conv1.bias"].data_ptr(), P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(),
                        self.a1p.data_ptr(), self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi,
-                       *lazy, self.xcur.data_ptr(), w2out, *rep, *self._c2[1:])
+                       *lazy, self.xcur.data_ptr(), w2out, *rep)
         if only in (None, 1):
             self._call("linear_fwd", self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
                        self.h1.data_ptr(), B, 500, 800, 1)
@@ -310,7 +299,7 @@ class FusedMnistTrainer:
             self._call("fc2_ce_dx", self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
                        self.target.data_ptr(), P["fc1.weight"].data_ptr(), self.loss_rows.data_ptr(),
                        self.dlogits.data_ptr(), self.dh1.data_ptr(), self.da2p.data_ptr(), B, 1.0 / B, bi, *conv1,
-                       pending, *o, *rep, *self._c2)
+                       pending, *o, *rep)
 
     def _backward(self):
         """``k_bwd_all``: the whole backward in one launch.  Fused-opt: every
@@ -324,7 +313,7 @@ class FusedMnistTrainer:
                    self.mom.data_ptr(), *self._offs, self.c2_ctr.data_ptr(),
                    None if go else self.batch_idx.data_ptr(), self.n_batches,
                    None if go else self.pending.data_ptr(), self.B, *self._opt_args(), self.c1rep.data_ptr(),
-                   self.c1_nrep, self.c1_stride, int(go), _lib.ptr(self.wpart), int(self.lazy_c2))
+                   self.c1_nrep, self.c1_stride, int(go), _lib.ptr(self.wpart))
 
     def _fc_role_args(self):
         lr, mom, wd, gs, nes = self._opt_args()
@@ -391,7 +380,7 @@ class FusedMnistTrainer:
     def _commit_launch(self):
         self._call("conv1_commit", self._params[self._c1:].data_ptr(), self.grads[self._c1:].data_ptr(),
                    self.mom[self._c1:].data_ptr(), self.numel - self._c1, self.pending.data_ptr(),
-                   *self._opt_args(), self.c1rep.data_ptr(), self.c1_nrep, self.c1_stride, *self._c2)
+                   *self._opt_args(), self.c1rep.data_ptr(), self.c1_nrep, self.c1_stride)
 
     def flush(self):
         """Commit an owed conv1 update (fused-opt) so the flat buffers hold

@@ -93,7 +93,7 @@ def test_conv12_fused_forward(B):
         _lib.check(L.pto_conv12_fwd_lazy_x(x.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
                                            a1p.data_ptr(), c1.data_ptr(), a2p.data_ptr(), c2.data_ptr(), B, None, None,
                                            None, 0, None, None, 0.0, 0.0, 1.0, 0, xo.data_ptr(), None, None, 1, 0,
-                                           None, None, _lib.stream_ptr()), "conv12")
+                                           _lib.stream_ptr()), "conv12")
         torch.cuda.synchronize()
         outs.append((a1p.clone(), a2p.clone(), c1.clone(), c2.clone()))
         assert torch.equal(xo.view(B, 1, 28, 28), x)

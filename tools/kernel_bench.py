@@ -46,14 +46,14 @@ def main():
             tr.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(), P["conv2.weight"].data_ptr(),
             P["conv2.bias"].data_ptr(), tr.a1p.data_ptr(), tr.code1.data_ptr(), tr.a2p.data_ptr(),
             tr.code2.data_ptr(), B, bi, None, None, 0, None, None, 0.0, 0.0, 1.0, 0, tr.xcur.data_ptr(), None, None,
-            1, 0, None, None, s),
+            1, 0, s),
         "F3 fc1_fwd": lambda: L.pto_linear_fwd(tr.a2p.data_ptr(), P["fc1.weight"].data_ptr(),
                                                P["fc1.bias"].data_ptr(), tr.h1.data_ptr(), B, 500, 800, 1, s),
         "F4dx fc2_ce_dx": lambda: L.pto_fc2_ce_dx(
             tr.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(), tr.target.data_ptr(),
             P["fc1.weight"].data_ptr(), tr.loss_rows.data_ptr(), tr.dlogits.data_ptr(), tr.dh1.data_ptr(),
             tr.da2p.data_ptr(), B, 1.0 / B, bi, tr._params[tr._c1:].data_ptr(), tr.grads[tr._c1:].data_ptr(),
-            tr.mom[tr._c1:].data_ptr(), tr.numel - tr._c1, None, *o, None, 1, 0, None, None, None, s),
+            tr.mom[tr._c1:].data_ptr(), tr.numel - tr._c1, None, *o, None, 1, 0, s),
         "B bwd_all(grads)": lambda: tr._backward(),
         "fc2_ce": lambda: L.pto_fc2_ce(tr.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
                                        tr.target.data_ptr(), None, tr.loss_rows.data_ptr(), tr.dlogits.data_ptr(),
