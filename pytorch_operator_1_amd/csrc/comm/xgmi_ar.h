@@ -351,6 +351,18 @@ __device__ __forceinline__ void ar_oneshot(const ArPeers* __restrict__ peers, lo
   const bool act = i < n4;
   const long long bytes = n4 * 16;
   float* const my_in = P->in[rank];
+  // the SGD epilogue's local operands (parameters, momentum, lr: nobody
+  // else writes them during the launch) are loaded before the barrier, so
+  // after it only the peer loads stand between the flag and the update
+  float4 pv = {0.f, 0.f, 0.f, 0.f}, mv = {0.f, 0.f, 0.f, 0.f};
+  float lr = 0.f;
+  if constexpr (SGD) {
+    if (act) {
+      pv = gld4(f.p + off + 4 * i);
+      mv = gld4(f.m + off + 4 * i);
+    }
+    lr = *f.a.lr;
+  }
   if (act && f.rep && f.nrep > 1 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
     fold_rep<CO>(f, mkbuf(my_in + off, bytes), off, i);
   if (!block_barrier<FENCED>(P, chan, 0, blk, rank, world, e, timeout, err)) return;
@@ -373,10 +385,7 @@ __device__ __forceinline__ void ar_oneshot(const ArPeers* __restrict__ peers, lo
   }
   if (act) {
     if constexpr (SGD) {
-      const float lr = *f.a.lr;
       const long long j = off + 4 * i;
-      float4 pv = gld4(f.p + j);
-      float4 mv = gld4(f.m + j);
       sgd4(f, j, a, pv, mv, lr);
       if (j >= f.zero_from) gst4(my_in + j, float4{0.f, 0.f, 0.f, 0.f});
     } else {
@@ -447,6 +456,15 @@ __device__ __forceinline__ void ar_role_sgd(const ArPeers* __restrict__ P, long 
     st4<CO>(mkbuf(P->tmp[rank] + off, bytes), i1, a);
   }
   const float lr = *f.a.lr;
+  // stage 2's local SGD operands before the barrier (only this thread
+  // writes them), so after it only the peer load is on the chain
+  const long long k = (long long)q * cs + j;
+  const bool v2 = in_group && j < cs && k < n4;
+  float4 pv = {0.f, 0.f, 0.f, 0.f}, mv = {0.f, 0.f, 0.f, 0.f};
+  if (v2) {
+    pv = gld4(f.p + off + 4 * k);
+    mv = gld4(f.m + off + 4 * k);
+  }
   if (!block_barrier<FENCED>(P, chan, 1, blk, rank, world, e, timeout, err)) return;
   // every peer has passed its stage 1, so its conv exchange of the same step
   // (which read the range zeroed here) is complete
@@ -456,12 +474,9 @@ __device__ __forceinline__ void ar_role_sgd(const ArPeers* __restrict__ P, long 
       gst4(f.ztail + 4 * z, float4{0.f, 0.f, 0.f, 0.f});
   }
   // stage 2: element j of chunk q from rank q's partial sums
-  const long long k = (long long)q * cs + j;
-  if (in_group && j < cs && k < n4) {
+  if (v2) {
     const float4 v = ld4<CO>(mkbuf(P->tmp[q] + off, bytes), k);
     const long long i = off + 4 * k;
-    float4 pv = gld4(f.p + i);
-    float4 mv = gld4(f.m + i);
     sgd4(f, i, v, pv, mv, lr);
     if (i >= f.zero_from) gst4(P->in[rank] + i, float4{0.f, 0.f, 0.f, 0.f});
   }
