@@ -12,6 +12,9 @@ Captures 32 consecutive fused-opt steps three ways and replays each graph
   fork_late  the same branch joined only before the NEXT step's F12, so the
              side kernel can overlap k_bwd_all (the shape an overlapped
              exchange on a second stream would have).
+With --ablate: also the step with ONE of its four launches left out
+(no_F12 / no_F3 / no_F4dx / no_bwd), i.e. each launch's marginal cost inside
+the replayed graph (the kernels then read stale activations: timing only).
 Timing only: the trainer state is rolled back afterwards, numerics are not
 checked.  Usage: python tools/fork_join_probe.py [--steps 32] [--reps 30]"""
 from __future__ import annotations
@@ -31,6 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--ablate", action="store_true")
     a = ap.parse_args()
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
 
@@ -44,6 +48,13 @@ def main():
     tiny = torch.zeros(64, device=dev)
 
     def step(mode: str):
+        if mode.startswith("no_"):
+            for which, name in enumerate(("F12", "F3", "F4dx")):
+                if mode != "no_" + name:
+                    tr._forward(only=which)
+            if mode != "no_bwd":
+                tr._backward()
+            return
         tr._forward()
         if mode == "plain":
             tr._backward()
@@ -59,7 +70,8 @@ def main():
             torch.cuda.current_stream(dev).wait_stream(side)
 
     graphs = {}
-    for mode in ("plain", "fork", "fork_late"):
+    modes = ["plain", "fork", "fork_late"] + (["no_F12", "no_F3", "no_F4dx", "no_bwd"] if a.ablate else [])
+    for mode in modes:
         with torch.cuda.stream(main_s):  # warm the branch outside capture
             step(mode)
         torch.cuda.synchronize()
