@@ -180,7 +180,8 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": round(value / (BASELINE_SAMPLES_PER_SEC_PER_RANK * n), 1),
             "dtype": "fp32",
-            "data": "synthetic (MNIST-shaped 1x28x28, resident in HBM), random-init weights",
+            "data": ("synthetic (MNIST-shaped 1x28x28, resident in HBM), random-init weights" if device.type == "cuda"
+                     else "synthetic (MNIST-shaped 1x28x28, in host memory), random-init weights"),
             "config": {
                 "model": "mnist-cnn (reference examples/mnist/mnist.py Net, 431,080 params)",
                 "global_batch": args.batch_size * n,
