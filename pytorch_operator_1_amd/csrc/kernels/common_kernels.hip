@@ -187,9 +187,49 @@ __global__ __launch_bounds__(64) void k_lane_ops_selftest(const float* __restric
   out[10 * 64 + l] = wave_max(x);
 }
 
+// Synthetic MNIST-shaped data (models/mnist.py synthetic_mnist): a
+// counter-based splitmix64 hash of (seed, image, pixel) -- the same formula
+// the host implements in numpy, so both produce identical values.  Label =
+// hash(seed, image, 784) % 10; pixel = clamp(u * 0.3 + 0.7 * [inside the
+// label's 6x6 blob], 0, 1), normalised like Normalize((0.1307,), (0.3081,)).
+// Every float operation is rounded separately (no contraction) to match the
+// host.  One thread per pixel; 785 counters per image.
+__device__ __forceinline__ unsigned long long smix64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(256) void k_synth_mnist(float* __restrict__ x, int64_t* __restrict__ y, long long n,
+                                                     unsigned long long key) {
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n * 784) return;
+  const long long i = t / 784;
+  const int p = (int)(t - i * 784);
+  const int lab = (int)(smix64((unsigned long long)(i * 785 + 784) * 0x9E3779B97F4A7C15ULL + key) % 10ULL);
+  const unsigned long long u64 = smix64((unsigned long long)(i * 785 + p) * 0x9E3779B97F4A7C15ULL + key);
+  const float u = (float)(u64 >> 40) * (1.0f / 16777216.0f);
+  const int r = p / 28, c = p - r * 28;
+  const int y0 = lab < 3 ? 2 : (lab < 6 ? 11 : (lab < 9 ? 20 : 11));
+  const int x0 = lab == 9 ? 8 : 2 + 9 * (lab % 3);
+  float v = __fmul_rn(u, 0.3f);
+  if (r >= y0 && r < y0 + 6 && c >= x0 && c < x0 + 6) v = __fadd_rn(v, 0.7f);
+  v = fminf(fmaxf(v, 0.f), 1.f);
+  x[t] = __fdiv_rn(__fsub_rn(v, 0.1307f), 0.3081f);
+  if (p == 0) y[i] = lab;
+}
+
 }  // namespace
 
 #define PTO_API extern "C" __attribute__((visibility("default")))
+
+// key = splitmix64(seed) (the host computes it the same way)
+PTO_API int pto_synth_mnist(float* x, int64_t* y, long long n, unsigned long long key, hipStream_t s) {
+  if (n < 0 || !x || !y) return -1;
+  if (n == 0) return 0;
+  const long long tot = n * 784;
+  hipLaunchKernelGGL(k_synth_mnist, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, x, y, n, key);
+  return (int)hipGetLastError();
+}
 
 PTO_API int pto_lane_ops_selftest(const float* a, const float* b, float* out, hipStream_t s) {
   hipLaunchKernelGGL(k_lane_ops_selftest, dim3(1), dim3(64), 0, s, a, b, out);

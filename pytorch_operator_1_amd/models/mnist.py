@@ -111,20 +111,57 @@ class MnistNet(nn.Module):
         return F.log_softmax(x, dim=1)
 
 
-def synthetic_mnist(n: int, device, seed: int = 1, dtype=torch.float32):
+# class -> top-left corner of its 6x6 blob (k_synth_mnist hard-codes the same table)
+BLOB_ROWS = (2, 2, 2, 11, 11, 11, 20, 20, 20, 11)
+BLOB_COLS = (2, 11, 20, 2, 11, 20, 2, 11, 20, 8)
+_GOLD = 0x9E3779B97F4A7C15
+_M64 = (1 << 64) - 1
+
+
+def _smix64_int(z: int) -> int:
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def _synth_key(seed: int) -> int:
+    return _smix64_int((int(seed) + _GOLD) & _M64)
+
+
+def synthetic_mnist(n: int, device, seed: int = 1, dtype=torch.float32, source: str = "torch"):
     """Synthetic MNIST-shaped data (normalised like ``Normalize((0.1307,),
     (0.3081,))``) with a learnable label rule, resident on ``device``.
 
     There is no network in this environment, so real MNIST cannot be
     downloaded; the label is a deterministic function of the image (which
     quadrant holds the brightest blob) so training visibly converges.
+
+    ``source="torch"`` (default): drawn from the torch CPU generator and
+    copied to ``device`` -- the same values on every device, the set the
+    numerics tests and the benchmark use.  ``source="hash"`` on a GPU: one
+    HIP launch (``k_synth_mnist``, common_kernels.hip) writes the set in
+    place from a counter-based hash of (seed, image, pixel), same
+    distribution, different values: no host generation, no host->device
+    copy and none of the framework's lazily loaded RNG kernels, which
+    together were ~0.4 s of a fresh job's submit -> first step (the
+    operator's training image uses it; train/mnist.py).
     """
+    dev = torch.device(device)
+    key = _synth_key(seed)
+    if dev.type == "cuda" and source == "hash":
+        from ..ops import _lib
+
+        x = torch.empty((n, 1, 28, 28), device=dev, dtype=torch.float32)
+        y = torch.empty(n, device=dev, dtype=torch.int64)
+        _lib.check(_lib.lib().pto_synth_mnist(x.data_ptr(), y.data_ptr(), n, key, _lib.stream_ptr(dev)),
+                   "synth_mnist")
+        return x.to(dtype), y
     g = torch.Generator(device="cpu").manual_seed(seed)
     labels = torch.randint(0, NUM_CLASSES, (n,), generator=g)
     imgs = torch.rand((n, 1, 28, 28), generator=g) * 0.3
     # Paint a class-dependent 6x6 blob: 10 classes -> 10 fixed positions.
-    ys = torch.tensor([2, 2, 2, 11, 11, 11, 20, 20, 20, 11])
-    xs = torch.tensor([2, 11, 20, 2, 11, 20, 2, 11, 20, 8])
+    ys = torch.tensor(BLOB_ROWS)
+    xs = torch.tensor(BLOB_COLS)
     # one broadcast mask instead of per-class fancy indexing (same values)
     r = torch.arange(28)
     y0, x0 = ys[labels][:, None], xs[labels][:, None]
@@ -132,4 +169,4 @@ def synthetic_mnist(n: int, device, seed: int = 1, dtype=torch.float32):
     cols = (r >= x0) & (r < x0 + 6)
     imgs[:, 0].add_((rows[:, :, None] & cols[:, None, :]).to(imgs.dtype), alpha=0.7)
     imgs = (imgs.clamp_(0, 1) - 0.1307) / 0.3081
-    return imgs.to(device=device, dtype=dtype), labels.to(device)
+    return imgs.to(device=dev, dtype=dtype), labels.to(dev)

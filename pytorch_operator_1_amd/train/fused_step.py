@@ -513,6 +513,19 @@ class FusedMnistTrainer:
         while it logs."""
         if n <= 0:
             return
+        if self.graph_mode == "full" and self._graphs is None and n == 1:
+            # the very first optimizer step runs from eager launches and the
+            # capture of the step graphs (tens of them, each warm-replayed)
+            # waits for the next run(): a job's first step is not queued
+            # behind it (submit -> first step).  Same kernels, same results.
+            self._align_ranks("first-step")  # xGMI: peers line up before cross-rank launches
+            self._eager_step()
+            if self.fused_opt:
+                self._commit_launch()  # like a closing graph: nothing owed after run()
+            self.steps_done += 1
+            self._owed = False
+            self.check_comm(blocking_check)
+            return
         if self.graph_mode == "full":
             self._ensure_captured()
             if self._graph_close:

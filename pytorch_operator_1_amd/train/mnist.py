@@ -112,8 +112,11 @@ def load_data(args, device, rank):
                 print(f"[pto] {args.dataset} from {d}: {len(ytr)} train / {len(yte)} test", flush=True)
             return (prep(xtr), torch.from_numpy(ytr).to(device), prep(xte), torch.from_numpy(yte).to(device))
     # reference-equivalent: every rank uses the same seed/order (no sampler)
-    xtr, ytr = synthetic_mnist(args.train_size, device, seed=args.seed)
-    xte, yte = synthetic_mnist(args.test_size, device, seed=args.seed + 7)
+    # generated on the GPU by one HIP launch (synthetic_mnist source="hash"):
+    # a fresh job reaches its first step without host-side data generation
+    src = "hash" if device.type == "cuda" else "torch"
+    xtr, ytr = synthetic_mnist(args.train_size, device, seed=args.seed, source=src)
+    xte, yte = synthetic_mnist(args.test_size, device, seed=args.seed + 7, source=src)
     return xtr, ytr, xte, yte
 
 

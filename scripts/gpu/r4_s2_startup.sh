@@ -1,0 +1,18 @@
+#!/bin/bash
+# first step eager + synthetic data generated on the GPU: startup phases,
+# submit -> first step through the stack, every GPU test, the driver's bench.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/st
+timeout -k 10 300 python tools/startup_probe.py > gpurun_out/st/startup2.json 2> gpurun_out/st/startup2.err || { tail -20 gpurun_out/st/startup2.err; exit 1; }
+cat gpurun_out/st/startup2.json
+timeout -k 10 300 python tools/first_step_latency.py --gpu --runs 3 --zygote 1 > gpurun_out/st/latency2.jsonl 2> gpurun_out/st/latency2.err || { tail -20 gpurun_out/st/latency2.err; exit 1; }
+cat gpurun_out/st/latency2.jsonl
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread > gpurun_out/st/pytest_gpu.log 2>&1
+rc=$?
+grep -E "passed|failed|FAILED" gpurun_out/st/pytest_gpu.log | tail -8
+case $rc in 0|1) ;; *) echo "pytest rc=$rc"; exit $rc;; esac
+timeout -k 10 300 python bench.py > gpurun_out/st/bench_default.json 2> gpurun_out/st/bench_default.err || { tail -20 gpurun_out/st/bench_default.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/st/bench_default.json')); print(d['value'], d['ms_per_step'], d.get('submit_to_first_step_s'), d['config']['final_loss'])"
+exit $rc

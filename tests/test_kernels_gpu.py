@@ -247,3 +247,46 @@ def test_cross_lane_helpers():
     np.testing.assert_array_equal(o[8], np.repeat(rows.max(1), 16))
     np.testing.assert_allclose(o[9], np.full(64, x.sum()), rtol=1e-5)
     np.testing.assert_array_equal(o[10], np.full(64, x.max()))
+
+
+def _synth_host(n: int, key: int):
+    """numpy twin of k_synth_mnist: same hash, same float32 rounding."""
+    import numpy as np
+
+    from pytorch_operator_1_amd.models.mnist import BLOB_COLS, BLOB_ROWS
+
+    r = np.arange(784) // 28
+    c = np.arange(784) % 28
+    with np.errstate(over="ignore"):
+        ctr = np.arange(n, dtype=np.uint64)[:, None] * np.uint64(785) + np.arange(785, dtype=np.uint64)[None]
+        z = ctr * np.uint64(0x9E3779B97F4A7C15) + np.uint64(key)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    lab = (z[:, 784] % np.uint64(10)).astype(np.int64)
+    u = (z[:, :784] >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    v = u * np.float32(0.3)
+    y0, x0 = np.array(BLOB_ROWS)[lab][:, None], np.array(BLOB_COLS)[lab][:, None]
+    blob = (r >= y0) & (r < y0 + 6) & (c >= x0) & (c < x0 + 6)
+    v = np.clip(np.where(blob, v + np.float32(0.7), v).astype(np.float32), np.float32(0), np.float32(1))
+    return (v - np.float32(0.1307)) / np.float32(0.3081), lab
+
+
+def test_synthetic_mnist_kernel_matches_host_formula():
+    """k_synth_mnist (the operator image's GPU data generator) against its
+    numpy twin: labels exact, pixels within 1e-6, balanced classes,
+    deterministic."""
+    from pytorch_operator_1_amd.models.mnist import _synth_key, synthetic_mnist
+
+    n = 3000
+    x, y = synthetic_mnist(n, DEV, seed=5, source="hash")
+    torch.cuda.synchronize()
+    hx, hy = _synth_host(n, _synth_key(5))
+    assert torch.equal(y.cpu(), torch.from_numpy(hy))  # labels: exact integer hash
+    # pixels: the same float32 operations; the device division may differ
+    # from the host's in the last bit
+    assert float((x.view(n, 784).cpu() - torch.from_numpy(hx)).abs().max()) < 1e-6
+    counts = torch.bincount(y.cpu(), minlength=10)
+    assert int(counts.min()) > n // 20
+    x2, y2 = synthetic_mnist(n, DEV, seed=5, source="hash")
+    assert torch.equal(x, x2) and torch.equal(y, y2)  # deterministic
