@@ -115,8 +115,11 @@ class FusedMnistTrainer:
             n = math.prod(shape)
             self._p[name] = self._params[off:off + n].view(shape)
             self.g[name] = self.grads[off:off + n].view(shape)
-        # same init as the stock module under the same seed
-        torch.manual_seed(seed)
+        # same init as the stock module under the same seed.  Only the CPU
+        # generator draws these values; torch.manual_seed would also seed the
+        # GPU generators, whose first touch costs ~0.11 s on the MI355X box
+        # (profiles/startup_latency_r4.md), and nothing here draws from them
+        torch.default_generator.manual_seed(seed)
         ref = MnistNet()
         with torch.no_grad():
             for name, t in ref.state_dict().items():

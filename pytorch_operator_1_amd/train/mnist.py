@@ -206,8 +206,15 @@ def _main(argv=None):
     args = parse_args(argv)
     use_cuda = not args.no_cuda and torch.cuda.is_available() and os.environ.get("PTO_NO_GPU") != "1"
     if use_cuda:
-        print("Using CUDA (HIP) on", torch.cuda.get_device_name(0))
-    torch.manual_seed(args.seed)
+        print("Using CUDA (HIP) on", pdist.gpu_name(0))
+    impl = args.impl or ("fused" if use_cuda else "eager")
+    if impl == "fused":
+        # the fused trainer draws only from the CPU generator (init weights,
+        # epoch shuffles); seeding the GPU generators too, as
+        # torch.manual_seed does, costs ~0.11 s of submit -> first step
+        torch.default_generator.manual_seed(args.seed)
+    else:
+        torch.manual_seed(args.seed)
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     rccl_log = (pdist.rccl_log_setup() if use_cuda and world_env > 1 and
                 pdist.resolve_backend(args.backend, True) == "nccl" else None)
@@ -228,7 +235,6 @@ def _main(argv=None):
     dataset_len = xtr.shape[0]
     shuffler = EpochShuffler(xtr, ytr, args.seed, enabled=not args.no_shuffle)
 
-    impl = args.impl or ("fused" if use_cuda else "eager")
     from .runner import build_trainer
 
     extra = {"comm": args.comm} if (args.comm and impl == "fused") else {}

@@ -69,6 +69,23 @@ def resolve_backend(name: str | None, use_gpu: bool) -> str:
     return be
 
 
+def gpu_count() -> int:
+    """Visible GPUs as the HIP runtime counts them (honours
+    ``HIP_VISIBLE_DEVICES``).  ``torch.cuda.device_count()`` on ROCm asks
+    amdsmi first, and its first ``amdsmi_init`` costs ~0.11 s on the MI355X
+    box, on a fresh job's submit -> first step path
+    (profiles/startup_latency_r4.md)."""
+    return int(torch._C._cuda_getDeviceCount()) if torch.cuda.is_available() else 0
+
+
+def gpu_name(index: int = 0) -> str:
+    """Marketing name of a visible GPU, without ``torch.cuda.device_count()``
+    (see :func:`gpu_count`)."""
+    torch.cuda.init()  # defines torch.cuda._get_device_properties (C++ binding)
+    props = getattr(torch.cuda, "_get_device_properties", None)
+    return props(index).name if props is not None else torch.cuda.get_device_name(index)
+
+
 def init_distributed(backend: str | None = None, use_gpu: bool | None = None,
                      timeout_s: float = 300.0) -> tuple[DistEnv, torch.device]:
     """Initialise the default process group from the env contract and pick
@@ -83,7 +100,7 @@ def init_distributed(backend: str | None = None, use_gpu: bool | None = None,
     if use_gpu is None:
         use_gpu = torch.cuda.is_available()
     if use_gpu:
-        n = torch.cuda.device_count()
+        n = gpu_count()
         device = torch.device("cuda", env.local_rank % max(n, 1))
         torch.cuda.set_device(device)
     else:
