@@ -370,53 +370,64 @@ inline unsigned grid_for(long long work, int per_block = NT) {
 // out[c][r] = in[r][c] for a [rows x cols] bf16 matrix (row strides ld_in /
 // ld_out).  Keeps the transposed weight copies W^T of the Llama linears
 // that make every dgrad GEMM K-contiguous (dX = dY (W^T)^T, the forward's
+// operand layout) and the transposed activations of the K-contiguous dW.
+// Register transpose, no LDS: each lane owns an 8x8 sub-tile -- eight 16-B
+// row loads in flight, 32 v_perm_b32, eight 16-B column stores.  Output
+// dword m of transposed row k is (R[2m][k], R[2m+1][k]): one byte permute of
+// input dwords R[2m].d[k/2] and R[2m+1].d[k/2] (low or high halves).  Lane
+// (g, ch) = (lane >> 3, lane & 7) takes rows 8g.., cols 8ch.. of its wave's
+// 64x64 tile, so each load instruction reads eight full 128-B row segments
+// and each store instruction writes eight full 128-B output-row segments.
+// A block is 4 waves side by side: a 64 x 256 input tile.
+__global__ __launch_bounds__(256) void k_transpose_bf16(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                        long long rows, long long cols, long long ld_in,
+                                                        long long ld_out, int vec) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long r = (long long)blockIdx.y * 64 + 8 * (lane >> 3);
+  const long long c = ((long long)blockIdx.x * 4 + w) * 64 + 8 * (lane & 7);
+  if (r >= rows || c >= cols) return;
+  const bool full = vec && r + 8 <= rows && c + 8 <= cols;
+  uint32_t a[8][4];
+  if (full) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint4 v = *reinterpret_cast<const uint4*>(in + (r + i) * ld_in + c);
+      a[i][0] = v.x; a[i][1] = v.y; a[i][2] = v.z; a[i][3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t lo = (r + i < rows && c + 2 * d < cols) ? in[(r + i) * ld_in + c + 2 * d] : 0u;
+        const uint32_t hi = (r + i < rows && c + 2 * d + 1 < cols) ? in[(r + i) * ld_in + c + 2 * d + 1] : 0u;
+        a[i][d] = lo | (hi << 16);
+      }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t sel = (k & 1) ? 0x07060302u : 0x05040100u;  // high / low halves of both dwords
+    uint32_t o[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) o[m] = __builtin_amdgcn_perm(a[2 * m + 1][k >> 1], a[2 * m][k >> 1], sel);
+    if (full) {
+      *reinterpret_cast<uint4*>(out + (c + k) * ld_out + r) = make_uint4(o[0], o[1], o[2], o[3]);
+    } else if (c + k < cols) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (r + e < rows) out[(c + k) * ld_out + r + e] = (uint16_t)((e & 1) ? (o[e >> 1] >> 16) : (o[e >> 1] & 0xffffu));
+    }
+  }
+}
+
+// out[c][r] = in[r][c] for a [rows x cols] bf16 matrix (row strides ld_in /
+// ld_out).  Keeps the transposed weight copies W^T of the Llama linears
+// that make every dgrad GEMM K-contiguous (dX = dY (W^T)^T, the forward's
 // operand layout).  64x64 tile per 256-thread block through LDS.  Global
 // loads AND stores are 8 lanes per 128-byte row (16 B each).  LDS image:
 // 128-B rows, 16-B chunk c of row r stored at chunk c ^ ((r >> 3) & 7), so
 // the column reads (8 consecutive rows 8k..8k+7 of one column per lane,
 // k = lane & 7) of a wave fall on 32 distinct banks.
-constexpr int TP = 64;
-__device__ __forceinline__ int tp_swz(int r, int ch) { return r * TP + 8 * (ch ^ ((r >> 3) & 7)); }
-
-__global__ __launch_bounds__(256) void k_transpose_bf16(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
-                                                        long long rows, long long cols, long long ld_in,
-                                                        long long ld_out) {
-  __shared__ __attribute__((aligned(16))) uint16_t t[TP * TP];
-  const long long r0 = (long long)blockIdx.y * TP, c0 = (long long)blockIdx.x * TP;
-  const int tid = threadIdx.x, lr = tid >> 3, ch = tid & 7;
-  const bool full = r0 + TP <= rows && c0 + TP <= cols && (ld_in & 7) == 0 && (ld_out & 7) == 0;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int r = lr + 32 * h;
-    uint4 v = {0u, 0u, 0u, 0u};
-    if (full) {
-      v = *reinterpret_cast<const uint4*>(in + (r0 + r) * ld_in + c0 + 8 * ch);
-    } else if (r0 + r < rows) {
-      uint16_t e[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) e[j] = (c0 + 8 * ch + j < cols) ? in[(r0 + r) * ld_in + c0 + 8 * ch + j] : (uint16_t)0;
-      v = *reinterpret_cast<uint4*>(e);
-    }
-    *reinterpret_cast<uint4*>(t + tp_swz(r, ch)) = v;
-  }
-  __syncthreads();
-  // output row oc (= input column), chunk k = input rows 8k..8k+7
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int oc = lr + 32 * h, k = ch;
-    uint16_t e[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) e[j] = t[tp_swz(8 * k + j, oc >> 3) + (oc & 7)];
-    if (full) {
-      *reinterpret_cast<uint4*>(out + (c0 + oc) * ld_out + r0 + 8 * k) = *reinterpret_cast<uint4*>(e);
-    } else if (c0 + oc < cols) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (r0 + 8 * k + j < rows) out[(c0 + oc) * ld_out + r0 + 8 * k + j] = e[j];
-    }
-  }
-}
-
 }  // namespace
 
 #define PTO_API extern "C" __attribute__((visibility("default")))
@@ -493,15 +504,16 @@ PTO_API int pto_ce_bwd(void* logits, const long long* labels, const float* lse, 
   return (int)hipGetLastError();
 }
 
-// out = in^T (bf16, [rows x cols] -> [cols x rows]); 16-byte aligned fast
-// path for whole 64x64 tiles, element-wise edges.
+// out = in^T (bf16, [rows x cols] -> [cols x rows]); 16-byte vector path
+// when both pointers are 16-B aligned and both row strides are multiples of
+// 8 elements, element-wise edges.
 PTO_API int pto_transpose_bf16(const void* in, void* out, long long rows, long long cols, long long ld_in,
                                long long ld_out, hipStream_t s) {
   if (rows <= 0 || cols <= 0) return 0;
-  if (ld_in < cols || ld_out < rows || (cols + TP - 1) / TP > 0x7fffffff || (rows + TP - 1) / TP > 65535) return -1;
-  if ((((uintptr_t)in) | ((uintptr_t)out)) & 15) return -1;
-  dim3 grid((unsigned)((cols + TP - 1) / TP), (unsigned)((rows + TP - 1) / TP));
+  if (ld_in < cols || ld_out < rows || (cols + 255) / 256 > 0x7fffffff || (rows + 63) / 64 > 65535) return -1;
+  const int vec = !(((((uintptr_t)in) | ((uintptr_t)out)) & 15) || (ld_in & 7) || (ld_out & 7));
+  dim3 grid((unsigned)((cols + 255) / 256), (unsigned)((rows + 63) / 64));
   hipLaunchKernelGGL(k_transpose_bf16, grid, dim3(256), 0, s, reinterpret_cast<const uint16_t*>(in),
-                     reinterpret_cast<uint16_t*>(out), rows, cols, ld_in, ld_out);
+                     reinterpret_cast<uint16_t*>(out), rows, cols, ld_in, ld_out, vec);
   return (int)hipGetLastError();
 }
