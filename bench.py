@@ -143,6 +143,9 @@ def main(argv=None):
 
     run = getattr(trainer, "run", None) or (lambda n: [trainer.step() for _ in range(n)])
     run(args.warmup)
+    # graph capture is setup, never timed: a warm-up of 0 or 1 step (the
+    # first step runs eagerly) would otherwise leave it to the timed run()
+    getattr(trainer, "prepare", lambda: None)()
     sync()
     pdist.barrier(device)
     sync()

@@ -507,6 +507,14 @@ class FusedMnistTrainer:
             self.comm_info["graph_mode"] = "split (capture failed)"
             self._capture()
 
+    def prepare(self):
+        """Capture the step graphs now (collective: every rank calls it at
+        the same point).  run() captures on its own when first asked for
+        more than one step; a benchmark calls this after its warm-up so its
+        timed region never includes capture, whatever the warm-up length."""
+        if self.graph_mode != "none":
+            self._ensure_captured()
+
     def run(self, n: int, blocking_check: bool = True):
         """Run exactly ``n`` training steps, then check the gradient
         transport's error word (a dead or stalled xGMI peer raises
