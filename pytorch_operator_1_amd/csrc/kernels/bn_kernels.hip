@@ -51,13 +51,14 @@ __device__ __forceinline__ V8 load8(const uint16_t* p) {
   }
   return o;
 }
-__device__ __forceinline__ void store8(uint16_t* p, const V8& a) {
+__device__ __forceinline__ uint4 store8(uint16_t* p, const V8& a) {
   uint4 r;
   r.x = (uint32_t)f2bf(a.v[0]) | ((uint32_t)f2bf(a.v[1]) << 16);
   r.y = (uint32_t)f2bf(a.v[2]) | ((uint32_t)f2bf(a.v[3]) << 16);
   r.z = (uint32_t)f2bf(a.v[4]) | ((uint32_t)f2bf(a.v[5]) << 16);
   r.w = (uint32_t)f2bf(a.v[6]) | ((uint32_t)f2bf(a.v[7]) << 16);
   *reinterpret_cast<uint4*>(p) = r;
+  return r;
 }
 __device__ __forceinline__ V8 loadf8(const float* p) {
   const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
@@ -178,15 +179,20 @@ __global__ __launch_bounds__(BN_FT) void k_bn_finalize(const float* __restrict__
 
 // y = [relu](x * scale + shift [+ res]); EW_U vectors per thread iteration,
 // all loads issued before the first use (RES/RELU are template parameters,
-// out-of-range slots load vector 0 and are not stored).
+// out-of-range slots load vector 0 and are not stored).  mask (optional):
+// one byte per 8-channel vector, bit j = (stored y_j > 0) -- the backward of
+// relu(bn(x) + res) reads it instead of y (1/16 of the bytes).
 constexpr int EW_U = 4;
 template <bool RES, bool RELU>
 __global__ __launch_bounds__(BN_T) void k_bn_apply(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                    uint16_t* __restrict__ y, long long n8, int C,
-                                                   const float* __restrict__ stat) {
-  const float* scale = stat + 2 * C;
-  const float* shift = stat + 3 * C;
+                                                   const float* __restrict__ stat, uint8_t* __restrict__ mask) {
   const long long stride = (long long)gridDim.x * BN_T;
+  // the grid stride (gridDim.x * 2048 elements) is a multiple of C (a power
+  // of two <= 2048): a thread's 8 channels never change, so its affine
+  // coefficients are loaded once, not per vector
+  const int c0 = (int)((((long long)blockIdx.x * BN_T + threadIdx.x) * 8) & (C - 1));
+  const V8 sc = loadf8(stat + 2 * C + c0), sh = loadf8(stat + 3 * C + c0);
   for (long long i0 = (long long)blockIdx.x * BN_T + threadIdx.x; i0 < n8; i0 += EW_U * stride) {
     V8 a[EW_U], r[EW_U];
     long long ii[EW_U];
@@ -200,30 +206,37 @@ __global__ __launch_bounds__(BN_T) void k_bn_apply(const uint16_t* __restrict__ 
 #pragma unroll
     for (int u = 0; u < EW_U; ++u) {
       if (ii[u] >= n8) continue;
-      const int c0 = (int)((ii[u] * 8) & (C - 1));  // C is a power of two
-      const V8 sc = loadf8(scale + c0), sh = loadf8(shift + c0);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float v = fmaf(a[u].v[j], sc.v[j], sh.v[j]);
         if (RES) v += r[u].v[j];
         a[u].v[j] = RELU ? fmaxf(v, 0.f) : v;
       }
-      store8(y + ii[u] * 8, a[u]);
+      const uint4 w = store8(y + ii[u] * 8, a[u]);
+      if (mask) {
+        const uint32_t h[4] = {w.x, w.y, w.z, w.w};
+        uint32_t b = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          b |= (bf2f((uint16_t)(h[j] & 0xffffu)) > 0.f ? 1u : 0u) << (2 * j) |
+               (bf2f((uint16_t)(h[j] >> 16)) > 0.f ? 1u : 0u) << (2 * j + 1);
+        mask[ii[u]] = (uint8_t)b;
+      }
     }
   }
 }
 
 // Backward reduction: g = dy * mask; per channel sums of g and g * xhat.
 // mode 0: no ReLU; 1: ReLU, mask recomputed from x (x*scale+shift > 0);
-// 2: ReLU after a residual add, mask = (y > 0), and g is stored (it is also
-// the gradient of the residual input).
+// 2: ReLU after a residual add, mask = (y > 0) from the forward's bitmask,
+// and g is stored (it is also the gradient of the residual input).
 // MODE is a template parameter so every load of an unrolled group is
 // issued before the first use (a runtime mode branch between them split the
 // group); the row bound is clamped instead of predicated for the same reason.
 template <int MODE>
 __global__ __launch_bounds__(BN_T) void k_bn_bwd_reduce(const uint16_t* __restrict__ dy,
                                                         const uint16_t* __restrict__ x,
-                                                        const uint16_t* __restrict__ y, long long M, int C,
+                                                        const uint8_t* __restrict__ ymask, long long M, int C,
                                                         int iters, const float* __restrict__ stat,
                                                         uint16_t* __restrict__ g_out, float* __restrict__ part) {
   __shared__ float red[4096];
@@ -232,9 +245,10 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_reduce(const uint16_t* __restri
   const V8 sc = loadf8(stat + 2 * C + c8), sh = loadf8(stat + 3 * C + c8);
   float s[8] = {}, q[8] = {};
   const long long r0 = (long long)blockIdx.x * iters * rpi + rsub;
-  constexpr int U = MODE == 2 ? BN_U / 2 : BN_U;  // 16-byte loads in flight: 2-3 streams x U rows
+  constexpr int U = BN_U;  // 16-byte loads in flight: 2 streams x U rows (+ U mask bytes in mode 2)
   for (int it = 0; it < iters; it += U) {
-    V8 g[U], a[U], yv[U];
+    V8 g[U], a[U];
+    uint32_t mk[U];
     bool ok[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -243,7 +257,7 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_reduce(const uint16_t* __restri
       const long long o = (ok[u] ? row : 0) * C + c8;  // row 0 when out of range: in bounds, masked below
       g[u] = load8(dy + o);
       a[u] = load8(x + o);
-      if (MODE == 2) yv[u] = load8(y + o);
+      if (MODE == 2) mk[u] = ymask[o >> 3];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -258,7 +272,7 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_reduce(const uint16_t* __restri
       } else if (MODE == 2) {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          if (!(yv[u].v[j] > 0.f)) g[u].v[j] = 0.f;
+          if (!((mk[u] >> j) & 1u)) g[u].v[j] = 0.f;
         const long long row = r0 + (long long)(it + u) * rpi;
         if (ok[u]) store8(g_out + row * C + c8, g[u]);
       }
@@ -303,6 +317,11 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_apply(const uint16_t* __restric
                                                        long long n8, int C, const float* __restrict__ stat,
                                                        const float* __restrict__ coef) {
   const long long stride = (long long)gridDim.x * BN_T;
+  // fixed channels per thread (see k_bn_apply): coefficients loaded once
+  const int c0 = (int)((((long long)blockIdx.x * BN_T + threadIdx.x) * 8) & (C - 1));
+  const V8 k1 = loadf8(coef + c0), k2 = loadf8(coef + C + c0), k3 = loadf8(coef + 2 * C + c0);
+  V8 sc{}, sh{};
+  if (MODE == 1) sc = loadf8(stat + 2 * C + c0), sh = loadf8(stat + 3 * C + c0);
   for (long long i0 = (long long)blockIdx.x * BN_T + threadIdx.x; i0 < n8; i0 += EW_U * stride) {
     V8 g[EW_U], a[EW_U];
     long long ii[EW_U];
@@ -316,10 +335,7 @@ __global__ __launch_bounds__(BN_T) void k_bn_bwd_apply(const uint16_t* __restric
 #pragma unroll
     for (int u = 0; u < EW_U; ++u) {
       if (ii[u] >= n8) continue;
-      const int c0 = (int)((ii[u] * 8) & (C - 1));  // C is a power of two
-      const V8 k1 = loadf8(coef + c0), k2 = loadf8(coef + C + c0), k3 = loadf8(coef + 2 * C + c0);
       if (MODE == 1) {
-        const V8 sc = loadf8(stat + 2 * C + c0), sh = loadf8(stat + 3 * C + c0);
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (!(fmaf(a[u].v[j], sc.v[j], sh.v[j]) > 0.f)) g[u].v[j] = 0.f;
@@ -339,7 +355,11 @@ bool bn_shape_ok(long long M, int C) {
 }
 
 // Reduction grid.  These passes stream HBM, so what matters is bytes in
-// flight: BN_U 16-byte loads per thread x resident threads.  Round 1 capped
+// flight: BN_U 16-byte loads per thread x resident threads.  Each block
+// streams one contiguous slab of rows; interleaving the blocks' rows (one
+// 4 KB chunk per block per iteration, a grid-wide contiguous window)
+// measured slower in round 4: stats 3.94 -> 3.78 TB/s and the ReLU backward
+// reduce 4.83 -> 3.99 TB/s at 411 MB (profiles/bn_r4.md).  Round 1 capped
 // the grid at 512 blocks (256 at C = 2048: one 4-wave block per CU) and ran
 // at ~40 % of HBM bandwidth; the default now allows 1024 blocks (4 per CU)
 // with >= 8 row iterations each, partials bounded to 4 M floats (16 MB).
@@ -377,7 +397,7 @@ PTO_API int pto_bn_scratch_floats(long long M, int C) {
 // backward); res / run_mean / run_var / nbt may be null.
 PTO_API int pto_bn_fwd(const void* x, const void* res, void* y, long long M, int C, const float* gamma,
                        const float* beta, float eps, float momentum, float* run_mean, float* run_var, long long* nbt,
-                       float* stat, float* scratch, int relu, hipStream_t s) {
+                       float* stat, float* scratch, int relu, void* mask, hipStream_t s) {
   if (!bn_shape_ok(M, C)) return -1;
   if ((((uintptr_t)x) | ((uintptr_t)y) | ((uintptr_t)res)) & 15) return -1;
   int nblk, iters;
@@ -390,22 +410,24 @@ PTO_API int pto_bn_fwd(const void* x, const void* res, void* y, long long M, int
   auto* ka = res ? (relu ? k_bn_apply<true, true> : k_bn_apply<true, false>)
                  : (relu ? k_bn_apply<false, true> : k_bn_apply<false, false>);
   hipLaunchKernelGGL(ka, dim3(elementwise_blocks(n8)), dim3(BN_T), 0, s, reinterpret_cast<const uint16_t*>(x),
-                     reinterpret_cast<const uint16_t*>(res), reinterpret_cast<uint16_t*>(y), n8, C, stat);
+                     reinterpret_cast<const uint16_t*>(res), reinterpret_cast<uint16_t*>(y), n8, C, stat,
+                     reinterpret_cast<uint8_t*>(mask));
   return (int)hipGetLastError();
 }
 
-// Backward.  mode 0/1/2 as k_bn_bwd_reduce; y needed for mode 2, where
-// g_out (= d residual) is also written.  coef: 3*C floats scratch.
-PTO_API int pto_bn_bwd(const void* dy, const void* x, const void* y, void* dx, void* g_out, long long M, int C,
+// Backward.  mode 0/1/2 as k_bn_bwd_reduce; ymask (the forward's ReLU
+// bitmask, M*C/8 bytes) needed for mode 2, where g_out (= d residual) is
+// also written.  coef: 3*C floats scratch.
+PTO_API int pto_bn_bwd(const void* dy, const void* x, const void* ymask, void* dx, void* g_out, long long M, int C,
                        const float* gamma, const float* stat, float* dgamma, float* dbeta, float* coef,
                        float* scratch, int mode, hipStream_t s) {
-  if (!bn_shape_ok(M, C) || mode < 0 || mode > 2 || (mode == 2 && (!y || !g_out))) return -1;
-  if ((((uintptr_t)dy) | ((uintptr_t)x) | ((uintptr_t)dx) | ((uintptr_t)y) | ((uintptr_t)g_out)) & 15) return -1;
+  if (!bn_shape_ok(M, C) || mode < 0 || mode > 2 || (mode == 2 && (!ymask || !g_out))) return -1;
+  if ((((uintptr_t)dy) | ((uintptr_t)x) | ((uintptr_t)dx) | ((uintptr_t)g_out)) & 15) return -1;
   int nblk, iters;
   bn_grid(M, C, &nblk, &iters);
   auto* kr = mode == 0 ? k_bn_bwd_reduce<0> : (mode == 1 ? k_bn_bwd_reduce<1> : k_bn_bwd_reduce<2>);
   hipLaunchKernelGGL(kr, dim3(nblk), dim3(BN_T), 0, s, reinterpret_cast<const uint16_t*>(dy),
-                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(y), M, C, iters, stat,
+                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint8_t*>(ymask), M, C, iters, stat,
                      reinterpret_cast<uint16_t*>(g_out), scratch);
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 31) / 32), dim3(BN_FT), 0, s, scratch, nblk, M, C, gamma,
                      stat, dgamma, dbeta, coef);

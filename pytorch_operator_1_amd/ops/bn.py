@@ -44,21 +44,25 @@ class _BNAct(torch.autograd.Function):
             res = residual.contiguous(memory_format=_CL)
             if res.shape != x.shape or res.dtype != x.dtype:
                 raise ValueError("BatchNormAct: residual must match the input")
+        ctx.mode = 2 if (residual is not None and relu) else (1 if relu else 0)
+        ctx.has_res = residual is not None
+        # relu(bn(x) + res): the backward's ReLU mask cannot be recomputed
+        # from x alone; one bit per element (bit j of byte i = y[8i + j] > 0)
+        # instead of re-reading y
+        mask = torch.empty(M * C // 8, device=dev, dtype=torch.uint8) if ctx.mode == 2 else None
         _lib.check(L.pto_bn_fwd(x.data_ptr(), None if res is None else res.data_ptr(), y.data_ptr(), M, C,
                                 weight.data_ptr(), bias.data_ptr(), eps, momentum,
                                 None if running_mean is None else running_mean.data_ptr(),
                                 None if running_var is None else running_var.data_ptr(),
                                 None if nbt is None else nbt.data_ptr(), stat.data_ptr(), scratch.data_ptr(),
-                                int(relu), _lib.stream_ptr(dev)), "bn_fwd")
-        ctx.mode = 2 if (residual is not None and relu) else (1 if relu else 0)
-        ctx.has_res = residual is not None
-        ctx.save_for_backward(x, y if ctx.mode == 2 else None, weight, stat)
+                                int(relu), None if mask is None else mask.data_ptr(), _lib.stream_ptr(dev)), "bn_fwd")
+        ctx.save_for_backward(x, mask, weight, stat)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         L = _lib.lib()
-        x, y, weight, stat = ctx.saved_tensors
+        x, mask, weight, stat = ctx.saved_tensors
         dy = dy.contiguous(memory_format=_CL)
         N, C, H, W = x.shape
         M = N * H * W
@@ -69,7 +73,7 @@ class _BNAct(torch.autograd.Function):
         dbeta = torch.empty(C, device=dev, dtype=torch.float32)
         coef = torch.empty(3 * C, device=dev, dtype=torch.float32)
         scratch = torch.empty(L.pto_bn_scratch_floats(M, C), device=dev, dtype=torch.float32)
-        _lib.check(L.pto_bn_bwd(dy.data_ptr(), x.data_ptr(), None if y is None else y.data_ptr(), dx.data_ptr(),
+        _lib.check(L.pto_bn_bwd(dy.data_ptr(), x.data_ptr(), None if mask is None else mask.data_ptr(), dx.data_ptr(),
                                 None if g is None else g.data_ptr(), M, C, weight.data_ptr(), stat.data_ptr(),
                                 dgamma.data_ptr(), dbeta.data_ptr(), coef.data_ptr(), scratch.data_ptr(), ctx.mode,
                                 _lib.stream_ptr(dev)), "bn_bwd")
