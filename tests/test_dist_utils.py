@@ -89,3 +89,21 @@ def test_describe_world_single_process_cpu():
 
     d = describe_world(torch.device("cpu"))
     assert d["pg_world_size"] == 1 and d["ranks"] == [{"device": "cpu"}]
+
+
+def test_gpu_count_without_a_gpu_and_no_amdsmi(monkeypatch):
+    """gpu_count() is the HIP runtime's count: 0 here, and it never calls
+    torch.cuda.device_count() (whose amdsmi probe costs ~0.11 s on the
+    MI355X box, profiles/startup_latency_r4.md)."""
+    import torch
+
+    from pytorch_operator_1_amd.utils import dist as pdist
+
+    def boom():
+        raise AssertionError("torch.cuda.device_count() called")
+
+    monkeypatch.setattr(torch.cuda, "device_count", boom)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: False)
+    assert pdist.gpu_count() == 0
+    env, device = pdist.init_distributed(None, use_gpu=False)
+    assert device.type == "cpu" and env.world_size >= 1
