@@ -78,9 +78,11 @@ def _launch_ranks(args, argv) -> int | None:
         return None
     host_ranks = args.cpu or os.environ.get("PTO_BACKEND") == "gloo"
     if not host_ranks:
-        # device_count() does not initialise HIP on this image (a child must
-        # not be started from a process that already did)
-        n_dev = torch.cuda.device_count()
+        # counted from KFD sysfs + the visibility env, never through torch:
+        # this parent starts the GPU ranks, so it must not initialise HIP
+        from pytorch_operator_1_amd.utils.dist import visible_gpu_count_no_hip
+
+        n_dev = visible_gpu_count_no_hip()
         if n_dev < args.gpus:
             print(f"[bench] error: --gpus {args.gpus} but only {n_dev} GPU(s) visible; refusing to measure fewer "
                   f"ranks (PTO_BACKEND=gloo rehearses several ranks on one GPU)", file=sys.stderr, flush=True)
@@ -135,7 +137,7 @@ def main(argv=None):
         data_kw = dict(data=x[env.rank::env.world_size].contiguous(), target=y[env.rank::env.world_size].contiguous())
     trainer = build_trainer(args.impl, device=device, batch_size=args.batch_size, lr=args.lr,
                             momentum=args.momentum, dataset_size=args.dataset_size,
-                            seed=1 + env.rank * 0, rank=env.rank, **data_kw)
+                            seed=1, rank=env.rank, **data_kw)
 
     def sync():
         if device.type == "cuda":

@@ -522,14 +522,12 @@ struct Agent {
       } else if (q.state == "waiting" && q.reason == "CrashLoopBackOff") {
         q.held = true;  // already owed a restart: it joins this wave
         q.held_delay = std::max(0.0, q.restart_at - mono_s());
-      } else if (q.state == "terminated" && q.exit_code == 0 && q.restart_policy == "OnFailure") {
-        // finished cleanly before a peer failed: the new wave needs every
-        // rank (WORLD_SIZE), so it rejoins -- without a restart of its own
-        q.state = "waiting";
-        q.reason = "CrashLoopBackOff";
-        q.held = true;
-        q.held_delay = 0;
       }
+      // a member that already exited 0 is NOT revived: in Kubernetes a pod
+      // whose containers all succeeded is terminal, and a succeeded Master
+      // completes the job (reference status.go:99-106) -- reviving it would
+      // rerun finished training over its outputs and move a Succeeded pod
+      // back to Running.  The wave goes on without it.
     }
     fprintf(stderr, "pto-node-agent: group %s: %s failed, restart wave %d (%d member(s) stopped)\n",
             name.c_str(), culprit.c_str(), g.wave, killed);

@@ -263,7 +263,10 @@ class XgmiAllReduce:
             chk = mine.clone()
             dist.all_reduce(chk, op=dist.ReduceOp.MAX, group=self.group)
             identical &= float((chk - mine).abs().max().item()) == 0.0
-        timed_out = int(self.err.item()) != 0
+        # agreed by every rank: a barrier that timed out on some
+        # ranks only must not send those ranks to close() while the others
+        # retry with the fenced protocol into the freed peer memory
+        timed_out = not self._agree(int(self.err.item()) == 0)
         self.buf.copy_(saved)
         torch.cuda.synchronize(self.device)
         # bf16: one rounding of the fp32 sum (<= 2^-9 relative)
@@ -326,16 +329,27 @@ class XgmiAllReduce:
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
             return float(t.item())
 
+        cur = torch.cuda.current_stream(self.device)
+
         def run_xgmi():
+            # on a side stream the kernel is ordered after everything queued
+            # on the current one (the snapshot, a previous RCCL call) and
+            # before anything queued after it
+            if stream is not None:
+                stream.wait_stream(cur)
             for c, (off, n) in enumerate(ranges):
                 self.allreduce_(off, n, chan=c % 2, stream=stream)
+            if stream is not None:
+                cur.wait_stream(stream)
 
         def run_rccl():
             for off, n in ranges:
                 dist.all_reduce(self.buf[off:off + n], group=self.group)
 
         saved = self.buf.clone()
-        run_xgmi(), run_rccl()  # warm
+        run_xgmi()  # warm
+        run_rccl()
+        torch.cuda.synchronize(self.device)
         tx, tr = timed(run_xgmi), timed(run_rccl)
         ok = self._agree(int(self.err.item()) == 0)
         self.buf.copy_(saved)
@@ -362,8 +376,16 @@ class XgmiAllReduce:
         return {"use_xgmi": ok, "correct": ok, "max_rel_err": 0.0 if ok else float("nan"), "timed_out": False,
                 "xgmi_us": round(tx, 2), "rccl_us": None, "protocol": self.protocol}
 
-    def close(self):
+    def close(self, sync: bool = True):
+        """Unmap the peers and free the flag page.  ``sync`` (collective
+        callers): wait for this rank's queued kernels and for every peer
+        first, so no peer's barrier can still write into the flag page or
+        read the buffers being released."""
         L = _lib.lib()
+        if sync and getattr(self, "_flags", None) and self.world > 1 and dist.is_available() \
+                and dist.is_initialized():
+            torch.cuda.synchronize(self.device)
+            dist.barrier(group=self.group)
         for p in getattr(self, "_opened", []):
             L.pto_ar_close_ipc_handle(p)
         self._opened = []

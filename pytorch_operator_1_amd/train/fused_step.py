@@ -524,7 +524,7 @@ class FusedMnistTrainer:
         while it logs."""
         if n <= 0:
             return
-        if self.graph_mode == "full" and self._graphs is None and n == 1:
+        if self.graph_mode == "full" and self._graphs is None and n == 1 and self.steps_done == 0:
             # the very first optimizer step runs from eager launches and the
             # capture of the step graphs (tens of them, each warm-replayed)
             # waits for the next run(): a job's first step is not queued

@@ -78,6 +78,50 @@ def gpu_count() -> int:
     return int(torch._C._cuda_getDeviceCount()) if torch.cuda.is_available() else 0
 
 
+KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def _visible_list(value: str | None) -> list[str] | None:
+    if value is None:
+        return None
+    return [v for v in (s.strip() for s in value.split(",")) if v]
+
+
+def visible_gpu_count_no_hip(env: dict | None = None, topology: str | None = None) -> int:
+    """GPUs a child process will see, counted WITHOUT the HIP runtime or
+    amdsmi (a launcher that starts rank processes must never initialise the
+    GPU itself -- on this pool a process that did may not start GPU
+    children).  Physical GPUs are the KFD topology nodes whose
+    ``gfx_target_version`` is non-zero (CPU nodes report 0); the
+    ``ROCR_VISIBLE_DEVICES`` list restricts them, and ``HIP_VISIBLE_DEVICES``
+    (or ``CUDA_VISIBLE_DEVICES``) indexes into what ROCr left."""
+    env = os.environ if env is None else env
+    topology = KFD_TOPOLOGY if topology is None else topology
+    n = 0
+    try:
+        for node in os.listdir(topology):
+            try:
+                with open(os.path.join(topology, node, "properties")) as f:
+                    for line in f:
+                        k, _, v = line.partition(" ")
+                        if k == "gfx_target_version":
+                            n += int(v.strip() or "0") != 0
+                            break
+            except (OSError, ValueError):
+                continue
+    except OSError:
+        n = 0
+    rocr = _visible_list(env.get("ROCR_VISIBLE_DEVICES"))
+    if rocr is not None:
+        n = min(n, len(rocr)) if n else len(rocr)
+    hip = _visible_list(env.get("HIP_VISIBLE_DEVICES"))
+    if hip is None:
+        hip = _visible_list(env.get("CUDA_VISIBLE_DEVICES"))
+    if hip is not None:
+        n = min(n, len(hip)) if n else len(hip)
+    return n
+
+
 def gpu_name(index: int = 0) -> str:
     """Marketing name of a visible GPU, without ``torch.cuda.device_count()``
     (see :func:`gpu_count`)."""

@@ -107,3 +107,59 @@ def test_gpu_count_without_a_gpu_and_no_amdsmi(monkeypatch):
     assert pdist.gpu_count() == 0
     env, device = pdist.init_distributed(None, use_gpu=False)
     assert device.type == "cpu" and env.world_size >= 1
+
+
+def _fake_kfd(tmp_path, versions):
+    root = tmp_path / "nodes"
+    for i, v in enumerate(versions):
+        d = root / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count {0 if v else 64}\nsimd_count 1024\ngfx_target_version {v}\n")
+    return str(root)
+
+
+def test_visible_gpu_count_from_kfd_sysfs(tmp_path):
+    """The launcher's GPU count: KFD topology nodes with a non-zero
+    gfx_target_version (node 0 is the CPU), restricted by the visibility
+    env lists -- no HIP, no amdsmi."""
+    from pytorch_operator_1_amd.utils.dist import visible_gpu_count_no_hip
+
+    topo = _fake_kfd(tmp_path, [0] + [90500] * 8)
+    assert visible_gpu_count_no_hip({}, topo) == 8
+    assert visible_gpu_count_no_hip({"HIP_VISIBLE_DEVICES": "0,1"}, topo) == 2
+    assert visible_gpu_count_no_hip({"ROCR_VISIBLE_DEVICES": "3,4,5", "HIP_VISIBLE_DEVICES": "0"}, topo) == 1
+    assert visible_gpu_count_no_hip({"CUDA_VISIBLE_DEVICES": "0,1,2,3"}, topo) == 4
+    assert visible_gpu_count_no_hip({"HIP_VISIBLE_DEVICES": ""}, topo) == 0
+    # more indices than GPUs: only the GPUs that exist
+    assert visible_gpu_count_no_hip({"HIP_VISIBLE_DEVICES": ",".join(map(str, range(12)))}, topo) == 8
+    # no KFD (this container): nothing but the env lists
+    assert visible_gpu_count_no_hip({}, str(tmp_path / "missing")) == 0
+    assert visible_gpu_count_no_hip({"HIP_VISIBLE_DEVICES": "0,1"}, str(tmp_path / "missing")) == 2
+
+
+def test_bench_launcher_never_touches_torch_cuda(monkeypatch, tmp_path):
+    """bench.py --gpus N (no WORLD_SIZE) counts GPUs without torch.cuda and
+    refuses to measure fewer ranks than asked for."""
+    import importlib.util
+    import os
+
+    import torch
+
+    def boom(*a, **k):
+        raise AssertionError("the launcher initialised HIP")
+
+    for name in ("device_count", "is_available", "init", "synchronize"):
+        monkeypatch.setattr(torch.cuda, name, boom)
+    monkeypatch.setattr(torch._C, "_cuda_getDeviceCount", boom, raising=False)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv("PTO_BACKEND", raising=False)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
+    from pytorch_operator_1_amd.utils import dist as pdist
+
+    monkeypatch.setattr(pdist, "KFD_TOPOLOGY", _fake_kfd(tmp_path, [0, 90500]))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    args = bench.parse_args(["--gpus", "4"])
+    assert bench._launch_ranks(args, ["--gpus", "4"]) == 2
