@@ -65,8 +65,8 @@
 // Two independent "channels" (flag sets + epochs) let two buckets be in
 // flight at once on different streams.
 //
-// Small buckets (<= AR_ONESHOT_MAX floats, e.g. MNIST's 100 KB conv bucket,
-// which sits on the step's critical path) use a one-shot variant instead:
+// Small buckets (<= AR_ONESHOT_MAX floats; MNIST's 100 KB conv bucket runs
+// the rank-split form of it, ar_role_oneshot_sgd) use a one-shot variant:
 // barrier 1, every rank reads the WHOLE range from all ranks and reduces it
 // in rank order (bit-identical everywhere; one element per thread, kept in
 // registers), barrier 2 (nobody reads my input any more), then the local
@@ -112,21 +112,12 @@ __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_1shot(const ArPee
   ar_oneshot<SGD, FENCED, AR_THREADS>(peers, off, n4, rank, world, chan, epochs, err, timeout, f, blockIdx.x);
 }
 
-template <bool FENCED>
-__global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_1shot_1bar(const ArPeers* __restrict__ peers,
-                                                                          long long off, long long n4, int rank,
-                                                                          int world, int chan,
-                                                                          uint32_t* __restrict__ epochs, int* err,
-                                                                          long long timeout, ArSgd f) {
-  ar_oneshot<true, FENCED, AR_THREADS, false>(peers, off, n4, rank, world, chan, epochs, err, timeout, f, blockIdx.x);
-}
-
-// The fc all-reduce of the overlapped MNIST step as a launch of its own:
-// EXACTLY the decomposition of the all-reduce role inside the F12 launch
-// (1024-thread workgroups, ar_role_sgd, role_blocks(n, world, 1024)), so a
-// rank that runs a step's fc exchange stand-alone interoperates with a peer
-// that ran the same exchange inside its F12 (block b covers the same
-// elements and advances the same epoch either way).
+// The fc / conv all-reduce roles of the overlapped MNIST step as launches of
+// their own: EXACTLY the decompositions of the roles inside the F12 launch
+// (1024-thread workgroups, ar_role_sgd / ar_role_oneshot_sgd), so a rank
+// that runs a step's exchange stand-alone interoperates with a peer that ran
+// the same exchange inside its F12 (block b covers the same elements and
+// advances the same epoch either way).
 constexpr int AR_ROLE_THREADS = 1024;
 template <bool FENCED>
 __global__ __launch_bounds__(AR_ROLE_THREADS) void k_xgmi_allreduce_role(const ArPeers* __restrict__ peers, long long off,
@@ -135,6 +126,16 @@ __global__ __launch_bounds__(AR_ROLE_THREADS) void k_xgmi_allreduce_role(const A
                                                                           long long timeout, ArSgd f) {
   __shared__ float4 lds[AR_ROLE_THREADS];
   ar_role_sgd<FENCED, AR_ROLE_THREADS>(peers, off, n4, rank, world, chan, epochs, err, timeout, f, blockIdx.x, lds);
+}
+
+template <bool FENCED>
+__global__ __launch_bounds__(AR_ROLE_THREADS) void k_xgmi_oneshot_role(const ArPeers* __restrict__ peers, long long off,
+                                                                       long long n4, int rank, int world, int chan,
+                                                                       uint32_t* __restrict__ epochs, int* err,
+                                                                       long long timeout, ArSgd f, int* ready) {
+  __shared__ float4 lds[AR_ROLE_THREADS];
+  ar_role_oneshot_sgd<FENCED, AR_ROLE_THREADS>(peers, off, n4, rank, world, chan, epochs, err, timeout, f, blockIdx.x,
+                                               lds, ready);
 }
 
 template <bool FENCED>
@@ -319,58 +320,11 @@ PTO_API int pto_ar_allreduce_bf16(const void* peers, long long off, long long n,
   return (int)hipGetLastError();
 }
 
-// One-shot all-reduce + SGD with ONE barrier (ar_oneshot BAR2 = false): the
-// conv part of the overlapped MNIST step.  Same arguments as
-// pto_ar_allreduce_sgd; n <= AR_ONESHOT_MAX and zero_from >= off + n (the
-// call writes nothing into the input range).
-PTO_API int pto_ar_allreduce_sgd_1bar(const void* peers, long long off, long long n, int rank, int world, int chan,
-                                      void* epochs, void* err, float* p, float* m, const float* lr, float mom,
-                                      float wd, float gscale, int nesterov, long long zero_from, long long* bidx,
-                                      long long nbatches, float* rep, int nrep, int rep_stride, long long rep_from,
-                                      hipStream_t s) {
-  if (n % 4 || off % 4 || n > AR_ONESHOT_MAX || world < 1 || world > AR_MAX_RANKS || chan < 0 ||
-      chan >= AR_CHANNELS || rank < 0 || rank >= world || !p || !m || !lr ||
-      ((((uintptr_t)p) | ((uintptr_t)m)) & 15) || (bidx && nbatches < 1) || zero_from < off + n)
-    return -1;
-  if (rep && (nrep < 1 || nrep > AR_MAX_REP || rep_stride % 4 || rep_from % 4 || (((uintptr_t)rep) & 15)))
-    return -1;
-  if (n == 0) return 0;
-  ArSgd f{};
-  f.p = p;
-  f.m = m;
-  f.a.lr = lr;
-  f.a.mom = mom;
-  f.a.wd = wd;
-  f.a.gscale = gscale;
-  f.a.nesterov = nesterov;
-  f.zero_from = zero_from;
-  f.bidx = bidx;
-  f.nbatches = nbatches;
-  f.rep = rep;
-  f.nrep = rep ? nrep : 1;
-  f.rep_stride = rep_stride;
-  f.rep_from = rep_from;
-  const dim3 g((unsigned)((n / 4 + AR_THREADS - 1) / AR_THREADS));
-  const ArPeers* P = reinterpret_cast<const ArPeers*>(peers);
-  if (g_protocol)
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce_1shot_1bar<true>), g, dim3(AR_THREADS), 0, s, P, off, n / 4,
-                       rank, world, chan, reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err),
-                       g_timeout_ticks, f);
-  else
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_allreduce_1shot_1bar<false>), g, dim3(AR_THREADS), 0, s, P, off, n / 4,
-                       rank, world, chan, reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err),
-                       g_timeout_ticks, f);
-  return (int)hipGetLastError();
-}
-
 // Stand-alone launch of the all-reduce-with-SGD ROLE (same arguments as
-// pto_conv12_fwd_ar's role part, same workgroup decomposition), plus an
-// optional local range [ztail, ztail + ztail_n) zeroed after the stage-1 barrier.
+// the fc role of pto_conv12_fwd_ar, same workgroup decomposition).
 PTO_API int pto_ar_role_sgd(const void* peers, long long off, long long n, int rank, int world, int chan, void* epochs,
                             void* err, int protocol, float* p, float* m, const float* lr, float mom, float wd,
-                            float gscale, int nesterov, long long zero_from, float* ztail, long long ztail_n,
-                            hipStream_t s) {
-  if (ztail_n % 4 || ztail_n < 0 || (ztail && (((uintptr_t)ztail) & 15))) return -1;
+                            float gscale, int nesterov, long long zero_from, hipStream_t s) {
   if (n <= AR_ONESHOT_MAX || n % 4 || off % 4 || n > AR_MAX_FLOATS || world < 1 || world > AR_MAX_RANKS ||
       chan < 0 || chan >= AR_CHANNELS || rank < 0 || rank >= world || !p || !m || !lr || !peers || protocol < 0 ||
       protocol > 1 || ((((uintptr_t)p) | ((uintptr_t)m)) & 15))
@@ -386,8 +340,6 @@ PTO_API int pto_ar_role_sgd(const void* peers, long long off, long long n, int r
   f.zero_from = zero_from;
   f.nbatches = 1;
   f.nrep = 1;
-  f.ztail = ztail_n ? ztail : nullptr;
-  f.ztail4 = ztail_n / 4;
   const ArPeers* P = reinterpret_cast<const ArPeers*>(peers);
   const int nb = role_blocks(n, world, AR_ROLE_THREADS);
   if (nb > AR_MAX_BLOCKS) return -1;
@@ -402,3 +354,48 @@ PTO_API int pto_ar_role_sgd(const void* peers, long long off, long long n, int r
                        g_timeout_ticks, f);
   return (int)hipGetLastError();
 }
+
+// Stand-alone launch of the conv role (ar_role_oneshot_sgd: one-shot
+// all-reduce + SGD of [off, off + n), replicas folded first, the gradient
+// zeroed after the second barrier, one add to *ready per workgroup) with
+// the decomposition it has inside the MNIST forward launch, so a rank that
+// closes a step's exchange here pairs block by block with a peer that runs
+// it inside its next forward.
+PTO_API int pto_ar_oneshot_role_sgd(const void* peers, long long off, long long n, int rank, int world, int chan,
+                                    void* epochs, void* err, int protocol, float* p, float* m, const float* lr,
+                                    float mom, float wd, float gscale, int nesterov, float* rep, int nrep,
+                                    int rep_stride, long long rep_from, int* ready, hipStream_t s) {
+  if (n > AR_ONESHOT_MAX || n < 4 || n % 4 || off % 4 || world < 1 || world > AR_MAX_RANKS || chan < 0 ||
+      chan >= AR_CHANNELS || rank < 0 || rank >= world || !p || !m || !lr || !peers || !ready || protocol < 0 ||
+      protocol > 1 || ((((uintptr_t)p) | ((uintptr_t)m)) & 15))
+    return -1;
+  if (rep && (nrep < 1 || nrep > AR_MAX_REP || rep_stride % 4 || rep_from % 4 || (((uintptr_t)rep) & 15)))
+    return -1;
+  ArSgd f{};
+  f.p = p;
+  f.m = m;
+  f.a.lr = lr;
+  f.a.mom = mom;
+  f.a.wd = wd;
+  f.a.gscale = gscale;
+  f.a.nesterov = nesterov;
+  f.zero_from = off;
+  f.nbatches = 1;
+  f.rep = rep;
+  f.nrep = rep ? nrep : 1;
+  f.rep_stride = rep_stride;
+  f.rep_from = rep_from;
+  const ArPeers* P = reinterpret_cast<const ArPeers*>(peers);
+  const int nb = oneshot_role_blocks(n, world, AR_ROLE_THREADS);
+  if (nb > AR_MAX_BLOCKS) return -1;
+  if (protocol)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_oneshot_role<true>), dim3(nb), dim3(AR_ROLE_THREADS), 0, s, P, off,
+                       n / 4, rank, world, chan, reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err),
+                       g_timeout_ticks, f, ready);
+  else
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_xgmi_oneshot_role<false>), dim3(nb), dim3(AR_ROLE_THREADS), 0, s, P, off,
+                       n / 4, rank, world, chan, reinterpret_cast<uint32_t*>(epochs), reinterpret_cast<int*>(err),
+                       g_timeout_ticks, f, ready);
+  return (int)hipGetLastError();
+}
+PTO_API int pto_ar_oneshot_role_blocks(long long n, int world) { return oneshot_role_blocks(n, world, AR_ROLE_THREADS); }

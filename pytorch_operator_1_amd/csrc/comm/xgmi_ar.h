@@ -19,7 +19,9 @@ constexpr int AR_MAX_RANKS = 8;
 // workgroups per launch: ceil(chunk / AR_THREADS) up to this cap, so every
 // thread handles ONE float4 per stage down to world 1-2 on MNIST's 1.7 MB
 constexpr int AR_MAX_BLOCKS = 256;
-constexpr int AR_CHANNELS = 2;
+// channels 0 and 1: the stand-alone all-reduces and the fc role of the
+// overlapped MNIST step; channel 2: that step's conv role (ar_role_oneshot_sgd)
+constexpr int AR_CHANNELS = 3;
 constexpr int AR_THREADS = 512;  // workgroup size of the stand-alone kernels
 constexpr int AR_MAX_REP = 256;  // gradient replicas folded before barrier 1 (launcher check)
 constexpr int AR_REP_CHUNK = 16;  // replica loads in flight at once
@@ -157,13 +159,6 @@ struct ArSgd {
   float* rep;
   int nrep, rep_stride;
   long long rep_from;
-  // optional local float4 range zeroed by ar_role_sgd once its stage-1
-  // barrier has passed (every peer has then finished the launches it queued
-  // before this one): the fc exchange of the overlapped MNIST step clears the
-  // conv gradients the one-shot conv exchange left behind, so the next
-  // backward accumulates from zero and a run() ends with zero gradients
-  float* ztail;
-  long long ztail4;
 };
 
 // Fold the local replicas into float4 element i4 (float offset 4*i4 from the
@@ -171,19 +166,21 @@ struct ArSgd {
 // Every replica load is issued before the first add; the folded value is
 // stored through `g` (write-through under the coherent protocol: peers read
 // it).
-template <bool COHERENT>
+// CHUNK: replica loads in flight at once (a role inside a 64-VGPR kernel
+// uses 8: the MNIST step's 7 extra replicas in one round, 32 VGPRs).
+template <bool COHERENT, int CHUNK = AR_REP_CHUNK>
 __device__ __forceinline__ void fold_rep(const ArSgd& f, const Buf& g, long long off, long long i4) {
   const long long fi = off + 4 * i4;  // float index in the whole buffer (rep_from's frame)
   if (!f.rep || f.nrep <= 1 || fi < f.rep_from || fi >= f.rep_from + f.rep_stride) return;
   const long long k = fi - f.rep_from;
   float4 a = gld4(g.p + 4 * i4);
-  for (int r0 = 0; r0 < f.nrep - 1; r0 += AR_REP_CHUNK) {  // replica order
-    float4 v[AR_REP_CHUNK];
+  for (int r0 = 0; r0 < f.nrep - 1; r0 += CHUNK) {  // replica order
+    float4 v[CHUNK];
 #pragma unroll
-    for (int r = 0; r < AR_REP_CHUNK; ++r)
+    for (int r = 0; r < CHUNK; ++r)
       v[r] = gld4(f.rep + (long long)min(r0 + r, f.nrep - 2) * f.rep_stride + k);
 #pragma unroll
-    for (int r = 0; r < AR_REP_CHUNK; ++r) {
+    for (int r = 0; r < CHUNK; ++r) {
       if (r0 + r >= f.nrep - 1) break;
       a.x += v[r].x; a.y += v[r].y; a.z += v[r].z; a.w += v[r].w;
       gst4(f.rep + (long long)(r0 + r) * f.rep_stride + k, float4{0.f, 0.f, 0.f, 0.f});
@@ -330,13 +327,8 @@ __device__ __forceinline__ void ar_twostage(const ArPeers* __restrict__ peers, l
   if (SGD && f.bidx && blk == 0 && threadIdx.x == 0) *f.bidx = (*f.bidx + 1) % f.nbatches;
 }
 
-// One-shot variant: n4 <= nblk * NT (one float4 per thread).  BAR2 = false
-// drops the second barrier ("nobody reads my input any more"): only for a
-// caller whose NEXT cross-rank barrier on another channel orders every
-// peer's reads of this call before any write of this rank's input range,
-// and which writes nothing into that range here (zero_from past the range;
-// the MNIST overlap schedule, fused_step.py).
-template <bool SGD, bool FENCED, int NT, bool BAR2 = true>
+// One-shot variant: n4 <= nblk * NT (one float4 per thread).
+template <bool SGD, bool FENCED, int NT>
 __device__ __forceinline__ void ar_oneshot(const ArPeers* __restrict__ peers, long long off, long long n4, int rank,
                                            int world, int chan, uint32_t* __restrict__ epochs, int* err,
                                            long long timeout, const ArSgd& f, int blk) {
@@ -378,11 +370,7 @@ __device__ __forceinline__ void ar_oneshot(const ArPeers* __restrict__ peers, lo
       if (q < world) a = add4(a, v[q]);
   }
   // every peer is done reading my input (on failure: nothing is written)
-  if constexpr (BAR2) {
-    if (!block_barrier<FENCED>(P, chan, 1, blk, rank, world, e, timeout, err)) return;
-  } else {
-    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
-  }
+  if (!block_barrier<FENCED>(P, chan, 1, blk, rank, world, e, timeout, err)) return;
   if (act) {
     if constexpr (SGD) {
       const long long j = off + 4 * i;
@@ -430,21 +418,13 @@ __device__ __forceinline__ void ar_role_sgd(const ArPeers* __restrict__ P, long 
   const bool in_group = q < world;
   const long long j = (long long)blk * S + sidx;  // element of every chunk this thread covers
   const long long bytes = n4 * 16;
-  // Barrier 0 ("every peer's input is complete") is NOT needed under the
-  // coherent protocol: this role always runs after the same step's conv
-  // exchange (ar_oneshot on the other channel, fused_step.py), and passing
-  // ITS barrier already means every peer finished the backward that wrote
-  // this range (end-of-kernel write-back before the peer's conv flag) and
-  // every peer finished its previous call of this role, including the
-  // stage-2 reads of tmp that stage 1 below overwrites (that call precedes
-  // the peer's conv exchange in stream order).  The sc0 sc1 loads below
-  // cannot hit stale cached copies.  The fenced protocol keeps barrier 0
-  // for its acquire (plain loads).
-  if constexpr (FENCED) {
-    if (!block_barrier<FENCED>(P, chan, 0, blk, rank, world, e, timeout, err)) return;
-  } else {
-    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
-  }
+  // barrier 0: every peer's input is complete (its backward has ended) and
+  // every peer has finished its previous call of this role, including the
+  // stage-2 reads of tmp that stage 1 below overwrites.  (Round 4 skipped it
+  // under the coherent protocol because a stand-alone conv exchange always
+  // preceded this role; the conv exchange now runs NEXT TO it, as
+  // ar_role_oneshot_sgd in the same launch, so nothing else orders it.)
+  if (!block_barrier<FENCED>(P, chan, 0, blk, rank, world, e, timeout, err)) return;
   // stage 1: my chunk's element j from rank q -> LDS, then rank-order sums
   const long long i1 = (long long)rank * cs + j;
   const bool v1 = in_group && j < cs && i1 < n4;
@@ -466,13 +446,6 @@ __device__ __forceinline__ void ar_role_sgd(const ArPeers* __restrict__ P, long 
     mv = gld4(f.m + off + 4 * k);
   }
   if (!block_barrier<FENCED>(P, chan, 1, blk, rank, world, e, timeout, err)) return;
-  // every peer has passed its stage 1, so its conv exchange of the same step
-  // (which read the range zeroed here) is complete
-  if (f.ztail) {
-    const long long nt = (long long)role_blocks(4 * n4, world, NT) * NT;
-    for (long long z = (long long)blk * NT + threadIdx.x; z < f.ztail4; z += nt)
-      gst4(f.ztail + 4 * z, float4{0.f, 0.f, 0.f, 0.f});
-  }
   // stage 2: element j of chunk q from rank q's partial sums
   if (v2) {
     const float4 v = ld4<CO>(mkbuf(P->tmp[q] + off, bytes), k);
@@ -480,6 +453,95 @@ __device__ __forceinline__ void ar_role_sgd(const ArPeers* __restrict__ P, long 
     sgd4(f, i, v, pv, mv, lr);
     if (i >= f.zero_from) gst4(P->in[rank] + i, float4{0.f, 0.f, 0.f, 0.f});
   }
+}
+
+// ------------------------------------------------ one-shot rank-split role --
+// The conv exchange of the overlapped MNIST step (<= AR_ONESHOT_MAX floats:
+// conv2 + conv1, 100 KB) as a ROLE of the NEXT step's forward launch, whose
+// conv workgroups wait on `ready` before they read the parameters it
+// updates -- so the exchange no longer costs a launch of its own between the
+// backward and that forward (fused_step.py, "ddp-xgmi" overlap).
+// Register-light like ar_role_sgd (the host kernel is capped at 64 VGPRs):
+// the block's NT threads are W groups of S = NT / W; block b covers elements
+// [b*S, b*S + S) of the range on every rank (same pairing on every rank), and
+// thread (q, s) loads rank q's element s into LDS.  Per workgroup:
+//   q = 0      prefetch its own parameter/momentum float4; fold this rank's
+//              gradient replicas into its gradient element (write-through)
+//   barrier 0  every peer's (folded) gradient is complete
+//   stage 1    every rank's element into LDS; q = 0 sums them in rank order
+//              (bit-identical on every rank), applies SGD, stores the
+//              parameter WRITE-THROUGH (system scope: the waiting conv
+//              workgroups on other XCDs read it with system-scope loads; no
+//              L2 of this XCD keeps a stale copy) and the momentum plainly
+//              (only the next launch reads it)
+//   publish    every wave drains its stores (vmcnt 0), workgroup barrier,
+//              ONE agent-scope add to *ready.  Done on failure too (nothing
+//              was written then and *err is set), so the waiting conv
+//              workgroups are always released and the grid drains.
+//   barrier 1  every peer has read this rank's gradient
+//   q = 0      zero this rank's gradient element: the next backward
+//              accumulates into it (a run() ends with zero conv gradients)
+// Hazards: a rank writes its gradient range only in the fold (before its
+// barrier-0 arrival) and in the zeroing (after barrier 1, i.e. after every
+// peer's stage-1 read of this call).  The conv workgroups read the updated
+// parameters only after *ready counts every role workgroup; the next writer
+// of those parameters is the next call of this role, a later launch.
+// *ready is reset by a later launch of the same step (the MNIST F4dx launch).
+template <bool FENCED, int NT>
+__device__ __forceinline__ void ar_role_oneshot_sgd(const ArPeers* __restrict__ P, long long off, long long n4,
+                                                    int rank, int world, int chan, uint32_t* __restrict__ epochs,
+                                                    int* err, long long timeout, const ArSgd& f, int blk,
+                                                    float4* lds, int* ready) {
+  constexpr bool CO = !FENCED;
+  __shared__ uint32_t s_epoch;
+  if (threadIdx.x == 0) s_epoch = epochs[chan * AR_MAX_BLOCKS + blk] + 1;
+  __syncthreads();
+  const uint32_t e = s_epoch;
+  if (threadIdx.x == 0) epochs[chan * AR_MAX_BLOCKS + blk] = e;
+  const int S = NT / world;
+  const int q = threadIdx.x / S, sidx = threadIdx.x - q * S;
+  const long long j = (long long)blk * S + sidx;
+  const bool valid = q < world && j < n4;
+  const bool own = q == 0 && valid;  // this thread updates element j
+  const long long bytes = n4 * 16;
+  float* const my_in = P->in[rank];
+  float4 pv = {0.f, 0.f, 0.f, 0.f}, mv = {0.f, 0.f, 0.f, 0.f};
+  float lr = 0.f;
+  if (own) {
+    // fold first (its 7 replica loads in one round), then the SGD operands,
+    // whose loads overlap the barrier
+    if (f.rep && f.nrep > 1 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+      fold_rep<CO, 8>(f, mkbuf(my_in + off, bytes), off, j);
+    pv = gld4(f.p + off + 4 * j);
+    mv = gld4(f.m + off + 4 * j);
+    lr = *f.a.lr;
+  }
+  const bool ok = block_barrier<FENCED>(P, chan, 0, blk, rank, world, e, timeout, err);
+  if (ok) {
+    if (valid) lds[q * S + sidx] = ld4<CO>(mkbuf(P->in[q] + off, bytes), j);
+    __syncthreads();
+    if (own) {
+      float4 a = lds[sidx];
+      for (int r = 1; r < world; ++r) a = add4(a, lds[r * S + sidx]);
+      const long long i = off + 4 * j;
+      sgd_elem(pv.x, a.x, mv.x, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+      sgd_elem(pv.y, a.y, mv.y, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+      sgd_elem(pv.z, a.z, mv.z, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+      sgd_elem(pv.w, a.w, mv.w, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
+      st4<true>(mkbuf(f.p + off, bytes), j, pv);
+      gst4(f.m + i, mv);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave: its parameter stores acknowledged
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!ok) return;
+  if (!block_barrier<FENCED>(P, chan, 1, blk, rank, world, e, timeout, err)) return;
+  if (own) gst4(my_in + off + 4 * j, float4{0.f, 0.f, 0.f, 0.f});
+}
+__host__ __device__ inline int oneshot_role_blocks(long long n, int world, int nt) {
+  const long long S = nt / world;
+  return (int)(((n / 4) + S - 1) / S);
 }
 
 // ---------------------------------------------------------------- bf16 --

@@ -98,6 +98,7 @@ struct Conv1Commit {
   SgdArgs a;
   float* rep;           // extra gradient replicas, summed into the update and re-zeroed
   int nrep, rep_stride;
+  int* zero_word;       // F4dx: reset to 0 (the overlapped step's conv-role counter), or nullptr
 };
 
 // Conv1Commit's update of 4 elements at i: the gradient is the sum of the
@@ -297,12 +298,20 @@ __global__ __launch_bounds__(256) void k_conv2_fwd(const float* __restrict__ a1p
 //  * lazy conv1 update (one-process schedule, LazyConv1), the image copy
 //    for the backward (xout) and the conv2.weight snapshot (w2out).
 //  * ARM != 0 (overlapped multi-GPU step, fused_step.py "ddp-xgmi"): the
-//    first ar.nblk blocks are the PREVIOUS step's fc-gradient all-reduce +
-//    SGD epilogue (xgmi_ar.h ar_role_sgd, protocol ARM-1), which nothing
-//    here reads.  The
-//    kernel is capped at 64 VGPRs (8 waves per SIMD) so an all-reduce block
-//    fits on a CU next to a conv block (61 KB of LDS each) and the exchange
-//    runs concurrently with the convolutions instead of after them.
+//    PREVIOUS step's gradient exchange runs as two roles ahead of the conv
+//    blocks in the grid (protocol ARM-1):
+//      cv.nblk blocks  the conv exchange (xgmi_ar.h ar_role_oneshot_sgd:
+//                      one-shot all-reduce + SGD of conv2/conv1, 100 KB);
+//                      the conv blocks wait on cv.ready (one lane, bounded)
+//                      before reading conv1/conv2, then read them with
+//                      system-scope loads.  No launch of its own between
+//                      the backward and this forward any more.
+//      ar.nblk blocks  the fc exchange (ar_role_sgd), which nothing here
+//                      reads: it runs concurrently with the convolutions.
+//    Role blocks come first in the grid, so they are resident before any
+//    conv block can wait on them.  B == 0: the roles alone (the closing
+//    launch of a captured run).  The kernel is capped at 64 VGPRs (8 waves
+//    per SIMD) so a role block fits on a CU next to a conv block.
 struct ArRole {
   const pto_ar::ArPeers* peers;
   long long off, n4;
@@ -311,27 +320,73 @@ struct ArRole {
   int* err;
   long long timeout;
   pto_ar::ArSgd f;
+  int* ready;  // conv role: one add per workgroup once its parameters are stored
 };
+
+// Read access to a parameter tensor.  SYS: system-scope buffer loads (sc0
+// sc1: miss this CU's L1 and serve the line written through by a role
+// workgroup of the SAME launch, wherever it ran); otherwise plain loads.
+template <bool SYS>
+struct ParamView {
+  const float* p;
+  __amdgpu_buffer_rsrc_t r;
+  PTO_DEV ParamView(const float* base, int n) : p(base) {
+    if constexpr (SYS) r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, n * 4, 0x00020000);
+  }
+  PTO_DEV float operator[](int i) const {
+    if constexpr (SYS)
+      return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, i * 4, 0, pto_ar::AUX_SYS));
+    else
+      return p[i];
+  }
+  PTO_DEV float4 v4(int i4) const {
+    if constexpr (SYS)
+      return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, i4 * 16, 0, pto_ar::AUX_SYS));
+    else
+      return reinterpret_cast<const float4*>(p)[i4];
+  }
+};
+
+// A conv workgroup of the overlapped step waits here (one lane) until every
+// conv-role workgroup of its launch has published (ar_role_oneshot_sgd), or
+// the exchange failed, or the bounded spin ran out (err bit 16).  Every role
+// workgroup publishes even on failure, so the spin ends in every case.
+PTO_DEV void wait_conv_role(const ArRole& cv) {
+  const long long t0 = wall_clock64();
+  while (__hip_atomic_load(cv.ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < cv.nblk) {
+    if (__hip_atomic_load(cv.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+    if (wall_clock64() - t0 > cv.timeout) {
+      atomicOr(cv.err, 16);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
 constexpr int W1PLD = 52;  // a channel pair's 25 interleaved taps, padded to whole float4
 template <int NTH, int ARM = 0>
 __global__ __launch_bounds__(NTH, ARM ? 2 * NTH / 256 : 1) void k_conv12_fwd2_t(
     const float* __restrict__ x, const float* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ a1p, uint8_t* __restrict__ code1,
     float* __restrict__ a2p, uint8_t* __restrict__ code2, int B, const long long* __restrict__ bidx, LazyConv1 lz,
-    ArRole ar) {
-  // all-reduce blocks FIRST in the grid: they are dispatched before the conv
-  // blocks, so their latency chain (two barriers, three memory rounds)
-  // starts at once and runs under the convolutions
+    ArRole ar, ArRole cv) {
+  // role blocks FIRST in the grid: they are dispatched before the conv
+  // blocks, so their latency chains start at once (and the conv blocks that
+  // wait on the conv role can never hold the CU slots it needs)
   int bx = (int)blockIdx.x;
   if constexpr (ARM != 0) {
-    if (bx < ar.nblk) {
+    if (bx < cv.nblk + ar.nblk) {
       __shared__ float4 ar_lds[NTH];
-      pto_ar::ar_role_sgd<ARM == 2, NTH>(ar.peers, ar.off, ar.n4, ar.rank, ar.world, ar.chan, ar.epochs, ar.err,
-                                         ar.timeout, ar.f, bx, ar_lds);
+      if (bx < cv.nblk)
+        pto_ar::ar_role_oneshot_sgd<ARM == 2, NTH>(cv.peers, cv.off, cv.n4, cv.rank, cv.world, cv.chan, cv.epochs,
+                                                   cv.err, cv.timeout, cv.f, bx, ar_lds, cv.ready);
+      else
+        pto_ar::ar_role_sgd<ARM == 2, NTH>(ar.peers, ar.off, ar.n4, ar.rank, ar.world, ar.chan, ar.epochs, ar.err,
+                                           ar.timeout, ar.f, bx - cv.nblk, ar_lds);
       return;
     }
-    bx -= ar.nblk;
+    bx -= cv.nblk + ar.nblk;
   }
+  constexpr bool SYS = ARM != 0;  // conv parameters written by this launch's conv role
   __shared__ float ws[16 * WS_LD];
   __shared__ __attribute__((aligned(16))) float in_s[A1P];
   __shared__ __attribute__((aligned(16))) float xs[784];
@@ -347,21 +402,26 @@ __global__ __launch_bounds__(NTH, ARM ? 2 * NTH / 256 : 1) void k_conv12_fwd2_t(
   const int tid = threadIdx.x;
   {
     x = batch_ptr(x, bidx, B * 784);
+    const float4 xv = tid < 196 ? reinterpret_cast<const float4*>(x + b * 784)[tid] : float4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (ARM != 0) {
+      if (tid == 0) wait_conv_role(cv);
+      __syncthreads();
+    }
     const int nrows = min(16, C2 - nt * 16);
-    const float4* wsrc = reinterpret_cast<const float4*>(w2 + nt * 16 * 500);
+    const ParamView<SYS> wsrc(w2 + nt * 16 * 500, nrows * 500);
     float4 wv[2048 / NTH];
 #pragma unroll
     for (int q = 0; q < 2048 / NTH; ++q) {
       const int e = tid + NTH * q;
-      wv[q] = (e < nrows * 125) ? wsrc[e] : float4{0.f, 0.f, 0.f, 0.f};
+      wv[q] = (e < nrows * 125) ? wsrc.v4(e) : float4{0.f, 0.f, 0.f, 0.f};
     }
-    const float4 xv = tid < 196 ? reinterpret_cast<const float4*>(x + b * 784)[tid] : float4{0.f, 0.f, 0.f, 0.f};
     constexpr int QW1 = (C1 * 26 + NTH - 1) / NTH;
     float wq[QW1], gq[QW1], mq[QW1];
+    const ParamView<SYS> w1v(w1, C1 * 25), b1v(b1, C1);
 #pragma unroll
     for (int q = 0; q < QW1; ++q) {
       const int e = tid + NTH * q;
-      wq[q] = e < C1 * 25 ? w1[e] : (e < C1 * 26 ? b1[e - C1 * 25] : 0.f);
+      wq[q] = e < C1 * 25 ? w1v[e] : (e < C1 * 26 ? b1v[e - C1 * 25] : 0.f);
     }
     int pend = 0;
     float lr = 0.f;
@@ -548,7 +608,7 @@ __global__ __launch_bounds__(NTH, ARM ? 2 * NTH / 256 : 1) void k_conv12_fwd2_t(
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) acc[rr] += red[pp * 1024 + t * 256 + rr * 64 + lane];
   if (n >= C2 || b >= B) return;
-  const float bn = b2[n];
+  const float bn = ParamView<SYS>(b2, C2)[n];
   float v[4] = {acc[0] + bn, acc[1] + bn, acc[2] + bn, acc[3] + bn};
   float o;
   uint8_t cd;
@@ -808,6 +868,7 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
   const int t = threadIdx.x;
   PTO_STAMP_SCOPE();
   if (blockIdx.x == (unsigned)(mtiles * ntiles)) {
+    if (cm.zero_word && t == 0) *cm.zero_word = 0;  // every waiter of the previous launch has finished
     if (cm.pending) {
       if (*cm.pending) {
         const float lr = *cm.a.lr;
@@ -1714,7 +1775,8 @@ struct BwdAllArgs {
   // grads_only (multi-GPU step): every gradient is written to the flat grad
   // buffer (g2w/gw1/gb1 accumulated atomically, the rest stored) and no
   // parameter is touched -- the all-reduce's SGD epilogue updates them;
-  // the cursor is left alone
+  // the cursor is advanced only if bidx is given (the overlapped xGMI step,
+  // whose exchange runs inside the next forward)
   int grads_only;
   float* g2b; float* g1w; float* g1b; float* gfw; float* gfb;  // grad slots of conv2.bias, fc1.w/b, fc2.w/b
 };
@@ -1737,9 +1799,9 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   int bid = blockIdx.x;
   PTO_STAMP_SCOPE();
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (bid == 0 && threadIdx.x == 0 && !A.grads_only) {  // no block of this launch reads the cursor
-    *A.bidx = (*A.bidx + 1) % A.nbatches;
-    *A.pending = 1;
+  if (bid == 0 && threadIdx.x == 0) {  // no block of this launch reads the cursor
+    if (A.bidx) *A.bidx = (*A.bidx + 1) % A.nbatches;
+    if (A.pending) *A.pending = 1;
   }
   // block order: the short independent ranges first (they must not queue
   // behind the LDS-heavy conv2 blocks for a CU slot), then conv2 wgrad,
@@ -1992,62 +2054,77 @@ PTO_API int pto_conv12_fwd_lazy_x(const float* x, const float* w1, const float* 
   LazyConv1 lz{g1f, m1f, pending, sgd_args(lr, mom, wd, gscale, nesterov), bias_off, xout, w2out, rep, nrep,
                rep_stride};
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv12_fwd2_t<1024, 0>), dim3(B * 4), dim3(1024), 0, s, x, w1, b1, w2, b2, a1p,
-                     code1, a2p, code2, B, bidx, lz, ArRole{});
+                     code1, a2p, code2, B, bidx, lz, ArRole{}, ArRole{});
   LAUNCH_CHECK();
 }
 
 extern "C" long long pto_ar_timeout_ticks();
 
-// F12 (plain forward: no lazy conv1 update) + the all-reduce of float range
-// [off, off + n) of the registered gradient buffers with the SGD epilogue on
-// p/m (zero_from: local gradient zeroed from there on), as extra workgroups
-// of the same launch (ArRole); [ztail, ztail + ztail_n) (the conv gradients
-// of the previous step, read by the peers' conv exchange) is zeroed by the
-// role's workgroups once their stage-1 barrier has passed.  protocol: 0 coherent, 1 fenced -- the one
-// the XgmiAllReduce instance of `peers` uses.
+// F12 (plain forward: no lazy conv1 update) + the previous step's gradient
+// exchange of the overlapped multi-GPU step as two roles of the same launch
+// (protocol: 0 coherent, 1 fenced -- the one the XgmiAllReduce instance of
+// `peers` uses; shared peers table, epochs and error word):
+//   conv role  one-shot all-reduce + SGD of [cv_off, cv_off + cv_n) on
+//              channel cv_chan, gradient replicas rep (nrep, rep_stride,
+//              from float index rep_from) folded first, gradient zeroed after
+//              its second barrier; the conv blocks wait on *ready
+//   fc role    rank-split all-reduce + SGD of [fc_off, fc_off + fc_n) on
+//              channel fc_chan, local gradient zeroed from fc_zero_from
+// B == 0: the two roles alone (the closing exchange of a captured run).
 PTO_API int pto_conv12_fwd_ar(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
                               float* a1p, uint8_t* code1, float* a2p, uint8_t* code2, int B, const long long* bidx,
-                              float* xout, const void* peers, long long off, long long n, int rank, int world,
-                              int chan, void* epochs, void* err, int protocol, float* p, float* m, const float* lr,
-                              float mom, float wd, float gscale, int nesterov, long long zero_from, float* ztail,
-                              long long ztail_n, hipStream_t s) {
+                              float* xout, const void* peers, int rank, int world, void* epochs, void* err,
+                              int protocol, float* p, float* m, const float* lr, float mom, float wd, float gscale,
+                              int nesterov, long long fc_off, long long fc_n, int fc_chan, long long fc_zero_from,
+                              long long cv_off, long long cv_n, int cv_chan, float* rep, int nrep, int rep_stride,
+                              long long rep_from, int* ready, hipStream_t s) {
   using namespace pto_ar;
-  if (ztail_n % 4 || ztail_n < 0 || (ztail && (((uintptr_t)ztail) & 15))) return -1;
-  if (n <= AR_ONESHOT_MAX || n % 4 || off % 4 || n > (1LL << 29) || world < 1 || world > AR_MAX_RANKS || chan < 0 ||
-      chan >= AR_CHANNELS || rank < 0 || rank >= world || !p || !m || !lr || !peers || protocol < 0 || protocol > 1 ||
-      ((((uintptr_t)p) | ((uintptr_t)m)) & 15))
+  if (fc_n <= AR_ONESHOT_MAX || fc_n % 4 || fc_off % 4 || fc_n > (1LL << 29) || cv_n > AR_ONESHOT_MAX || cv_n < 4 ||
+      cv_n % 4 || cv_off % 4 || world < 1 || world > AR_MAX_RANKS || fc_chan < 0 || fc_chan >= AR_CHANNELS ||
+      cv_chan < 0 || cv_chan >= AR_CHANNELS || fc_chan == cv_chan || rank < 0 || rank >= world || !p || !m || !lr ||
+      !peers || !ready || protocol < 0 || protocol > 1 || B < 0 || ((((uintptr_t)p) | ((uintptr_t)m)) & 15))
+    return -1;
+  if (rep && (nrep < 1 || nrep > AR_MAX_REP || rep_stride % 4 || rep_from % 4 || (((uintptr_t)rep) & 15)))
     return -1;
   LazyConv1 lz{nullptr, nullptr, nullptr, sgd_args(lr, mom, wd, gscale, nesterov), 0, xout, nullptr, nullptr, 1, 0};
-  ArRole ar;
-  ar.peers = reinterpret_cast<const ArPeers*>(peers);
-  ar.off = off;
-  ar.n4 = n / 4;
-  ar.rank = rank;
-  ar.world = world;
-  ar.chan = chan;
-  ar.nblk = role_blocks(n, world, 1024);
-  if (ar.nblk > AR_MAX_BLOCKS) return -1;
-  ar.epochs = reinterpret_cast<uint32_t*>(epochs);
-  ar.err = reinterpret_cast<int*>(err);
-  ar.timeout = pto_ar_timeout_ticks();
-  ar.f = ArSgd{};
-  ar.f.p = p;
-  ar.f.m = m;
-  ar.f.a = sgd_args(lr, mom, wd, gscale, nesterov);
-  ar.f.zero_from = zero_from;
-  ar.f.bidx = nullptr;
-  ar.f.nbatches = 1;
-  ar.f.rep = nullptr;
-  ar.f.nrep = 1;
-  ar.f.ztail = ztail_n ? ztail : nullptr;
-  ar.f.ztail4 = ztail_n / 4;
-  const dim3 g((unsigned)(B * 4 + ar.nblk));
+  ArRole ar{}, cv{};
+  for (ArRole* r : {&ar, &cv}) {
+    r->peers = reinterpret_cast<const ArPeers*>(peers);
+    r->rank = rank;
+    r->world = world;
+    r->epochs = reinterpret_cast<uint32_t*>(epochs);
+    r->err = reinterpret_cast<int*>(err);
+    r->timeout = pto_ar_timeout_ticks();
+    r->f = ArSgd{};
+    r->f.p = p;
+    r->f.m = m;
+    r->f.a = sgd_args(lr, mom, wd, gscale, nesterov);
+    r->f.nbatches = 1;
+    r->f.nrep = 1;
+    r->ready = ready;
+  }
+  ar.off = fc_off;
+  ar.n4 = fc_n / 4;
+  ar.chan = fc_chan;
+  ar.nblk = role_blocks(fc_n, world, 1024);
+  ar.f.zero_from = fc_zero_from;
+  cv.off = cv_off;
+  cv.n4 = cv_n / 4;
+  cv.chan = cv_chan;
+  cv.nblk = oneshot_role_blocks(cv_n, world, 1024);
+  cv.f.zero_from = cv_off;
+  cv.f.rep = rep;
+  cv.f.nrep = rep ? nrep : 1;
+  cv.f.rep_stride = rep_stride;
+  cv.f.rep_from = rep_from;
+  if (ar.nblk > AR_MAX_BLOCKS || cv.nblk > AR_MAX_BLOCKS) return -1;
+  const dim3 g((unsigned)(B * 4 + ar.nblk + cv.nblk));
   if (protocol)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv12_fwd2_t<1024, 2>), g, dim3(1024), 0, s, x, w1, b1, w2, b2, a1p, code1,
-                       a2p, code2, B, bidx, lz, ar);
+                       a2p, code2, B, bidx, lz, ar, cv);
   else
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv12_fwd2_t<1024, 1>), g, dim3(1024), 0, s, x, w1, b1, w2, b2, a1p, code1,
-                       a2p, code2, B, bidx, lz, ar);
+                       a2p, code2, B, bidx, lz, ar, cv);
   LAUNCH_CHECK();
 }
 
@@ -2134,17 +2211,19 @@ PTO_API int pto_conv2_bwd(const float* g2, const uint8_t* code2, const float* a1
 }
 
 // F4dx (k_fc2_ce_dx_mf) + one extra block committing conv1's owed update
-// (pending != nullptr; flat range p1/g1/m1 of n1 floats + replicas).
+// (pending != nullptr; flat range p1/g1/m1 of n1 floats + replicas) and
+// resetting *zero_word (non-null: the overlapped step's conv-role counter,
+// which the previous F12 launch's conv blocks waited on).
 PTO_API int pto_fc2_ce_dx(const float* h1, const float* w2, const float* b2, const int64_t* labels, const float* w1,
                           float* loss_rows, float* dlogits, float* dh1, float* da2p, int B, float inv_b,
                           const long long* bidx, float* p1, float* g1, float* m1, int n1, const int* pending,
                           const float* lr, float mom, float wd, float gscale, int nesterov, float* rep, int nrep,
-                          int rep_stride, hipStream_t s) {
+                          int rep_stride, int* zero_word, hipStream_t s) {
   if (n1 % 4 || rep_stride % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1) | ((uintptr_t)rep)) & 15))
     return -1;
   if ((((uintptr_t)h1) | ((uintptr_t)w2)) & 15) return -1;  // float4 staging of the h1 tile and W2
   if (nrep < 1 || nrep > C1_MAXREP || (nrep > 1 && !rep)) return -1;
-  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), rep, nrep, rep_stride};
+  Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), rep, nrep, rep_stride, zero_word};
   const int nblk = ((B + 15) / 16) * ((F1IN + 15) / 16);
   hipLaunchKernelGGL(k_fc2_ce_dx_mf, dim3(nblk + 1), dim3(FDX_WAVES * 64), 0, s, h1, w2, b2, labels, w1, loss_rows,
                      dlogits, dh1, da2p, B, inv_b, bidx, cm);
@@ -2195,7 +2274,8 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
                         int rep_stride, int grads_only, float* wpart, hipStream_t s) {
   if (!ctr) return -1;
   if (((uintptr_t)(grads_only ? p + off_c2w : w2f)) & 7) return -1;  // float2 staging of the W2 slice
-  if (!grads_only && (!bidx || !pending || !w2f || nbatches < 1)) return -1;
+  if (!grads_only && (!bidx || !pending || !w2f)) return -1;
+  if (bidx && nbatches < 1) return -1;
   if (B < 1 || nrep < 1 || nrep > C1_MAXREP || (nrep > 1 && !c1rep)) return -1;
   if (wpart && nrep != B) return -1;  // deterministic mode: one conv1 replica per sample
   BwdAllArgs A;

@@ -146,8 +146,7 @@ class XgmiAllReduce:
     def allreduce_sgd_(self, offset: int, n: int, params: torch.Tensor, mom: torch.Tensor, lr_dev: torch.Tensor,
                        momentum: float, weight_decay: float, gscale: float, nesterov: bool, zero_from: int,
                        cursor: torch.Tensor | None = None, n_batches: int = 1, chan: int = 0, stream=None,
-                       replicas: torch.Tensor | None = None, n_replicas: int = 1, rep_from: int = 0,
-                       single_barrier: bool = False):
+                       replicas: torch.Tensor | None = None, n_replicas: int = 1, rep_from: int = 0):
         """All-reduce ``buf[offset:offset+n]`` and apply SGD-momentum with
         the (``gscale``-scaled) result to ``params``/``mom`` (flat buffers in
         the gradient layout) inside the same launch; the local gradient is
@@ -155,11 +154,7 @@ class XgmiAllReduce:
         advanced mod ``n_batches`` after the update.  ``replicas``: extra
         local copies of the gradient range ``[rep_from, numel)`` (replica r
         >= 1 at ``replicas[(r-1)*(numel-rep_from):]``), folded into the
-        gradient and zeroed before the exchange.  ``single_barrier``: the
-        one-shot form without its second barrier (``pto_ar_allreduce_sgd_1bar``;
-        range <= 65536 floats, nothing zeroed) -- only when the caller's next
-        barrier on another channel already orders the peers' reads of this
-        call before its next write of the range (fused_step.py overlap)."""
+        gradient and zeroed before the exchange."""
         if self.align != 4:
             raise ValueError("XgmiAllReduce: the SGD epilogue needs an fp32 buffer")
         if n % 4 or offset % 4:
@@ -178,8 +173,7 @@ class XgmiAllReduce:
                 raise ValueError("XgmiAllReduce: replica buffer too small for n_replicas")
             rep = replicas.data_ptr()
         _lib.check(_lib.lib().pto_ar_set_protocol(PROTOCOLS[self.protocol]), "ar_set_protocol")
-        fn = _lib.lib().pto_ar_allreduce_sgd_1bar if single_barrier else _lib.lib().pto_ar_allreduce_sgd
-        _lib.check(fn(self.peers.data_ptr(), offset, n, self.rank, self.world, chan,
+        _lib.check(_lib.lib().pto_ar_allreduce_sgd(self.peers.data_ptr(), offset, n, self.rank, self.world, chan,
                                                    self.epochs.data_ptr(), self.err.data_ptr(), params.data_ptr(),
                                                    mom.data_ptr(), lr_dev.data_ptr(), momentum, weight_decay, gscale,
                                                    int(nesterov), zero_from, cur, n_batches, rep,
@@ -189,18 +183,31 @@ class XgmiAllReduce:
     def role_args(self, offset: int, n: int, chan: int, params: torch.Tensor, mom: torch.Tensor,
                   lr_dev: torch.Tensor, momentum: float, weight_decay: float, gscale: float, nesterov: bool,
                   zero_from: int) -> tuple:
-        """Arguments of an all-reduce-with-SGD run as extra workgroups of
-        another launch (``pto_conv12_fwd_ar``): peers table, range, rank,
-        world, channel, epochs, error word, protocol, the update's buffers
-        and hyper-parameters."""
+        """Arguments of the stand-alone role launchers (``pto_ar_role_sgd``,
+        and ``pto_ar_oneshot_role_sgd`` after dropping ``zero_from``): peers
+        table, range, rank, world, channel, epochs, error word, protocol, the
+        update's buffers and hyper-parameters.  Every role waits for its
+        peers itself (barrier 0), whatever ran before it on the stream."""
         if n % 4 or offset % 4 or offset + n > self.buf.numel():
             raise ValueError("XgmiAllReduce: bad range for an all-reduce role")
+        return (self.peers.data_ptr(), offset, n, self.rank, self.world, chan, self.epochs.data_ptr(),
+                self.err.data_ptr(), PROTOCOLS[self.protocol],
+                *self.update_args(params, mom, lr_dev, momentum, weight_decay, gscale, nesterov), zero_from)
+
+    def update_args(self, params: torch.Tensor, mom: torch.Tensor, lr_dev: torch.Tensor, momentum: float,
+                    weight_decay: float, gscale: float, nesterov: bool) -> tuple:
+        """(params, momentum, lr pointer, momentum, weight decay, grad scale,
+        nesterov) of an SGD epilogue, checked against the gradient buffer."""
         for t in (params, mom):
             if t.dtype != torch.float32 or t.numel() != self.buf.numel() or t.device != self.device:
                 raise ValueError("XgmiAllReduce: params/momentum must match the gradient buffer")
-        return (self.peers.data_ptr(), offset, n, self.rank, self.world, chan, self.epochs.data_ptr(),
-                self.err.data_ptr(), PROTOCOLS[self.protocol], params.data_ptr(), mom.data_ptr(), lr_dev.data_ptr(),
-                momentum, weight_decay, gscale, int(nesterov), zero_from)
+        return (params.data_ptr(), mom.data_ptr(), lr_dev.data_ptr(), momentum, weight_decay, gscale, int(nesterov))
+
+    def exchange_args(self) -> tuple:
+        """(peers table, rank, world, epochs, error word, protocol): the part
+        of ``pto_conv12_fwd_ar``'s arguments that names this instance."""
+        return (self.peers.data_ptr(), self.rank, self.world, self.epochs.data_ptr(), self.err.data_ptr(),
+                PROTOCOLS[self.protocol])
 
     def error_word(self) -> int:
         """Device error word (synchronises with the current stream)."""

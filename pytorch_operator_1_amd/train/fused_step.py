@@ -29,7 +29,13 @@ knobs):
       conv1's update) and ``k_bwd_all`` (the whole backward, every other
       parameter updated by the block that finishes its gradient).
   ``ddp-xgmi``: the same four launches with ``k_bwd_all`` in grads-only
-      mode, then ONE xGMI all-reduce of the flat buffer whose epilogue is the
+      mode.  Overlapped (default): step k's gradient exchange runs as two
+      roles of step k+1's F12 launch -- the conv exchange (one-shot, 100 KB,
+      the conv blocks wait for it) and the fc exchange (1.6 MB, under the
+      convolutions) -- so the multi-GPU step has no launch more than the
+      one-process step; the last step of a run closes with both roles in a
+      launch of their own.  Whole-buffer (``overlap=False``): ONE xGMI
+      all-reduce of the flat buffer after the backward, whose epilogue is the
       SGD update (+ conv1 replica fold, gradient zeroing, cursor advance).
   ``ddp-rccl``: the grads-only step, one RCCL all-reduce of the gradients
       and their conv1 replica tail, one SGD launch (``k_ddp_sgd``: replica
@@ -60,6 +66,9 @@ from ..ops import _lib
 # us for R = 8 vs 1, profiles/bwd_all_r2.md); the readers (F12's lazy
 # update, the commit, the xGMI fold) sum them in replica order
 C1_REPLICAS = 8
+
+# xGMI channels of the overlapped step's two exchange roles (xgmi_ar.h)
+FC_CHAN, CONV_CHAN = 1, 2
 
 # Graph capture is thread-local: with "global" capture a HIP call from ANY
 # other thread of the process while a step is being captured -- e.g. the
@@ -176,19 +185,21 @@ class FusedMnistTrainer:
         self.c1_stride = self.numel - self._c1
         self.schedule = "fused-opt" if not self.ddp else ("ddp-xgmi" if self._xgmi is not None else "ddp-rccl")
         # ddp-xgmi overlap: step k's all-reduce is split at the fc | conv
-        # boundary.  The conv part (100 KB, conv1 replicas folded, cursor
-        # advance) runs right after the backward (one-shot kernel, channel
-        # 0): the next F12 reads those weights.  The fc part (1.6 MB, 94% of
-        # the bytes) runs as extra workgroups of step k+1's F12 launch
-        # (channel 1), which reads no fc parameter, so the exchange overlaps
-        # the convolutions; F3 of step k+1 is its first reader.  The last
-        # step of every graph / eager step closes with a stand-alone fc
-        # all-reduce, so every run() leaves complete updates.
+        # boundary and BOTH parts run as roles of step k+1's F12 launch:
+        # the conv part (100 KB, one-shot, conv1 replicas folded; channel 2)
+        # first in the grid -- F12's conv blocks wait for it (self._ready)
+        # before they read conv1/conv2 -- and the fc part (1.6 MB, 94% of the
+        # bytes; channel 1), which F12 does not read, under the convolutions
+        # (F3 of step k+1 is its first reader).  k_bwd_all advances the
+        # cursor.  The last step of every graph / eager run closes with both
+        # roles in a launch of their own, so every run() leaves complete
+        # updates and zero gradients.
         if overlap is None:
             overlap = os.environ.get("PTO_XGMI_OVERLAP", "1") == "1"
         self.overlap = self._xgmi is not None and bool(overlap)
+        self._ready = torch.zeros(1, device=device, dtype=torch.int32)  # conv-role publish counter (overlap)
         if self.overlap:
-            self.comm_info["overlap"] = "fc all-reduce under the next step's F12 (same launch)"
+            self.comm_info["overlap"] = "conv + fc all-reduce as roles of the next step's F12 launch"
         nrep_tail = max(1, self.c1_nrep - 1) * self.c1_stride
         if self.schedule == "ddp-rccl":
             self._ar_buf = torch.zeros(total + nrep_tail, **f32)
@@ -260,11 +271,11 @@ class FusedMnistTrainer:
         timing probes under tools/."""
         self._forward(only=which)
 
-    def _forward(self, only: int | None = None, fc_owed: bool = False):
+    def _forward(self, only: int | None = None, owed: bool = False):
         """F12, F3, F4dx.  Fused-opt: F12 applies conv1's owed update on the
         fly (lazy) and F4dx commits it; F4dx's d(a2p) feeds the backward.
-        ``fc_owed`` (ddp-xgmi overlap): F12 also runs the previous step's fc
-        all-reduce + SGD as extra workgroups."""
+        ``owed`` (ddp-xgmi overlap): F12 also runs the previous step's
+        exchange (conv + fc all-reduce with SGD) as extra workgroups."""
         L, s, B, P = self.L, self._s(), self.B, self._p
         c = _lib.check
         bi = self.batch_idx.data_ptr()
@@ -280,16 +291,8 @@ class FusedMnistTrainer:
             lazy = (None, None, 0, None, None, 0.0, 0.0, 1.0, 0)
             w2out, pending = None, None
             conv1 = (conv1[0], None, conv1[2], conv1[3])  # F4dx's spare block idles
-        if only in (None, 0) and fc_owed:
-            # the all-reduce role also zeroes the previous step's conv grads
-            # once its stage-1 barrier has passed (every peer's conv exchange,
-            # which read them, is complete), before this step's backward
-            zt = self.grads[self._split:]
-            c(L.pto_conv12_fwd_ar(self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
-                                  P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(),
-                                  self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi,
-                                  self.xcur.data_ptr(), *self._fc_role_args(), zt.data_ptr(), zt.numel(), s),
-              "conv12_fwd_ar")
+        if only in (None, 0) and owed:
+            self._exchange_launch(B)
         elif only in (None, 0):
             self._call("conv12_fwd_lazy_x", self.data.data_ptr(), P["conv1.weight"].data_ptr(),
                        P["conv1.bias"].data_ptr(), P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(),
@@ -302,7 +305,7 @@ class FusedMnistTrainer:
             self._call("fc2_ce_dx", self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
                        self.target.data_ptr(), P["fc1.weight"].data_ptr(), self.loss_rows.data_ptr(),
                        self.dlogits.data_ptr(), self.dh1.data_ptr(), self.da2p.data_ptr(), B, 1.0 / B, bi, *conv1,
-                       pending, *o, *rep)
+                       pending, *o, *rep, self._ready.data_ptr() if self.overlap else None)
 
     def _backward(self):
         """``k_bwd_all``: the whole backward in one launch.  Fused-opt: every
@@ -310,47 +313,46 @@ class FusedMnistTrainer:
         conv1's update becomes owed.  DDP (grads-only): every gradient lands
         in the flat buffer and nothing else changes."""
         go = self.ddp
+        cursor = not go or self.overlap  # overlapped xGMI step: no exchange launch after this one
         self._call("bwd_all", self.da2p.data_ptr(), self.code2.data_ptr(), self.a1p.data_ptr(), _lib.ptr(self.w2f),
                    self.xcur.data_ptr(), self.code1.data_ptr(), self.dh1.data_ptr(), self.a2p.data_ptr(),
                    self.h1.data_ptr(), self.dlogits.data_ptr(), self._params.data_ptr(), self.grads.data_ptr(),
                    self.mom.data_ptr(), *self._offs, self.c2_ctr.data_ptr(),
-                   None if go else self.batch_idx.data_ptr(), self.n_batches,
+                   self.batch_idx.data_ptr() if cursor else None, self.n_batches,
                    None if go else self.pending.data_ptr(), self.B, *self._opt_args(), self.c1rep.data_ptr(),
                    self.c1_nrep, self.c1_stride, int(go), _lib.ptr(self.wpart))
 
-    def _fc_role_args(self):
+    def _exchange_launch(self, B: int):
+        """ddp-xgmi overlap: the previous step's exchange as the two roles of
+        ``pto_conv12_fwd_ar`` -- with B > 0 inside this step's F12 launch,
+        with B == 0 as a launch of its own (the close of a run).  The conv
+        role (channel CONV_CHAN) updates conv2/conv1 and zeroes their
+        gradients; the fc role (FC_CHAN) updates fc1/fc2.  Every rank runs
+        the same roles with the same workgroup decomposition either way, so
+        ranks whose run() chunks differ still pair up block by block."""
+        L, P = self.L, self._p
         lr, mom, wd, gs, nes = self._opt_args()
-        return self._xgmi.role_args(0, self._split, 1, self._params, self.mom, self.lr_dev, mom, wd, gs, bool(nes),
-                                    self.numel)
+        x = self._xgmi
+        _lib.check(L.pto_conv12_fwd_ar(
+            self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
+            P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(), self.code1.data_ptr(),
+            self.a2p.data_ptr(), self.code2.data_ptr(), B, self.batch_idx.data_ptr(), self.xcur.data_ptr(),
+            *x.exchange_args(), *x.update_args(self._params, self.mom, self.lr_dev, mom, wd, gs, bool(nes)),
+            0, self._split, FC_CHAN, self.numel,
+            self._split, self.numel - self._split, CONV_CHAN,
+            self.c1rep.data_ptr(), self.c1_nrep, self.c1_stride, self._c1, self._ready.data_ptr(), self._s()),
+            "conv12_fwd_ar" if B else "exchange_close")
 
-    def _close_fc(self):
-        """ddp-xgmi overlap: the owed fc all-reduce + SGD as a launch of its
-        own (end of a graph / eager step), with the F12 role's exact
-        workgroup decomposition -- ranks whose run() chunks differ (one
-        closes a step's exchange, its peer runs it inside F12) still pair up
-        block by block.  After its stage-1 barrier it also zeroes this rank's
-        conv gradients (every peer has finished the conv exchange that read
-        them), so a run() leaves all gradients zero; inside a graph the
-        next step's F12 all-reduce role does the same."""
-        zt = self.grads[self._split:]
-        _lib.check(self.L.pto_ar_role_sgd(*self._fc_role_args(), zt.data_ptr(), zt.numel(), self._s()),
-                   "ar_role_sgd")
+    def _close_exchange(self):
+        """ddp-xgmi overlap: the owed exchange as a launch of its own (end of
+        a graph / eager run), so a run() leaves complete updates."""
+        self._exchange_launch(0)
 
     def _allreduce_update(self):
         """DDP: gradient all-reduce + SGD (+ zeroing of the accumulated conv
-        grads and the cursor advance).  ddp-xgmi overlap: the conv range
-        only (the fc range is owed to the next F12 / the closing launch)."""
+        grads and the cursor advance).  ddp-xgmi overlap: nothing here (the
+        whole exchange is owed to the next F12 / the closing launch)."""
         if self._xgmi is not None and self.overlap:
-            # one barrier: the fc exchange that follows (channel 1, in the
-            # next F12 or the closing launch) orders every peer's reads of
-            # these conv grads before this rank's next write of them -- the
-            # zeroing in the next F4dx and the next backward's atomics
-            lr, mom, wd, gs, nes = self._opt_args()
-            self._xgmi.allreduce_sgd_(self._split, self.numel - self._split, params=self._params, mom=self.mom,
-                                      lr_dev=self.lr_dev, momentum=mom, weight_decay=wd, gscale=gs,
-                                      nesterov=bool(nes), zero_from=self.numel, cursor=self.batch_idx,
-                                      n_batches=self.n_batches, replicas=self.c1rep, n_replicas=self.c1_nrep,
-                                      rep_from=self._c1, chan=0, single_barrier=True)
             return
         if self._xgmi is not None:
             lr, mom, wd, gs, nes = self._opt_args()
@@ -373,12 +375,12 @@ class FusedMnistTrainer:
         """One step's launches.  ``first``/``last``: its place in a captured
         run (ddp-xgmi overlap: only a non-first step's F12 carries the
         previous step's fc all-reduce; the last step closes it)."""
-        self._forward(fc_owed=self.overlap and not first)
+        self._forward(owed=self.overlap and not first)
         self._backward()
         if self.ddp:
             self._allreduce_update()
             if self.overlap and last:
-                self._close_fc()
+                self._close_exchange()
 
     def _commit_launch(self):
         self._call("conv1_commit", self._params[self._c1:].data_ptr(), self.grads[self._c1:].data_ptr(),
@@ -418,7 +420,7 @@ class FusedMnistTrainer:
             pdist.host_barrier(tag=f"xgmi-{tag}")
 
     def _state(self):
-        return (self._params, self.mom, self.grads, self.batch_idx, self.pending, self.c1rep)
+        return (self._params, self.mom, self.grads, self.batch_idx, self.pending, self.c1rep, self._ready)
 
     def _graph_sizes(self) -> list[int]:
         if self.fused_opt:

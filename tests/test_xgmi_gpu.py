@@ -471,14 +471,17 @@ def test_xgmi_allreduce_uneven_load():
 
 
 def _overlap_pair_worker(rank, world, port, q):
-    """The overlapped MNIST step's exchange pair at any world size: the
-    one-barrier one-shot all-reduce + SGD of a conv-sized range (chan 0,
-    NO second barrier), then the rank-split fc role (chan 1, 1024-thread
-    workgroups, S = 1024 / world threads per rank group) + SGD, which zeroes
-    the conv range after its first barrier -- the barrier that must order
-    every peer's one-shot reads before that zeroing.  Parameters and
-    momentum vs the same SGD in torch on the exact sum, every rank
-    bit-identical, the conv range zero after every pair."""
+    """The overlapped MNIST step's exchange at any world size: the one-shot
+    rank-split conv role (channel 2: replicas folded, all-reduce + SGD,
+    parameter written through, one publish per workgroup, gradient and
+    replicas zeroed after its second barrier) and the rank-split fc role
+    (channel 1, barrier 0 of its own).  Even ranks run both roles as ONE
+    launch (the MNIST forward launch with no conv blocks, as a run's
+    closing exchange), odd ranks as two stand-alone launches: the
+    decompositions must pair block by block.  Parameters and momentum vs the
+    same SGD in torch on the exact sum (folded replicas included), every
+    rank bit-identical, gradients and replicas zero after every exchange,
+    the publish counter = role workgroups per call."""
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         import torch.distributed as dist
@@ -491,8 +494,12 @@ def _overlap_pair_worker(rank, world, port, q):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         nfc, nconv = 81_920, 25_664  # fc range > the one-shot limit, conv range = MNIST's
         n = nfc + nconv
+        stride, nrep = 576, 4  # replicated tail (MNIST: conv1, 8 replicas)
+        rep_from = n - stride
         lr, mom, wd = 0.05, 0.9, 1e-3
         buf = torch.zeros(n, device=dev)
+        rep = torch.zeros((nrep - 1) * stride, device=dev)
+        ready = torch.zeros(1, dtype=torch.int32, device=dev)
         ar = XgmiAllReduce(buf, timeout_ms=20000)
         p = torch.randn(n, generator=torch.Generator(device=dev).manual_seed(7), device=dev)
         m = torch.zeros(n, device=dev)
@@ -500,37 +507,53 @@ def _overlap_pair_worker(rank, world, port, q):
         lr_dev = torch.tensor([lr], device=dev)
         L = _lib.lib()
         s = torch.cuda.current_stream(dev).cuda_stream
-        worst, zero_ok = 0.0, True
+        cnb = L.pto_ar_oneshot_role_blocks(nconv, world)
+        worst, zero_ok, ready_ok = 0.0, True, True
         for it in range(8):
             _fill(buf, rank, 700 + it)
-            ar.allreduce_sgd_(nfc, nconv, params=p, mom=m, lr_dev=lr_dev, momentum=mom, weight_decay=wd,
-                              gscale=1.0 / world, nesterov=True, zero_from=n, chan=0, single_barrier=True)
-            zt = buf[nfc:]
-            _lib.check(L.pto_ar_role_sgd(*ar.role_args(0, nfc, 1, p, m, lr_dev, mom, wd, 1.0 / world, True, n),
-                                         zt.data_ptr(), zt.numel(), s), "ar_role_sgd")
+            g = torch.Generator(device=dev).manual_seed(9000 + 31 * it + rank)
+            rep.copy_(torch.randn(rep.shape, generator=g, device=dev))
+            mine = buf.clone()
+            for r in range(nrep - 1):
+                mine[rep_from:] += rep[r * stride:(r + 1) * stride]
+            tot = mine.cpu()
+            dist.all_reduce(tot)  # the exact sum over ranks (gloo, fp32)
+            ready.zero_()
+            upd = ar.update_args(p, m, lr_dev, mom, wd, 1.0 / world, True)
+            if rank % 2 == 0:
+                _lib.check(L.pto_conv12_fwd_ar(*([None] * 9), 0, None, None, *ar.exchange_args(), *upd,
+                                               0, nfc, 1, n, nfc, nconv, 2, rep.data_ptr(), nrep, stride, rep_from,
+                                               ready.data_ptr(), s), "conv12_fwd_ar(B=0)")
+            else:
+                _lib.check(L.pto_ar_oneshot_role_sgd(*ar.role_args(nfc, nconv, 2, p, m, lr_dev, mom, wd,
+                                                                   1.0 / world, True, n)[:-1],
+                                                     rep.data_ptr(), nrep, stride, rep_from, ready.data_ptr(), s),
+                           "ar_oneshot_role_sgd")
+                _lib.check(L.pto_ar_role_sgd(*ar.role_args(0, nfc, 1, p, m, lr_dev, mom, wd, 1.0 / world, True, n),
+                                             s), "ar_role_sgd")
             torch.cuda.synchronize(dev)
-            d = _expected(n, world, 700 + it, dev) / world + wd * pr
+            d = tot.to(dev) / world + wd * pr
             mr.mul_(mom).add_(d)
             pr.sub_(lr * (d + mom * mr))
             worst = max(worst, (p - pr).abs().max().item(), (m - mr).abs().max().item())
-            zero_ok &= float(buf[nfc:].abs().max()) == 0.0
+            zero_ok &= float(buf[nfc:].abs().max()) == 0.0 and float(rep.abs().max()) == 0.0
+            ready_ok &= int(ready.item()) == cnb
         ar.check()
         allv = [None] * world
         dist.all_gather_object(allv, p.cpu())
         same = all(torch.equal(allv[0], v) for v in allv)
         ar.close()
         dist.destroy_process_group()
-        q.put((rank, worst, same, zero_ok))
+        q.put((rank, worst, same, zero_ok and ready_ok))
     except Exception as e:  # noqa: BLE001
         q.put((rank, repr(e), False, False))
         raise
 
 
-@pytest.mark.parametrize("world", [3, 8])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_xgmi_overlap_pair_any_world(world):
-    """World sizes the 2/4-rank tests do not reach: 3 (S = 341, idle
-    threads in every role workgroup) and 8 (the node's full world, 8 rank
-    groups of 128 threads)."""
+    """World sizes 2, 3 (S = 341, idle threads in every role workgroup) and
+    8 (the node's full world, 8 rank groups of 128 threads)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
