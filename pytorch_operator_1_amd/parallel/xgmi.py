@@ -84,6 +84,15 @@ class XgmiAllReduce:
         self._flags = fl.value
         self.epochs = torch.zeros(L.pto_ar_epoch_words(), dtype=torch.int32, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        # True if two ranks of the group share one GPU.  Their kernels then
+        # compete for the same CUs, and the hardware dispatches each
+        # launch's workgroups in order: a launch whose workgroups spin on a
+        # peer's launch (every exchange role does) may hold the CUs that the
+        # peer's launch needs to even start.  Roles alone keep that bounded
+        # (they wait only on roles); a launch whose OTHER workgroups also
+        # wait on its roles (the overlapped MNIST forward) does not, so
+        # the trainer keeps the exchange in a launch of its own then.
+        self.colocated = False
         if self.world == 1:
             self._opened = []
             self._set_peers(L, [[buf.data_ptr()], [self.tmp.data_ptr()], [self._flags]])
@@ -95,8 +104,16 @@ class XgmiAllReduce:
             off = ctypes.c_longlong()
             _lib.check(L.pto_ar_get_ipc_handle(p, h, ctypes.byref(off)), "ar_get_ipc_handle")
             mine.append((h.raw, off.value))
+        # the device of every rank: ranks that SHARE a GPU (rehearsals,
+        # tests on a one-GPU box) cannot run schedules whose workgroups wait
+        # on each other inside one launch (see :attr:`colocated`)
+        props = torch.cuda.get_device_properties(self.device)
+        me = (props.pci_domain_id, props.pci_bus_id, props.pci_device_id, str(getattr(props, "uuid", "")))
         allh = [None] * self.world
-        dist.all_gather_object(allh, mine, group=group)
+        dist.all_gather_object(allh, (mine, me), group=group)
+        devs = [d for _, d in allh]
+        allh = [h for h, _ in allh]
+        self.colocated = len(set(devs)) < self.world
         self._opened = []
         ptrs = [[0] * self.world for _ in range(3)]
         ok = 1

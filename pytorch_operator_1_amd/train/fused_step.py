@@ -198,8 +198,15 @@ class FusedMnistTrainer:
             overlap = os.environ.get("PTO_XGMI_OVERLAP", "1") == "1"
         self.overlap = self._xgmi is not None and bool(overlap)
         self._ready = torch.zeros(1, device=device, dtype=torch.int32)  # conv-role publish counter (overlap)
+        # ranks sharing one GPU (rehearsals, the one-GPU test box): the same
+        # two roles, but as a launch of their own right after the backward --
+        # F12's conv blocks waiting on them could hold the CUs a co-located
+        # peer needs to reach its own roles (XgmiAllReduce.colocated)
+        self._inline = self.overlap and not self._xgmi.colocated
         if self.overlap:
-            self.comm_info["overlap"] = "conv + fc all-reduce as roles of the next step's F12 launch"
+            self.comm_info["overlap"] = ("conv + fc all-reduce as roles of the next step's F12 launch" if self._inline
+                                         else "conv + fc all-reduce roles in one launch after the backward "
+                                              "(ranks share a GPU)")
         nrep_tail = max(1, self.c1_nrep - 1) * self.c1_stride
         if self.schedule == "ddp-rccl":
             self._ar_buf = torch.zeros(total + nrep_tail, **f32)
@@ -305,7 +312,7 @@ class FusedMnistTrainer:
             self._call("fc2_ce_dx", self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
                        self.target.data_ptr(), P["fc1.weight"].data_ptr(), self.loss_rows.data_ptr(),
                        self.dlogits.data_ptr(), self.dh1.data_ptr(), self.da2p.data_ptr(), B, 1.0 / B, bi, *conv1,
-                       pending, *o, *rep, self._ready.data_ptr() if self.overlap else None)
+                       pending, *o, *rep, self._ready.data_ptr() if self._inline else None)
 
     def _backward(self):
         """``k_bwd_all``: the whole backward in one launch.  Fused-opt: every
@@ -375,11 +382,11 @@ class FusedMnistTrainer:
         """One step's launches.  ``first``/``last``: its place in a captured
         run (ddp-xgmi overlap: only a non-first step's F12 carries the
         previous step's fc all-reduce; the last step closes it)."""
-        self._forward(owed=self.overlap and not first)
+        self._forward(owed=self._inline and not first)
         self._backward()
         if self.ddp:
             self._allreduce_update()
-            if self.overlap and last:
+            if self.overlap and (last or not self._inline):
                 self._close_exchange()
 
     def _commit_launch(self):
@@ -726,9 +733,15 @@ def autotune_schedule(cands: list, rc: FusedMnistTrainer, verify_steps: int = 8,
         rc.run(verify_steps)
         torch.cuda.synchronize(dev)
         ok_c = []
+        from ..parallel.xgmi import XgmiTimeout
+
         for xg in cands:
             xg._align_ranks("tune-verify")
-            xg.run(verify_steps)
+            stalled = None
+            try:
+                xg.run(verify_steps)
+            except XgmiTimeout as e:  # this variant stalls here: every rank drops it (same collectives below)
+                stalled = str(e)[:200]
             torch.cuda.synchronize(dev)
             err = 0.0
             for name, pv in xg.p.items():
@@ -738,8 +751,10 @@ def autotune_schedule(cands: list, rc: FusedMnistTrainer, verify_steps: int = 8,
             chk = mine.clone() if dist.get_backend() == "nccl" else mine.cpu()
             dist.all_reduce(chk, op=dist.ReduceOp.MAX)
             identical = bool(torch.equal(chk.to(mine.device), mine))
-            ok = agree(err <= 1e-4 and identical and xg._xgmi.error_word() == 0)
+            ok = agree(stalled is None and err <= 1e-4 and identical and xg._xgmi.error_word() == 0)
             out["candidates"][_variant(xg)] = {"param_rel_err": err, "identical": identical, "correct": ok}
+            if stalled:
+                out["candidates"][_variant(xg)]["error"] = stalled
             ok_c.append(ok)
         times = {}
         for xg, ok in zip(cands, ok_c):
