@@ -163,8 +163,11 @@ def main(argv=None):
     elapsed = time.perf_counter() - t0
     elapsed = pdist.all_reduce_max(elapsed, device)
     loss = trainer.last_loss()
-    # evidence of the world that was measured (outside the timed region)
+    # evidence of the world that was measured (outside the timed region):
+    # the ranks, their devices and transports, and whether the replicas
+    # still hold bit-identical parameters after the timed steps
     world = pdist.describe_world(device, rccl_log)
+    identical = pdist.ranks_bit_identical(_param_tensors(trainer), device)
     comm = dict(getattr(trainer, "comm_info", None) or {})
     comm.update(world)
 
@@ -204,49 +207,87 @@ def main(argv=None):
                 "grad_allreduce": comm,
             },
         }
+        if identical is not None:
+            out["ranks_bit_identical"] = identical
     pdist.cleanup()
-    if out is not None and n == 1 and not args.no_latency and os.environ.get("BENCH_LATENCY", "1") == "1":
-        # second half of the BASELINE metric, outside the timed region: the
-        # trainer's buffers are released first (the job runs on this GPU)
+    if out is not None and not args.no_latency and os.environ.get("BENCH_LATENCY", "1") == "1":
+        # second half of the BASELINE metric, outside the timed region, on
+        # rank 0 after the process group is gone: a job of n replicas
+        # (Master=1, Worker=n-1) submitted through the whole operator stack.
+        # The trainer's buffers are released first (the job runs on these
+        # GPUs); the other ranks have nothing left to do and exit.
         del trainer, run
         if device.type == "cuda":
             torch.cuda.synchronize(device)
             torch.cuda.empty_cache()
-        lat = measure_submit_to_first_step(gpu=device.type == "cuda")
+        lat = measure_submit_to_first_step(gpu=device.type == "cuda", replicas=n)
         out["submit_to_first_step_s"] = lat.get("submit_to_first_step_s")
         out["config"]["submit_to_first_step"] = lat
     if out is not None:
         print(json.dumps(out), flush=True)
+    if identical is False:
+        print("[bench] error: the data-parallel replicas diverged (parameters not bit-identical across ranks)",
+              file=sys.stderr, flush=True)
+        return 3
 
 
-def measure_submit_to_first_step(gpu: bool, timeout: float = 240.0) -> dict:
+def _param_tensors(trainer) -> list:
+    """The parameters whose replicas must agree across ranks."""
+    p = getattr(trainer, "params", None)
+    if isinstance(p, torch.Tensor):
+        return [p]
+    m = getattr(trainer, "model", None)
+    return [t for t in m.parameters()] if m is not None else []
+
+
+def measure_submit_to_first_step(gpu: bool, replicas: int = 1, timeout: float = 240.0) -> dict:
     """CRD-submit -> first optimizer step through the whole local stack:
     in-process API store + PyTorchJob controller + node manager, whose C++
     node agent and warm interpreter (zygote) are fresh CHILD processes of
-    this one (nothing is exec'ed in place), then the trainer process they
-    start.  One Master replica (``amd.com/gpu: 1``, fused HIP trainer) on
-    the GPU, or the eager trainer over gloo with ``--cpu``.  The node is up
-    before the job arrives (the zygote's imports are done), like the
-    reference's cluster, whose submit -> Running was 121 s (CPU) / 334 s
-    (GPU) (BASELINE.md)."""
+    this one (nothing is exec'ed in place), then the trainer processes they
+    start.  ``replicas`` = 1 Master + (replicas - 1) Workers, each with
+    ``amd.com/gpu: 1`` and the fused HIP trainer over RCCL (the reference's
+    GPU figure is for a Master + Worker job), or the eager trainer over
+    gloo with ``--cpu``.  With fewer GPUs than replicas (a rehearsal on a
+    one-GPU box) the node offers each GPU to several replicas and the job
+    uses gloo.  The first step is the Master's.  The node is up before the
+    job arrives (the zygote's imports are done), like the reference's
+    cluster, whose submit -> Running was 121 s (CPU) / 334 s (GPU)
+    (BASELINE.md)."""
+    import math
     import tempfile
 
     from pytorch_operator_1_amd.api.types import new_job
     from pytorch_operator_1_amd.cluster import LocalCluster
+    from pytorch_operator_1_amd.utils.dist import visible_gpu_count_no_hip
 
-    res = {"replicas": "Master=1", "trainer": "fused (HIP graphs)" if gpu else "eager (gloo, CPU)"}
+    share = 1
+    if gpu and replicas > 1:
+        share = max(1, math.ceil(replicas / max(1, visible_gpu_count_no_hip())))
+    res = {"replicas": "Master=1" + (f", Worker={replicas - 1}" if replicas > 1 else ""),
+           "trainer": "fused (HIP graphs)" if gpu else "eager (gloo, CPU)"}
+    if share > 1:
+        res["gpu_share"] = share
     os.environ.setdefault("PTO_ZYGOTE", "1")
+    # this process may be a torchrun rank: the node agent and its pods must
+    # not inherit the launcher's rendezvous (TORCHELASTIC_USE_AGENT_STORE
+    # would make every replica a client of a store nobody hosts)
+    scrub = [k for k in os.environ if k.startswith(("TORCHELASTIC_", "NCCL_DEBUG")) or k in
+             ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE", "ROLE_RANK",
+              "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT", "TORCH_NCCL_ASYNC_ERROR_HANDLING")]
+    saved_env = {k: os.environ.pop(k) for k in scrub}
     t_start = time.time()
     try:
         with tempfile.TemporaryDirectory(prefix="pto-bench-") as d, \
-                LocalCluster(gpus=None if gpu else 0, log_dir=d, serve_http=False) as c:
+                LocalCluster(gpus=None if gpu else 0, log_dir=d, serve_http=False, gpu_share=share) as c:
             res["zygote_warm"] = bool(c.kubelet.agent.wait_warm(120))
             res["node_startup_s"] = round(time.time() - t_start, 3)
-            margs = (["--backend", "rccl", "--impl", "fused"] if gpu else ["--backend", "gloo", "--no-cuda",
-                                                                          "--train-size", "2560"])
+            backend = "gloo" if (not gpu or share > 1) else "rccl"
+            margs = (["--backend", backend, "--impl", "fused"] if gpu else ["--backend", "gloo", "--no-cuda",
+                                                                           "--train-size", "2560"])
             margs += ["--max-steps", "20", "--log-interval", "10", "--no-test", "--dir", ""]
-            job = new_job("bench-latency", image="pto/pytorch-mnist:rocm", master_args=margs, workers=0,
-                          gpus=1 if gpu else 0)
+            job = new_job("bench-latency", image="pto/pytorch-mnist:rocm", master_args=margs,
+                          workers=replicas - 1, gpus=1 if gpu else 0)
             t0 = time.time()
             c.submit(job)
             j = c.wait_for_condition("bench-latency", timeout=timeout)
@@ -260,6 +301,8 @@ def measure_submit_to_first_step(gpu: bool, timeout: float = 240.0) -> dict:
                 res["log_tail"] = c.pod_log("default", "bench-latency-master-0")[-500:]
     except Exception as e:  # noqa: BLE001 - the throughput result still stands
         res["error"] = f"{type(e).__name__}: {e}"[:500]
+    finally:
+        os.environ.update(saved_env)
     return res
 
 
@@ -288,6 +331,7 @@ def run_model_bench(args, env, device, pdist, rccl_log=None):
     pdist.barrier(device)
     torch.cuda.synchronize(device)
     elapsed = pdist.all_reduce_max(time.perf_counter() - t0, device)
+    identical = pdist.ranks_bit_identical(_param_tensors(trainer), device)
     breakdown = None
     if args.breakdown:  # separate, untimed pass so event records do not perturb the measurement
         trainer.timer.enabled = True
@@ -311,6 +355,8 @@ def run_model_bench(args, env, device, pdist, rccl_log=None):
         cfg.update(trainer.describe())
         cfg["world"] = world
         cfg["grad_allreduce"] = dict(getattr(trainer.bucketer, "comm_info", {}) or {})
+        if identical is not None:
+            cfg["ranks_bit_identical"] = identical
         if breakdown:
             cfg["phase_ms"] = breakdown
         if hasattr(trainer, "flops_per_step"):
@@ -324,6 +370,9 @@ def run_model_bench(args, env, device, pdist, rccl_log=None):
                           "data": "synthetic (random tokens / ImageNet-shaped images), random-init weights",
                           "config": cfg}), flush=True)
     pdist.cleanup()
+    if identical is False:
+        print("[bench] error: the data-parallel replicas diverged", file=sys.stderr, flush=True)
+        return 3
 
 
 if __name__ == "__main__":

@@ -138,6 +138,69 @@ __global__ __launch_bounds__(AR_ROLE_THREADS) void k_xgmi_oneshot_role(const ArP
                                                lds, ready);
 }
 
+// ------------------------------------------------------ parameter hash --
+// Cross-rank consistency check of a data-parallel run (fused_step.py): a
+// 64-bit hash of this rank's parameters, published into the hash ring of
+// EVERY rank's flag page, so each rank's host can compare its own hash with
+// every peer's for the same sequence number (XgmiAllReduce.check_hashes).
+// Replicas updated by the same all-reduced gradient hold bit-identical
+// parameters; a lost or stale peer read anywhere shows up as a mismatch.
+// The hash is a SUM over 32-bit words of a 64-bit mix of (index, bits), so
+// workgroups combine with one 64-bit atomic add each, in any order.  The
+// workgroup whose arrival is last (ticket counter; every adder drained its
+// atomic first) publishes {seq, hash} -- hash stored, drained, then seq
+// stored, so a reader that sees seq also sees the hash -- and re-arms the
+// accumulator and the ticket for the next call.
+// st: [0] accumulator, [1] ticket, [2] sequence number (int64, zeroed at setup).
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
+  x += 0x9e3779b97f4a7c15ULL;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+  return x ^ (x >> 31);
+}
+constexpr int HASH_THREADS = 256;
+__global__ __launch_bounds__(HASH_THREADS) void k_param_hash(const ArPeers* __restrict__ P, const uint4* __restrict__ p,
+                                                             long long n4, int rank, int world,
+                                                             unsigned long long* __restrict__ st) {
+  __shared__ unsigned long long red[HASH_THREADS / 64];
+  __shared__ int s_last;
+  unsigned long long h = 0;
+  for (long long i = (long long)blockIdx.x * HASH_THREADS + threadIdx.x; i < n4; i += (long long)gridDim.x * HASH_THREADS) {
+    const uint4 v = p[i];
+    const unsigned long long k = (unsigned long long)i << 34;
+    h += mix64(k | v.x) + mix64(k | (1ULL << 32) | v.y) + mix64(k | (2ULL << 32) | v.z) + mix64(k | (3ULL << 32) | v.w);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long b = 0;
+    for (int w = 0; w < HASH_THREADS / 64; ++w) b += red[w];
+    atomicAdd(st, b);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the add performed before the ticket
+    const unsigned long long old = atomicAdd(st + 1, 1ULL);
+    s_last = old == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last || threadIdx.x >= world) return;
+  // last arriver: lanes 0..world-1 publish into rank t's page
+  const unsigned long long tot = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long seq = st[2] + 1;
+  const int t = threadIdx.x;
+  uint32_t* e = P->flags[t] + AR_FLAG_WORDS + ((int)(seq % AR_HASH_RING) * AR_MAX_RANKS + rank) * 4;
+  __hip_atomic_store(G(e + 2), (uint32_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(G(e + 3), (uint32_t)(tot >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(G(e + 1), (uint32_t)(seq >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(G(e + 0), (uint32_t)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t == 0) {
+    st[0] = 0;
+    st[1] = 0;
+    st[2] = seq;
+  }
+}
+
 template <bool FENCED>
 __global__ __launch_bounds__(AR_THREADS) void k_xgmi_allreduce_bf16(const ArPeers* __restrict__ peers, long long off,
                                                                     long long nv, int rank, int world, int chan,
@@ -187,7 +250,9 @@ int launch(const void* peers, long long off, long long n, int rank, int world, i
 
 // ---------------------------------------------------------------- host API
 PTO_API int pto_ar_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
-PTO_API int pto_ar_flag_bytes(int) { return AR_FLAG_WORDS * (int)sizeof(uint32_t); }
+PTO_API int pto_ar_flag_bytes(int) { return AR_PAGE_WORDS * (int)sizeof(uint32_t); }
+PTO_API int pto_ar_hash_offset_words() { return AR_FLAG_WORDS; }
+PTO_API int pto_ar_hash_ring() { return AR_HASH_RING; }
 PTO_API int pto_ar_max_ranks() { return AR_MAX_RANKS; }
 PTO_API int pto_ar_peers_bytes() { return (int)sizeof(ArPeers); }
 PTO_API int pto_ar_epoch_words() { return AR_CHANNELS * AR_MAX_BLOCKS; }
@@ -210,9 +275,9 @@ PTO_API long long pto_ar_timeout_ticks() { return g_timeout_ticks; }
 
 // Flags: uncached device memory, zeroed.
 PTO_API int pto_ar_alloc_flags(void** out) {
-  hipError_t e = hipExtMallocWithFlags(out, (size_t)AR_FLAG_WORDS * sizeof(uint32_t), hipDeviceMallocUncached);
+  hipError_t e = hipExtMallocWithFlags(out, (size_t)AR_PAGE_WORDS * sizeof(uint32_t), hipDeviceMallocUncached);
   if (e != hipSuccess) return (int)e;
-  return (int)hipMemset(*out, 0, (size_t)AR_FLAG_WORDS * sizeof(uint32_t));
+  return (int)hipMemset(*out, 0, (size_t)AR_PAGE_WORDS * sizeof(uint32_t));
 }
 PTO_API int pto_ar_free(void* p) { return (int)hipFree(p); }
 
@@ -233,6 +298,32 @@ PTO_API int pto_ar_open_ipc_handle(const void* handle, void** ptr_out) {
 PTO_API int pto_ar_close_ipc_handle(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
 
 PTO_API int pto_ar_blocks(long long n, int world) { return blocks_for(n, world); }
+
+// Publish a 64-bit hash of n floats at p (16-byte aligned, n % 4 == 0) into
+// every rank's hash ring (k_param_hash).  st: 3 zeroed int64 of this rank.
+PTO_API int pto_ar_param_hash(const void* peers, const float* p, long long n, int rank, int world, void* st,
+                              hipStream_t s) {
+  if (!peers || !p || !st || n % 4 || n <= 0 || (((uintptr_t)p) & 15) || world < 1 || world > AR_MAX_RANKS ||
+      rank < 0 || rank >= world)
+    return -1;
+  const long long n4 = n / 4;
+  const long long nb_need = (n4 + HASH_THREADS - 1) / HASH_THREADS;
+  const int nb = (int)(nb_need < 64 ? nb_need : 64);
+  hipLaunchKernelGGL(k_param_hash, dim3(nb), dim3(HASH_THREADS), 0, s, reinterpret_cast<const ArPeers*>(peers),
+                     reinterpret_cast<const uint4*>(p), n4, rank, world,
+                     reinterpret_cast<unsigned long long*>(st));
+  return (int)hipGetLastError();
+}
+
+// Copy nwords 32-bit words of device memory (e.g. this rank's flag page)
+// into host memory (synchronous).
+PTO_API int pto_ar_read_words(const void* src, void* dst, long long nwords) {
+  return (int)hipMemcpy(dst, src, (size_t)nwords * 4, hipMemcpyDeviceToHost);
+}
+// The same, queued on stream s (dst: pinned host memory).
+PTO_API int pto_ar_read_words_async(const void* src, void* dst, long long nwords, hipStream_t s) {
+  return (int)hipMemcpyAsync(dst, src, (size_t)nwords * 4, hipMemcpyDeviceToHost, s);
+}
 
 // Largest range (floats) one call may cover: the buffer descriptors of the
 // coherent protocol address it with 32-bit byte offsets.

@@ -58,6 +58,12 @@ __host__ __device__ constexpr int flag_index(int chan, int phase, int block, int
   return ((chan * 2 + phase) * AR_MAX_BLOCKS + block) * AR_MAX_RANKS + src;
 }
 constexpr int AR_FLAG_WORDS = AR_CHANNELS * 2 * AR_MAX_BLOCKS * AR_MAX_RANKS;
+// parameter-hash ring after the flags (k_param_hash): AR_HASH_RING entries per
+// source rank, each {seq lo, seq hi, hash lo, hash hi}; entry (seq % RING) of
+// rank q is written by rank q into EVERY rank's page
+constexpr int AR_HASH_RING = 4;
+constexpr int AR_HASH_WORDS = AR_HASH_RING * AR_MAX_RANKS * 4;
+constexpr int AR_PAGE_WORDS = AR_FLAG_WORDS + AR_HASH_WORDS;
 
 // float4 access to a buffer that peers read or write.  COHERENT: system-
 // scope buffer loads/stores (sc0 sc1), i.e. write-through stores and loads

@@ -154,6 +154,11 @@ _SIGS = {
     "pto_ar_open_ipc_handle": [_P, ctypes.POINTER(ctypes.c_void_p)],
     "pto_ar_close_ipc_handle": [_P],
     "pto_ar_blocks": [_L, _I],
+    "pto_ar_hash_offset_words": [],
+    "pto_ar_hash_ring": [],
+    "pto_ar_param_hash": [_P, _P, _L, _I, _I, _P, _P],
+    "pto_ar_read_words": [_P, _P, _L],
+    "pto_ar_read_words_async": [_P, _P, _L, _P],
     "pto_ar_allreduce": [_P, _L, _L, _I, _I, _I, _P, _P, _P],
     "pto_ar_timeout_ticks": [],
     "pto_ar_allreduce_bf16": [_P, _L, _L, _I, _I, _I, _P, _P, _P],

@@ -49,6 +49,13 @@ class XgmiTimeout(RuntimeError):
     """A barrier of the xGMI all-reduce timed out: a peer died or stalled."""
 
 
+class XgmiDivergence(XgmiTimeout):
+    """Two ranks of a data-parallel run hold different parameters after the
+    same step (:meth:`XgmiAllReduce.check_hashes`): some exchange read a
+    stale or incomplete peer value.  Retryable like a timeout (the job
+    restarts from its last checkpoint, where the ranks agreed)."""
+
+
 class XgmiAllReduce:
     def __init__(self, buf: torch.Tensor, group=None, timeout_ms: int | None = None, protocol: str | None = None):
         """``buf``: this rank's fp32 or bf16 gradient buffer (same numel on
@@ -84,6 +91,8 @@ class XgmiAllReduce:
         self._flags = fl.value
         self.epochs = torch.zeros(L.pto_ar_epoch_words(), dtype=torch.int32, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.hash_state = torch.zeros(3, dtype=torch.int64, device=self.device)  # k_param_hash: acc, ticket, seq
+        self.hashes_compared = 0
         # True if two ranks of the group share one GPU.  Their kernels then
         # compete for the same CUs, and the hardware dispatches each
         # launch's workgroups in order: a launch whose workgroups spin on a
@@ -226,20 +235,92 @@ class XgmiAllReduce:
         return (self.peers.data_ptr(), self.rank, self.world, self.epochs.data_ptr(), self.err.data_ptr(),
                 PROTOCOLS[self.protocol])
 
+    def hash_params(self, params: torch.Tensor, stream=None):
+        """Enqueue k_param_hash: a 64-bit hash of ``params`` (fp32, the same
+        layout on every rank) published with the next sequence number into
+        every rank's hash ring.  Graph-capturable (one launch)."""
+        if params.dtype != torch.float32 or not params.is_contiguous() or params.numel() % 4:
+            raise ValueError("XgmiAllReduce.hash_params: contiguous fp32 tensor, numel % 4 == 0")
+        s = (stream or torch.cuda.current_stream(self.device)).cuda_stream
+        _lib.check(_lib.lib().pto_ar_param_hash(self.peers.data_ptr(), params.data_ptr(), params.numel(), self.rank,
+                                                self.world, self.hash_state.data_ptr(), s), "ar_param_hash")
+
+    def _parse_ring(self, words) -> list[list[tuple[int, int]]]:
+        L = _lib.lib()
+        ring, nmax = L.pto_ar_hash_ring(), L.pto_ar_max_ranks()
+        w = [int(x) & 0xFFFFFFFF for x in words]
+        out = []
+        for slot in range(ring):
+            row = []
+            for q in range(self.world):
+                b = (slot * nmax + q) * 4
+                row.append((w[b] | (w[b + 1] << 32), w[b + 2] | (w[b + 3] << 32)))
+            out.append(row)
+        return out
+
+    def _read_ring(self) -> list[list[tuple[int, int]]]:
+        L = _lib.lib()
+        buf = (ctypes.c_uint32 * (L.pto_ar_hash_ring() * L.pto_ar_max_ranks() * 4))()
+        _lib.check(L.pto_ar_read_words(ctypes.c_void_p(self._flags + 4 * L.pto_ar_hash_offset_words()), buf,
+                                       len(buf)), "ar_read_words")
+        return self._parse_ring(buf)
+
+    def _ring_mismatch(self, words) -> bool:
+        for row in self._parse_ring(words.tolist()):
+            seq, h = row[self.rank]
+            if seq and any(q != self.rank and sq == seq and hq != h for q, (sq, hq) in enumerate(row)):
+                return True
+        return False
+
+    def check_hashes(self) -> int:
+        """Compare this rank's published parameter hashes with every peer's
+        for each sequence number both have published (the last
+        ``pto_ar_hash_ring()`` of them); raise :class:`XgmiDivergence` on a
+        mismatch that a re-read 2 ms later confirms.  Returns how many
+        (peer, sequence) pairs were compared.  Host-side: no collective, no
+        device synchronisation beyond the copy of the page."""
+        def mismatches(ring):
+            bad, n = [], 0
+            for row in ring:
+                seq, h = row[self.rank]
+                if seq == 0:
+                    continue
+                for q, (sq, hq) in enumerate(row):
+                    if q != self.rank and sq == seq:
+                        n += 1
+                        if hq != h:
+                            bad.append((q, seq))
+            return bad, n
+
+        bad, n = mismatches(self._read_ring())
+        if bad:
+            time.sleep(0.002)  # a peer may have been between its hash and its seq store
+            bad, n = mismatches(self._read_ring())
+        if bad:
+            raise XgmiDivergence(f"xGMI data-parallel ranks diverged: parameter hash of rank {self.rank} differs "
+                                 f"from (peer, step) {bad[:4]}")
+        self.hashes_compared += n
+        return n
+
     def error_word(self) -> int:
         """Device error word (synchronises with the current stream)."""
         return int(self.err.item())
 
-    def poll(self):
+    def poll(self, hashes: bool = False):
         """Non-blocking check: raise :class:`XgmiTimeout` for the error word
         captured by the PREVIOUS poll (by now long complete on the device),
         then enqueue a copy of the current one into pinned host memory.  A
         failure therefore surfaces one call later than with :meth:`check`,
-        but the host never waits for the device here."""
+        but the host never waits for the device here.  ``hashes``: the same
+        for the parameter-hash ring (a mismatch is confirmed by a blocking
+        :meth:`check_hashes` before it raises)."""
+        L = _lib.lib()
         if not hasattr(self, "_poll_buf"):
             self._poll_buf = torch.zeros(2, dtype=self.err.dtype, pin_memory=True)
             self._poll_ev = [None, None]
             self._poll_i = 0
+            words = L.pto_ar_hash_ring() * L.pto_ar_max_ranks() * 4
+            self._poll_ring = torch.zeros(2, words, dtype=torch.int32, pin_memory=True)
         prev = self._poll_i ^ 1
         if self._poll_ev[prev] is not None:
             self._poll_ev[prev].synchronize()
@@ -248,8 +329,16 @@ class XgmiAllReduce:
             if e:
                 raise XgmiTimeout(f"xGMI all-reduce barrier timed out after {self.timeout_ms} ms "
                                   f"(phase mask {e}): a peer rank died or stalled")
+            if hashes and self._ring_mismatch(self._poll_ring[prev]):
+                self.check_hashes()  # confirms (and raises) or clears a torn read
         i = self._poll_i
         self._poll_buf[i:i + 1].copy_(self.err.view(-1)[:1], non_blocking=True)
+        if hashes:
+            _lib.check(L.pto_ar_read_words_async(ctypes.c_void_p(self._flags + 4 * L.pto_ar_hash_offset_words()),
+                                                 ctypes.c_void_p(self._poll_ring[i].data_ptr()),
+                                                 self._poll_ring.shape[1],
+                                                 torch.cuda.current_stream(self.device).cuda_stream),
+                       "ar_read_words_async")
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
         self._poll_ev[i] = ev

@@ -169,6 +169,7 @@ class FusedMnistTrainer:
         self.lr_dev = torch.tensor([self.lr], **f32)
         self.steps_done = 0
         self._owed = False  # host view: a conv1 update may be owed (fused-opt)
+        self._eager_first = True  # the first run(1) of this trainer: eager launches, capture deferred
 
         # gradient transport (same decision on every rank)
         self._xgmi, self.comm_info = None, {"transport": "none" if self.world == 1 else "rccl"}
@@ -203,6 +204,13 @@ class FusedMnistTrainer:
         # F12's conv blocks waiting on them could hold the CUs a co-located
         # peer needs to reach its own roles (XgmiAllReduce.colocated)
         self._inline = self.overlap and not self._xgmi.colocated
+        # every captured graph ends with a hash of this rank's parameters
+        # published into every rank's flag page; run() compares them
+        # (XgmiAllReduce.check_hashes): a rank whose exchange read a stale
+        # peer value is caught within one graph, not left to diverge
+        self._hash = self._xgmi is not None and self.world > 1
+        if self._hash:
+            self.comm_info["consistency"] = "parameter hash of every rank after every captured graph"
         if self.overlap:
             self.comm_info["overlap"] = ("conv + fc all-reduce as roles of the next step's F12 launch" if self._inline
                                          else "conv + fc all-reduce roles in one launch after the backward "
@@ -473,6 +481,8 @@ class FusedMnistTrainer:
             with torch.cuda.graph(gk, capture_error_mode=_CAPTURE_MODE):
                 for i in range(k):
                     self._eager_step(first=i == 0, last=i == k - 1)
+                if self._hash:
+                    self._xgmi.hash_params(self._params)
             self._graph_pow[k] = gk
         # fused-opt: a "closing" graph per run length 1..unroll whose last
         # node commits the owed conv1 update, so run(n) needs no flush after
@@ -533,7 +543,8 @@ class FusedMnistTrainer:
         while it logs."""
         if n <= 0:
             return
-        if self.graph_mode == "full" and self._graphs is None and n == 1 and self.steps_done == 0:
+        eager_first, self._eager_first = self._eager_first, False
+        if self.graph_mode == "full" and self._graphs is None and n == 1 and eager_first:
             # the very first optimizer step runs from eager launches and the
             # capture of the step graphs (tens of them, each warm-replayed)
             # waits for the next run(): a job's first step is not queued
@@ -584,13 +595,18 @@ class FusedMnistTrainer:
         self._owed = self.fused_opt
 
     def check_comm(self, blocking: bool = True):
-        """Raise if the xGMI all-reduce reported a barrier timeout (no-op for
-        RCCL/gloo, whose failures raise from the collective itself)."""
+        """Raise if the xGMI all-reduce reported a barrier timeout, or if a
+        peer published a different parameter hash after the same graph
+        (:class:`~pytorch_operator_1_amd.parallel.xgmi.XgmiDivergence`); a
+        no-op for RCCL/gloo, whose failures raise from the collective
+        itself."""
         if self._xgmi is not None:
             if blocking:
                 self._xgmi.check()
+                if self._hash:
+                    self._xgmi.check_hashes()
             else:
-                self._xgmi.poll()
+                self._xgmi.poll(hashes=self._hash)
 
     @property
     def needs_host_barrier(self) -> bool:
@@ -655,6 +671,22 @@ class FusedMnistTrainer:
         self.lr = float(lr)
         self.lr_dev.fill_(self.lr)
 
+    def _adopt(self, other: "FusedMnistTrainer"):
+        """Take over ``other``'s training state (same model, same data): the
+        parameters, momentum, cursor, step count and lr -- a schedule race's
+        twins start where the trainer stands, and the winner continues from
+        there.  Both must have finished their work (no owed update)."""
+        other.flush()
+        torch.cuda.synchronize(self.device)
+        with torch.no_grad():
+            self._params.copy_(other._params)
+            self.mom.copy_(other.mom)
+            self.batch_idx.copy_(other.batch_idx)
+        self.steps_done = other.steps_done
+        self._eager_first = other._eager_first
+        self.set_lr(other.lr)
+        torch.cuda.synchronize(self.device)
+
     # ------------------------------------------------------------------ state
     def state_dict(self):
         """Module-style state (same keys as the reference ``Net``) plus the
@@ -687,29 +719,38 @@ def _variant(tr: FusedMnistTrainer) -> str:
     return tr.schedule + ("+overlap" if tr.overlap else "")
 
 
-def autotune_schedule(cands: list, rc: FusedMnistTrainer, verify_steps: int = 8, reps: int = 3) -> dict:
+def autotune_schedule(cands: list, rc: FusedMnistTrainer, verify_steps: int = 8, reps: int = 5,
+                      margin_us: float = 0.5) -> dict:
     """Decide between multi-GPU step variants on the steps themselves: the
-    xGMI candidates (``ddp-xgmi`` with and without the F12 overlap) and the
-    ``ddp-rccl`` reference trainer ``rc`` (same init, same data) each run
-    ``verify_steps`` captured steps; every candidate's parameters must agree
-    with the RCCL step's (max relative error per tensor <= 1e-4: different
-    summation orders) and be bit-identical on every rank.  Then each
-    replays ``reps`` of its ``unroll``-step graph, timed on the host (max
-    over ranks), and the fastest correct one is kept.  Every trainer is
-    rolled back to its initial state.  Collective: every rank calls it with
-    the same trainers in the same order."""
+    xGMI candidates (``ddp-xgmi`` with and without the F12 overlap; the
+    FIRST is the preferred one) and the ``ddp-rccl`` reference trainer
+    ``rc`` (same state, same data) each run ``verify_steps`` captured steps;
+    every candidate's parameters must agree with the RCCL step's (max
+    relative error per tensor <= 1e-4: different summation orders) and be
+    bit-identical on every rank; a candidate that stalls (XgmiTimeout) is
+    dropped.  Then ``reps`` rounds replay each correct candidate's
+    ``unroll``-step graph in turn (interleaved, so a drift of the box's
+    clock or of a peer's load hits every candidate alike), timed on the host
+    (max over ranks); the per-candidate median decides, and the preferred
+    candidate is kept unless another is faster by more than ``margin_us``
+    per step (a sub-microsecond coin flip must not pick the schedule).
+    The spread of every candidate's samples is recorded.  Every trainer is
+    rolled back to the state it had on entry.  Collective: every rank calls
+    it with the same trainers in the same order."""
+    from ..parallel.xgmi import XgmiTimeout
     from ..utils import dist as pdist
 
     dev = rc.device
     everyone = list(cands) + [rc]
     snaps = [[t.clone() for t in tr._state()] for tr in everyone]
+    steps0 = [tr.steps_done for tr in everyone]
 
     def restore():
         torch.cuda.synchronize(dev)
-        for tr, snap in zip(everyone, snaps):
+        for tr, snap, s0 in zip(everyone, snaps, steps0):
             for d, s_ in zip(tr._state(), snap):
                 d.copy_(s_)
-            tr.steps_done, tr._owed = 0, False
+            tr.steps_done, tr._owed = s0, False
         torch.cuda.synchronize(dev)
 
     def agree(flag: bool) -> bool:
@@ -717,24 +758,20 @@ def autotune_schedule(cands: list, rc: FusedMnistTrainer, verify_steps: int = 8,
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return t.item() == 1.0
 
-    def timed(tr) -> float:
+    def timed_once(tr) -> float:
         tr._align_ranks("tune-time")
-        tr.run(tr.unroll)  # warm
-        torch.cuda.synchronize(dev)
         pdist.barrier(dev)
-        tr._align_ranks("tune-time2")
         t0 = time.perf_counter()
-        tr.run(reps * tr.unroll)
+        tr.run(tr.unroll)
         torch.cuda.synchronize(dev)
-        return pdist.all_reduce_max((time.perf_counter() - t0) / (reps * tr.unroll) * 1e6, dev)
+        return pdist.all_reduce_max((time.perf_counter() - t0) / tr.unroll * 1e6, dev)
 
-    out: dict = {"verify_steps": verify_steps, "timed_steps": reps * rc.unroll, "candidates": {}}
+    out: dict = {"verify_steps": verify_steps, "timed_steps": reps * rc.unroll, "margin_us": margin_us,
+                 "candidates": {}}
     try:
         rc.run(verify_steps)
         torch.cuda.synchronize(dev)
         ok_c = []
-        from ..parallel.xgmi import XgmiTimeout
-
         for xg in cands:
             xg._align_ranks("tune-verify")
             stalled = None
@@ -756,35 +793,96 @@ def autotune_schedule(cands: list, rc: FusedMnistTrainer, verify_steps: int = 8,
             if stalled:
                 out["candidates"][_variant(xg)]["error"] = stalled
             ok_c.append(ok)
-        times = {}
-        for xg, ok in zip(cands, ok_c):
-            if ok:
-                t = timed(xg)
-                ok = agree(xg._xgmi.error_word() == 0)
-                out["candidates"][_variant(xg)].update(step_us=round(t, 2), correct=ok)
-                if ok:
-                    times[_variant(xg)] = t
-        times[_variant(rc)] = timed(rc)
-        out["candidates"][_variant(rc)] = {"step_us": round(times[_variant(rc)], 2)}
-        out["kept"] = min(times, key=times.get)
+        racers = [xg for xg, ok in zip(cands, ok_c) if ok] + [rc]
+        for tr in racers:  # warm: graphs captured and uploaded
+            tr._align_ranks("tune-warm")
+            tr.run(tr.unroll)
+            torch.cuda.synchronize(dev)
+        samples = {_variant(tr): [] for tr in racers}
+        for _ in range(reps):
+            for tr in racers:
+                samples[_variant(tr)].append(timed_once(tr))
+        for tr in racers:
+            if tr._xgmi is not None and not agree(tr._xgmi.error_word() == 0):
+                samples.pop(_variant(tr))
+                out["candidates"][_variant(tr)]["correct"] = False
+        med = {}
+        for v, xs in samples.items():
+            xs = sorted(xs)
+            med[v] = xs[len(xs) // 2]
+            out["candidates"].setdefault(v, {}).update(step_us=round(med[v], 2),
+                                                       spread_us=round(xs[-1] - xs[0], 2))
+        pref = _variant(cands[0]) if cands and _variant(cands[0]) in med else None
+        best = min(med, key=med.get)
+        out["kept"] = pref if pref is not None and med[best] >= med[pref] - margin_us else best
         out["correct"] = all(ok_c)
     finally:
         restore()
     return out
 
 
-def build_fused_trainer(device, **kw) -> FusedMnistTrainer:
-    """The fused trainer, with the multi-GPU schedule chosen on the real
-    links: at world size > 1 and ``comm="auto"`` (``PTO_COMM``), a trainer
-    whose verified xGMI all-reduce was set up (F12-overlapped) is raced
-    against a whole-buffer xGMI twin and an RCCL-schedule twin on the same
-    data (:func:`autotune_schedule`); the fastest is returned (the others'
-    peer mappings are closed) and the race is recorded in
-    ``comm_info["schedule_autotune"]``."""
-    comm = kw.get("comm") or os.environ.get("PTO_COMM", "auto")
-    tr = FusedMnistTrainer(device, **kw)
-    if tr.world == 1 or comm != "auto" or tr.schedule != "ddp-xgmi":
-        return tr
+class RacedTrainer:
+    """What :func:`build_fused_trainer` returns at world size > 1: the
+    verified overlapped xGMI trainer, whose schedule race
+    (:func:`autotune_schedule`) is DEFERRED to the start of the second
+    ``run()``/``step()``/``prepare()`` call, so a job's first optimizer step
+    is not queued behind it (submit -> first step).  The race starts from
+    the state that step left; the winner takes over that state (a copy of
+    its parameters, momentum, cursor, step count and lr) and every
+    attribute access goes to it from then on.  Collective like the trainer:
+    every rank makes the same calls."""
+
+    def __init__(self, tr: FusedMnistTrainer, kw: dict):
+        object.__setattr__(self, "_tr", tr)
+        object.__setattr__(self, "_kw", kw)
+        object.__setattr__(self, "_calls", 0)
+
+    def __getattr__(self, name):
+        return getattr(object.__getattribute__(self, "_tr"), name)
+
+    def __setattr__(self, name, value):
+        setattr(self._tr, name, value)
+
+    @property
+    def trainer(self) -> FusedMnistTrainer:
+        return self._tr
+
+    def _maybe_race(self, now: bool = False):
+        """Race on the second call (or ``now``); the first call is the job's
+        first optimizer step."""
+        if self._kw is None:
+            return
+        calls = self._calls
+        object.__setattr__(self, "_calls", calls + 1)
+        if calls == 0 and not now:
+            return
+        kw, tr = self._kw, self._tr
+        object.__setattr__(self, "_kw", None)
+        keep = _race(tr, kw)
+        if keep is not tr:
+            keep._adopt(tr)
+            object.__setattr__(self, "_tr", keep)
+
+    def run(self, n: int, blocking_check: bool = True):
+        self._maybe_race()
+        return self._tr.run(n, blocking_check)
+
+    def step(self):
+        self._maybe_race()
+        return self._tr.step()
+
+    def prepare(self):
+        """A benchmark's prepare() (after its warm-up): race now, then
+        capture, so the timed region runs the kept schedule."""
+        self._maybe_race(now=True)
+        return self._tr.prepare()
+
+
+def _race(tr: FusedMnistTrainer, kw: dict) -> FusedMnistTrainer:
+    """Build the twins of ``tr`` (whole-buffer xGMI, RCCL schedule; same
+    data), bring them to ``tr``'s state, race them (:func:`autotune_schedule`)
+    and close the losers' peer mappings.  Returns the kept trainer."""
+    device = tr.device
     data = dict(data=tr.data.view(-1, 784), target=tr.target.view(-1))
     cands = [tr]
     if tr.overlap:
@@ -792,6 +890,8 @@ def build_fused_trainer(device, **kw) -> FusedMnistTrainer:
         if plain.schedule == "ddp-xgmi":
             cands.append(plain)
     twin = FusedMnistTrainer(device, **dict(kw, comm="rccl", **data))
+    for t in cands[1:] + [twin]:
+        t._adopt(tr)
     res = autotune_schedule(cands, twin)
     everyone = cands + [twin]
     keep = next(t for t in everyone if _variant(t) == res["kept"])
@@ -807,3 +907,18 @@ def build_fused_trainer(device, **kw) -> FusedMnistTrainer:
     if keep._xgmi is None:
         keep.comm_info["xgmi_verify"] = {k: v for k, v in tr.comm_info.items() if k != "world_size"}
     return keep
+
+
+def build_fused_trainer(device, **kw):
+    """The fused trainer, with the multi-GPU schedule chosen on the real
+    links: at world size > 1 and ``comm="auto"`` (``PTO_COMM``), the
+    verified overlapped xGMI trainer is returned wrapped in a
+    :class:`RacedTrainer`, which races it against a whole-buffer xGMI twin
+    and an RCCL-schedule twin on the same data after the job's first step
+    (:func:`autotune_schedule`); the race is recorded in
+    ``comm_info["schedule_autotune"]``."""
+    comm = kw.get("comm") or os.environ.get("PTO_COMM", "auto")
+    tr = FusedMnistTrainer(device, **kw)
+    if tr.world == 1 or comm != "auto" or tr.schedule != "ddp-xgmi":
+        return tr
+    return RacedTrainer(tr, kw)

@@ -125,7 +125,7 @@ def load_data(args, device, rank):
 # restartPolicy ExitCode the survivors are recreated too and every rank
 # resumes from the latest checkpoint (kill/rejoin).
 RETRYABLE_EXIT = 138
-_COMM_ERRORS = ("XgmiTimeout", "StaleRendezvous", "host barrier", "Connection closed by peer", "Connection reset by peer", "NCCL", "RCCL", "Broken pipe",
+_COMM_ERRORS = ("XgmiTimeout", "XgmiDivergence", "StaleRendezvous", "host barrier", "Connection closed by peer", "Connection reset by peer", "NCCL", "RCCL", "Broken pipe",
                 "timed out", "Timeout", "DistBackendError", "ProcessGroup", "Gloo", "gloo")
 
 

@@ -254,6 +254,38 @@ def all_reduce_max(value: float, device: torch.device) -> float:
     return float(t.item())
 
 
+def params_fingerprint(tensors, chunk: int = 1 << 22) -> int:
+    """Exact 64-bit fingerprint of the BITS of ``tensors`` (any float
+    dtype): sum over elements of (raw bits) x (a position weight), in int64
+    arithmetic, so it is bit-exact and independent of reduction order.  Two
+    replicas of a data-parallel model agree iff (up to a negligible
+    collision chance) their parameters are bit-identical."""
+    h = 0
+    pos = 0
+    for t in tensors:
+        v = t.detach().contiguous().view(-1)
+        iv = {4: torch.int32, 2: torch.int16, 8: torch.int64, 1: torch.uint8}[v.element_size()]
+        v = v.view(iv)
+        for i in range(0, v.numel(), chunk):
+            c = v[i:i + chunk].to(torch.int64)
+            w = (torch.arange(c.numel(), device=c.device, dtype=torch.int64) + (pos + i)) % 1_000_003 + 1
+            h = (h + int((c * w).sum().item())) & 0xFFFFFFFFFFFFFFFF
+        pos += v.numel()
+    return h
+
+
+def ranks_bit_identical(tensors, device: torch.device) -> bool | None:
+    """Whether every rank holds bit-identical ``tensors`` (the data-parallel
+    replicas after a run): their fingerprints all-gathered and compared.
+    Collective; None without a process group of more than one rank."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return None
+    fp = params_fingerprint(tensors)
+    allfp = [None] * dist.get_world_size()
+    dist.all_gather_object(allfp, fp)
+    return len(set(allfp)) == 1
+
+
 def rccl_log_setup() -> str | None:
     """Route RCCL's INFO log (communicator init and transport selection
     only: no per-collective lines) to a per-process file, so the transport

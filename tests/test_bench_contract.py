@@ -32,6 +32,12 @@ def test_bench_two_ranks_cpu_json_line(sampler):
     assert d["n_gpus"] == 2 and d["steps"] == 6 and d["warmup"] == 2 and d["scaling"] == "weak"
     assert d["value"] > 0 and d["config"]["global_batch"] == 128 and d["config"]["parallelism"] == "dp2"
     assert ("DistributedSampler" in d["config"]["sampler"]) == sampler
+    # the replicas were compared after the timed steps (DDP keeps them identical)
+    assert d["ranks_bit_identical"] is True
+    # submit -> first step of a Master + Worker job through the operator stack
+    lat = d["config"]["submit_to_first_step"]
+    assert lat["replicas"] == "Master=1, Worker=1" and lat.get("job_state") == "Succeeded", lat
+    assert 0 < d["submit_to_first_step_s"] < 120, lat
 
 
 def test_bench_single_rank_reports_submit_to_first_step():
@@ -94,3 +100,20 @@ def test_bench_world_size_mismatch_is_an_error():
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
     assert out.returncode == 2 and "WORLD_SIZE=3" in out.stderr
     assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_params_fingerprint_is_bit_exact():
+    """The replica check's fingerprint: equal for equal bits, different for
+    a one-ulp change or a permutation, dtype-agnostic."""
+    import torch
+
+    from pytorch_operator_1_amd.utils.dist import params_fingerprint
+
+    a = [torch.randn(1000), torch.randn(37, 5).to(torch.bfloat16)]
+    b = [t.clone() for t in a]
+    assert params_fingerprint(a) == params_fingerprint(b)
+    b[0][17] = torch.nextafter(b[0][17], torch.tensor(float("inf")))
+    assert params_fingerprint(a) != params_fingerprint(b)
+    c = [a[0].flip(0), a[1]]
+    assert params_fingerprint(a) != params_fingerprint(c)
+    assert params_fingerprint(a, chunk=64) == params_fingerprint(a)

@@ -58,18 +58,25 @@ def _worker(rank, world, port, q, comm, steps=STEPS):
     dist.init_process_group("gloo")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    pre = 0
     if race:
-        # the schedule race of build_fused_trainer: the verified xGMI step vs
-        # the collective step on the same data, both rolled back afterwards
+        # the schedule race of build_fused_trainer, deferred past the job's
+        # first step: the verified xGMI steps vs the collective step from the
+        # state that step left, every candidate rolled back afterwards, the
+        # winner continuing from it
         tr = build_fused_trainer(dev, batch_size=64, dataset_size=N, seed=1, rank=rank, comm="auto")
+        tr.run(1)  # the first optimizer step: eager launches, no race in front of it
+        assert "schedule_autotune" not in tr.comm_info
+        tr.prepare()  # the race (a second run()/step() would start it too), then capture
+        pre = 1
         res = tr.comm_info["schedule_autotune"]
         cands = res["candidates"]
         assert res["correct"] and set(cands) == {"ddp-xgmi+overlap", "ddp-xgmi", "ddp-rccl"}, res
         for name in ("ddp-xgmi+overlap", "ddp-xgmi"):
             assert cands[name]["identical"] and cands[name]["param_rel_err"] < 1e-4, res
-        assert all(c["step_us"] > 0 for c in cands.values()), res
+        assert all(c["step_us"] > 0 and c["spread_us"] >= 0 for c in cands.values()), res
         assert res["kept"] == tr.schedule + ("+overlap" if tr.overlap else ""), res
-        assert tr.steps_done == 0 and int(tr.batch_idx.item()) == 0
+        assert tr.steps_done == 1 and int(tr.batch_idx.item()) == 1
     else:
         tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=N, seed=1, rank=rank, comm=comm)
     if race:
@@ -83,7 +90,7 @@ def _worker(rank, world, port, q, comm, steps=STEPS):
         assert tr.comm_info["correct"] is False and tr.comm_info["use_xgmi"] is False, tr.comm_info
     assert tr.comm_info["world_size"] == 2
     if steps == STEPS:
-        for _ in range(steps):
+        for _ in range(steps - pre):
             tr.step()
     else:
         tr.run(steps)  # the long run goes through the captured multi-step graphs
@@ -160,3 +167,73 @@ def _run_and_compare(comm, steps, tol):
         got = flat[off:off + t.numel()].view(shape)
         err = ((got - t.cpu()).abs().max() / t.abs().max()).item()
         assert err < tol, (name, err)
+
+
+def _diverge_worker(rank, world, port, q, flip):
+    """Self-verifying multi-GPU run: every captured graph
+    ends with a hash of the rank's parameters published into every rank's
+    flag page; run() compares them.  ``flip``: after two clean chunks rank 1
+    perturbs one parameter -- the next graph's hashes must differ and every
+    rank must raise XgmiDivergence (retryable exit 138 in the trainer CLI)."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+        import torch.distributed as dist
+
+        from pytorch_operator_1_amd.parallel.xgmi import XgmiDivergence
+        from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+        from pytorch_operator_1_amd.utils import dist as pdist
+
+        dist.init_process_group("gloo")
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=N, seed=1, rank=rank, comm="xgmi", unroll=8)
+        assert tr._hash and "consistency" in tr.comm_info
+        for _ in range(2):
+            tr.run(8)
+        compared = tr._xgmi.hashes_compared
+        detected = None
+        if flip:
+            if rank == 1:
+                with torch.no_grad():
+                    tr._params[1000] += 1e-3
+            pdist.host_barrier(tag="flip")
+            try:
+                tr.run(8)  # its last graph hashed the perturbed parameters
+            except XgmiDivergence as e:
+                detected = str(e)
+            pdist.host_barrier(tag="after")  # every rank's hash of that graph is published by now
+            if detected is None:
+                try:
+                    tr.check_comm()
+                except XgmiDivergence as e:
+                    detected = str(e)
+        else:
+            tr.run(8, blocking_check=False)
+            tr.run(8, blocking_check=False)
+            pdist.host_barrier(tag="after")
+            tr.check_comm()
+        q.put((rank, compared, detected, tr._xgmi.hashes_compared))
+        os._exit(0)  # peers may still spin on a rank that raised; the test only needs the verdicts
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), None, 0))
+        raise
+
+
+@pytest.mark.parametrize("flip", [False, True])
+def test_xgmi_ranks_self_verify_parameter_hash(flip):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_diverge_worker, args=(r, 2, port, q, flip)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = collect(q, ps, 2, timeout=110)
+    for p in ps:
+        p.join(30)
+    for rank, compared, detected, total in res:
+        assert not isinstance(compared, str), compared
+        assert compared > 0, (rank, compared)  # clean chunks: hashes of the same graphs compared, all equal
+        if flip:
+            assert detected and "diverged" in detected, (rank, detected)
+        else:
+            assert detected is None and total > compared, (rank, total)
