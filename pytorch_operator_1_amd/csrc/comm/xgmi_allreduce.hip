@@ -447,20 +447,24 @@ PTO_API int pto_ar_role_sgd(const void* peers, long long off, long long n, int r
 }
 
 // Stand-alone launch of the conv role (ar_role_oneshot_sgd: one-shot
-// all-reduce + SGD of [off, off + n), replicas folded first, the gradient
-// zeroed after the second barrier, one add to *ready per workgroup) with
+// all-reduce + SGD of [off, off + n) with the gradient replicas of
+// [rep_from, rep_from + rep_stride) at float index rep_base of the registered
+// buffer, gradient and replicas zeroed after the second barrier, one add to
+// *ready per workgroup) with
 // the decomposition it has inside the MNIST forward launch, so a rank that
 // closes a step's exchange here pairs block by block with a peer that runs
 // it inside its next forward.
 PTO_API int pto_ar_oneshot_role_sgd(const void* peers, long long off, long long n, int rank, int world, int chan,
                                     void* epochs, void* err, int protocol, float* p, float* m, const float* lr,
-                                    float mom, float wd, float gscale, int nesterov, float* rep, int nrep,
+                                    float mom, float wd, float gscale, int nesterov, long long rep_base, int nrep,
                                     int rep_stride, long long rep_from, int* ready, hipStream_t s) {
   if (n > AR_ONESHOT_MAX || n < 4 || n % 4 || off % 4 || world < 1 || world > AR_MAX_RANKS || chan < 0 ||
       chan >= AR_CHANNELS || rank < 0 || rank >= world || !p || !m || !lr || !peers || !ready || protocol < 0 ||
       protocol > 1 || ((((uintptr_t)p) | ((uintptr_t)m)) & 15))
     return -1;
-  if (rep && (nrep < 1 || nrep > AR_MAX_REP || rep_stride % 4 || rep_from % 4 || (((uintptr_t)rep) & 15)))
+  if (nrep < 1 || nrep > AR_MAX_REP || (nrep > 1 && (rep_stride % 4 || rep_from % 4 || rep_base % 4 ||
+                                                      rep_base < off + n || rep_from < off ||
+                                                      rep_from + rep_stride > off + n)))
     return -1;
   ArSgd f{};
   f.p = p;
@@ -472,10 +476,10 @@ PTO_API int pto_ar_oneshot_role_sgd(const void* peers, long long off, long long 
   f.a.nesterov = nesterov;
   f.zero_from = off;
   f.nbatches = 1;
-  f.rep = rep;
-  f.nrep = rep ? nrep : 1;
+  f.nrep = nrep;
   f.rep_stride = rep_stride;
   f.rep_from = rep_from;
+  f.rep_base = rep_base;
   const ArPeers* P = reinterpret_cast<const ArPeers*>(peers);
   const int nb = oneshot_role_blocks(n, world, AR_ROLE_THREADS);
   if (nb > AR_MAX_BLOCKS) return -1;

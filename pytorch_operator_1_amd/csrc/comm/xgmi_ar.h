@@ -102,13 +102,16 @@ __device__ __forceinline__ void st4(const Buf& b, long long i4, float4 v) {
 // FENCED: system release before the flag store, system acquire after the
 // wait; otherwise the drained write-through stores need no release and the
 // consumer's sc0 sc1 loads no acquire.
-template <bool FENCED>
+// DRAIN = false: no store of this workgroup precedes the barrier (nothing
+// to publish), so the arriving lanes do not wait for the workgroup's
+// outstanding loads -- e.g. the SGD operands prefetched just before.
+template <bool FENCED, bool DRAIN = true>
 __device__ __forceinline__ bool block_barrier(const ArPeers* __restrict__ P, int chan, int phase, int b, int rank,
                                               int world, uint32_t e, long long timeout, int* err) {
   __shared__ int s_fail[2];
   const int t = threadIdx.x;
   if (t == 0) s_fail[phase] = 0;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave: its stores acknowledged
+  if constexpr (DRAIN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave: its stores acknowledged
   __syncthreads();
   if (t < world) {
     bool dead = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
@@ -165,6 +168,9 @@ struct ArSgd {
   float* rep;
   int nrep, rep_stride;
   long long rep_from;
+  // ar_role_oneshot_sgd: the replicas live in the registered buffer itself,
+  // replica 1 at this float index (peers read them; `rep` is unused)
+  long long rep_base;
 };
 
 // Fold the local replicas into float4 element i4 (float offset 4*i4 from the
@@ -468,13 +474,18 @@ __device__ __forceinline__ void ar_role_sgd(const ArPeers* __restrict__ P, long 
 // updates -- so the exchange no longer costs a launch of its own between the
 // backward and that forward (fused_step.py, "ddp-xgmi" overlap).
 // Register-light like ar_role_sgd (the host kernel is capped at 64 VGPRs):
-// the block's NT threads are W groups of S = NT / W; block b covers elements
-// [b*S, b*S + S) of the range on every rank (same pairing on every rank), and
-// thread (q, s) loads rank q's element s into LDS.  Per workgroup:
-//   q = 0      prefetch its own parameter/momentum float4; fold this rank's
-//              gradient replicas into its gradient element (write-through)
-//   barrier 0  every peer's (folded) gradient is complete
-//   stage 1    every rank's element into LDS; q = 0 sums them in rank order
+// the block's NT threads are W groups of S = NT / W; block b covers float4
+// groups [b*S, b*S + S) of the range on every rank (same pairing on every
+// rank), and thread (q, s) reads rank q's group s.  Per workgroup:
+//   barrier 0  every peer's backward has ended (its gradient is complete).
+//              Nothing is stored before it, so the lanes arrive at once
+//              (no drain) while the SGD operands are being loaded.
+//   stage 1    thread (q, s) loads rank q's gradient group and, inside the
+//              replicated range (rep_off: the gradient replicas of the
+//              backward's atomics live in the SAME registered buffer, replica
+//              r >= 1 at rep_off + (r-1)*rep_stride), rank q's replicas,
+//              summed in replica order -- no local fold store and no drain
+//              before the barrier; q = 0 sums the W values in rank order
 //              (bit-identical on every rank), applies SGD, stores the
 //              parameter WRITE-THROUGH (system scope: the waiting conv
 //              workgroups on other XCDs read it with system-scope loads; no
@@ -484,15 +495,16 @@ __device__ __forceinline__ void ar_role_sgd(const ArPeers* __restrict__ P, long 
 //              ONE agent-scope add to *ready.  Done on failure too (nothing
 //              was written then and *err is set), so the waiting conv
 //              workgroups are always released and the grid drains.
-//   barrier 1  every peer has read this rank's gradient
-//   q = 0      zero this rank's gradient element: the next backward
-//              accumulates into it (a run() ends with zero conv gradients)
-// Hazards: a rank writes its gradient range only in the fold (before its
-// barrier-0 arrival) and in the zeroing (after barrier 1, i.e. after every
-// peer's stage-1 read of this call).  The conv workgroups read the updated
-// parameters only after *ready counts every role workgroup; the next writer
-// of those parameters is the next call of this role, a later launch.
-// *ready is reset by a later launch of the same step (the MNIST F4dx launch).
+//   barrier 1  every peer has read this rank's gradient and replicas
+//   q = 0      zero this rank's gradient group and its replicas: the next
+//              backward accumulates into them (a run() ends with zero conv
+//              gradients)
+// Hazards: a rank writes its gradient range and replicas only after
+// barrier 1 (every peer's stage-1 read of this call is done).  The conv
+// workgroups read the updated parameters only after *ready counts every
+// role workgroup; the next writer of those parameters is the next call of
+// this role, a later launch.  *ready is reset by a later launch of the same
+// step (the MNIST F4dx launch).
 template <bool FENCED, int NT>
 __device__ __forceinline__ void ar_role_oneshot_sgd(const ArPeers* __restrict__ P, long long off, long long n4,
                                                     int rank, int world, int chan, uint32_t* __restrict__ epochs,
@@ -508,34 +520,47 @@ __device__ __forceinline__ void ar_role_oneshot_sgd(const ArPeers* __restrict__ 
   const int q = threadIdx.x / S, sidx = threadIdx.x - q * S;
   const long long j = (long long)blk * S + sidx;
   const bool valid = q < world && j < n4;
-  const bool own = q == 0 && valid;  // this thread updates element j
-  const long long bytes = n4 * 16;
-  float* const my_in = P->in[rank];
+  const bool own = q == 0 && valid;  // this thread updates element group j
+  // replicated range: [f.rep_from, f.rep_from + rep_stride) (float index)
+  const long long fi = off + 4 * j;
+  const bool repl = valid && f.nrep > 1 && fi >= f.rep_from && fi < f.rep_from + f.rep_stride;
+  const long long rep_base = f.rep_base;
+  const long long span = f.nrep > 1 ? rep_base + (long long)(f.nrep - 1) * f.rep_stride : off + 4 * n4;
   float4 pv = {0.f, 0.f, 0.f, 0.f}, mv = {0.f, 0.f, 0.f, 0.f};
   float lr = 0.f;
   if (own) {
-    // fold first (its 7 replica loads in one round), then the SGD operands,
-    // whose loads overlap the barrier
-    if (f.rep && f.nrep > 1 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-      fold_rep<CO, 8>(f, mkbuf(my_in + off, bytes), off, j);
-    pv = gld4(f.p + off + 4 * j);
-    mv = gld4(f.m + off + 4 * j);
+    pv = gld4(f.p + fi);
+    mv = gld4(f.m + fi);
     lr = *f.a.lr;
   }
-  const bool ok = block_barrier<FENCED>(P, chan, 0, blk, rank, world, e, timeout, err);
+  const bool ok = block_barrier<FENCED, false>(P, chan, 0, blk, rank, world, e, timeout, err);
   if (ok) {
-    if (valid) lds[q * S + sidx] = ld4<CO>(mkbuf(P->in[q] + off, bytes), j);
+    if (valid) {
+      const Buf g = mkbuf(P->in[q], span * 4);
+      float4 a = ld4<CO>(g, fi / 4);
+      if (repl) {
+        const long long k4 = (rep_base + (fi - f.rep_from)) / 4, st4 = f.rep_stride / 4;
+        for (int r0 = 0; r0 < f.nrep - 1; r0 += 8) {  // replica order, 8 loads in flight
+          float4 v[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] = ld4<CO>(g, k4 + (long long)min(r0 + r, f.nrep - 2) * st4);
+#pragma unroll
+          for (int r = 0; r < 8; ++r)
+            if (r0 + r < f.nrep - 1) a = add4(a, v[r]);
+        }
+      }
+      lds[q * S + sidx] = a;
+    }
     __syncthreads();
     if (own) {
       float4 a = lds[sidx];
       for (int r = 1; r < world; ++r) a = add4(a, lds[r * S + sidx]);
-      const long long i = off + 4 * j;
       sgd_elem(pv.x, a.x, mv.x, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
       sgd_elem(pv.y, a.y, mv.y, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
       sgd_elem(pv.z, a.z, mv.z, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
       sgd_elem(pv.w, a.w, mv.w, lr, f.a.mom, f.a.wd, f.a.gscale, f.a.nesterov);
-      st4<true>(mkbuf(f.p + off, bytes), j, pv);
-      gst4(f.m + i, mv);
+      st4<true>(mkbuf(f.p + off, n4 * 16), j, pv);
+      gst4(f.m + fi, mv);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave: its parameter stores acknowledged
@@ -543,7 +568,13 @@ __device__ __forceinline__ void ar_role_oneshot_sgd(const ArPeers* __restrict__ 
   if (threadIdx.x == 0) __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (!ok) return;
   if (!block_barrier<FENCED>(P, chan, 1, blk, rank, world, e, timeout, err)) return;
-  if (own) gst4(my_in + off + 4 * j, float4{0.f, 0.f, 0.f, 0.f});
+  if (own) {
+    float* const my = P->in[rank];
+    gst4(my + fi, float4{0.f, 0.f, 0.f, 0.f});
+    if (repl)
+      for (int r = 0; r < f.nrep - 1; ++r)
+        gst4(my + rep_base + (long long)r * f.rep_stride + (fi - f.rep_from), float4{0.f, 0.f, 0.f, 0.f});
+  }
 }
 __host__ __device__ inline int oneshot_role_blocks(long long n, int world, int nt) {
   const long long S = nt / world;

@@ -2065,9 +2065,11 @@ extern "C" long long pto_ar_timeout_ticks();
 // (protocol: 0 coherent, 1 fenced -- the one the XgmiAllReduce instance of
 // `peers` uses; shared peers table, epochs and error word):
 //   conv role  one-shot all-reduce + SGD of [cv_off, cv_off + cv_n) on
-//              channel cv_chan, gradient replicas rep (nrep, rep_stride,
-//              from float index rep_from) folded first, gradient zeroed after
-//              its second barrier; the conv blocks wait on *ready
+//              channel cv_chan; the gradient replicas of [rep_from, rep_from
+//              + rep_stride) are part of the registered buffer (replica r >=
+//              1 at float index rep_base + (r-1)*rep_stride) and every rank
+//              reads every rank's; gradient and replicas zeroed after its
+//              second barrier; the conv blocks wait on *ready
 //   fc role    rank-split all-reduce + SGD of [fc_off, fc_off + fc_n) on
 //              channel fc_chan, local gradient zeroed from fc_zero_from
 // B == 0: the two roles alone (the closing exchange of a captured run).
@@ -2076,15 +2078,17 @@ PTO_API int pto_conv12_fwd_ar(const float* x, const float* w1, const float* b1, 
                               float* xout, const void* peers, int rank, int world, void* epochs, void* err,
                               int protocol, float* p, float* m, const float* lr, float mom, float wd, float gscale,
                               int nesterov, long long fc_off, long long fc_n, int fc_chan, long long fc_zero_from,
-                              long long cv_off, long long cv_n, int cv_chan, float* rep, int nrep, int rep_stride,
-                              long long rep_from, int* ready, hipStream_t s) {
+                              long long cv_off, long long cv_n, int cv_chan, long long rep_base, int nrep,
+                              int rep_stride, long long rep_from, int* ready, hipStream_t s) {
   using namespace pto_ar;
   if (fc_n <= AR_ONESHOT_MAX || fc_n % 4 || fc_off % 4 || fc_n > (1LL << 29) || cv_n > AR_ONESHOT_MAX || cv_n < 4 ||
       cv_n % 4 || cv_off % 4 || world < 1 || world > AR_MAX_RANKS || fc_chan < 0 || fc_chan >= AR_CHANNELS ||
       cv_chan < 0 || cv_chan >= AR_CHANNELS || fc_chan == cv_chan || rank < 0 || rank >= world || !p || !m || !lr ||
       !peers || !ready || protocol < 0 || protocol > 1 || B < 0 || ((((uintptr_t)p) | ((uintptr_t)m)) & 15))
     return -1;
-  if (rep && (nrep < 1 || nrep > AR_MAX_REP || rep_stride % 4 || rep_from % 4 || (((uintptr_t)rep) & 15)))
+  if (nrep < 1 || nrep > AR_MAX_REP || (nrep > 1 && (rep_stride % 4 || rep_from % 4 || rep_base % 4 ||
+                                                      rep_base < cv_off + cv_n || rep_from < cv_off ||
+                                                      rep_from + rep_stride > cv_off + cv_n)))
     return -1;
   LazyConv1 lz{nullptr, nullptr, nullptr, sgd_args(lr, mom, wd, gscale, nesterov), 0, xout, nullptr, nullptr, 1, 0};
   ArRole ar{}, cv{};
@@ -2113,10 +2117,10 @@ PTO_API int pto_conv12_fwd_ar(const float* x, const float* w1, const float* b1, 
   cv.chan = cv_chan;
   cv.nblk = oneshot_role_blocks(cv_n, world, 1024);
   cv.f.zero_from = cv_off;
-  cv.f.rep = rep;
-  cv.f.nrep = rep ? nrep : 1;
+  cv.f.nrep = nrep;
   cv.f.rep_stride = rep_stride;
   cv.f.rep_from = rep_from;
+  cv.f.rep_base = rep_base;
   if (ar.nblk > AR_MAX_BLOCKS || cv.nblk > AR_MAX_BLOCKS) return -1;
   const dim3 g((unsigned)(B * 4 + ar.nblk + cv.nblk));
   if (protocol)

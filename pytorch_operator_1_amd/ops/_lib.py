@@ -100,7 +100,7 @@ _SIGS = {
     # fused-optimizer schedule of the single-process MNIST step
     "pto_conv12_fwd_lazy_x": [_P] * 9 + [_I, _P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _P, _P, _P, _I, _I, _P],
     "pto_conv12_fwd_ar": [_P] * 9 + [_I, _P, _P, _P, _I, _I, _P, _P, _I, _P, _P, _P, _F, _F, _F, _I,
-                                     _L, _L, _I, _L, _L, _L, _I, _P, _I, _I, _L, _P, _P],
+                                     _L, _L, _I, _L, _L, _L, _I, _L, _I, _I, _L, _P, _P],
     "pto_synth_mnist": [_P, _P, _L, ctypes.c_ulonglong, _P],
     "pto_bwd_all": [_P] * 13 + [_L] * 8 + [_P, _P, _L, _P, _I, _P, _F, _F, _F, _I, _P, _I, _I, _I, _P, _P],
     "pto_conv1_commit": [_P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _P, _I, _I, _P],
@@ -163,7 +163,7 @@ _SIGS = {
     "pto_ar_timeout_ticks": [],
     "pto_ar_allreduce_bf16": [_P, _L, _L, _I, _I, _I, _P, _P, _P],
     "pto_ar_role_sgd": [_P, _L, _L, _I, _I, _I, _P, _P, _I, _P, _P, _P, _F, _F, _F, _I, _L, _P],
-    "pto_ar_oneshot_role_sgd": [_P, _L, _L, _I, _I, _I, _P, _P, _I, _P, _P, _P, _F, _F, _F, _I, _P, _I, _I, _L, _P,
+    "pto_ar_oneshot_role_sgd": [_P, _L, _L, _I, _I, _I, _P, _P, _I, _P, _P, _P, _F, _F, _F, _I, _L, _I, _I, _L, _P,
                                 _P],
     "pto_ar_oneshot_role_blocks": [_L, _I],
     "pto_ar_allreduce_sgd": [_P, _L, _L, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _F, _I, _L, _P, _L, _P, _I, _I, _L,

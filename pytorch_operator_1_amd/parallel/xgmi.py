@@ -178,8 +178,8 @@ class XgmiAllReduce:
         the gradient layout) inside the same launch; the local gradient is
         zeroed from ``zero_from`` on and ``cursor`` (int64 device scalar) is
         advanced mod ``n_batches`` after the update.  ``replicas``: extra
-        local copies of the gradient range ``[rep_from, numel)`` (replica r
-        >= 1 at ``replicas[(r-1)*(numel-rep_from):]``), folded into the
+        local copies of the gradient range ``[rep_from, params.numel())``
+        (replica r >= 1 at ``replicas[(r-1)*(params.numel()-rep_from):]``), folded into the
         gradient and zeroed before the exchange."""
         if self.align != 4:
             raise ValueError("XgmiAllReduce: the SGD epilogue needs an fp32 buffer")
@@ -188,11 +188,11 @@ class XgmiAllReduce:
         if offset + n > self.buf.numel():
             raise ValueError("XgmiAllReduce: range outside the registered buffer")
         for t in (params, mom):
-            if t.dtype != torch.float32 or t.numel() != self.buf.numel() or t.device != self.device:
-                raise ValueError("XgmiAllReduce: params/momentum must match the gradient buffer")
+            if t.dtype != torch.float32 or t.numel() < offset + n or t.device != self.device:
+                raise ValueError("XgmiAllReduce: params/momentum must cover the range (gradient layout)")
         s = (stream or torch.cuda.current_stream(self.device)).cuda_stream
         cur = cursor.data_ptr() if cursor is not None else None
-        rep_stride = self.buf.numel() - rep_from
+        rep_stride = params.numel() - rep_from  # the replicated range runs to the end of the gradient layout
         rep = None
         if replicas is not None and n_replicas > 1:
             if replicas.numel() < (n_replicas - 1) * rep_stride or replicas.device != self.device:
@@ -223,10 +223,11 @@ class XgmiAllReduce:
     def update_args(self, params: torch.Tensor, mom: torch.Tensor, lr_dev: torch.Tensor, momentum: float,
                     weight_decay: float, gscale: float, nesterov: bool) -> tuple:
         """(params, momentum, lr pointer, momentum, weight decay, grad scale,
-        nesterov) of an SGD epilogue, checked against the gradient buffer."""
+        nesterov) of an SGD epilogue, in the gradient layout (the registered
+        buffer may extend past them: e.g. gradient replicas)."""
         for t in (params, mom):
-            if t.dtype != torch.float32 or t.numel() != self.buf.numel() or t.device != self.device:
-                raise ValueError("XgmiAllReduce: params/momentum must match the gradient buffer")
+            if t.dtype != torch.float32 or t.numel() > self.buf.numel() or t.device != self.device:
+                raise ValueError("XgmiAllReduce: params/momentum must be fp32 in the gradient layout")
         return (params.data_ptr(), mom.data_ptr(), lr_dev.data_ptr(), momentum, weight_decay, gscale, int(nesterov))
 
     def exchange_args(self) -> tuple:

@@ -117,7 +117,16 @@ class FusedMnistTrainer:
         self.numel = total
         f32 = dict(device=device, dtype=torch.float32)
         self._params = torch.zeros(total, **f32)
-        self.grads = torch.zeros(total, **f32)
+        # gradients + the conv1 replica tail in ONE allocation: the RCCL
+        # schedule all-reduces both in one message; the xGMI exchange
+        # registers both, so peers read each other's replicas directly (no
+        # fold on the exchange's critical path)
+        self.c1_nrep = B if self.deterministic else C1_REPLICAS
+        self.c1_stride = total - offs["conv1.weight"][0]
+        nrep_tail = max(1, self.c1_nrep - 1) * self.c1_stride
+        self._ar_buf = torch.zeros(total + nrep_tail, **f32)
+        self.grads = self._ar_buf[:total]
+        self.c1rep = self._ar_buf[total:]
         self.mom = torch.zeros(total, **f32)
         self._p, self.g = {}, {}
         for name, (off, shape) in offs.items():
@@ -178,12 +187,10 @@ class FusedMnistTrainer:
         if self.deterministic and self.ddp and self._xgmi is None:
             raise RuntimeError("PTO_DETERMINISTIC=1 with DDP needs the xGMI all-reduce (its SGD epilogue folds the "
                                "per-sample conv1 replicas in order)")
-        # conv1 replicas: fused-opt readers and the xGMI epilogue fold them
-        # locally; on the RCCL schedule they are a tail of the gradient
-        # allocation, all-reduced with it in one message and folded by the
-        # optimizer launch (k_ddp_sgd)
-        self.c1_nrep = B if self.deterministic else C1_REPLICAS
-        self.c1_stride = self.numel - self._c1
+        # conv1 replicas (the tail of _ar_buf): fused-opt readers and the
+        # whole-buffer xGMI epilogue fold them locally; the overlapped xGMI
+        # exchange reads every rank's; the RCCL schedule all-reduces them
+        # with the gradients and folds them in the optimizer launch
         self.schedule = "fused-opt" if not self.ddp else ("ddp-xgmi" if self._xgmi is not None else "ddp-rccl")
         # ddp-xgmi overlap: step k's all-reduce is split at the fc | conv
         # boundary and BOTH parts run as roles of step k+1's F12 launch:
@@ -215,16 +222,6 @@ class FusedMnistTrainer:
             self.comm_info["overlap"] = ("conv + fc all-reduce as roles of the next step's F12 launch" if self._inline
                                          else "conv + fc all-reduce roles in one launch after the backward "
                                               "(ranks share a GPU)")
-        nrep_tail = max(1, self.c1_nrep - 1) * self.c1_stride
-        if self.schedule == "ddp-rccl":
-            self._ar_buf = torch.zeros(total + nrep_tail, **f32)
-            self.grads = self._ar_buf[:total]
-            for name, (off, shape) in offs.items():
-                self.g[name] = self.grads[off:off + math.prod(shape)].view(shape)
-            self.c1rep = self._ar_buf[total:]
-        else:
-            self._ar_buf = self.grads
-            self.c1rep = torch.zeros(nrep_tail, **f32)
 
         # graph modes: "full" = whole steps (collectives included) in HIP
         # graphs; "split" = the collective issued between two graphs (a
@@ -248,7 +245,7 @@ class FusedMnistTrainer:
         from ..parallel.xgmi import XgmiAllReduce
 
         try:
-            ar = XgmiAllReduce(self.grads)
+            ar = XgmiAllReduce(self._ar_buf)
         except (RuntimeError, ValueError) as e:  # collective failure: every rank raises
             if self.comm == "xgmi":
                 raise
@@ -355,7 +352,7 @@ class FusedMnistTrainer:
             *x.exchange_args(), *x.update_args(self._params, self.mom, self.lr_dev, mom, wd, gs, bool(nes)),
             0, self._split, FC_CHAN, self.numel,
             self._split, self.numel - self._split, CONV_CHAN,
-            self.c1rep.data_ptr(), self.c1_nrep, self.c1_stride, self._c1, self._ready.data_ptr(), self._s()),
+            self.numel, self.c1_nrep, self.c1_stride, self._c1, self._ready.data_ptr(), self._s()),
             "conv12_fwd_ar" if B else "exchange_close")
 
     def _close_exchange(self):

@@ -213,6 +213,8 @@ def _diverge_worker(rank, world, port, q, flip):
             pdist.host_barrier(tag="after")
             tr.check_comm()
         q.put((rank, compared, detected, tr._xgmi.hashes_compared))
+        q.close()
+        q.join_thread()  # the verdict is flushed to the parent before the hard exit
         os._exit(0)  # peers may still spin on a rank that raised; the test only needs the verdicts
     except Exception as e:  # noqa: BLE001
         q.put((rank, repr(e), None, 0))

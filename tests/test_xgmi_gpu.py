@@ -472,9 +472,10 @@ def test_xgmi_allreduce_uneven_load():
 
 def _overlap_pair_worker(rank, world, port, q):
     """The overlapped MNIST step's exchange at any world size: the one-shot
-    rank-split conv role (channel 2: replicas folded, all-reduce + SGD,
-    parameter written through, one publish per workgroup, gradient and
-    replicas zeroed after its second barrier) and the rank-split fc role
+    rank-split conv role (channel 2: every rank's gradient AND replicas
+    read from the registered buffer and summed, all-reduce + SGD, parameter
+    written through, one publish per workgroup, gradient and replicas
+    zeroed after its second barrier) and the rank-split fc role
     (channel 1, barrier 0 of its own).  Even ranks run both roles as ONE
     launch (the MNIST forward launch with no conv blocks, as a run's
     closing exchange), odd ranks as two stand-alone launches: the
@@ -497,10 +498,10 @@ def _overlap_pair_worker(rank, world, port, q):
         stride, nrep = 576, 4  # replicated tail (MNIST: conv1, 8 replicas)
         rep_from = n - stride
         lr, mom, wd = 0.05, 0.9, 1e-3
-        buf = torch.zeros(n, device=dev)
-        rep = torch.zeros((nrep - 1) * stride, device=dev)
+        full = torch.zeros(n + (nrep - 1) * stride, device=dev)  # gradients + replicas, registered together
+        buf, rep = full[:n], full[n:]
         ready = torch.zeros(1, dtype=torch.int32, device=dev)
-        ar = XgmiAllReduce(buf, timeout_ms=20000)
+        ar = XgmiAllReduce(full, timeout_ms=20000)
         p = torch.randn(n, generator=torch.Generator(device=dev).manual_seed(7), device=dev)
         m = torch.zeros(n, device=dev)
         pr, mr = p.clone(), m.clone()
@@ -522,12 +523,12 @@ def _overlap_pair_worker(rank, world, port, q):
             upd = ar.update_args(p, m, lr_dev, mom, wd, 1.0 / world, True)
             if rank % 2 == 0:
                 _lib.check(L.pto_conv12_fwd_ar(*([None] * 9), 0, None, None, *ar.exchange_args(), *upd,
-                                               0, nfc, 1, n, nfc, nconv, 2, rep.data_ptr(), nrep, stride, rep_from,
+                                               0, nfc, 1, n, nfc, nconv, 2, n, nrep, stride, rep_from,
                                                ready.data_ptr(), s), "conv12_fwd_ar(B=0)")
             else:
                 _lib.check(L.pto_ar_oneshot_role_sgd(*ar.role_args(nfc, nconv, 2, p, m, lr_dev, mom, wd,
                                                                    1.0 / world, True, n)[:-1],
-                                                     rep.data_ptr(), nrep, stride, rep_from, ready.data_ptr(), s),
+                                                     n, nrep, stride, rep_from, ready.data_ptr(), s),
                            "ar_oneshot_role_sgd")
                 _lib.check(L.pto_ar_role_sgd(*ar.role_args(0, nfc, 1, p, m, lr_dev, mom, wd, 1.0 / world, True, n),
                                              s), "ar_role_sgd")
