@@ -275,6 +275,8 @@ PTO_API long long pto_ar_timeout_ticks() { return g_timeout_ticks; }
 
 // Flags: uncached device memory, zeroed.
 PTO_API int pto_ar_alloc_flags(void** out) {
+  // (ordinary device memory measured the same barrier latency at world 1:
+  // profiles/exchange_r5.md)
   hipError_t e = hipExtMallocWithFlags(out, (size_t)AR_PAGE_WORDS * sizeof(uint32_t), hipDeviceMallocUncached);
   if (e != hipSuccess) return (int)e;
   return (int)hipMemset(*out, 0, (size_t)AR_PAGE_WORDS * sizeof(uint32_t));

@@ -13,6 +13,14 @@
 
 #include "sgd_f32.h"
 
+// Phase timestamps for the timing probes under tools/probes (which define
+// PTO_STAMP before including the kernel sources); nothing in the shipped
+// library.
+#ifndef PTO_STAMP
+#define PTO_STAMP(k) ((void)0)
+#define PTO_STAMP_SCOPE()
+#endif
+
 namespace pto_ar {
 
 constexpr int AR_MAX_RANKS = 8;
@@ -105,16 +113,20 @@ __device__ __forceinline__ void st4(const Buf& b, long long i4, float4 v) {
 // DRAIN = false: no store of this workgroup precedes the barrier (nothing
 // to publish), so the arriving lanes do not wait for the workgroup's
 // outstanding loads -- e.g. the SGD operands prefetched just before.
+// err0 >= 0: the caller's copy of *err (loaded with its other operands at
+// entry), so the arriving lanes store their flag without a round trip to
+// *err first; a failure of another workgroup since then is still seen in
+// the wait loop.
 template <bool FENCED, bool DRAIN = true>
 __device__ __forceinline__ bool block_barrier(const ArPeers* __restrict__ P, int chan, int phase, int b, int rank,
-                                              int world, uint32_t e, long long timeout, int* err) {
+                                              int world, uint32_t e, long long timeout, int* err, int err0 = -1) {
   __shared__ int s_fail[2];
   const int t = threadIdx.x;
   if (t == 0) s_fail[phase] = 0;
   if constexpr (DRAIN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave: its stores acknowledged
   __syncthreads();
   if (t < world) {
-    bool dead = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    bool dead = (err0 >= 0 ? err0 : __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0;
     if (!dead) {
       if constexpr (FENCED) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back this XCD's L2
@@ -124,14 +136,19 @@ __device__ __forceinline__ bool block_barrier(const ArPeers* __restrict__ P, int
                          __HIP_MEMORY_SCOPE_SYSTEM);
       gu32* f = G(P->flags[rank] + flag_index(chan, phase, b, t));
       const long long t0 = wall_clock64();
-      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
-        if (wall_clock64() - t0 > timeout) {
-          atomicOr(err, 1 << phase);
+      for (;;) {
+        // the flag and the error word in flight together: one round trip
+        // per poll
+        const uint32_t v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const int ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v == e) break;
+        // another block (or an earlier launch) already gave up: stop now
+        if (ev != 0) {
           dead = true;
           break;
         }
-        // another block (or an earlier launch) already gave up: stop now
-        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+        if (wall_clock64() - t0 > timeout) {
+          atomicOr(err, 1 << phase);
           dead = true;
           break;
         }
@@ -148,6 +165,49 @@ __device__ __forceinline__ bool block_barrier(const ArPeers* __restrict__ P, int
   }
   __syncthreads();
   return s_fail[phase] == 0;
+}
+
+// The waiting half of a barrier whose arrival was an atomic INCREMENT of
+// every peer's flag slot (not a store of the epoch): the arrival needs no
+// epoch and no error word, so it goes out at workgroup entry; the slot's
+// count equals the epoch as long as every call of the channel arrives this
+// way.  Lanes < world poll their source's slot until it reaches e.
+template <bool FENCED>
+__device__ __forceinline__ bool block_wait(const ArPeers* __restrict__ P, int chan, int phase, int b, int rank,
+                                           int world, uint32_t e, long long timeout, int* err) {
+  __shared__ int s_failw;
+  const int t = threadIdx.x;
+  if (t == 0) s_failw = 0;
+  __syncthreads();
+  if (t < world) {
+    bool dead = false;
+    gu32* f = G(P->flags[rank] + flag_index(chan, phase, b, t));
+    const long long t0 = wall_clock64();
+    for (;;) {
+      const uint32_t v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const int ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v == e) break;
+      if (ev != 0) {
+        dead = true;
+        break;
+      }
+      if (wall_clock64() - t0 > timeout) {
+        atomicOr(err, 1 << phase);
+        dead = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if constexpr (FENCED) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (dead) s_failw = 1;
+  }
+  __syncthreads();
+  return s_failw == 0;
 }
 
 // Fused optimizer epilogue of the all-reduce: own parameters/momentum (same
@@ -436,7 +496,9 @@ __device__ __forceinline__ void ar_role_sgd(const ArPeers* __restrict__ P, long 
   // under the coherent protocol because a stand-alone conv exchange always
   // preceded this role; the conv exchange now runs NEXT TO it, as
   // ar_role_oneshot_sgd in the same launch, so nothing else orders it.)
-  if (!block_barrier<FENCED>(P, chan, 0, blk, rank, world, e, timeout, err)) return;
+  // Nothing is stored before it: no drain, and *err was read at entry.
+  const int err0 = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!block_barrier<FENCED, false>(P, chan, 0, blk, rank, world, e, timeout, err, err0)) return;
   // stage 1: my chunk's element j from rank q -> LDS, then rank-order sums
   const long long i1 = (long long)rank * cs + j;
   const bool v1 = in_group && j < cs && i1 < n4;
@@ -478,8 +540,10 @@ __device__ __forceinline__ void ar_role_sgd(const ArPeers* __restrict__ P, long 
 // groups [b*S, b*S + S) of the range on every rank (same pairing on every
 // rank), and thread (q, s) reads rank q's group s.  Per workgroup:
 //   barrier 0  every peer's backward has ended (its gradient is complete).
-//              Nothing is stored before it, so the lanes arrive at once
-//              (no drain) while the SGD operands are being loaded.
+//              Nothing of this call precedes it, so the lanes arrive at
+//              workgroup entry by an atomic increment of every peer's slot
+//              (no drain, no epoch read first) and wait while the epoch and
+//              the SGD operands are being loaded.
 //   stage 1    thread (q, s) loads rank q's gradient group and, inside the
 //              replicated range (rep_off: the gradient replicas of the
 //              backward's atomics live in the SAME registered buffer, replica
@@ -511,6 +575,14 @@ __device__ __forceinline__ void ar_role_oneshot_sgd(const ArPeers* __restrict__ 
                                                     int* err, long long timeout, const ArSgd& f, int blk,
                                                     float4* lds, int* ready) {
   constexpr bool CO = !FENCED;
+  // barrier 0 arrival first thing: nothing of this call precedes it (the
+  // gradient it announces was written by the previous launch), so no drain,
+  // no epoch and no error word are needed to send it (block_wait).  A rank
+  // whose exchange already failed still announces its raw gradient; it is
+  // absent from barrier 1, where its peers then fail too.
+  if (threadIdx.x < world)
+    __hip_atomic_fetch_add(G(P->flags[threadIdx.x] + flag_index(chan, 0, blk, rank)), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
   __shared__ uint32_t s_epoch;
   if (threadIdx.x == 0) s_epoch = epochs[chan * AR_MAX_BLOCKS + blk] + 1;
   __syncthreads();
@@ -533,7 +605,8 @@ __device__ __forceinline__ void ar_role_oneshot_sgd(const ArPeers* __restrict__ 
     mv = gld4(f.m + fi);
     lr = *f.a.lr;
   }
-  const bool ok = block_barrier<FENCED, false>(P, chan, 0, blk, rank, world, e, timeout, err);
+  const bool ok = block_wait<FENCED>(P, chan, 0, blk, rank, world, e, timeout, err);
+  PTO_STAMP(1);
   if (ok) {
     if (valid) {
       const Buf g = mkbuf(P->in[q], span * 4);
@@ -563,11 +636,14 @@ __device__ __forceinline__ void ar_role_oneshot_sgd(const ArPeers* __restrict__ 
       gst4(f.m + fi, mv);
     }
   }
+  PTO_STAMP(2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave: its parameter stores acknowledged
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  PTO_STAMP(3);
   if (!ok) return;
   if (!block_barrier<FENCED>(P, chan, 1, blk, rank, world, e, timeout, err)) return;
+  PTO_STAMP(4);
   if (own) {
     float* const my = P->in[rank];
     gst4(my + fi, float4{0.f, 0.f, 0.f, 0.f});

@@ -353,13 +353,16 @@ struct ParamView {
 // workgroup publishes even on failure, so the spin ends in every case.
 PTO_DEV void wait_conv_role(const ArRole& cv) {
   const long long t0 = wall_clock64();
-  while (__hip_atomic_load(cv.ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < cv.nblk) {
-    if (__hip_atomic_load(cv.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+  for (;;) {
+    // the counter and the error word in flight together: one round trip per poll
+    const int r = __hip_atomic_load(cv.ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int ev = __hip_atomic_load(cv.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (r >= cv.nblk || ev != 0) break;
     if (wall_clock64() - t0 > cv.timeout) {
       atomicOr(cv.err, 16);
       break;
     }
-    __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_s_sleep(1);
   }
 }
 constexpr int W1PLD = 52;  // a channel pair's 25 interleaved taps, padded to whole float4
@@ -375,6 +378,7 @@ __global__ __launch_bounds__(NTH, ARM ? 2 * NTH / 256 : 1) void k_conv12_fwd2_t(
   int bx = (int)blockIdx.x;
   if constexpr (ARM != 0) {
     if (bx < cv.nblk + ar.nblk) {
+      PTO_STAMP_SCOPE();
       __shared__ float4 ar_lds[NTH];
       if (bx < cv.nblk)
         pto_ar::ar_role_oneshot_sgd<ARM == 2, NTH>(cv.peers, cv.off, cv.n4, cv.rank, cv.world, cv.chan, cv.epochs,
@@ -406,6 +410,7 @@ __global__ __launch_bounds__(NTH, ARM ? 2 * NTH / 256 : 1) void k_conv12_fwd2_t(
     if constexpr (ARM != 0) {
       if (tid == 0) wait_conv_role(cv);
       __syncthreads();
+      PTO_STAMP(5);
     }
     const int nrows = min(16, C2 - nt * 16);
     const ParamView<SYS> wsrc(w2 + nt * 16 * 500, nrows * 500);

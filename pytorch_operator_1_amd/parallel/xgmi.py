@@ -372,8 +372,9 @@ class XgmiAllReduce:
             torch.cuda.synchronize(self.device)
             for off, n in ranges:
                 bad = max(bad, (self.buf[off:off + n].float() - ref[off:off + n]).abs().max().item() / scale)
-            # every rank must hold identical values (fixed summation order)
-            mine = self.buf.float()
+            # every rank must hold identical values in the reduced ranges
+            # (fixed summation order); the rest of the buffer is per-rank
+            mine = torch.cat([self.buf[off:off + n].float() for off, n in ranges])
             chk = mine.clone()
             dist.all_reduce(chk, op=dist.ReduceOp.MAX, group=self.group)
             identical &= float((chk - mine).abs().max().item()) == 0.0
