@@ -317,7 +317,7 @@ class FusedMnistTrainer:
             self._call("fc2_ce_dx", self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
                        self.target.data_ptr(), P["fc1.weight"].data_ptr(), self.loss_rows.data_ptr(),
                        self.dlogits.data_ptr(), self.dh1.data_ptr(), self.da2p.data_ptr(), B, 1.0 / B, bi, *conv1,
-                       pending, *o, *rep, self._ready.data_ptr() if self._inline else None)
+                       pending, *o, *rep, self._ready.data_ptr() if self.overlap else None)
 
     def _backward(self):
         """``k_bwd_all``: the whole backward in one launch.  Fused-opt: every
@@ -357,8 +357,23 @@ class FusedMnistTrainer:
 
     def _close_exchange(self):
         """ddp-xgmi overlap: the owed exchange as a launch of its own (end of
-        a graph / eager run), so a run() leaves complete updates."""
-        self._exchange_launch(0)
+        a graph / eager run), so a run() leaves complete updates.  Ranks
+        sharing a GPU run the two roles as two launches (same workgroup
+        decompositions, so they still pair with any peer): each launch then
+        needs fewer co-resident spinning workgroups on the shared CUs."""
+        if self._inline:
+            self._exchange_launch(0)
+            return
+        L, x = self.L, self._xgmi
+        lr, mom, wd, gs, nes = self._opt_args()
+        upd = x.update_args(self._params, self.mom, self.lr_dev, mom, wd, gs, bool(nes))
+        _lib.check(L.pto_ar_oneshot_role_sgd(x.peers.data_ptr(), self._split, self.numel - self._split, x.rank,
+                                             x.world, CONV_CHAN, x.epochs.data_ptr(), x.err.data_ptr(),
+                                             x.exchange_args()[5], *upd, self.numel, self.c1_nrep, self.c1_stride,
+                                             self._c1, self._ready.data_ptr(), self._s()), "ar_oneshot_role_sgd")
+        _lib.check(L.pto_ar_role_sgd(x.peers.data_ptr(), 0, self._split, x.rank, x.world, FC_CHAN, x.epochs.data_ptr(),
+                                     x.err.data_ptr(), x.exchange_args()[5], *upd, self.numel, self._s()),
+                   "ar_role_sgd")
 
     def _allreduce_update(self):
         """DDP: gradient all-reduce + SGD (+ zeroing of the accumulated conv
