@@ -57,6 +57,9 @@ def parse_args(argv=None):
     p.add_argument("--no-latency", action="store_true",
                    help="skip the submit -> first-step measurement (default: measured at world size 1, after "
                         "the throughput run, through the whole operator stack)")
+    p.add_argument("--force-ddp", action="store_true",
+                   help="large models at --gpus 1: the whole DDP path (flat buckets, comm stream, per-bucket "
+                        "collectives over a 1-rank RCCL group, xGMI hook) -- its cost on one GPU")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args(argv)
 
@@ -101,11 +104,34 @@ def _launch_ranks(args, argv) -> int | None:
     return subprocess.call(cmd)
 
 
+_RESULT_FD = None
+
+
+def _reserve_stdout():
+    """The contract is ONE JSON line on stdout.  Libraries print banners
+    there from C (RCCL's "RCCL version : ..." block at communicator init), so
+    the real stdout is kept aside and fd 1 -- C and Python alike -- goes to
+    stderr for the rest of the run; :func:`_emit` writes the result line to
+    the kept descriptor."""
+    global _RESULT_FD
+    if _RESULT_FD is None:
+        sys.stdout.flush()
+        _RESULT_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def _emit(line: str):
+    sys.stdout.flush()
+    fd = _RESULT_FD if _RESULT_FD is not None else 1
+    os.write(fd, (line + "\n").encode())
+
+
 def main(argv=None):
     args = parse_args(argv)
     rc = _launch_ranks(args, argv)
     if rc is not None:
         return rc
+    _reserve_stdout()
     mnist = args.model == "mnist"
     if args.steps is None:
         args.steps = 2000 if mnist else 20
@@ -224,7 +250,7 @@ def main(argv=None):
         out["submit_to_first_step_s"] = lat.get("submit_to_first_step_s")
         out["config"]["submit_to_first_step"] = lat
     if out is not None:
-        print(json.dumps(out), flush=True)
+        _emit(json.dumps(out))
     if identical is False:
         print("[bench] error: the data-parallel replicas diverged (parameters not bit-identical across ranks)",
               file=sys.stderr, flush=True)
@@ -316,11 +342,22 @@ def run_model_bench(args, env, device, pdist, rccl_log=None):
 
     if device.type != "cuda":
         raise SystemExit(f"--model {args.model} needs a GPU")
+    force = bool(args.force_ddp)
+    if force and env.world_size == 1 and not torch.distributed.is_initialized():
+        # a real 1-rank RCCL group on 127.0.0.1, so every bucket's collective is issued
+        import socket
+
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        torch.distributed.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                             device_id=device)
     if args.model == "resnet50":
-        trainer = ResNetTrainer(device, batch_size=args.batch_size, seed=env.rank)
+        trainer = ResNetTrainer(device, batch_size=args.batch_size, seed=env.rank, force_ddp=force)
     else:
         trainer = LlamaTrainer(device, model=args.model, batch_size=args.batch_size, seq_len=args.seq_len,
-                               seed=env.rank, checkpoint=args.checkpoint)
+                               seed=env.rank, checkpoint=args.checkpoint, force_ddp=force)
     trainer.run(args.warmup)
     torch.cuda.synchronize(device)
     pdist.barrier(device)
@@ -346,7 +383,8 @@ def run_model_bench(args, env, device, pdist, rccl_log=None):
     if env.rank == 0:
         cfg = {"model": args.model, "global_batch": args.batch_size * n, "per_rank_batch": args.batch_size,
                "seq_len": args.seq_len if args.model.startswith("llama") else None,
-               "parallelism": f"dp{n}", "backend": (torch.distributed.get_backend() if n > 1 else "none"),
+               "parallelism": f"dp{n}" + (" (DDP path forced: 1-rank RCCL group)" if force and n == 1 else ""),
+               "backend": (torch.distributed.get_backend() if (n > 1 or force) else "none"),
                "bucket_mb": round(max((b["hi"] - b["lo"]) * trainer.bucketer.flat[b["dtype"]].element_size()
                                       for b in trainer.bucketer.buckets) / 2**20, 1)
                if trainer.bucketer.buckets else None,
@@ -359,16 +397,23 @@ def run_model_bench(args, env, device, pdist, rccl_log=None):
             cfg["ranks_bit_identical"] = identical
         if breakdown:
             cfg["phase_ms"] = breakdown
+        if args.model.startswith("llama") and n == 1:
+            # what one rank of the N=8 run holds: this run's peak plus, when it
+            # ran without buckets, the flat bf16 gradient buffer DDP adds
+            extra = 0 if trainer.bucketer.flat else sum(p.numel() * p.element_size()
+                                                        for p in trainer.model.parameters())
+            cfg["projected_dp8_peak_gb"] = round((torch.cuda.max_memory_allocated(device) + extra) / 1e9, 1)
+            cfg["hbm_gb"] = round(torch.cuda.get_device_properties(device).total_memory / 1e9, 1)
         if hasattr(trainer, "flops_per_step"):
             cfg["mfu"] = round(trainer.flops_per_step() * args.steps / elapsed / MI355X_BF16_DENSE_FLOPS, 4)
         unit = "images/s" if args.model == "resnet50" else "tokens/s"
         metric = "images/sec ResNet-50 DDP bf16" if args.model == "resnet50" else f"tokens/sec {args.model} DDP bf16"
-        print(json.dumps({"metric": metric, "value": round(value, 1), "unit": unit, "n_gpus": n,
+        _emit(json.dumps({"metric": metric, "value": round(value, 1), "unit": unit, "n_gpus": n,
                           "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
                           "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
                           "data": "synthetic (random tokens / ImageNet-shaped images), random-init weights",
-                          "config": cfg}), flush=True)
+                          "config": cfg}))
     pdist.cleanup()
     if identical is False:
         print("[bench] error: the data-parallel replicas diverged", file=sys.stderr, flush=True)

@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.bn import BatchNormAct
+from ..ops.conv1x1 import GradStash, conv1x1_res, gemm_supported
 
 
 class Bottleneck(nn.Module):
@@ -34,7 +35,14 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         # BN + ReLU (+ the residual add) are one fused pass each way on the
-        # GPU (ops/bn.py); state-dict keys are the stock ones
+        # GPU (ops/bn.py); in an identity block the residual's gradient is
+        # folded into conv1's input-gradient GEMM instead of an autograd add
+        # (ops/conv1x1.py); state-dict keys are the stock ones
+        if self.downsample is None and gemm_supported(x, self.conv1) and self.bn3.can_fuse(x):
+            stash = GradStash()
+            y = self.bn1(conv1x1_res(x, self.conv1, stash), relu=True)
+            y = self.bn2(self.conv2(y), relu=True)
+            return self.bn3(self.conv3(y), residual=x, relu=True, stash=stash)
         idt = x if self.downsample is None else self.downsample[1](self.downsample[0](x))
         y = self.bn1(self.conv1(x), relu=True)
         y = self.bn2(self.conv2(y), relu=True)

@@ -30,7 +30,7 @@ def fused_supported(x: torch.Tensor) -> bool:
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, residual, relu, momentum, eps):
+    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, residual, relu, momentum, eps, stash):
         L = _lib.lib()
         x = x.contiguous(memory_format=_CL)
         N, C, H, W = x.shape
@@ -46,6 +46,7 @@ class _BNAct(torch.autograd.Function):
                 raise ValueError("BatchNormAct: residual must match the input")
         ctx.mode = 2 if (residual is not None and relu) else (1 if relu else 0)
         ctx.has_res = residual is not None
+        ctx.stash = stash  # residual gradient handed to the block's conv1 GEMM (ops/conv1x1.py)
         # relu(bn(x) + res): the backward's ReLU mask cannot be recomputed
         # from x alone; one bit per element (bit j of byte i = y[8i + j] > 0)
         # instead of re-reading y
@@ -78,24 +79,33 @@ class _BNAct(torch.autograd.Function):
                                 dgamma.data_ptr(), dbeta.data_ptr(), coef.data_ptr(), scratch.data_ptr(), ctx.mode,
                                 _lib.stream_ptr(dev)), "bn_bwd")
         dres = (g if ctx.mode == 2 else dy) if ctx.has_res else None
-        return dx, dgamma.to(weight.dtype), dbeta.to(weight.dtype), None, None, None, dres, None, None, None
+        if dres is not None and ctx.stash is not None:
+            ctx.stash.put(dres)  # accumulated by conv1's input-gradient GEMM instead of an autograd add
+            dres = None
+        return dx, dgamma.to(weight.dtype), dbeta.to(weight.dtype), None, None, None, dres, None, None, None, None
 
 
 def bn_act(x, weight, bias, running_mean=None, running_var=None, num_batches_tracked=None, residual=None,
-           relu=False, momentum: float = 0.1, eps: float = 1e-5):
+           relu=False, momentum: float = 0.1, eps: float = 1e-5, stash=None):
     """Training-mode ``[relu](batch_norm(x) [+ residual])`` on a bf16
-    channels-last HIP tensor; running statistics updated in place."""
+    channels-last HIP tensor; running statistics updated in place.
+    ``stash``: the residual's gradient goes there instead of to autograd."""
     return _BNAct.apply(x, weight, bias, running_mean, running_var, num_batches_tracked, residual, relu,
-                        float(momentum), float(eps))
+                        float(momentum), float(eps), stash)
 
 
 class BatchNormAct(nn.BatchNorm2d):
-    def forward(self, x, residual=None, relu: bool = False):  # noqa: D102
-        if self.training and self.momentum is not None and self.affine and fused_supported(x):
+    def can_fuse(self, x) -> bool:
+        return bool(self.training and self.momentum is not None and self.affine and fused_supported(x))
+
+    def forward(self, x, residual=None, relu: bool = False, stash=None):  # noqa: D102
+        if self.can_fuse(x):
             nbt = self.num_batches_tracked if self.track_running_stats else None
             rm = self.running_mean if self.track_running_stats else None
             rv = self.running_var if self.track_running_stats else None
-            return bn_act(x, self.weight, self.bias, rm, rv, nbt, residual, relu, self.momentum, self.eps)
+            return bn_act(x, self.weight, self.bias, rm, rv, nbt, residual, relu, self.momentum, self.eps, stash)
+        if stash is not None:
+            raise ValueError("BatchNormAct: a gradient stash needs the fused path")
         y = super().forward(x)
         if residual is not None:
             y = y + residual

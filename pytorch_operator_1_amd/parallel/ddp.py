@@ -54,15 +54,21 @@ class GradBucketer:
     """
 
     def __init__(self, module: torch.nn.Module, bucket_mb: float | None = None, process_group=None,
-                 overlap: bool = True, mode: str | None = None, comm: str | None = None):
+                 overlap: bool = True, mode: str | None = None, comm: str | None = None, force_ddp: bool = False):
         """``comm``: "auto" (default, ``PTO_COMM``): per-bucket xGMI kernel
         vs RCCL by measurement; "xgmi": every bucket on the kernel; "rccl":
-        never the kernel."""
+        never the kernel.  ``force_ddp``: the multi-rank machinery (flat
+        buckets, copy mode, comm stream, per-bucket collectives over the
+        process group, xGMI hook) even in a group of one rank -- the DDP
+        code path's cost measured on one GPU."""
         self.module = module
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
-        self.overlap = overlap and self.world > 1
-        self.mode = mode or os.environ.get("PTO_GRAD_MODE") or ("copy" if self.world > 1 else "none")
+        self.ddp = self.world > 1 or force_ddp
+        if force_ddp and not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("GradBucketer(force_ddp=True) needs a process group (a 1-rank group is fine)")
+        self.overlap = overlap and self.ddp
+        self.mode = mode or os.environ.get("PTO_GRAD_MODE") or ("copy" if self.ddp else "none")
         if self.mode not in ("view", "copy", "none"):
             raise ValueError(f"GradBucketer: unknown mode {self.mode}")
         params = [p for p in module.parameters() if p.requires_grad]
@@ -120,7 +126,7 @@ class GradBucketer:
         comm = comm or os.environ.get("PTO_COMM", "auto")
         if comm not in ("auto", "xgmi", "rccl"):
             raise ValueError(f"GradBucketer: comm must be auto, xgmi or rccl, not {comm!r}")
-        if self.world > 1 and comm != "rccl" and dev.type == "cuda":
+        if self.ddp and comm != "rccl" and dev.type == "cuda":
             self._setup_xgmi(comm)
         self.reset()
 
@@ -209,7 +215,7 @@ class GradBucketer:
                     else:
                         v.copy_(p.grad)
                     p.grad = v
-        if self.world > 1:
+        if self.ddp:
             if not self.overlap:
                 for i in range(len(self.buckets)):
                     self._launch(i)

@@ -94,7 +94,8 @@ class CheckpointMixin:
 
 class ResNetTrainer(CheckpointMixin):
     def __init__(self, device, batch_size: int = 256, image_size: int = 224, lr: float = 0.1,
-                 momentum: float = 0.9, weight_decay: float = 1e-4, seed: int = 0, bucket_mb: float | None = None):
+                 momentum: float = 0.9, weight_decay: float = 1e-4, seed: int = 0, bucket_mb: float | None = None,
+                 force_ddp: bool = False):
         from ..models.resnet import resnet50, synthetic_images
 
         torch.manual_seed(seed)
@@ -105,7 +106,7 @@ class ResNetTrainer(CheckpointMixin):
         self.batch_size = batch_size
         self.model = resnet50().to(device=device, memory_format=torch.channels_last)
         self.model.train()
-        self.bucketer = GradBucketer(self.model, bucket_mb=bucket_mb)
+        self.bucketer = GradBucketer(self.model, bucket_mb=bucket_mb, force_ddp=force_ddp)
         if device.type == "cuda":
             self.opt = FusedSGD(self.model.parameters(), lr=lr, momentum=momentum, weight_decay=weight_decay)
         else:
@@ -150,7 +151,7 @@ class ResNetTrainer(CheckpointMixin):
 class LlamaTrainer(CheckpointMixin):
     def __init__(self, device, model: str = "llama3-8b", batch_size: int = 2, seq_len: int = 4096,
                  lr: float = 3e-4, weight_decay: float = 0.1, seed: int = 0, checkpoint: str = "none",
-                 impl: str | None = None, bucket_mb: float | None = None):
+                 impl: str | None = None, bucket_mb: float | None = None, force_ddp: bool = False):
         from ..models.llama import CONFIGS, Llama, synthetic_tokens
 
         torch.manual_seed(seed)
@@ -165,7 +166,7 @@ class LlamaTrainer(CheckpointMixin):
         self.transposed_dgrad = impl == "hip" and os.environ.get("PTO_WT", "1") == "1"
         if self.transposed_dgrad:
             self.model.enable_transposed_dgrad()
-        self.bucketer = GradBucketer(self.model, bucket_mb=bucket_mb)
+        self.bucketer = GradBucketer(self.model, bucket_mb=bucket_mb, force_ddp=force_ddp)
         if device.type == "cuda":
             self.opt = FusedAdamW(self.model.parameters(), lr=lr, betas=(0.9, 0.95), eps=1e-8,
                                   weight_decay=weight_decay)

@@ -94,3 +94,75 @@ def test_resnet_fused_bn_grads_match_stock_bn():
         if ef > 1.5 * es + 0.02:
             worse.append((n, ef, es))
     assert not worse, worse[:5]
+
+
+@pytest.mark.parametrize("down", [False, True])
+def test_conv1x1_gemm_bottleneck_matches_miopen(down):
+    """ops/conv1x1.py: in an identity bottleneck, bn3's residual gradient
+    folded into conv1's input-gradient GEMM instead of autograd's add (a
+    downsample block keeps the stock path).  Every gradient (input included)
+    under bf16 autocast must be as close to an fp32 run as the stock path's
+    (PTO_CONV1X1_GEMM=0) is."""
+    import os
+
+    from pytorch_operator_1_amd.models.resnet import Bottleneck
+
+    torch.manual_seed(0)
+    cin = 128 if down else 256
+    blocks = [Bottleneck(cin, 64, stride=1, down=down).to(DEV, memory_format=torch.channels_last) for _ in range(3)]
+    for b in blocks[1:]:
+        b.load_state_dict(blocks[0].state_dict())
+    x0 = torch.randn(4, cin, 28, 28, device=DEV).contiguous(memory_format=torch.channels_last)
+    dout = torch.randn(4, 256, 28, 28, device=DEV).contiguous(memory_format=torch.channels_last)
+    grads = []
+    for blk, mode in zip(blocks, ("gemm", "miopen", "fp32")):
+        os.environ["PTO_CONV1X1_GEMM"] = "0" if mode == "miopen" else "1"
+        try:
+            # the block input is the previous block's bf16 output under autocast
+            x = (x0 if mode == "fp32" else x0.to(torch.bfloat16)).clone().requires_grad_(True)
+            with torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=mode != "fp32"):
+                out = blk(x)
+            out.float().backward(dout)
+        finally:
+            os.environ.pop("PTO_CONV1X1_GEMM", None)
+        g = {n: p.grad.float().clone() for n, p in blk.named_parameters() if p.grad is not None}
+        g["input"] = x.grad.float().clone()
+        grads.append(g)
+    gemm, mi, ref = grads
+    worse = []
+    for n, gr in ref.items():
+        if gr.norm() == 0:
+            continue
+        eg, em = relerr(gemm[n], gr), relerr(mi[n], gr)
+        if eg > 1.5 * em + 0.02:
+            worse.append((n, eg, em))
+    assert not worse, worse[:5]
+    assert set(gemm) == set(ref)
+
+
+def test_conv1x1_res_fp32_matches_conv_plus_residual():
+    """fp32: conv1x1_res's input gradient = F.conv2d's input gradient + the
+    stashed residual gradient (one GEMM with beta = 1); output and weight
+    gradient equal F.conv2d's."""
+    import torch.nn as nn
+
+    from pytorch_operator_1_amd.ops.conv1x1 import GradStash, conv1x1_res
+
+    torch.manual_seed(1)
+    conv = nn.Conv2d(96, 40, 1, bias=False).to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(3, 96, 17, 19, device=DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    x2 = x.detach().clone().requires_grad_(True)
+    res = torch.randn_like(x).contiguous(memory_format=torch.channels_last)
+    st = GradStash()
+    y = conv1x1_res(x, conv, st)
+    dy = torch.randn_like(y)
+    st.put(res.clone())
+    y.backward(dy)
+    gw = conv.weight.grad.clone()
+    conv.weight.grad = None
+    y2 = conv(x2)
+    y2.backward(dy)
+    assert relerr(y, y2) < 1e-5
+    assert relerr(x.grad, x2.grad + res) < 1e-5
+    assert relerr(gw, conv.weight.grad) < 1e-5
+    assert gw.stride() == conv.weight.stride()
