@@ -318,7 +318,10 @@ def measure_submit_to_first_step(gpu: bool, replicas: int = 1, timeout: float = 
             c.submit(job)
             j = c.wait_for_condition("bench-latency", timeout=timeout)
             pod = c.store.get("pods", "default", "bench-latency-master-0")
-            first = (pod["metadata"].get("annotations") or {}).get("pto.amd.com/first-step-unix")
+            ann = pod["metadata"].get("annotations") or {}
+            first = ann.get("pto.amd.com/first-step-unix")
+            if ann.get("pto.amd.com/startup-phases"):
+                res["master_phases_s"] = json.loads(ann["pto.amd.com/startup-phases"])
             res["job_state"] = j["status"]["conditions"][-1]["type"]
             if first is not None:
                 res["submit_to_first_step_s"] = round(float(first) - t0, 3)

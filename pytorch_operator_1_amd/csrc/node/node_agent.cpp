@@ -119,6 +119,7 @@ struct Group {
 // ---------------------------------------------------------------- zygote --
 struct Zygote {
   std::string python, module = "pytorch_operator_1_amd.node.zygote", pypath;
+  bool spare = false;  // a warm SPARE: runs one container itself instead of forking it
   pid_t pid = -1;
   int fd = -1;
   bool ready = false;
@@ -149,7 +150,10 @@ struct Zygote {
       if (old && *old) pp = pp.empty() ? std::string(old) : pp + ":" + old;
       if (!pp.empty()) setenv("PYTHONPATH", pp.c_str(), 1);
       std::string fds = std::to_string(fd);
-      execlp(python.c_str(), python.c_str(), "-m", module.c_str(), "--fd", fds.c_str(), (char*)nullptr);
+      if (spare)
+        execlp(python.c_str(), python.c_str(), "-m", module.c_str(), "--fd", fds.c_str(), "--spare", (char*)nullptr);
+      else
+        execlp(python.c_str(), python.c_str(), "-m", module.c_str(), "--fd", fds.c_str(), (char*)nullptr);
       _exit(127);
     }
     close(sv[1]);
@@ -269,6 +273,14 @@ struct Agent {
   double backoff_base = 0.2, backoff_max = 10.0;
   bool quit = false;
   Zygote zygote;
+  // Warm spare for the containers that must NOT be forked from the zygote
+  // (the rendezvous store host of a multi-rank job: its TCPStore server hung
+  // in forked interpreters): an exec'ed interpreter that has already done the
+  // zygote's imports and runs exactly one container itself -- the cold
+  // `import torch` (~2.4 s on the MI355X box) is off that replica's submit ->
+  // first step path.  A used spare is replaced at once.
+  Zygote spare;
+  long long spares_used = 0;
 
   void discover_gpus(int forced) {
     if (forced >= 0) {
@@ -334,8 +346,41 @@ struct Agent {
     return true;
   }
 
+  bool start_spare(Proc& p) {
+    if (!p.exec_only || !spare.enabled() || !spare.ready || !spare.eligible(p.argv)) return false;
+    Json req = Json::object();
+    Json argv = Json::array();
+    for (auto& a : p.argv) argv.push(a);
+    req["argv"] = argv;
+    Json env = Json::object();
+    for (auto& kv : p.env) env[kv.first] = kv.second;
+    req["env"] = env;
+    req["cwd"] = p.cwd;
+    req["log"] = p.log;
+    Json cpus = Json::array();
+    for (int c : p.cpus) cpus.push(c);
+    req["cpus"] = cpus;
+    const pid_t sp = spare.pid;
+    pid_t pid = spare.spawn(req);
+    if (pid <= 0 || pid != sp) return false;  // spawn() already dropped a broken spare
+    // the spare process IS the container from now on: forget it as a spare
+    if (spare.fd >= 0) close(spare.fd);
+    spare.fd = -1;
+    spare.pid = -1;
+    spare.ready = false;
+    ++spares_used;
+    spare.start();  // the next one warms up meanwhile
+    p.pid = pid;
+    p.state = "running";
+    p.reason = "";
+    p.started_at = now_s();
+    p.launcher = "spare";
+    return true;
+  }
+
   void start(Proc& p) {
     if (start_zygote(p)) return;
+    if (start_spare(p)) return;
     p.launcher = "exec";
     int pipefd[2];
     if (pipe2(pipefd, O_CLOEXEC) != 0) pipefd[0] = pipefd[1] = -1;
@@ -456,6 +501,12 @@ struct Agent {
       fprintf(stderr, "pto-node-agent: zygote %d exited (status %d); containers fall back to fork/exec\n",
               (int)pid, status);
       zygote.died();
+      return;
+    }
+    if (pid == spare.pid) {  // died before it was used: exec'ed launches until a new one is warm
+      fprintf(stderr, "pto-node-agent: spare interpreter %d exited (status %d)\n", (int)pid, status);
+      spare.died();
+      spare.start();
       return;
     }
     for (auto& kv : procs) {
@@ -727,6 +778,8 @@ struct Agent {
       z["pid"] = (long long)zygote.pid;
       z["spawned"] = zygote.spawned;
       z["fallbacks"] = zygote.fallbacks;
+      z["spare_ready"] = spare.ready;
+      z["spares_used"] = spares_used;
       r["zygote"] = z;
     }
     else if (op == "spawn") r = spawn(req);
@@ -771,7 +824,7 @@ static bool reap_one(Agent& ag) {
   memset(&si, 0, sizeof si);
   if (waitid(P_ALL, 0, &si, WEXITED | WNOHANG | WNOWAIT) != 0 || si.si_pid == 0) return false;
   const pid_t pid = si.si_pid;
-  if (pid != ag.zygote.pid) ::kill(-pid, SIGKILL);
+  if (pid != ag.zygote.pid && pid != ag.spare.pid) ::kill(-pid, SIGKILL);
   int st = 0;
   if (waitpid(pid, &st, 0) != pid) return false;
   ag.on_exit(pid, st);
@@ -815,6 +868,10 @@ int main(int argc, char** argv) {
   // reaper so waitpid() sees them like our own children
   prctl(PR_SET_CHILD_SUBREAPER, 1);
   ag.zygote.start();
+  ag.spare.python = ag.zygote.python;
+  ag.spare.pypath = ag.zygote.pypath;
+  ag.spare.spare = true;
+  ag.spare.start();
 
   int lfd = -1;
   std::vector<Client> clients;
@@ -839,9 +896,11 @@ int main(int argc, char** argv) {
     pfds.push_back({sfd, POLLIN, 0});
     if (lfd >= 0) pfds.push_back({lfd, POLLIN, 0});
     if (ag.zygote.fd >= 0 && !ag.zygote.ready) pfds.push_back({ag.zygote.fd, POLLIN, 0});
+    if (ag.spare.fd >= 0 && !ag.spare.ready) pfds.push_back({ag.spare.fd, POLLIN, 0});
     for (auto& c : clients) pfds.push_back({c.fd, POLLIN, 0});
     poll(pfds.data(), pfds.size(), 50);
     ag.zygote.poll_ready();
+    ag.spare.poll_ready();
     // signals
     signalfd_siginfo si;
     while (read(sfd, &si, sizeof si) == (ssize_t)sizeof si) {
@@ -903,6 +962,10 @@ int main(int argc, char** argv) {
   if (ag.zygote.fd >= 0) {
     close(ag.zygote.fd);
     ag.zygote.fd = -1;
+  }
+  if (ag.spare.fd >= 0) {  // an unused spare ends on EOF too
+    close(ag.spare.fd);
+    ag.spare.fd = -1;
   }
   for (auto& kv : ag.procs)
     if (kv.second.state == "running" && kv.second.pid > 0) ::kill(-kv.second.pid, SIGTERM);

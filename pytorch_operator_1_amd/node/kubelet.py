@@ -103,6 +103,7 @@ DEFAULT_IMAGES = {
     "pto/python:rocm": [sys.executable],
 }
 FIRST_STEP_ANNOTATION = "pto.amd.com/first-step-unix"
+STARTUP_ANNOTATION = "pto.amd.com/startup-phases"  # the trainer's own startup breakdown (JSON)
 THROUGHPUT_ANNOTATION = "pto.amd.com/samples-per-sec"
 GPUS_ANNOTATION = "pto.amd.com/gpus"
 EFFECTIVE_ENV_ANNOTATION = "pto.amd.com/effective-env"
@@ -736,6 +737,8 @@ class Kubelet:
                         created = self._job_created(pod, job)
                         if created is not None:
                             m.submit_to_first_step.labels(job=job).set(max(0.0, float(rec["t"]) - created))
+                if ev == "startup":
+                    ann[STARTUP_ANNOTATION] = json.dumps({k: v for k, v in rec.items() if k != "event"})
                 if "samples_per_sec" in rec:
                     ann[THROUGHPUT_ANNOTATION] = str(rec["samples_per_sec"])
                     if m is not None:

@@ -25,6 +25,11 @@ module/script as ``__main__``.  Nothing is exec'ed.
 
 Protocol: JSON lines on the inherited socket ``--fd``; the first line the
 zygote writes is ``{"ready": true, "pid": ...}``.
+
+``--spare``: the same warm interpreter, but it runs the FIRST container it
+is asked for itself, without forking (the agent keeps one ready for the
+containers that must not start in a forked interpreter: the rendezvous
+store host of a multi-rank job, node/kubelet.py), and is then replaced.
 """
 from __future__ import annotations
 
@@ -83,6 +88,9 @@ def _preload():
 
 def _run_container(req: dict) -> int:
     """Body of the container process; returns its exit code."""
+    import time
+
+    t_enter = time.time()
     os.setsid()
     for s in (signal.SIGTERM, signal.SIGCHLD, signal.SIGPIPE, signal.SIGHUP):
         signal.signal(s, signal.SIG_DFL)
@@ -147,6 +155,9 @@ def _run_container(req: dict) -> int:
         setattr(sys, f"__{n}__", stream)
     extra_path = [p for p in env.get("PYTHONPATH", "").split(os.pathsep) if p]
     import runpy
+
+    # startup evidence for the trainer's own breakdown (train/mnist.py)
+    os.environ["PTO_ZYGOTE_T"] = f"{t_enter:.6f},{time.time():.6f}"
 
     code = 0
     try:
@@ -224,6 +235,9 @@ def _spawn(req: dict, sock_fd: int) -> int:
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description="pto warm interpreter (started by pto-node-agent)")
     ap.add_argument("--fd", type=int, required=True, help="inherited socket to the agent")
+    ap.add_argument("--spare", action="store_true",
+                    help="warm SPARE: run the first requested container in this very process (no fork), for "
+                         "containers that must not start in a forked interpreter (the agent starts the next one)")
     args = ap.parse_args(argv)
     # interactive signals go to the agent; the zygote ends when its socket does
     signal.signal(signal.SIGINT, signal.SIG_IGN)
@@ -246,6 +260,17 @@ def main(argv=None) -> int:
                 continue
             try:
                 req = json.loads(line)
+                if args.spare:
+                    # this process becomes the container: it is the agent's
+                    # own child, so it is reaped, killed and restarted like
+                    # an exec'ed one
+                    reply({"ok": True, "pid": os.getpid(), "seq": req.get("seq")})
+                    rf.close()
+                    try:
+                        os.close(args.fd)
+                    except OSError:
+                        pass
+                    os._exit(_run_container(req))
                 reply({"ok": True, "pid": _spawn(req, args.fd), "seq": req.get("seq")})
             except Exception as e:  # noqa: BLE001 - reported; the agent falls back to fork/exec
                 reply({"ok": False, "error": f"{type(e).__name__}: {e}"})

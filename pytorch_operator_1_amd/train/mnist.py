@@ -203,6 +203,7 @@ class EpochShuffler:
 
 
 def _main(argv=None):
+    t_main = time.time()
     args = parse_args(argv)
     use_cuda = not args.no_cuda and torch.cuda.is_available() and os.environ.get("PTO_NO_GPU") != "1"
     if use_cuda:
@@ -219,6 +220,7 @@ def _main(argv=None):
     rccl_log = (pdist.rccl_log_setup() if use_cuda and world_env > 1 and
                 pdist.resolve_backend(args.backend, True) == "nccl" else None)
     env, device = pdist.init_distributed(args.backend, use_gpu=use_cuda)
+    t_pg = time.time()
     if env.is_distributed:
         print(f"Using distributed PyTorch with {dist.get_backend()} backend")
     rank, world = env.rank, env.world_size
@@ -238,21 +240,26 @@ def _main(argv=None):
     from .runner import build_trainer
 
     extra = {"comm": args.comm} if (args.comm and impl == "fused") else {}
+    t_data = time.time()
     trainer = build_trainer(impl, device=device, batch_size=args.batch_size, lr=args.lr, momentum=args.momentum,
                             dataset_size=xtr.shape[0], seed=args.seed, rank=rank, data=xtr, target=ytr, **extra)
-    comm_info = getattr(trainer, "comm_info", None)
-    if comm_info and world > 1:
-        print(f"[pto] gradient all-reduce: {comm_info}", flush=True)
-        metrics.emit(event="comm", rank=rank, **{k: v for k, v in comm_info.items() if not isinstance(v, dict)})
-    if world > 1:
-        # which devices the world spans and the transport RCCL picked per
-        # peer (P2P/IPC over xGMI vs SHM): the trainer's constructor ran the
-        # first collective, so the connections exist
-        w = pdist.describe_world(device, rccl_log)
-        if rank == 0:
-            print(f"[pto] world: {json.dumps(w)}", flush=True)
-        metrics.emit(event="world", rank=rank, pg_world_size=w["pg_world_size"],
-                     rccl_transport=json.dumps(w.get("rccl_transport", {})))
+    t_trainer = time.time()
+
+    def report_world():
+        """Evidence, not setup (after the first step): the transport and
+        which devices the world spans (RCCL's per-peer transport choice,
+        P2P/IPC over xGMI vs SHM)."""
+        comm_info = getattr(trainer, "comm_info", None)
+        if comm_info and world > 1:
+            print(f"[pto] gradient all-reduce: {comm_info}", flush=True)
+            metrics.emit(event="comm", rank=rank, **{k: v for k, v in comm_info.items() if not isinstance(v, dict)})
+        if world > 1:
+            w = pdist.describe_world(device, rccl_log)
+            if rank == 0:
+                print(f"[pto] world: {json.dumps(w)}", flush=True)
+            metrics.emit(event="world", rank=rank, pg_world_size=w["pg_world_size"],
+                         rccl_transport=json.dumps(w.get("rccl_transport", {})))
+
     start_step = 0
     path, st = resume_state(args.checkpoint_dir, rank, world)
     if st is not None:
@@ -346,8 +353,24 @@ def _main(argv=None):
         if first:
             if device.type == "cuda":
                 torch.cuda.synchronize(device)
-            metrics.emit(event="first_step", t=time.time(), rank=rank)
+            t_first = time.time()
+            metrics.emit(event="first_step", t=t_first, rank=rank)
+            try:
+                import psutil
+
+                t_proc = psutil.Process().create_time()
+            except Exception:  # noqa: BLE001 - timing evidence only
+                t_proc = t_main
+            # where a replica's submit -> first step went (process start is
+            # the fork of the node's warm interpreter)
+            zt = [float(v) for v in os.environ.get("PTO_ZYGOTE_T", "").split(",") if v]
+            zyg = ({"fork_to_setup_s": round(zt[0] - t_proc, 4), "zygote_setup_s": round(zt[1] - zt[0], 4),
+                    "runpy_to_main_s": round(t_main - zt[1], 4)} if len(zt) == 2 else {})
+            metrics.emit(event="startup", rank=rank, process_to_main_s=round(t_main - t_proc, 4), **zyg,
+                         pg_init_s=round(t_pg - t_main, 4), data_s=round(t_data - t_pg, 4),
+                         trainer_s=round(t_trainer - t_data, 4), first_step_s=round(t_first - t_trainer, 4))
             first = False
+            report_world()
             t_last = time.time()
         if batch_idx % args.log_interval == 0:
             lv = loss_async() if loss_async is not None else trainer.last_loss()

@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/final5
 mkdir -p $O
-timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread > $O/pytest_gpu.log 2>&1
+timeout -k 10 1100 python -u -m pytest tests -m gpu -v -s --timeout 150 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?
 grep -E "passed|failed" $O/pytest_gpu.log | tail -2; grep FAILED $O/pytest_gpu.log | head
 case $rc in 0|1) ;; *) echo "pytest rc=$rc"; exit $rc;; esac

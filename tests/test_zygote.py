@@ -70,7 +70,8 @@ def test_zygote_container_argv_env_cwd_log_exit(agent, tmp_path):
     info = json.loads(out.read_text())
     assert info["argv"][1:] == ["exit", "3"] and info["main"] == "__main__"
     assert info["env"]["HIP_VISIBLE_DEVICES"] == "1" and "PYTHONPATH" not in info["env"]
-    assert set(info["env"]) <= set(env) | {"PWD", "USE_LIBUV"}  # + the store backend a fork can run
+    # + the store backend a fork can run, and the launcher's startup timestamps
+    assert set(info["env"]) <= set(env) | {"PWD", "USE_LIBUV", "PTO_ZYGOTE_T"}
     assert info["env"]["USE_LIBUV"] == "0"
     assert info["cwd"] == str(cwd)
     assert info["torch_loaded"]  # warm: torch came from the zygote's imports
@@ -130,3 +131,41 @@ def test_eligibility_rules():
     assert not eligible([py, "-c", "print(1)"], py)
     assert not eligible([py, "-m"], py)
     assert not eligible(["/bin/sh", "x.py"], py)
+
+
+def test_exec_only_container_runs_in_a_warm_spare(agent, tmp_path):
+    """A container that must not be forked from the zygote (launcher "exec":
+    the rendezvous store host of a multi-rank job) runs in the agent's warm
+    SPARE interpreter -- an exec'ed process that already did the zygote's
+    imports and becomes the container itself -- and a new spare warms up for
+    the next one.  Same container contract as a forked one."""
+    end = time.time() + 120
+    while not agent.ping()["zygote"].get("spare_ready") and time.time() < end:
+        time.sleep(0.1)
+    assert agent.ping()["zygote"]["spare_ready"]
+    used0 = agent.ping()["zygote"]["spares_used"]
+    out = tmp_path / "out.json"
+    log = tmp_path / "s.log"
+    env = {"OUT": str(out), "RANK": "0", "WORLD_SIZE": "2", "PATH": os.environ.get("PATH", "")}
+    agent.spawn("z/spare", [sys.executable, _script(tmp_path), "exit", "5"], env=env, log=str(log), launcher="exec")
+    st = wait_state(agent, "z/spare", lambda s: s["state"] == "terminated")
+    assert st["launcher"] == "spare" and st["exit_code"] == 5
+    info = json.loads(out.read_text())
+    assert info["argv"][1:] == ["exit", "5"] and info["main"] == "__main__"
+    assert info["torch_loaded"]  # warm: imported before the request came
+    assert info["pgid"] == info["pid"] and info["env"]["WORLD_SIZE"] == "2"
+    text = log.read_text()
+    assert "STDOUT-LINE" in text and "STDERR-LINE" in text
+    z = agent.ping()["zygote"]
+    assert z["spares_used"] == used0 + 1
+    end = time.time() + 120  # the replacement warms up
+    while not agent.ping()["zygote"].get("spare_ready") and time.time() < end:
+        time.sleep(0.1)
+    assert agent.ping()["zygote"]["spare_ready"]
+    # a killed spare container is reaped like any other
+    agent.spawn("z/spare2", [sys.executable, _script(tmp_path), "sleep"], env=env, log=str(log), launcher="exec")
+    st = wait_state(agent, "z/spare2", lambda s: s["state"] == "running")
+    assert st["launcher"] == "spare"
+    agent.kill("z/spare2", signal=9)
+    st = wait_state(agent, "z/spare2", lambda s: s["state"] == "terminated")
+    assert st["exit_code"] == 137
