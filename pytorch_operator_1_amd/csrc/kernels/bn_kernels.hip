@@ -381,6 +381,101 @@ int elementwise_blocks(long long n8) {
   return (int)(b < 1 ? 1 : b);
 }
 
+
+// ------------------------------------------------------------ max pool ----
+// The ResNet stem's 3x3 / stride-2 / pad-1 max pool over channels-last bf16
+// (relu(bn1(conv1)) -> layer1), forward and backward, 8 channels (16 B) per
+// thread.  Forward writes the pooled map and one argmax code per output
+// element (tap index kh*K+kw, uint8); backward is a GATHER: every input
+// element sums dy over the (<= 4 at stride 2) windows whose code points at
+// it, so there are no atomics and no zero-fill of dx (PyTorch's NHWC kernels
+// took 0.62 + 0.25 ms/step for this, profiles/resnet50_window_r4.md).
+// Semantics of torch.nn.functional.max_pool2d: padding never wins, the first
+// maximum in (kh, kw) order wins a tie, NaN propagates.
+struct PoolShape {
+  int N, H, W, C, OH, OW, K, S, P;
+};
+
+__global__ __launch_bounds__(BN_T) void k_maxpool_fwd(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                      uint8_t* __restrict__ code, PoolShape sh) {
+  // 32-bit index math (the launcher checks the element count fits): the
+  // 64-bit divisions of the first version were most of the kernel's time
+  const uint32_t c8n = (uint32_t)sh.C >> 3;
+  const uint32_t t = blockIdx.x * BN_T + threadIdx.x;
+  if (t >= (uint32_t)sh.N * sh.OH * sh.OW * c8n) return;
+  const int c8 = (int)(t % c8n);
+  uint32_t pix = t / c8n;
+  const int ow = (int)(pix % (uint32_t)sh.OW);
+  pix /= (uint32_t)sh.OW;
+  const int oh = (int)(pix % (uint32_t)sh.OH);
+  const int n = (int)(pix / (uint32_t)sh.OH);
+  // torch's loop: maxval = -inf, index = the first in-bounds tap, then
+  // "if (val > maxval || isnan(val))" in (kh, kw) order
+  const int h0 = oh * sh.S - sh.P, w0 = ow * sh.S - sh.P;
+  const int kh0 = max(0, -h0), kw0 = max(0, -w0);
+  float m[8];
+  int k[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m[j] = -__builtin_inff();
+    k[j] = kh0 * sh.K + kw0;
+  }
+  for (int kh = kh0; kh < sh.K && h0 + kh < sh.H; ++kh)
+    for (int kw = kw0; kw < sh.K && w0 + kw < sh.W; ++kw) {
+      const V8 v = load8(x + (((long long)n * sh.H + h0 + kh) * sh.W + w0 + kw) * sh.C + c8 * 8);
+      const int tap = kh * sh.K + kw;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (v.v[j] > m[j] || __builtin_isnan(v.v[j])) {
+          m[j] = v.v[j];
+          k[j] = tap;
+        }
+    }
+  const long long o = (((long long)n * sh.OH + oh) * sh.OW + ow) * sh.C + c8 * 8;
+  V8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r.v[j] = m[j];
+  store8(y + o, r);
+  uint2 cd;
+  cd.x = (uint32_t)k[0] | ((uint32_t)k[1] << 8) | ((uint32_t)k[2] << 16) | ((uint32_t)k[3] << 24);
+  cd.y = (uint32_t)k[4] | ((uint32_t)k[5] << 8) | ((uint32_t)k[6] << 16) | ((uint32_t)k[7] << 24);
+  *reinterpret_cast<uint2*>(code + o) = cd;
+}
+
+__global__ __launch_bounds__(BN_T) void k_maxpool_bwd(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ code,
+                                                      uint16_t* __restrict__ dx, PoolShape sh) {
+  const uint32_t c8n = (uint32_t)sh.C >> 3;
+  const uint32_t t = blockIdx.x * BN_T + threadIdx.x;
+  if (t >= (uint32_t)sh.N * sh.H * sh.W * c8n) return;
+  const int c8 = (int)(t % c8n);
+  uint32_t pix = t / c8n;
+  const int iw = (int)(pix % (uint32_t)sh.W);
+  pix /= (uint32_t)sh.W;
+  const int ih = (int)(pix % (uint32_t)sh.H);
+  const int n = (int)(pix / (uint32_t)sh.H);
+  // windows oh with oh*S - P <= ih <= oh*S - P + K - 1
+  const int hp = ih + sh.P, wp = iw + sh.P;
+  const int oh0 = hp >= sh.K ? (hp - sh.K) / sh.S + 1 : 0, oh1 = min(sh.OH - 1, hp / sh.S);
+  const int ow0 = wp >= sh.K ? (wp - sh.K) / sh.S + 1 : 0, ow1 = min(sh.OW - 1, wp / sh.S);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int oh = oh0; oh <= oh1; ++oh)
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      const int tap = (hp - oh * sh.S) * sh.K + (wp - ow * sh.S);
+      const long long o = (((long long)n * sh.OH + oh) * sh.OW + ow) * sh.C + c8 * 8;
+      const uint2 cd = *reinterpret_cast<const uint2*>(code + o);
+      const V8 g = load8(dy + o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t cj = ((j < 4 ? cd.x : cd.y) >> (8 * (j & 3))) & 0xffu;
+        if ((int)cj == tap) acc[j] += g.v[j];
+      }
+    }
+  V8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r.v[j] = acc[j];
+  store8(dx + (((long long)n * sh.H + ih) * sh.W + iw) * sh.C + c8 * 8, r);
+}
+
 }  // namespace
 
 #define PTO_API extern "C" __attribute__((visibility("default")))
@@ -436,5 +531,37 @@ PTO_API int pto_bn_bwd(const void* dy, const void* x, const void* ymask, void* d
   auto* kb = mode == 1 ? k_bn_bwd_apply<1> : k_bn_bwd_apply<0>;  // mode 2 applies like 0 (g stored)
   hipLaunchKernelGGL(kb, dim3(elementwise_blocks(n8)), dim3(BN_T), 0, s, reinterpret_cast<const uint16_t*>(gsrc),
                      reinterpret_cast<const uint16_t*>(x), reinterpret_cast<uint16_t*>(dx), n8, C, stat, coef);
+  return (int)hipGetLastError();
+}
+
+// Max pool (channels-last bf16, C % 8 == 0, K*K <= 255): y [N, OH, OW, C],
+// code [N, OH, OW, C] uint8; backward dx [N, H, W, C] fully written.
+static bool pool_ok(const PoolShape& sh, const void* a, const void* b) {
+  return sh.N > 0 && sh.H > 0 && sh.W > 0 && sh.C > 0 && sh.C % 8 == 0 && sh.K > 0 && sh.K * sh.K <= 255 &&
+         sh.S > 0 && sh.P >= 0 && 2 * sh.P <= sh.K && sh.OH == (sh.H + 2 * sh.P - sh.K) / sh.S + 1 &&
+         sh.OW == (sh.W + 2 * sh.P - sh.K) / sh.S + 1 && sh.OH > 0 && sh.OW > 0 &&
+         (long long)sh.N * sh.H * sh.W * sh.C < (1ll << 31) &&  // 32-bit element indices in the kernels
+         !((((uintptr_t)a) | ((uintptr_t)b)) & 15);
+}
+
+PTO_API int pto_maxpool_fwd(const void* x, void* y, void* code, int N, int H, int W, int C, int OH, int OW, int K,
+                            int S, int P, hipStream_t s) {
+  const PoolShape sh{N, H, W, C, OH, OW, K, S, P};
+  if (!pool_ok(sh, x, y) || (((uintptr_t)code) & 7)) return -1;
+  const long long total = (long long)N * OH * OW * (C / 8);
+  hipLaunchKernelGGL(k_maxpool_fwd, dim3((unsigned)((total + BN_T - 1) / BN_T)), dim3(BN_T), 0, s,
+                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<uint16_t*>(y),
+                     reinterpret_cast<uint8_t*>(code), sh);
+  return (int)hipGetLastError();
+}
+
+PTO_API int pto_maxpool_bwd(const void* dy, const void* code, void* dx, int N, int H, int W, int C, int OH, int OW,
+                            int K, int S, int P, hipStream_t s) {
+  const PoolShape sh{N, H, W, C, OH, OW, K, S, P};
+  if (!pool_ok(sh, dy, dx) || (((uintptr_t)code) & 7)) return -1;
+  const long long total = (long long)N * H * W * (C / 8);
+  hipLaunchKernelGGL(k_maxpool_bwd, dim3((unsigned)((total + BN_T - 1) / BN_T)), dim3(BN_T), 0, s,
+                     reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint8_t*>(code),
+                     reinterpret_cast<uint16_t*>(dx), sh);
   return (int)hipGetLastError();
 }

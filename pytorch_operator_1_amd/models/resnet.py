@@ -15,7 +15,8 @@ import torch
 import torch.nn as nn
 
 from ..ops.bn import BatchNormAct
-from ..ops.conv1x1 import GradStash, conv1x1_res, gemm_supported
+from ..ops.conv1x1 import GradStash, conv1x1, conv1x1_res, gemm_supported
+from ..ops.pool import MaxPool2d
 
 
 class Bottleneck(nn.Module):
@@ -33,20 +34,26 @@ class Bottleneck(nn.Module):
         self.downsample = (nn.Sequential(nn.Conv2d(cin, cout, 1, stride=stride, bias=False), BatchNormAct(cout))
                            if down else None)
 
+    @staticmethod
+    def _c1(conv, x):
+        """1x1 convs (the downsample ones strided): backward on hipBLASLt
+        (ops/conv1x1.py)."""
+        return conv1x1(x, conv) if gemm_supported(x, conv) else conv(x)
+
     def forward(self, x):
         # BN + ReLU (+ the residual add) are one fused pass each way on the
         # GPU (ops/bn.py); in an identity block the residual's gradient is
         # folded into conv1's input-gradient GEMM instead of an autograd add
         # (ops/conv1x1.py); state-dict keys are the stock ones
-        if self.downsample is None and gemm_supported(x, self.conv1) and self.bn3.can_fuse(x):
+        if self.downsample is None and gemm_supported(x, self.conv1, stride1=True) and self.bn3.can_fuse(x):
             stash = GradStash()
             y = self.bn1(conv1x1_res(x, self.conv1, stash), relu=True)
             y = self.bn2(self.conv2(y), relu=True)
-            return self.bn3(self.conv3(y), residual=x, relu=True, stash=stash)
-        idt = x if self.downsample is None else self.downsample[1](self.downsample[0](x))
-        y = self.bn1(self.conv1(x), relu=True)
+            return self.bn3(self._c1(self.conv3, y), residual=x, relu=True, stash=stash)
+        idt = x if self.downsample is None else self.downsample[1](self._c1(self.downsample[0], x))
+        y = self.bn1(self._c1(self.conv1, x), relu=True)
         y = self.bn2(self.conv2(y), relu=True)
-        return self.bn3(self.conv3(y), residual=idt, relu=True)
+        return self.bn3(self._c1(self.conv3, y), residual=idt, relu=True)
 
 
 class ResNet(nn.Module):
@@ -54,7 +61,7 @@ class ResNet(nn.Module):
         super().__init__()
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = BatchNormAct(64)
-        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.maxpool = MaxPool2d(3, stride=2, padding=1)  # HIP gather-backward pool (ops/pool.py)
         cin, stages = 64, []
         for i, (n, width) in enumerate(zip(layers, (64, 128, 256, 512))):
             stride = 1 if i == 0 else 2

@@ -1,20 +1,36 @@
-"""The residual gradient of a ResNet identity bottleneck folded into conv1's
+"""ResNet's 1x1 stride-1 convolutions with their backward on hipBLASLt,
+and the residual gradient of an identity bottleneck folded into conv1's
 input-gradient GEMM.
 
-In an identity bottleneck the block input ``x`` feeds both ``conv1`` and the
-identity path (``bn3(..., residual=x)``), so autograd adds the two input
-gradients with a separate elementwise kernel (16 of them per ResNet-50 step,
-1.33 ms of a 30 ms step: profiles/resnet50_window_r4.md).  Here the fused
-BatchNorm backward of ``bn3`` hands its residual gradient to a
-:class:`GradStash` instead of returning it, and ``conv1``'s backward computes
-``dX = g_res + dY W`` as ONE hipBLASLt GEMM with beta = 1, in place on the
-residual gradient: a 1x1 stride-1 convolution over NHWC memory is exactly
-``Y[M, Co] = X[M, Ci] W[Co, Ci]^T`` (M = N*H*W), so its input gradient is
-``dY[M, Co] W[Co, Ci]`` with no layout change.  The forward and the weight
-gradient stay MIOpen's (tools/conv1x1_bench.py: a GEMM with K = N*H*W is
-4-10x slower than MIOpen's weight-gradient solvers on these shapes, while
-the data-gradient GEMM with the accumulation beats MIOpen's data-gradient
-conv plus the add it replaces on all four identity-block shapes).
+A 1x1 stride-1 convolution over NHWC memory is exactly
+``Y[M, Co] = X[M, Ci] W[Co, Ci]^T`` (M = N*H*W), so:
+
+* input gradient ``dX = dY W`` is one GEMM with no layout change.  In an
+  identity bottleneck the block input ``x`` feeds both ``conv1`` and the
+  identity path (``bn3(..., residual=x)``), so autograd would add the two
+  input gradients with a separate elementwise kernel (16 per ResNet-50
+  step, 1.33 ms of a 30 ms step: profiles/resnet50_window_r4.md).  Here the
+  fused BatchNorm backward of ``bn3`` hands its residual gradient to a
+  :class:`GradStash` and ``conv1``'s GEMM accumulates onto it in place
+  (beta = 1).
+* weight gradient ``dW = dY^T X`` has K = N*H*W (up to 800k) and a tiny
+  output (down to 64 x 64): one GEMM has a single output tile and ran 4-10x
+  slower than MIOpen.  It is split over K instead: S batched GEMMs of
+  ~3,136 rows each with fp32 outputs (``bmm(out_dtype=float32)``), then
+  their sum -- as fast as or faster than MIOpen's weight-gradient solvers on
+  every ResNet-50 shape (profiles/raw/r5/conv1x1_splitk.jsonl), and the
+  gradient comes out in fp32 directly (no bf16 round trip, no cast kernel).
+* the strided 1x1 convs (the downsample of layers 2-4) take the same
+  GEMMs on the stride-2 sub-grid; their input gradient is scattered into a
+  zeroed full-size tensor.
+
+This is also what lets the whole ResNet step be captured in a HIP graph:
+MIOpen's GEMM-based 1x1 backward solvers zero their outputs with a memset
+that a captured graph does not replay (from the second replay on, the stale
+contents of the graph's pool leaked into the gradients of layer 1 and the
+stem: tools/probes/graph_alias_probe.py).
+
+The forward stays MIOpen's (faster than the GEMM on most shapes).
 """
 from __future__ import annotations
 
@@ -46,60 +62,108 @@ class GradStash:
         return g
 
 
-def gemm_supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
-    return (x.is_cuda and x.dim() == 4 and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
-            and conv.padding == (0, 0) and conv.groups == 1 and conv.bias is None
-            and os.environ.get("PTO_CONV1X1_GEMM", "1") == "1")
+def gemm_supported(x: torch.Tensor, conv: nn.Conv2d, stride1: bool = False) -> bool:
+    """1x1 bias-free conv, stride 1 (or equal strides, unless ``stride1``)."""
+    st = conv.stride
+    return (x.is_cuda and x.dim() == 4 and conv.kernel_size == (1, 1) and st[0] == st[1]
+            and (st == (1, 1) or not stride1) and conv.padding == (0, 0) and conv.dilation == (1, 1)
+            and conv.groups == 1 and conv.bias is None and os.environ.get("PTO_CONV1X1_GEMM", "1") == "1")
 
 
-class _Conv1x1Res(torch.autograd.Function):
-    """A 1x1 stride-1 convolution whose INPUT gradient also carries a
-    stashed residual gradient: forward and weight gradient stay MIOpen's
-    (its weight-gradient solvers beat a hipBLASLt GEMM with K = N*H*W by
-    4-10x on these shapes, profiles/resnet50_r5.md); the input gradient is
-    ONE hipBLASLt GEMM accumulating into the residual gradient in place
-    (beta = 1), which is faster than MIOpen's data-gradient conv + the
-    separate add it replaces on every ResNet-50 identity block."""
+def _splitk(m: int) -> int:
+    """Batches of the split-K weight gradient: ~3,136 rows each, dividing M."""
+    s = max(1, m // 3136)
+    while m % s:
+        s -= 1
+    return s
+
+
+def weight_grad_1x1(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    """``dY^T X`` in fp32 for ``dy2`` [M, Co], ``x2`` [M, Ci] (bf16)."""
+    m, co = dy2.shape
+    ci = x2.shape[1]
+    s = _splitk(m)
+    kw = {} if dy2.dtype == torch.float32 else {"out_dtype": torch.float32}
+    if s == 1:
+        return torch.mm(dy2.t(), x2, **kw)
+    part = torch.bmm(dy2.view(s, m // s, co).transpose(1, 2), x2.view(s, m // s, ci), **kw)
+    return part.sum(0)
+
+
+class _Conv1x1(torch.autograd.Function):
+    """A 1x1 bias-free convolution (stride s): MIOpen forward, GEMM input
+    gradient (accumulating a stashed residual gradient, if any; at s > 1
+    scattered into a zeroed full-size gradient), split-K GEMM weight
+    gradient in fp32 (from the strided sub-grid of x at s > 1)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stash, dtype):
+    def forward(ctx, x, weight, stash, dtype, stride=1):
         x = x.to(dtype).contiguous(memory_format=_CL)
         wb = weight.to(dtype)
         if wb.dim() == 4 and not wb.is_contiguous(memory_format=_CL):
             wb = wb.contiguous(memory_format=_CL)
         ctx.save_for_backward(x, wb)
-        ctx.stash, ctx.wdtype = stash, weight.dtype
+        ctx.stash, ctx.wdtype, ctx.stride = stash, weight.dtype, stride
         ctx.wshape, ctx.wstride = weight.shape, weight.stride()
-        return F.conv2d(x, wb)
+        return F.conv2d(x, wb, stride=stride)
 
     @staticmethod
     def backward(ctx, dy):
         x, wb = ctx.saved_tensors
+        s = ctx.stride
+        xfull = x
+        if s > 1:  # the pixels a strided 1x1 conv reads
+            x = x[:, :, ::s, ::s].contiguous(memory_format=_CL)
         N, ci, H, W = x.shape
         co = wb.shape[0]
         dy = dy.to(wb.dtype).contiguous(memory_format=_CL)
-        _, dw, _ = torch.ops.aten.convolution_backward(dy, x, wb, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
-                                                       [False, True, False])
-        dw = dw.to(ctx.wdtype)
-        if dw.stride() != ctx.wstride:
-            dw = torch.empty_strided(ctx.wshape, ctx.wstride, dtype=dw.dtype, device=dw.device).copy_(dw)
         dy2 = dy.permute(0, 2, 3, 1).reshape(-1, co)
-        w2 = wb.reshape(co, ci)
-        extra = ctx.stash.take() if ctx.stash is not None else None
-        if extra is not None:
-            g = extra.to(dy2.dtype).contiguous(memory_format=_CL)
-            dx2 = g.permute(0, 2, 3, 1).reshape(-1, ci).addmm_(dy2, w2)  # dX = g_res + dY W, in place
-        else:
-            dx2 = torch.mm(dy2, w2)
-        return dx2.view(N, H, W, ci).permute(0, 3, 1, 2), dw, None, None
+        x2 = x.permute(0, 2, 3, 1).reshape(-1, ci)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = weight_grad_1x1(dy2, x2).to(ctx.wdtype)
+            # the parameter's own layout (channels_last [Co, Ci, 1, 1] and
+            # contiguous share strides only up to the size-1 dims)
+            dw = dw.view(co, ci, 1, 1).as_strided(ctx.wshape, ctx.wstride) if dw.is_contiguous() else dw
+        dx = None
+        if ctx.needs_input_grad[0]:
+            w2 = wb.reshape(co, ci)
+            extra = ctx.stash.take() if ctx.stash is not None else None
+            if extra is not None:
+                g = extra.to(dy2.dtype).contiguous(memory_format=_CL)
+                dx2 = g.permute(0, 2, 3, 1).reshape(-1, ci).addmm_(dy2, w2)  # dX = g_res + dY W, in place
+            else:
+                dx2 = torch.mm(dy2, w2)
+            dx = dx2.view(N, H, W, ci).permute(0, 3, 1, 2)
+            if s > 1:
+                full = torch.zeros_like(xfull, memory_format=_CL)
+                full[:, :, ::s, ::s] = dx
+                dx = full
+        elif ctx.stash is not None:
+            ctx.stash.take()
+        return dx, dw, None, None, None
+
+
+def _dtype(x):
+    return torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+
+
+def conv1x1(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+    """``conv(x)`` for a 1x1 bias-free conv, any equal stride (see
+    :class:`_Conv1x1`).  Dtype: the autocast dtype when autocast is on, else
+    x's."""
+    if not gemm_supported(x, conv):
+        raise ValueError("conv1x1: needs a 1x1 bias-free conv on a HIP tensor")
+    dtype = _dtype(x)
+    with torch.autocast("cuda", enabled=False):
+        return _Conv1x1.apply(x, conv.weight, None, dtype, conv.stride[0])
 
 
 def conv1x1_res(x: torch.Tensor, conv: nn.Conv2d, stash: GradStash) -> torch.Tensor:
-    """``conv(x)`` for a 1x1 stride-1 bias-free conv whose input gradient
-    also receives ``stash``'s residual gradient (see :class:`_Conv1x1Res`).
-    Dtype: the autocast dtype when autocast is on, else x's."""
-    if not gemm_supported(x, conv):
+    """:func:`conv1x1` whose input gradient also receives ``stash``'s
+    residual gradient."""
+    if not gemm_supported(x, conv, stride1=True):
         raise ValueError("conv1x1_res: needs a 1x1 stride-1 bias-free conv on a HIP tensor")
-    dtype = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+    dtype = _dtype(x)
     with torch.autocast("cuda", enabled=False):
-        return _Conv1x1Res.apply(x, conv.weight, stash, dtype)
+        return _Conv1x1.apply(x, conv.weight, stash, dtype, 1)

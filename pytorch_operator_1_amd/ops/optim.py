@@ -49,8 +49,34 @@ class _TableMixin:
         self._gptrs = _grad_ptrs(self.param_groups)
 
 
+def _to_device(host: torch.Tensor, device, pending: list | None, reserved: list | None = None):
+    """``host.to(device)``; while a HIP graph is being captured the copy is
+    deferred (``pending``, see :meth:`FusedSGD.finish_capture`): the launch
+    recorded into the graph only needs the device address, and a host->device
+    copy cannot be captured.  The destination must come from ``reserved``
+    (allocated before the capture): a tensor allocated DURING the capture
+    lives in the graph's private pool, whose blocks the captured kernels
+    reuse for their own temporaries -- a replay would overwrite the table."""
+    if pending is None or not torch.cuda.is_current_stream_capturing():
+        return host.to(device)
+    for i, t in enumerate(reserved or []):
+        if t.shape == host.shape and t.dtype == host.dtype:
+            dev = reserved.pop(i)
+            break
+    else:
+        raise RuntimeError("FusedSGD: call prepare_capture() before capturing step() into a HIP graph")
+    pending.append((dev, host))
+    return dev
+
+
 class SgdTable:
-    def __init__(self, triples, device, keep_grads: bool = True):
+    @staticmethod
+    def table_shapes(ntensors: int):
+        """(bytes of the record table, entries of the block-start array)."""
+        return ctypes.sizeof(_SgdTensor) * ntensors, ntensors
+
+    def __init__(self, triples, device, keep_grads: bool = True, pending: list | None = None,
+                 reserved: list | None = None):
         L = _lib.lib()
         self.L = L
         recs, starts, nb = [], [], 0
@@ -69,8 +95,8 @@ class SgdTable:
         raw = (_SgdTensor * len(recs))(*[_SgdTensor(*r) for r in recs])
         host = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(raw), ctypes.sizeof(raw))),
                                 dtype=torch.uint8)
-        self.table = host.to(device)
-        self.starts = torch.tensor(starts, dtype=torch.int32, device=device)
+        self.table = _to_device(host, device, pending, reserved)
+        self.starts = _to_device(torch.tensor(starts, dtype=torch.int32), device, pending, reserved)
 
     def step(self, lr_dev, lr, momentum, weight_decay, grad_scale, nesterov, zero_grad=True, stream=None,
              batch_cursor=None, n_batches=1):
@@ -97,6 +123,10 @@ class FusedSGD(_TableMixin, torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, momentum=momentum, weight_decay=weight_decay, nesterov=nesterov))
         self._tables = None
         self._gptrs = None
+        self._pending: list = []
+        self._reserved: list = []
+        self._lr_dev: list | None = None  # per-group device learning rates of a captured step
+        self._lr_host: list = []
 
     def _build(self):
         self._tables = []
@@ -110,7 +140,39 @@ class FusedSGD(_TableMixin, torch.optim.Optimizer):
                     st["momentum_buffer"] = torch.zeros_like(p)
                 triples.append((p.data, p.grad, st.get("momentum_buffer")))
             dev = group["params"][0].device
-            self._tables.append(SgdTable(triples, dev, keep_grads=False))
+            self._tables.append(SgdTable(triples, dev, keep_grads=False, pending=self._pending,
+                                         reserved=self._reserved))
+
+    def prepare_capture(self):
+        """Before capturing :meth:`step` into a HIP graph: allocate (outside
+        the graph's memory pool) the launch tables the captured step will use."""
+        self._reserved = []
+        self._lr_dev, self._lr_host = [], []
+        for group in self.param_groups:
+            nbytes, nstarts = SgdTable.table_shapes(len(group["params"]))
+            dev = group["params"][0].device
+            self._reserved.append(torch.empty(nbytes, dtype=torch.uint8, device=dev))
+            self._reserved.append(torch.empty(nstarts, dtype=torch.int32, device=dev))
+            # the captured launch reads lr from device memory: LR schedules keep working
+            self._lr_dev.append(torch.full((1,), float(group["lr"]), dtype=torch.float32, device=dev))
+            self._lr_host.append(float(group["lr"]))
+
+    def sync_lr(self):
+        """Before replaying a captured step: push changed learning rates to
+        the device scalars the graph reads (momentum / weight decay / nesterov
+        are fixed at capture)."""
+        for i, group in enumerate(self.param_groups):
+            if self._lr_dev is not None and float(group["lr"]) != self._lr_host[i]:
+                self._lr_dev[i].fill_(float(group["lr"]))
+                self._lr_host[i] = float(group["lr"])
+
+    def finish_capture(self):
+        """After capturing :meth:`step` into a HIP graph: upload the launch
+        tables built during the capture (the graph's gradient tensors)."""
+        for dev, host in self._pending:
+            dev.copy_(host)
+        self._pending = []
+        self._reserved = []
 
     @torch.no_grad()
     def step(self, closure=None, grad_scale: float = 1.0, zero_grad: bool = False):
@@ -119,9 +181,10 @@ class FusedSGD(_TableMixin, torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         self._refresh()
-        for group, table in zip(self.param_groups, self._tables):
-            table.step(None, group["lr"], group["momentum"], group["weight_decay"], grad_scale, group["nesterov"],
-                       zero_grad=zero_grad)
+        capturing = self._lr_dev is not None and torch.cuda.is_current_stream_capturing()
+        for i, (group, table) in enumerate(zip(self.param_groups, self._tables)):
+            table.step(self._lr_dev[i] if capturing else None, group["lr"], group["momentum"],
+                       group["weight_decay"], grad_scale, group["nesterov"], zero_grad=zero_grad)
         return loss
 
     def zero_grad(self, set_to_none: bool = False):

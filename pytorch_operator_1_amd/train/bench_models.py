@@ -87,15 +87,29 @@ class CheckpointMixin:
             self.opt._step = int(meta["opt_step"])
         if hasattr(self.opt, "_tables"):
             self.opt._tables = None  # launch tables point at the old state tensors
+        if getattr(self, "_graph", None) is not None:  # a captured step holds the old addresses too
+            self._graph = None
+            self._eager_done = 0
         refresh = getattr(self.model, "refresh_transposed", None)
         if refresh is not None and getattr(self, "transposed_dgrad", False):
             refresh()
 
 
 class ResNetTrainer(CheckpointMixin):
+    """``graph`` (``PTO_STEP_GRAPH=1``): replay the whole step (forward,
+    loss, backward, FusedSGD) as ONE captured HIP graph after
+    ``EAGER_STEPS`` eager steps (MIOpen's solver search, library handles and
+    the optimizer state are created eagerly); single-process runs only
+    (``GradBucketer`` mode ``none``).  Off by default: at batch 256 the GPU
+    is never starved by the ~1,400 eager launches per step (26.74 vs 26.73
+    ms/step measured, profiles/resnet50_r5.md), so the graph buys nothing
+    here -- it is for smaller per-GPU batches, where launch latency shows."""
+
+    EAGER_STEPS = 2
+
     def __init__(self, device, batch_size: int = 256, image_size: int = 224, lr: float = 0.1,
                  momentum: float = 0.9, weight_decay: float = 1e-4, seed: int = 0, bucket_mb: float | None = None,
-                 force_ddp: bool = False):
+                 force_ddp: bool = False, graph: bool | None = None):
         from ..models.resnet import resnet50, synthetic_images
 
         torch.manual_seed(seed)
@@ -116,8 +130,42 @@ class ResNetTrainer(CheckpointMixin):
         self._loss = None
         self.steps_done = 0
         self.timer = StepTimer(device, enabled=False)
+        if graph is None:
+            graph = os.environ.get("PTO_STEP_GRAPH", "0") == "1"
+        self.use_graph = bool(graph) and device.type == "cuda" and self.bucketer.mode == "none"
+        self._graph = None
+        self._eager_done = 0
 
     def step(self):
+        if not self.use_graph or self._eager_done < self.EAGER_STEPS:
+            self._eager_step()
+            self._eager_done += 1
+            return
+        if self._graph is None:
+            self._capture()
+        self.opt.sync_lr()
+        self._graph.replay()
+        self.steps_done += 1
+
+    def _capture(self):
+        """Record one whole step into a HIP graph (nothing executes while
+        capturing: :meth:`step` replays it right after)."""
+        torch.cuda.synchronize(self.device)
+        self.bucketer.release()  # grads None: the captured backward allocates them in the graph's pool
+        self.opt.prepare_capture()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+                out = self.model(self.x)
+            loss = F.cross_entropy(out.float(), self.y)
+            loss.backward()
+            self.bucketer.finish()
+            self.opt.step(grad_scale=self.bucketer.grad_scale, zero_grad=self.bucketer.optimizer_zeroes_grads)
+        self.opt.finish_capture()  # the launch table of the graph's gradients
+        self._loss = loss.detach()
+        self._graph = g
+
+    def _eager_step(self):
         t = self.timer
         with t.phase("forward"), torch.autocast(device_type=self.device.type, dtype=torch.bfloat16):
             out = self.model(self.x)
@@ -145,7 +193,9 @@ class ResNetTrainer(CheckpointMixin):
 
     def describe(self) -> dict:
         return {"model": "resnet50 (v1.5, 25.6M params)", "input_shape": [3, 224, 224],
-                "optimizer": "SGD momentum=0.9 wd=1e-4 (FusedSGD HIP)", "amp": "bf16 autocast, fp32 master"}
+                "optimizer": "SGD momentum=0.9 wd=1e-4 (FusedSGD HIP)", "amp": "bf16 autocast, fp32 master",
+                "step": (f"whole step replayed as one HIP graph (after {self.EAGER_STEPS} eager steps)"
+                         if self.use_graph else "eager")}
 
 
 class LlamaTrainer(CheckpointMixin):

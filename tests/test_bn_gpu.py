@@ -98,9 +98,10 @@ def test_resnet_fused_bn_grads_match_stock_bn():
 
 @pytest.mark.parametrize("down", [False, True])
 def test_conv1x1_gemm_bottleneck_matches_miopen(down):
-    """ops/conv1x1.py: in an identity bottleneck, bn3's residual gradient
-    folded into conv1's input-gradient GEMM instead of autograd's add (a
-    downsample block keeps the stock path).  Every gradient (input included)
+    """ops/conv1x1.py: the block's 1x1 convs with GEMM input gradients and
+    split-K fp32 weight gradients; in an identity bottleneck bn3's residual
+    gradient folded into conv1's input-gradient GEMM instead of autograd's
+    add.  Every gradient (input included)
     under bf16 autocast must be as close to an fp32 run as the stock path's
     (PTO_CONV1X1_GEMM=0) is."""
     import os
@@ -166,3 +167,71 @@ def test_conv1x1_res_fp32_matches_conv_plus_residual():
     assert relerr(x.grad, x2.grad + res) < 1e-5
     assert relerr(gw, conv.weight.grad) < 1e-5
     assert gw.stride() == conv.weight.stride()
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_conv1x1_matches_fp32_conv(stride):
+    """ops/conv1x1.py conv1x1 in fp32 (stride 1 and the strided downsample
+    form): output, input and weight gradients equal F.conv2d's."""
+    import torch.nn as nn
+
+    from pytorch_operator_1_amd.ops.conv1x1 import conv1x1
+
+    torch.manual_seed(stride)
+    conv = nn.Conv2d(48, 80, 1, stride=stride, bias=False).to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(2, 48, 15, 14, device=DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    x2 = x.detach().clone().requires_grad_(True)
+    y = conv1x1(x, conv)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    gw = conv.weight.grad.clone()
+    conv.weight.grad = None
+    y2 = conv(x2)
+    y2.backward(dy)
+    assert y.shape == y2.shape and relerr(y, y2) < 1e-5
+    assert relerr(x.grad, x2.grad) < 1e-5
+    assert relerr(gw, conv.weight.grad) < 1e-5 and gw.stride() == conv.weight.stride()
+
+
+@pytest.mark.parametrize("M,co,ci", [(6272, 64, 256), (12544, 512, 128), (1000, 40, 96)])
+def test_splitk_weight_grad_matches_fp32(M, co, ci):
+    """ops/conv1x1.py weight_grad_1x1: S batched GEMMs over K = N*H*W with
+    fp32 outputs, summed, vs an fp32 matmul of the same bf16 values."""
+    from pytorch_operator_1_amd.ops.conv1x1 import _splitk, weight_grad_1x1
+
+    torch.manual_seed(M)
+    dy = torch.randn(M, co, device=DEV).bfloat16()
+    x = torch.randn(M, ci, device=DEV).bfloat16()
+    got = weight_grad_1x1(dy, x)
+    assert got.dtype == torch.float32 and got.shape == (co, ci)
+    assert (_splitk(M) > 1) == (M >= 6272)
+    assert relerr(got, dy.float().t() @ x.float()) < 1e-5
+
+
+@pytest.mark.parametrize("shape,k,s,p", [((4, 64, 112, 112), 3, 2, 1), ((3, 16, 7, 9), 3, 2, 1),
+                                         ((2, 8, 10, 10), 2, 2, 0), ((2, 24, 9, 8), 3, 1, 1)])
+def test_maxpool_matches_fp32_reference(shape, k, s, p):
+    """HIP max pool (ops/pool.py) vs F.max_pool2d in fp32 on the same bf16
+    values: forward bitwise (a max selects an input), backward through the
+    argmax codes -- including ties (coarsely quantised inputs: the first
+    maximum wins, as in torch) and windows whose taps overlap."""
+    from pytorch_operator_1_amd.ops.pool import _MaxPool, maxpool_supported
+
+    torch.manual_seed(sum(shape) + k)
+    x = (torch.randint(-4, 5, shape, device=DEV).float() / 2).bfloat16().contiguous(memory_format=torch.channels_last)
+    assert maxpool_supported(x, k, s, p)
+    xr = x.float().detach().requires_grad_(True)
+    yr = F.max_pool2d(xr, k, s, p)
+    xh = x.detach().requires_grad_(True)
+    yh = _MaxPool.apply(xh, k, s, p)
+    assert yh.shape == yr.shape and yh.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(yh.float(), yr.detach())
+    g = torch.randn_like(yr).bfloat16()
+    yr.backward(g.float())
+    yh.backward(g)
+    assert xh.grad.dtype == torch.bfloat16
+    torch.testing.assert_close(xh.grad.float(), xr.grad.bfloat16().float(), rtol=1e-2, atol=1e-2)
+    # NaN propagates like torch
+    xn = x.clone()
+    xn[0, 0, 1, 1] = float("nan")
+    assert torch.equal(torch.isnan(_MaxPool.apply(xn, k, s, p).float()), torch.isnan(F.max_pool2d(xn.float(), k, s, p)))

@@ -220,13 +220,55 @@ def test_llama_trainer_learns_and_native_lib_loaded():
 def test_resnet_trainer_steps():
     from pytorch_operator_1_amd.train.bench_models import ResNetTrainer
 
-    tr = ResNetTrainer(torch.device(DEV), batch_size=8, image_size=64, lr=0.05)
+    tr = ResNetTrainer(torch.device(DEV), batch_size=8, image_size=64, lr=0.05, graph=False)
     tr.run(6)
     torch.cuda.synchronize()
     assert tr.last_loss() == tr.last_loss()  # finite
     w = tr.model.fc.weight
     # single process: gradients are autograd's own tensors, dropped after the fused step
     assert tr.bucketer.mode == "none" and w.grad is None
+
+
+def test_resnet_graph_step_matches_eager():
+    """The whole-step HIP graph (forward, loss, backward, FusedSGD captured
+    once, replayed per step) trains like the eager step.  MIOpen's
+    weight-gradient solvers accumulate with atomics, so two EAGER runs
+    already differ; the graph run must stay within the same spread
+    (per tensor, distance relative to how far training moved it).  Then: a
+    learning-rate change reaches the replayed step (device-resident lr), and
+    the launch table lives outside the graph's memory pool."""
+    from pytorch_operator_1_amd.train.bench_models import ResNetTrainer
+
+    def run(graph):
+        tr = ResNetTrainer(torch.device(DEV), batch_size=8, image_size=64, lr=0.02, seed=3, graph=graph)
+        init = {k: v.detach().float().clone() for k, v in tr.model.state_dict().items()}
+        tr.run(6)
+        torch.cuda.synchronize()
+        assert (tr._graph is not None) == graph and tr.steps_done == 6
+        return tr, init, {k: v.detach().float().clone() for k, v in tr.model.state_dict().items()}
+
+    _, init, a = run(False)
+    _, _, b = run(False)
+    tr, _, c = run(True)
+    d_ee, d_ge = [], []
+    for k in a:
+        if not a[k].is_floating_point():
+            assert torch.equal(a[k], c[k]), k  # num_batches_tracked: the graph's kernel counts replays
+            continue
+        moved = (a[k] - init[k]).norm().item() + 1e-12
+        d_ee.append((b[k] - a[k]).norm().item() / moved)
+        d_ge.append((c[k] - a[k]).norm().item() / moved)
+    mean = lambda v: sum(v) / len(v)  # noqa: E731
+    assert mean(d_ge) <= 2.0 * mean(d_ee) + 0.02, (mean(d_ge), mean(d_ee))
+    assert tr.opt._pending == [] and tr.opt._reserved == []
+    # lr = 0 through the device scalar: the replayed SGD leaves every weight alone
+    for g in tr.opt.param_groups:
+        g["lr"] = 0.0
+    before = {n: p.detach().clone() for n, p in tr.model.named_parameters()}
+    tr.step()
+    torch.cuda.synchronize()
+    for n, p in tr.model.named_parameters():
+        assert torch.equal(p.detach(), before[n]), n
 
 
 @pytest.mark.parametrize("model,extra", [("llama3-tiny", ["--seq-len", "256"]),

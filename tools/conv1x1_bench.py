@@ -57,7 +57,13 @@ def main():
         r["miopen_wgrad"] = timeit(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False]))
         r["gemm_wgrad"] = timeit(lambda: torch.mm(dy2.t(), x2))
-        r["gemm_wgrad_f32out"] = timeit(lambda: torch.mm(dy2.t().float(), x2.float()) if False else torch.mm(x2.t(), dy2))
+        r["gemm_wgrad_f32out"] = timeit(lambda: torch.mm(x2.t(), dy2))
+        M = x2.shape[0]
+        for S in (16, 64, 256):  # split-K over the N*H*W rows: S batched GEMMs, fp32 out, then the sum
+            if M % S:
+                continue
+            dyb, xb = dy2.view(S, M // S, co).transpose(1, 2), x2.view(S, M // S, ci)
+            r[f"bmm_wgrad_s{S}"] = timeit(lambda: torch.bmm(dyb, xb, out_dtype=torch.float32).sum(0))
         print(json.dumps(r), flush=True)
 
 

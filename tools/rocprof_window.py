@@ -22,6 +22,7 @@ def main():
     p.add_argument("--marker", required=True, help="substring of the kernel that ends each step")
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--top", type=int, default=30)
+    p.add_argument("--seq", action="store_true", help="also list the last step's dispatches in order")
     a = p.parse_args()
     import sqlite3
     import glob
@@ -49,6 +50,13 @@ def main():
     for name, (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top]:
         nm = name if len(name) <= 100 else name[:100] + "…"
         print(f"| `{nm}` | {n / a.steps:.1f} | {t / 1e6 / a.steps:.3f} | {100 * t / busy:.1f} |")
+    if a.seq:  # the last step in dispatch order: who runs next to whom
+        print("\n| # | kernel | us | gap before (us) |\n|---:|---|---:|---:|")
+        last = rows[marks[-2] + 1:marks[-1] + 1]
+        prev_end = last[0][1]
+        for i, (name, s, e) in enumerate(last):
+            print(f"| {i} | `{name[:90]}` | {(e - s) / 1e3:.1f} | {(s - prev_end) / 1e3:.1f} |")
+            prev_end = e
 
 
 if __name__ == "__main__":
