@@ -50,6 +50,15 @@ class Bottleneck(nn.Module):
             y = self.bn1(conv1x1_res(x, self.conv1, stash), relu=True)
             y = self.bn2(self.conv2(y), relu=True)
             return self.bn3(self._c1(self.conv3, y), residual=x, relu=True, stash=stash)
+        if (self.downsample is not None and gemm_supported(x, self.downsample[0])
+                and gemm_supported(x, self.conv1)):
+            # both 1x1 convs read x: one input gradient, the second GEMM
+            # accumulating onto the first (no autograd add)
+            merge = GradStash()
+            idt = self.downsample[1](conv1x1(x, self.downsample[0], merge))
+            y = self.bn1(conv1x1(x, self.conv1, merge), relu=True)
+            y = self.bn2(self.conv2(y), relu=True)
+            return self.bn3(self._c1(self.conv3, y), residual=idt, relu=True)
         idt = x if self.downsample is None else self.downsample[1](self._c1(self.downsample[0], x))
         y = self.bn1(self._c1(self.conv1, x), relu=True)
         y = self.bn2(self.conv2(y), relu=True)

@@ -97,13 +97,13 @@ class _Conv1x1(torch.autograd.Function):
     gradient in fp32 (from the strided sub-grid of x at s > 1)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stash, dtype, stride=1):
+    def forward(ctx, x, weight, stash, dtype, stride=1, merge=None):
         x = x.to(dtype).contiguous(memory_format=_CL)
         wb = weight.to(dtype)
         if wb.dim() == 4 and not wb.is_contiguous(memory_format=_CL):
             wb = wb.contiguous(memory_format=_CL)
         ctx.save_for_backward(x, wb)
-        ctx.stash, ctx.wdtype, ctx.stride = stash, weight.dtype, stride
+        ctx.stash, ctx.wdtype, ctx.stride, ctx.merge = stash, weight.dtype, stride, merge
         ctx.wshape, ctx.wstride = weight.shape, weight.stride()
         return F.conv2d(x, wb, stride=stride)
 
@@ -128,35 +128,51 @@ class _Conv1x1(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             w2 = wb.reshape(co, ci)
-            extra = ctx.stash.take() if ctx.stash is not None else None
-            if extra is not None:
-                g = extra.to(dy2.dtype).contiguous(memory_format=_CL)
-                dx2 = g.permute(0, 2, 3, 1).reshape(-1, ci).addmm_(dy2, w2)  # dX = g_res + dY W, in place
+            base = ctx.stash.take() if ctx.stash is not None else None
+            first = False
+            if ctx.merge is not None:  # a sibling conv reads the same x (downsample block)
+                sib = ctx.merge.take()
+                first = sib is None
+                base = base if first else sib
+            if base is not None:
+                base = base.to(dy2.dtype).contiguous(memory_format=_CL)
+            if s == 1 and base is not None:
+                dx2 = base.permute(0, 2, 3, 1).reshape(-1, ci).addmm_(dy2, w2)  # dX = base + dY W, in place
+                dx = dx2.view(N, H, W, ci).permute(0, 3, 1, 2)
             else:
-                dx2 = torch.mm(dy2, w2)
-            dx = dx2.view(N, H, W, ci).permute(0, 3, 1, 2)
-            if s > 1:
-                full = torch.zeros_like(xfull, memory_format=_CL)
-                full[:, :, ::s, ::s] = dx
-                dx = full
+                dx = torch.mm(dy2, w2).view(N, H, W, ci).permute(0, 3, 1, 2)
+                if s > 1:
+                    full = base if base is not None else torch.zeros_like(xfull, memory_format=_CL)
+                    if base is not None:
+                        full[:, :, ::s, ::s] += dx
+                    else:
+                        full[:, :, ::s, ::s] = dx
+                    dx = full
+            if first:  # the sibling's backward adds its own part onto this one
+                ctx.merge.put(dx)
+                dx = None
         elif ctx.stash is not None:
             ctx.stash.take()
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 def _dtype(x):
     return torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
 
 
-def conv1x1(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+def conv1x1(x: torch.Tensor, conv: nn.Conv2d, merge: GradStash | None = None) -> torch.Tensor:
     """``conv(x)`` for a 1x1 bias-free conv, any equal stride (see
-    :class:`_Conv1x1`).  Dtype: the autocast dtype when autocast is on, else
-    x's."""
+    :class:`_Conv1x1`).  ``merge``: shared with the one other conv1x1 that
+    reads the same ``x`` (a downsample block's conv1 and downsample conv):
+    whichever backward runs second accumulates its input gradient onto the
+    first one's (GEMM beta = 1, or a strided in-place add) instead of
+    autograd adding the two.  Dtype: the autocast dtype when autocast is on,
+    else x's."""
     if not gemm_supported(x, conv):
         raise ValueError("conv1x1: needs a 1x1 bias-free conv on a HIP tensor")
     dtype = _dtype(x)
     with torch.autocast("cuda", enabled=False):
-        return _Conv1x1.apply(x, conv.weight, None, dtype, conv.stride[0])
+        return _Conv1x1.apply(x, conv.weight, None, dtype, conv.stride[0], merge)
 
 
 def conv1x1_res(x: torch.Tensor, conv: nn.Conv2d, stash: GradStash) -> torch.Tensor:
@@ -166,4 +182,4 @@ def conv1x1_res(x: torch.Tensor, conv: nn.Conv2d, stash: GradStash) -> torch.Ten
         raise ValueError("conv1x1_res: needs a 1x1 stride-1 bias-free conv on a HIP tensor")
     dtype = _dtype(x)
     with torch.autocast("cuda", enabled=False):
-        return _Conv1x1.apply(x, conv.weight, stash, dtype, 1)
+        return _Conv1x1.apply(x, conv.weight, stash, dtype, 1, None)

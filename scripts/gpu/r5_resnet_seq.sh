@@ -15,3 +15,6 @@ timeout -k 10 400 rocprofv3 --kernel-trace -d /tmp/prof_rs -o run -- python3 "$R
 grep '^{' $O/prof.log | cut -c1-200
 python3 "$R/tools/rocprof_window.py" /tmp/prof_rs --marker sgd --steps 2 --top 45 --seq > $O/window.md
 head -30 $O/window.md
+cd "$R"
+timeout -k 10 400 python bench.py --model resnet50 --steps 20 --warmup 5 --no-latency --force-ddp > $O/bench_ddp.json 2> $O/bench_ddp.err || { tail -20 $O/bench_ddp.err; exit 1; }
+cut -c1-300 $O/bench_ddp.json

@@ -96,12 +96,13 @@ def test_resnet_fused_bn_grads_match_stock_bn():
     assert not worse, worse[:5]
 
 
-@pytest.mark.parametrize("down", [False, True])
-def test_conv1x1_gemm_bottleneck_matches_miopen(down):
+@pytest.mark.parametrize("down,stride", [(False, 1), (True, 1), (True, 2)])
+def test_conv1x1_gemm_bottleneck_matches_miopen(down, stride):
     """ops/conv1x1.py: the block's 1x1 convs with GEMM input gradients and
     split-K fp32 weight gradients; in an identity bottleneck bn3's residual
     gradient folded into conv1's input-gradient GEMM instead of autograd's
-    add.  Every gradient (input included)
+    add; in a downsample block (stride 1 or 2) the two 1x1 convs' input
+    gradients merged into one tensor.  Every gradient (input included)
     under bf16 autocast must be as close to an fp32 run as the stock path's
     (PTO_CONV1X1_GEMM=0) is."""
     import os
@@ -110,11 +111,12 @@ def test_conv1x1_gemm_bottleneck_matches_miopen(down):
 
     torch.manual_seed(0)
     cin = 128 if down else 256
-    blocks = [Bottleneck(cin, 64, stride=1, down=down).to(DEV, memory_format=torch.channels_last) for _ in range(3)]
+    blocks = [Bottleneck(cin, 64, stride=stride, down=down).to(DEV, memory_format=torch.channels_last)
+              for _ in range(3)]
     for b in blocks[1:]:
         b.load_state_dict(blocks[0].state_dict())
     x0 = torch.randn(4, cin, 28, 28, device=DEV).contiguous(memory_format=torch.channels_last)
-    dout = torch.randn(4, 256, 28, 28, device=DEV).contiguous(memory_format=torch.channels_last)
+    dout = torch.randn(4, 256, 28 // stride, 28 // stride, device=DEV).contiguous(memory_format=torch.channels_last)
     grads = []
     for blk, mode in zip(blocks, ("gemm", "miopen", "fp32")):
         os.environ["PTO_CONV1X1_GEMM"] = "0" if mode == "miopen" else "1"
