@@ -126,6 +126,13 @@ def _emit(line: str):
     os.write(fd, (line + "\n").encode())
 
 
+def _xgmi_failure(e: BaseException) -> bool:
+    """A failure of the peer-memory exchange (bounded spin timed out, ranks'
+    parameter hashes diverged) -- the cases the RCCL schedule can stand in for."""
+    names = {c.__name__ for c in type(e).__mro__}
+    return bool(names & {"XgmiTimeout", "XgmiDivergence"}) or "xgmi" in str(e).lower()
+
+
 def main(argv=None):
     args = parse_args(argv)
     rc = _launch_ranks(args, argv)
@@ -169,25 +176,69 @@ def main(argv=None):
         if device.type == "cuda":
             torch.cuda.synchronize(device)
 
-    run = getattr(trainer, "run", None) or (lambda n: [trainer.step() for _ in range(n)])
-    run(args.warmup)
-    # graph capture is setup, never timed: a warm-up of 0 or 1 step (the
-    # first step runs eagerly) would otherwise leave it to the timed run()
-    getattr(trainer, "prepare", lambda: None)()
-    sync()
-    pdist.barrier(device)
-    sync()
-    t0 = time.perf_counter()
-    run(args.steps)  # exactly K optimizer steps
-    # the fused-optimizer schedule applies conv1's update of step i inside
-    # step i+1's launches: commit the last one inside the timed region so it
-    # holds K complete updates
-    getattr(trainer, "flush", lambda: None)()
-    sync()
-    pdist.barrier(device)
-    sync()
-    elapsed = time.perf_counter() - t0
-    elapsed = pdist.all_reduce_max(elapsed, device)
+    injected = []
+
+    def measure(trainer):
+        """Warm-up, then EXACTLY K timed steps; (elapsed, None), or (None,
+        reason) when the peer-memory exchange failed.  Its failures reach
+        every rank (a rank whose peer stopped times out waiting for it; the
+        parameter-hash check runs on all of them), and the status all-reduces
+        double as the timing barriers, so the ranks leave together."""
+        run = getattr(trainer, "run", None) or (lambda n: [trainer.step() for _ in range(n)])
+        status, reason = 0.0, None
+        try:
+            if os.environ.get("PTO_BENCH_INJECT_XGMI_FAILURE") in ("all", str(env.rank)) and not injected:
+                injected.append(1)  # test hook: the exchange "times out" once
+                from pytorch_operator_1_amd.parallel.xgmi import XgmiTimeout
+
+                raise XgmiTimeout("injected by PTO_BENCH_INJECT_XGMI_FAILURE")
+            run(args.warmup)
+            # graph capture is setup, never timed: a warm-up of 0 or 1 step (the
+            # first step runs eagerly) would otherwise leave it to the timed run()
+            getattr(trainer, "prepare", lambda: None)()
+            sync()
+        except Exception as e:  # noqa: BLE001 - only comm failures are handled
+            if not _xgmi_failure(e):
+                raise
+            status, reason = 1.0, f"warm-up: {type(e).__name__}: {e}"[:300]
+        if pdist.all_reduce_max(status, device):  # also the barrier before the timed region
+            return None, reason or "a peer rank's exchange failed"
+        sync()
+        t0 = time.perf_counter()
+        try:
+            run(args.steps)  # exactly K optimizer steps
+            # the fused-optimizer schedule applies conv1's update of step i inside
+            # step i+1's launches: commit the last one inside the timed region so it
+            # holds K complete updates
+            getattr(trainer, "flush", lambda: None)()
+            sync()
+        except Exception as e:  # noqa: BLE001
+            if not _xgmi_failure(e):
+                raise
+            status, reason = 1.0, f"timed run: {type(e).__name__}: {e}"[:300]
+        if pdist.all_reduce_max(status, device):  # the barrier after it
+            return None, reason or "a peer rank's exchange failed"
+        sync()
+        elapsed = time.perf_counter() - t0
+        return pdist.all_reduce_max(elapsed, device), None
+
+    def make():
+        return build_trainer(args.impl, device=device, batch_size=args.batch_size, lr=args.lr,
+                             momentum=args.momentum, dataset_size=args.dataset_size,
+                             seed=1, rank=env.rank, **data_kw)
+
+    elapsed, failed = measure(trainer)
+    if elapsed is None:
+        # the xGMI schedule failed mid-run (bounded spin timed out, or the
+        # in-graph parameter hashes of the ranks diverged): report the RCCL
+        # schedule's number instead of none, and say so in the JSON
+        print(f"[bench] xGMI exchange failed ({failed}); re-measuring on the RCCL schedule", file=sys.stderr)
+        os.environ["PTO_COMM"] = "rccl"
+        trainer = make()
+        elapsed, again = measure(trainer)
+        if elapsed is None:
+            raise SystemExit(f"[bench] the RCCL schedule failed too: {again}")
+    run = None
     loss = trainer.last_loss()
     # evidence of the world that was measured (outside the timed region):
     # the ranks, their devices and transports, and whether the replicas
@@ -196,6 +247,8 @@ def main(argv=None):
     identical = pdist.ranks_bit_identical(_param_tensors(trainer), device)
     comm = dict(getattr(trainer, "comm_info", None) or {})
     comm.update(world)
+    if failed:
+        comm["xgmi_failed_fell_back_to_rccl"] = failed
 
     n = env.world_size
     ms_per_step = elapsed / args.steps * 1e3

@@ -117,3 +117,23 @@ def test_params_fingerprint_is_bit_exact():
     c = [a[0].flip(0), a[1]]
     assert params_fingerprint(a) != params_fingerprint(c)
     assert params_fingerprint(a, chunk=64) == params_fingerprint(a)
+
+
+def test_bench_falls_back_to_rccl_when_xgmi_fails():
+    """N > 1: when the peer-memory exchange fails (a bounded spin timing
+    out, or diverged parameter hashes -- both seen by every rank, since the
+    peers wait on / compare each other; injected here on all ranks), the
+    ranks agree through the status all-reduces that double as the timing
+    barriers, the job is re-measured on the RCCL schedule and the JSON says
+    so instead of losing the data point."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                                                            "LOCAL_RANK")}
+    env.update(OMP_NUM_THREADS="2", PTO_BENCH_INJECT_XGMI_FAILURE="all")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--gpus", "2", "--steps", "4", "--warmup", "1",
+           "--dataset-size", "640", "--no-latency"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = json.loads([line for line in out.stdout.splitlines() if line.startswith("{")][0])
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert "injected" in d["config"]["grad_allreduce"]["xgmi_failed_fell_back_to_rccl"]
+    assert "re-measuring on the RCCL schedule" in out.stderr
