@@ -252,6 +252,72 @@ __global__ __launch_bounds__(NT) void k_swiglu_bwd(const uint16_t* __restrict__ 
   }
 }
 
+// SwiGLU backward that ALSO writes the gradient transposed, dgu_t [2F][M]:
+// what the gate|up projection's K-contiguous weight gradient consumes
+// (ops/llm.py _LinearTW, dW = dgu^T X from K(token)-contiguous operands), so
+// the step no longer transposes the largest activation gradient of the MLP
+// ([16384 x 28672] per layer on Llama-3-8B) in a pass of its own.  Block =
+// 64 tokens x 64 features: each thread computes 2 tokens x 8 features of dg
+// and du, stores them row-major as k_swiglu_bwd, and drops them into two LDS
+// tiles [feature][token] (row pitch 66 halves: the paired-token 32-bit
+// writes of a wave spread over the banks); the transposed rows then leave as
+// 16-byte stores, 128 contiguous bytes per feature row and tile.
+constexpr int SWT = 64;       // tokens and features per block
+constexpr int SWT_LD = 66;    // LDS row pitch (halves)
+__global__ __launch_bounds__(NT) void k_swiglu_bwd_t(const uint16_t* __restrict__ gu, const uint16_t* __restrict__ dout,
+                                                     uint16_t* __restrict__ dgu, uint16_t* __restrict__ dgu_t,
+                                                     long long M, int F) {
+  __shared__ __attribute__((aligned(16))) uint16_t tg[SWT * SWT_LD], tu[SWT * SWT_LD];
+  const int ntf = F / SWT;
+  const long long m0 = (long long)(blockIdx.x / ntf) * SWT;
+  const int f0 = (blockIdx.x % ntf) * SWT;
+  const int t = threadIdx.x, fg = t & 7, tp = t >> 3;  // 8 features at 8*fg, tokens 2tp, 2tp+1
+  const int c = f0 + 8 * fg;
+  V8 dg[2], du[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const long long m = m0 + 2 * tp + k;
+    const bool ok = m < M;
+    const long long mm = ok ? m : m0;
+    const V8 g = ld8(gu + mm * 2 * F + c), u = ld8(gu + mm * 2 * F + F + c), d = ld8(dout + mm * F + c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float sg = sigmoidf(g.v[e]);  // the same expressions as k_swiglu_bwd (bit-equal dgu)
+      const float silu = g.v[e] * sg;
+      du[k].v[e] = d.v[e] * silu;
+      dg[k].v[e] = d.v[e] * u.v[e] * sg * (1.f + g.v[e] * (1.f - sg));
+    }
+    if (ok) {
+      st8(dgu + m * 2 * F + c, dg[k]);
+      st8(dgu + m * 2 * F + F + c, du[k]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {  // the token pair as one 32-bit word per feature
+    const int row = (8 * fg + e) * SWT_LD + 2 * tp;
+    *reinterpret_cast<uint32_t*>(tg + row) = (uint32_t)f2bf(dg[0].v[e]) | ((uint32_t)f2bf(dg[1].v[e]) << 16);
+    *reinterpret_cast<uint32_t*>(tu + row) = (uint32_t)f2bf(du[0].v[e]) | ((uint32_t)f2bf(du[1].v[e]) << 16);
+  }
+  __syncthreads();
+  // 2 x 64 feature rows x 8 chunks of 8 tokens = 1024 16-byte stores, 4 per thread
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int idx = t + NT * q, half = idx >> 9, r = (idx >> 3) & 63, ch = idx & 7;
+    const uint16_t* src = (half ? tu : tg) + r * SWT_LD + 8 * ch;
+    const long long m = m0 + 8 * ch;
+    if (m >= M) continue;
+    const long long orow = (long long)(half ? F : 0) + f0 + r;
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = *reinterpret_cast<const uint32_t*>(src + 2 * j);
+    if (m + 8 <= M) {
+      *reinterpret_cast<uint4*>(dgu_t + orow * M + m) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      for (int j = 0; j < 8 && m + j < M; ++j) dgu_t[orow * M + m + j] = src[j];
+    }
+  }
+}
+
 // ---------------------------------------------------------------- RoPE
 // qkv row m = (b*S + s) has nh heads of D at stride row_stride; rotate the
 // first nrot heads (q and k).  rotate_half convention: pairs (i, i + D/2).
@@ -471,6 +537,17 @@ PTO_API int pto_swiglu_bwd(const void* gu, const void* dout, void* dgu, long lon
   if (F % 8) return -1;
   hipLaunchKernelGGL(k_swiglu_bwd, dim3(grid_for(M * (F / 8))), dim3(NT), 0, s, (const uint16_t*)gu,
                      (const uint16_t*)dout, (uint16_t*)dgu, M, F);
+  return (int)hipGetLastError();
+}
+
+// dgu_t: [2F][M] (row stride M, M % 8 == 0 for the vector stores' alignment).
+PTO_API int pto_swiglu_bwd_t(const void* gu, const void* dout, void* dgu, void* dgu_t, long long M, int F,
+                             hipStream_t s) {
+  if (F % SWT || M < 1 || M % 8 || (((uintptr_t)dgu_t) & 15)) return -1;
+  const long long blocks = ((M + SWT - 1) / SWT) * (F / SWT);
+  if (blocks > 0x7fffffff) return -1;
+  hipLaunchKernelGGL(k_swiglu_bwd_t, dim3((unsigned)blocks), dim3(NT), 0, s, (const uint16_t*)gu,
+                     (const uint16_t*)dout, (uint16_t*)dgu, (uint16_t*)dgu_t, M, F);
   return (int)hipGetLastError();
 }
 

@@ -125,7 +125,11 @@ class LlamaBlock(nn.Module):
             ctx = self._attend(qkv, B, S)
         attn = _lin(ctx, self.wo)
         h, y = llm.add_rmsnorm(h, attn, self.ffn_norm, c.norm_eps)
-        mlp = _lin(llm.swiglu(_lin(y, self.w13)), self.w2)
+        # the SwiGLU backward hands w13's weight gradient its output
+        # gradient already transposed (ops/llm.py TStash)
+        st = llm.TStash() if getattr(self.w13, "dw_kcontig", False) and os.environ.get("PTO_SWIGLU_T", "1") == "1" \
+            else None
+        mlp = _lin(llm.swiglu(_lin(y, self.w13, st), st), self.w2)
         return h, mlp
 
     def forward_torch(self, h, delta, rope, B, S):
@@ -148,7 +152,7 @@ class LlamaBlock(nn.Module):
         return h, mlp
 
 
-def _lin(x, mod: nn.Linear):
+def _lin(x, mod: nn.Linear, tstash=None):
     """Bias-free linear; with a transposed weight copy attached
     (:meth:`Llama.enable_transposed_dgrad`) the input gradient uses it."""
     wt = getattr(mod, "weight_t", None)
@@ -156,7 +160,7 @@ def _lin(x, mod: nn.Linear):
         return F.linear(x, mod.weight)
     from ..ops import llm
 
-    return llm.linear_tw(x, mod.weight, wt, getattr(mod, "dw_kcontig", False))
+    return llm.linear_tw(x, mod.weight, wt, getattr(mod, "dw_kcontig", False), tstash)
 
 
 def _rmsnorm_ref(x, w, eps):

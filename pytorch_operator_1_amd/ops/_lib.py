@@ -123,6 +123,7 @@ _SIGS = {
     "pto_rmsnorm_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
     "pto_swiglu_fwd": [_P, _P, _L, _I, _P],
     "pto_swiglu_bwd": [_P, _P, _P, _L, _I, _P],
+    "pto_swiglu_bwd_t": [_P, _P, _P, _P, _L, _I, _P],
     "pto_rope": [_P, _P, _P, _P, _L, _I, _I, _I, _I, _L, _I, _P],
     "pto_ce_fwd": [_P, _P, _P, _P, _L, _I, _L, _P],
     "pto_ce_bwd": [_P, _P, _P, _P, _L, _I, _L, _P],

@@ -82,9 +82,25 @@ def rmsnorm(x, weight, eps: float = 1e-5):
     return _AddRMSNorm.apply(x, None, weight, eps)
 
 
+class TStash:
+    """A gradient handed TRANSPOSED from one backward node to the next: the
+    SwiGLU backward writes d(gate|up)^T while it computes d(gate|up), and the
+    gate|up projection's K-contiguous weight gradient (:class:`_LinearTW`)
+    takes it instead of transposing the [tokens x 2F] gradient itself."""
+
+    __slots__ = ("t",)
+
+    def __init__(self):
+        self.t = None
+
+    def take(self):
+        t, self.t = self.t, None
+        return t
+
+
 class _SwiGLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, gu):
+    def forward(ctx, gu, tstash=None):
         gu = _req(gu, "swiglu")
         F2 = gu.shape[-1]
         M = gu.numel() // F2
@@ -92,6 +108,7 @@ class _SwiGLU(torch.autograd.Function):
         _lib.check(_lib.lib().pto_swiglu_fwd(gu.data_ptr(), out.data_ptr(), M, F2 // 2, _lib.stream_ptr(gu.device)),
                    "swiglu_fwd")
         ctx.save_for_backward(gu)
+        ctx.tstash = tstash
         return out
 
     @staticmethod
@@ -101,14 +118,23 @@ class _SwiGLU(torch.autograd.Function):
         M = gu.numel() // F2
         dout = dout.contiguous()
         dgu = torch.empty_like(gu)
-        _lib.check(_lib.lib().pto_swiglu_bwd(gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), M, F2 // 2,
-                                             _lib.stream_ptr(gu.device)), "swiglu_bwd")
-        return dgu
+        st = ctx.tstash
+        if st is not None and M % 8 == 0 and (F2 // 2) % 64 == 0:
+            dgu_t = torch.empty(F2, M, device=gu.device, dtype=gu.dtype)
+            _lib.check(_lib.lib().pto_swiglu_bwd_t(gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), dgu_t.data_ptr(),
+                                                   M, F2 // 2, _lib.stream_ptr(gu.device)), "swiglu_bwd_t")
+            st.t = dgu_t
+        else:
+            _lib.check(_lib.lib().pto_swiglu_bwd(gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), M, F2 // 2,
+                                                 _lib.stream_ptr(gu.device)), "swiglu_bwd")
+        return dgu, None
 
 
-def swiglu(gu):
-    """``silu(gu[..., :F]) * gu[..., F:]`` for the fused gate|up projection."""
-    return _SwiGLU.apply(gu)
+def swiglu(gu, tstash: TStash | None = None):
+    """``silu(gu[..., :F]) * gu[..., F:]`` for the fused gate|up projection.
+    ``tstash``: also hand the transposed input gradient to the producer of
+    ``gu`` (see :class:`TStash`)."""
+    return _SwiGLU.apply(gu, tstash)
 
 
 class _RoPE(torch.autograd.Function):
@@ -271,9 +297,9 @@ class _LinearTW(torch.autograd.Function):
     (profiles/llama8b_step_rocprof.md)."""
 
     @staticmethod
-    def forward(ctx, x, w, wt, dw_kcontig):
+    def forward(ctx, x, w, wt, dw_kcontig, tstash=None):
         ctx.save_for_backward(x, wt)
-        ctx.dw_kcontig = dw_kcontig
+        ctx.dw_kcontig, ctx.tstash = dw_kcontig, tstash
         return torch.nn.functional.linear(x, w)
 
     @staticmethod
@@ -291,16 +317,19 @@ class _LinearTW(torch.autograd.Function):
                 # 0.38 + 0.14 ms at 4x4096 tokens)
                 xt = transpose_into(x2.contiguous(), torch.empty(x2.shape[1], x2.shape[0], device=x2.device,
                                                                   dtype=x2.dtype))
-                dyt = transpose_into(dy2.contiguous(), torch.empty(dy2.shape[1], dy2.shape[0], device=dy2.device,
-                                                                    dtype=dy2.dtype))
+                dyt = ctx.tstash.take() if ctx.tstash is not None else None  # written by the SwiGLU backward
+                if dyt is None or dyt.shape != (dy2.shape[1], dy2.shape[0]):
+                    dyt = transpose_into(dy2.contiguous(), torch.empty(dy2.shape[1], dy2.shape[0],
+                                                                        device=dy2.device, dtype=dy2.dtype))
                 dw = dyt.mm(xt.t())
             else:
                 dw = dy2.t().mm(x2)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
-def linear_tw(x, w, wt, dw_kcontig: bool = False):
+def linear_tw(x, w, wt, dw_kcontig: bool = False, tstash: TStash | None = None):
     """``F.linear(x, w)`` with the dgrad taken from ``wt`` (== ``w.t()``,
     kept current by the caller after every weight update); ``dw_kcontig``:
-    weight gradient from transposed activations."""
-    return _LinearTW.apply(x, w, wt, dw_kcontig)
+    weight gradient from transposed activations (``tstash``: the output
+    gradient's transpose, if the next op's backward provides it)."""
+    return _LinearTW.apply(x, w, wt, dw_kcontig, tstash)
