@@ -476,6 +476,116 @@ __global__ __launch_bounds__(BN_T) void k_maxpool_bwd(const uint16_t* __restrict
   store8(dx + (((long long)n * sh.H + ih) * sh.W + iw) * sh.C + c8 * 8, r);
 }
 
+
+// ------------------------------------------------------------ the stem ----
+// ResNet-50's first convolution (7x7, stride 2, pad 3, 3 -> 64 channels,
+// 224 -> 112) over channels-last bf16, as an implicit GEMM on MFMA.  MIOpen
+// ran it as an asm implicit GEMM after zero-filling the 411 MB output
+// (0.36 + 0.09 ms/step, profiles/resnet50_r5.md).
+//   GEMM: M = output pixels of one output row (112, padded to 4 x 32), N =
+//   64 channels (2 x 32), K = 7 filter rows x 24: per filter row the 21 (kw,
+//   c) taps at t = 1 + 3 kw + c, zero weights at t = 0, 22, 23, plus 8 zero
+//   k at the end (176 = 11 MFMA k-steps of 16).
+//   LDS: the 7 input rows of an output row, row element (iw + 3)*3 + c + 1,
+//   so tap t of output pixel ow sits at element 6 ow + t: every A fragment
+//   (8 consecutive k) is 4 dword reads, and a source row (224 x 3 bf16 =
+//   336 dwords) lands 5 dwords in, dword-aligned on both sides.
+//   Block = 4 waves, STEM_ROWS output rows; wave w owns output pixels
+//   32w..32w+31 and both channel halves (2 accumulators); the weight
+//   fragments (prepared once per step by k_stem_wprep) stay in registers
+//   for all the block's rows; the next row's input is loaded into registers
+//   while the current one computes; outputs leave through LDS as 16-byte
+//   row stores.
+typedef __bf16 stem_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float stem_f32x16 __attribute__((ext_vector_type(16)));
+constexpr int STEM_KP = 176, STEM_RW = 696, STEM_ROWS = 8, STEM_OPITCH = 72;
+constexpr int STEM_LOADS = (7 * 336 + 255) / 256;  // input dwords per thread per output row
+
+// wp[co][k] (bf16) from the OIHW-indexed weight with arbitrary strides
+__global__ __launch_bounds__(256) void k_stem_wprep(const float* __restrict__ w, long long s0, long long s1,
+                                                    long long s2, long long s3, uint16_t* __restrict__ wp) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= 64 * STEM_KP) return;
+  const int co = i / STEM_KP, k = i - co * STEM_KP, kh = k / 24, t = k - kh * 24;
+  float v = 0.f;
+  if (kh < 7 && t >= 1 && t <= 21) {
+    const int kw = (t - 1) / 3, c = (t - 1) - 3 * kw;
+    v = w[co * s0 + c * s1 + kh * s2 + kw * s3];
+  }
+  wp[i] = f2bf(v);
+}
+
+__device__ __forceinline__ void stem_load_row(const uint32_t* __restrict__ x, int N, int r, uint32_t (&v)[STEM_LOADS]) {
+  // the 7 input rows of output row r (= n*112 + oh), as dwords; 0 outside
+  const int tid = threadIdx.x;
+  const bool live = r < N * 112;
+  const int n = live ? r / 112 : 0, oh = live ? r - n * 112 : 0;
+#pragma unroll
+  for (int q = 0; q < STEM_LOADS; ++q) {
+    const int d = tid + 256 * q, kh = d / 336, j = d - kh * 336;
+    const int ih = 2 * oh - 3 + kh;
+    v[q] = (live && d < 7 * 336 && ih >= 0 && ih < 224) ? x[((long long)n * 224 + ih) * 336 + j] : 0u;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_stem_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ wp,
+                                                  uint16_t* __restrict__ y, int N) {
+  __shared__ __attribute__((aligned(16))) uint32_t in_s[(7 * STEM_RW + 96) / 2];
+  __shared__ __attribute__((aligned(16))) uint16_t out_s[128 * STEM_OPITCH];
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  // zero the never-written dwords of every row once (pad and iw < 0 / >= 224)
+  for (int i = tid; i < (7 * STEM_RW + 96) / 2; i += 256) in_s[i] = 0u;
+  // weight fragments: B[k = 8(l>>5)+j][col = l&31], both channel halves
+  stem_bf16x8 bf[2][11];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int s = 0; s < 11; ++s)
+      bf[h][s] = *reinterpret_cast<const stem_bf16x8*>(wp + (32 * h + (lane & 31)) * STEM_KP + 16 * s + 8 * (lane >> 5));
+  const int rows = N * 112;
+  const int r0 = blockIdx.x * STEM_ROWS;
+  const uint32_t* x32 = reinterpret_cast<const uint32_t*>(x);
+  uint32_t nxt[STEM_LOADS];
+  stem_load_row(x32, N, r0, nxt);
+  const int ow = 32 * wv + (lane & 31);  // this lane's A row (output pixel)
+  for (int rr = 0; rr < STEM_ROWS; ++rr) {
+    const int r = r0 + rr;
+    if (r >= rows) break;
+    __syncthreads();  // the previous row's LDS reads / out_s reads are done
+#pragma unroll
+    for (int q = 0; q < STEM_LOADS; ++q) {
+      const int d = tid + 256 * q, kh = d / 336, j = d - kh * 336;
+      if (d < 7 * 336) in_s[kh * (STEM_RW / 2) + 5 + j] = nxt[q];
+    }
+    __syncthreads();
+    if (rr + 1 < STEM_ROWS) stem_load_row(x32, N, r + 1, nxt);  // in flight while this row computes
+    stem_f32x16 acc0 = {}, acc1 = {};
+#pragma unroll
+    for (int s = 0; s < 11; ++s) {
+      const int k0 = 16 * s + 8 * (lane >> 5);
+      const int kh = min(k0 / 24, 6), t0 = k0 - (k0 / 24) * 24;  // k >= 168: zero weights, any finite A
+      const uint32_t* a = in_s + (kh * STEM_RW + 6 * ow + t0) / 2;
+      const uint32_t av[4] = {a[0], a[1], a[2], a[3]};
+      const stem_bf16x8 A = __builtin_bit_cast(stem_bf16x8, av);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, bf[0][s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, bf[1][s], acc1, 0, 0, 0);
+    }
+    // C: col = l&31 (channel), row = (i&3) + 8(i>>2) + 4(l>>5) (pixel in the wave's 32)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int px = 32 * wv + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+      out_s[px * STEM_OPITCH + (lane & 31)] = f2bf(acc0[i]);
+      out_s[px * STEM_OPITCH + 32 + (lane & 31)] = f2bf(acc1[i]);
+    }
+    __syncthreads();
+    uint16_t* yr = y + (long long)r * 112 * 64;
+    for (int c = tid; c < 112 * 8; c += 256) {  // 112 pixels x 8 chunks of 8 channels
+      const int px = c >> 3, ch = c & 7;
+      *reinterpret_cast<uint4*>(yr + px * 64 + 8 * ch) = *reinterpret_cast<const uint4*>(out_s + px * STEM_OPITCH + 8 * ch);
+    }
+  }
+}
+
 }  // namespace
 
 #define PTO_API extern "C" __attribute__((visibility("default")))
@@ -563,5 +673,20 @@ PTO_API int pto_maxpool_bwd(const void* dy, const void* code, void* dx, int N, i
   hipLaunchKernelGGL(k_maxpool_bwd, dim3((unsigned)((total + BN_T - 1) / BN_T)), dim3(BN_T), 0, s,
                      reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint8_t*>(code),
                      reinterpret_cast<uint16_t*>(dx), sh);
+  return (int)hipGetLastError();
+}
+
+// The ResNet stem conv (7x7 / 2 / pad 3, 3 -> 64, 224 -> 112) over
+// channels-last bf16.  w: fp32 [64][3][7][7] indexed with element strides
+// s0..s3; wp: 64*176 bf16 scratch (rebuilt every call: the weights change
+// every step).
+PTO_API int pto_stem_fwd(const void* x, const float* w, long long s0, long long s1, long long s2, long long s3,
+                         void* wp, void* y, int N, hipStream_t s) {
+  if (N < 1 || ((((uintptr_t)x) | ((uintptr_t)wp) | ((uintptr_t)y)) & 15)) return -1;
+  hipLaunchKernelGGL(k_stem_wprep, dim3((64 * STEM_KP + 255) / 256), dim3(256), 0, s, w, s0, s1, s2, s3,
+                     reinterpret_cast<uint16_t*>(wp));
+  const int blocks = (N * 112 + STEM_ROWS - 1) / STEM_ROWS;
+  hipLaunchKernelGGL(k_stem_fwd, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(x),
+                     reinterpret_cast<const uint16_t*>(wp), reinterpret_cast<uint16_t*>(y), N);
   return (int)hipGetLastError();
 }

@@ -17,6 +17,7 @@ import torch.nn as nn
 from ..ops.bn import BatchNormAct
 from ..ops.conv1x1 import GradStash, conv1x1, conv1x1_res, gemm_supported
 from ..ops.pool import MaxPool2d
+from ..ops.stem import stem_conv
 
 
 class Bottleneck(nn.Module):
@@ -93,7 +94,7 @@ class ResNet(nn.Module):
                     nn.init.zeros_(m.bn3.weight)
 
     def forward(self, x):
-        x = self.maxpool(self.bn1(self.conv1(x), relu=True))
+        x = self.maxpool(self.bn1(stem_conv(x, self.conv1), relu=True))  # MFMA stem kernel (ops/stem.py)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 

@@ -138,6 +138,7 @@ _SIGS = {
     "pto_bn_fwd": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _I, _P, _P],
     "pto_bn_bwd": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _I, _P],
     "pto_maxpool_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    "pto_stem_fwd": [_P, _P, _L, _L, _L, _L, _P, _P, _I, _P],
     "pto_maxpool_bwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     # causal GQA flash attention, head_dim 128 (csrc/kernels/attention.hip)
     "pto_attn_fwd": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _L, _L, _L, _L, _F, _P],

@@ -126,7 +126,10 @@ class ResNetTrainer(CheckpointMixin):
         else:
             self.opt = _TorchOpt(torch.optim.SGD(self.model.parameters(), lr=lr, momentum=momentum,
                                                  weight_decay=weight_decay))
-        self.x, self.y = synthetic_images(batch_size, device, image_size, seed=seed)
+        # images arrive in the compute dtype on the GPU (what a GPU-side
+        # decode/normalise stage hands over); the model casts nothing per step
+        self.x, self.y = synthetic_images(batch_size, device, image_size, seed=seed,
+                                          dtype=torch.bfloat16 if device.type == "cuda" else torch.float32)
         self._loss = None
         self.steps_done = 0
         self.timer = StepTimer(device, enabled=False)
