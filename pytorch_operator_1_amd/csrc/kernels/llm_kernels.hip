@@ -137,29 +137,56 @@ __global__ __launch_bounds__(NT) void k_add_rmsnorm_fwd(const uint16_t* __restri
 }
 
 // One block per group of rows; dw partial sums in registers -> part[G][D].
+// V = 8-column vectors per thread (D <= V * 2048): the register arrays are
+// sized for the real width.  Every load of row i+1 (h, dy, the residual
+// gradient, rstd) is issued before row i's block reduction, so the row loop
+// is not one memory round trip per row behind the reduction (Llama-3-8B:
+// 157 us per call at 3.5 TB/s before).
+template <int V>
 __global__ __launch_bounds__(NT) void k_rmsnorm_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ h,
                                                     const uint16_t* __restrict__ w, const float* __restrict__ rstd,
                                                     const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
                                                     float* __restrict__ part, int M, int D) {
   __shared__ float red[4];
-  V8 wv[RMS_MAXV], dwacc[RMS_MAXV];
+  V8 wv[V], dwacc[V];
 #pragma unroll
-  for (int j = 0; j < RMS_MAXV; ++j) {
+  for (int j = 0; j < V; ++j) {
     const int c = (j * NT + threadIdx.x) * 8;
     if (c < D) wv[j] = ld8(w + c);
 #pragma unroll
     for (int e = 0; e < 8; ++e) dwacc[j].v[e] = 0.f;
   }
-  for (long long row = blockIdx.x; row < M; row += gridDim.x) {
-    const float rs = rstd[row];
-    V8 hv[RMS_MAXV], gv[RMS_MAXV];
-    float dot = 0.f;
+  V8 hn[V], gn[V], rn[V];
+  float rsn = 0.f;
+  auto load = [&](long long row) {
+    if (row >= M) return;
+    rsn = rstd[row];
 #pragma unroll
-    for (int j = 0; j < RMS_MAXV; ++j) {
+    for (int j = 0; j < V; ++j) {
       const int c = (j * NT + threadIdx.x) * 8;
       if (c < D) {
-        hv[j] = ld8(h + row * D + c);
-        gv[j] = ld8(dy + row * D + c);
+        hn[j] = ld8(h + row * D + c);
+        gn[j] = ld8(dy + row * D + c);
+        if (dres) rn[j] = ld8(dres + row * D + c);
+      }
+    }
+  };
+  load(blockIdx.x);
+  for (long long row = blockIdx.x; row < M; row += gridDim.x) {
+    const float rs = rsn;
+    V8 hv[V], gv[V], rv[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      hv[j] = hn[j];
+      gv[j] = gn[j];
+      rv[j] = rn[j];
+    }
+    load(row + gridDim.x);  // in flight during this row's math and reduction
+    float dot = 0.f;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int c = (j * NT + threadIdx.x) * 8;
+      if (c < D) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float n = bf2f(f2bf(hv[j].v[e] * rs));
@@ -171,24 +198,18 @@ __global__ __launch_bounds__(NT) void k_rmsnorm_bwd(const uint16_t* __restrict__
     }
     const float k = block_sum(dot, red) * rs * rs * rs / (float)D;
 #pragma unroll
-    for (int j = 0; j < RMS_MAXV; ++j) {
+    for (int j = 0; j < V; ++j) {
       const int c = (j * NT + threadIdx.x) * 8;
       if (c < D) {
         V8 o;
-        if (dres) {
-          o = ld8(dres + row * D + c);
-        } else {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) o.v[e] = 0.f;
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o.v[e] += rs * gv[j].v[e] - k * hv[j].v[e];
+        for (int e = 0; e < 8; ++e) o.v[e] = (dres ? rv[j].v[e] : 0.f) + (rs * gv[j].v[e] - k * hv[j].v[e]);
         st8(dx + row * D + c, o);
       }
     }
   }
 #pragma unroll
-  for (int j = 0; j < RMS_MAXV; ++j) {
+  for (int j = 0; j < V; ++j) {
     const int c = (j * NT + threadIdx.x) * 8;
     if (c < D) {
       float4* pp = reinterpret_cast<float4*>(part + (long long)blockIdx.x * D + c);
@@ -198,18 +219,43 @@ __global__ __launch_bounds__(NT) void k_rmsnorm_bwd(const uint16_t* __restrict__
   }
 }
 
-// dw[c] = sum_g part[g][c]; 64 columns x 4 row-slices per block.
+// dw[c] = bf16(sum_g part[g][c]): 64 columns per block as 16 float4 column
+// quads x 16 row slices, 8 independent 16-byte loads in flight per thread
+// (the first version summed with one dependent load per iteration: 64 us per
+// call for 1024 x 4096 partials, 65 calls per Llama-3-8B step); the 16
+// slices are combined in a fixed order (deterministic).
 __global__ __launch_bounds__(NT) void k_colsum_bf16(const float* __restrict__ part, uint16_t* __restrict__ dw, int G,
                                                     int D) {
-  __shared__ float s[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int sl = threadIdx.x >> 6;
-  float a = 0.f;
-  if (c < D)
-    for (int g = sl; g < G; g += 4) a += part[(long long)g * D + c];
-  s[sl][threadIdx.x & 63] = a;
+  __shared__ float4 s[16][16];
+  const int q = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + 4 * q;
+  float4 a = {0.f, 0.f, 0.f, 0.f};
+  if (c < D) {
+    int g = sl;
+    for (; g + 16 * 7 < G; g += 16 * 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(part + (long long)(g + 16 * u) * D + c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w;
+      }
+    }
+    for (; g < G; g += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (long long)g * D + c);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  s[sl][q] = a;
   __syncthreads();
-  if (sl == 0 && c < D) dw[c] = f2bf(s[0][threadIdx.x] + s[1][threadIdx.x] + s[2][threadIdx.x] + s[3][threadIdx.x]);
+  if (sl == 0 && c < D) {
+    float4 t = s[0][q];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) {
+      t.x += s[r][q].x; t.y += s[r][q].y; t.z += s[r][q].z; t.w += s[r][q].w;
+    }
+    dw[c] = f2bf(t.x); dw[c + 1] = f2bf(t.y); dw[c + 2] = f2bf(t.z); dw[c + 3] = f2bf(t.w);
+  }
 }
 
 // ---------------------------------------------------------------- SwiGLU
@@ -257,52 +303,57 @@ __global__ __launch_bounds__(NT) void k_swiglu_bwd(const uint16_t* __restrict__ 
 // (ops/llm.py _LinearTW, dW = dgu^T X from K(token)-contiguous operands), so
 // the step no longer transposes the largest activation gradient of the MLP
 // ([16384 x 28672] per layer on Llama-3-8B) in a pass of its own.  Block =
-// 64 tokens x 64 features: each thread computes 2 tokens x 8 features of dg
+// 128 tokens x 64 features: each thread computes 4 tokens x 8 features of dg
 // and du, stores them row-major as k_swiglu_bwd, and drops them into two LDS
-// tiles [feature][token] (row pitch 66 halves: the paired-token 32-bit
+// tiles [feature][token] (row pitch 130 halves: the paired-token 32-bit
 // writes of a wave spread over the banks); the transposed rows then leave as
-// 16-byte stores, 128 contiguous bytes per feature row and tile.
-constexpr int SWT = 64;       // tokens and features per block
-constexpr int SWT_LD = 66;    // LDS row pitch (halves)
+// 16-byte stores, 256 contiguous bytes per feature row and tile (64-token
+// tiles, 128-byte rows, measured 4.2 TB/s).
+constexpr int SWT = 64;        // features per block
+constexpr int SWT_M = 128;     // tokens per block
+constexpr int SWT_LD = 130;    // LDS row pitch (halves)
 __global__ __launch_bounds__(NT) void k_swiglu_bwd_t(const uint16_t* __restrict__ gu, const uint16_t* __restrict__ dout,
                                                      uint16_t* __restrict__ dgu, uint16_t* __restrict__ dgu_t,
                                                      long long M, int F) {
   __shared__ __attribute__((aligned(16))) uint16_t tg[SWT * SWT_LD], tu[SWT * SWT_LD];
   const int ntf = F / SWT;
-  const long long m0 = (long long)(blockIdx.x / ntf) * SWT;
+  const long long m0 = (long long)(blockIdx.x / ntf) * SWT_M;
   const int f0 = (blockIdx.x % ntf) * SWT;
-  const int t = threadIdx.x, fg = t & 7, tp = t >> 3;  // 8 features at 8*fg, tokens 2tp, 2tp+1
+  const int t = threadIdx.x, fg = t & 7, tq = t >> 3;  // 8 features at 8*fg, tokens 2tq, 2tq+1, 64+2tq, 65+2tq
   const int c = f0 + 8 * fg;
-  V8 dg[2], du[2];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const long long m = m0 + 2 * tp + k;
-    const bool ok = m < M;
-    const long long mm = ok ? m : m0;
-    const V8 g = ld8(gu + mm * 2 * F + c), u = ld8(gu + mm * 2 * F + F + c), d = ld8(dout + mm * F + c);
+  for (int half = 0; half < 2; ++half) {
+    V8 dg[2], du[2];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float sg = sigmoidf(g.v[e]);  // the same expressions as k_swiglu_bwd (bit-equal dgu)
-      const float silu = g.v[e] * sg;
-      du[k].v[e] = d.v[e] * silu;
-      dg[k].v[e] = d.v[e] * u.v[e] * sg * (1.f + g.v[e] * (1.f - sg));
+    for (int k = 0; k < 2; ++k) {
+      const long long m = m0 + 64 * half + 2 * tq + k;
+      const bool ok = m < M;
+      const long long mm = ok ? m : m0;
+      const V8 g = ld8(gu + mm * 2 * F + c), u = ld8(gu + mm * 2 * F + F + c), d = ld8(dout + mm * F + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float sg = sigmoidf(g.v[e]);  // the same expressions as k_swiglu_bwd
+        const float silu = g.v[e] * sg;
+        du[k].v[e] = d.v[e] * silu;
+        dg[k].v[e] = d.v[e] * u.v[e] * sg * (1.f + g.v[e] * (1.f - sg));
+      }
+      if (ok) {
+        st8(dgu + m * 2 * F + c, dg[k]);
+        st8(dgu + m * 2 * F + F + c, du[k]);
+      }
     }
-    if (ok) {
-      st8(dgu + m * 2 * F + c, dg[k]);
-      st8(dgu + m * 2 * F + F + c, du[k]);
-    }
-  }
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {  // the token pair as one 32-bit word per feature
-    const int row = (8 * fg + e) * SWT_LD + 2 * tp;
-    *reinterpret_cast<uint32_t*>(tg + row) = (uint32_t)f2bf(dg[0].v[e]) | ((uint32_t)f2bf(dg[1].v[e]) << 16);
-    *reinterpret_cast<uint32_t*>(tu + row) = (uint32_t)f2bf(du[0].v[e]) | ((uint32_t)f2bf(du[1].v[e]) << 16);
+    for (int e = 0; e < 8; ++e) {  // the token pair as one 32-bit word per feature
+      const int row = (8 * fg + e) * SWT_LD + 64 * half + 2 * tq;
+      *reinterpret_cast<uint32_t*>(tg + row) = (uint32_t)f2bf(dg[0].v[e]) | ((uint32_t)f2bf(dg[1].v[e]) << 16);
+      *reinterpret_cast<uint32_t*>(tu + row) = (uint32_t)f2bf(du[0].v[e]) | ((uint32_t)f2bf(du[1].v[e]) << 16);
+    }
   }
   __syncthreads();
-  // 2 x 64 feature rows x 8 chunks of 8 tokens = 1024 16-byte stores, 4 per thread
+  // 2 x 64 feature rows x 16 chunks of 8 tokens = 2048 16-byte stores, 8 per thread
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int idx = t + NT * q, half = idx >> 9, r = (idx >> 3) & 63, ch = idx & 7;
+  for (int q = 0; q < 8; ++q) {
+    const int idx = t + NT * q, half = idx >> 10, r = (idx >> 4) & 63, ch = idx & 15;
     const uint16_t* src = (half ? tu : tg) + r * SWT_LD + 8 * ch;
     const long long m = m0 + 8 * ch;
     if (m >= M) continue;
@@ -520,8 +571,10 @@ PTO_API int pto_rmsnorm_bwd(const void* dy, const void* h, const void* w, const 
   if (D % 8 || D > RMS_MAXV * NT * 8) return -1;
   if (M <= 0) return 0;
   const int G = pto_rmsnorm_bwd_groups(M);
-  hipLaunchKernelGGL(k_rmsnorm_bwd, dim3(G), dim3(NT), 0, s, (const uint16_t*)dy, (const uint16_t*)h,
-                     (const uint16_t*)w, rstd, (const uint16_t*)dres, (uint16_t*)dx, part, (int)M, D);
+  const int V = (D + 8 * NT - 1) / (8 * NT);
+  auto* kb = V <= 1 ? k_rmsnorm_bwd<1> : V == 2 ? k_rmsnorm_bwd<2> : V == 3 ? k_rmsnorm_bwd<3> : k_rmsnorm_bwd<4>;
+  hipLaunchKernelGGL(kb, dim3(G), dim3(NT), 0, s, (const uint16_t*)dy, (const uint16_t*)h, (const uint16_t*)w, rstd,
+                     (const uint16_t*)dres, (uint16_t*)dx, part, (int)M, D);
   hipLaunchKernelGGL(k_colsum_bf16, dim3((D + 63) / 64), dim3(NT), 0, s, part, (uint16_t*)dw, G, D);
   return (int)hipGetLastError();
 }
@@ -544,7 +597,7 @@ PTO_API int pto_swiglu_bwd(const void* gu, const void* dout, void* dgu, long lon
 PTO_API int pto_swiglu_bwd_t(const void* gu, const void* dout, void* dgu, void* dgu_t, long long M, int F,
                              hipStream_t s) {
   if (F % SWT || M < 1 || M % 8 || (((uintptr_t)dgu_t) & 15)) return -1;
-  const long long blocks = ((M + SWT - 1) / SWT) * (F / SWT);
+  const long long blocks = ((M + SWT_M - 1) / SWT_M) * (F / SWT);
   if (blocks > 0x7fffffff) return -1;
   hipLaunchKernelGGL(k_swiglu_bwd_t, dim3((unsigned)blocks), dim3(NT), 0, s, (const uint16_t*)gu,
                      (const uint16_t*)dout, (uint16_t*)dgu, (uint16_t*)dgu_t, M, F);

@@ -57,3 +57,16 @@ for name, din, dout in [("wqkv", 4096, 6144), ("wo", 4096, 4096), ("w13", 4096, 
     t_f = timeit(lambda: torch.nn.functional.linear(x, w))
     print(f"{name}: X^T dY {t_a:.3f} ms ({fl / t_a / 1e9:.0f} TF) | K-contig X^T dY {t_b:.3f} ms "
           f"({fl / t_b / 1e9:.0f} TF) | forward x W^T {t_f:.3f} ms ({fl / t_f / 1e9:.0f} TF)", flush=True)
+
+# input gradient dX = dY W: from W itself (B operand N-contiguous) vs from the
+# W^T copy the step keeps (K-contiguous, what F.linear(dY, W^T) runs)
+print("--- dgrad forms", flush=True)
+for name, din, dout in [("wqkv", 4096, 6144), ("wo", 4096, 4096), ("w13", 4096, 28672), ("w2", 14336, 4096)]:
+    dy = torch.randn(T, dout, device=dev).bfloat16()
+    w = torch.randn(dout, din, device=dev).bfloat16()
+    wt = w.t().contiguous()
+    fl = 2 * T * din * dout
+    t_w = timeit(lambda: dy.mm(w))
+    t_wt = timeit(lambda: torch.nn.functional.linear(dy, wt))
+    print(f"{name}: dY W {t_w:.3f} ms ({fl / t_w / 1e9:.0f} TF) | dY (W^T)^T {t_wt:.3f} ms ({fl / t_wt / 1e9:.0f} TF)",
+          flush=True)
