@@ -21,13 +21,15 @@ def _rms_ref(h, w, eps):
     return w.float() * (hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + eps))
 
 
-@pytest.mark.parametrize("D", [256, 4096, 1000 * 8])
+# D picks the backward's per-thread vector count (V = 1..4); M > 1024 gives
+# each workgroup several rows, so the next-row prefetch runs.
+@pytest.mark.parametrize("D", [200, 256, 4096, 5120, 1000 * 8])
 @pytest.mark.parametrize("res", [False, True])
-def test_add_rmsnorm_fwd_bwd(D, res):
+@pytest.mark.parametrize("M", [333, 2500])
+def test_add_rmsnorm_fwd_bwd(D, res, M):
     from pytorch_operator_1_amd.ops import llm
 
     torch.manual_seed(0)
-    M = 333
     x = torch.randn(M, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     r = torch.randn(M, D, device=DEV, dtype=torch.bfloat16, requires_grad=True) if res else None
     w = (1 + 0.1 * torch.randn(D, device=DEV)).bfloat16().requires_grad_()
