@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-5 check of the committed tree: every GPU test, smoke(), the default
 # bench, the driver's 20-step command, and a 2-rank self-launched rehearsal
-# (two ranks sharing the one GPU, gloo) with its N>1 JSON evidence.
+# (two ranks sharing the one GPU, gloo) with its N>1 JSON evidence, then
+# the ResNet-50 and Llama-3-8B benches (BASELINE configs 3-4).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -18,4 +19,8 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_driver.json 2
 for f in bench_default bench_driver; do python -c "import json; d=json.load(open('$O/$f.json')); print('$f', d['value'], d['ms_per_step'], d.get('submit_to_first_step_s'))"; done
 PTO_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 200 --warmup 5 > $O/reh2.json 2> $O/reh2.err || { tail -30 $O/reh2.err; exit 1; }
 python -c "import json; d=json.loads([l for l in open('$O/reh2.json') if l.startswith('{')][0]); print('reh2', d['value'], d['ms_per_step'], d.get('submit_to_first_step_s'), d.get('ranks_bit_identical'), d['config']['grad_allreduce'].get('schedule_autotune', {}).get('kept'))"
+for m in resnet50 llama3-8b; do
+timeout -k 10 600 python bench.py --model $m --steps 20 --warmup 5 --no-latency > $O/bench_$m.json 2> $O/bench_$m.err || { tail -20 $O/bench_$m.err; exit 1; }
+python -c "import json; d=json.load(open('$O/bench_$m.json')); print('$m', d['value'], d['ms_per_step'])"
+done
 exit $rc
