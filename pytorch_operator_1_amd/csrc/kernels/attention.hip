@@ -209,17 +209,30 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_attn_fwd(const __bf16* __restri
   TILE_LOAD_W(tv, vb, sh.v_rs);
   TILE_STORE_W(tk, smem);
   TILE_STORE_W(tv, smem + TILE_B);
+  {  // tile 1 in flight across the first barrier (tile 0 again when there is none)
+    const int kn = ntiles > 1 ? KT : 0;
+    TILE_LOAD_W(tk, kb + (long long)kn * sh.k_rs, sh.k_rs);
+    TILE_LOAD_W(tv, vb + (long long)kn * sh.v_rs, sh.v_rs);
+  }
   __syncthreads();
 
   // unrolled x2 so the LDS ring slot is a compile-time constant: the
-  // lane-dependent LDS addresses stay loop-invariant (immediate offsets)
+  // lane-dependent LDS addresses stay loop-invariant (immediate offsets).
+  // Staging is split across the barrier: tile t+1 (loaded during step t-1)
+  // is written to the other slot at the top of step t, then tile t+2's loads
+  // are issued, so they land under step t's math AND the barrier after it.
   auto step_fn = [&](const int t, auto bufc) {
     constexpr int SLOT = decltype(bufc)::value;
     const int k0 = t * KT;
     const char* ktile = smem + SLOT * 2 * TILE_B;
     const char* vtile = ktile + TILE_B;
-    {  // next tile in flight during this tile's math (the last iteration re-reads its own)
-      const int kn = (t + 1 < ntiles) ? k0 + KT : k0;
+    if (t + 1 < ntiles) {
+      char* nt = smem + (SLOT ^ 1) * 2 * TILE_B;
+      TILE_STORE_W(tk, nt);
+      TILE_STORE_W(tv, nt + TILE_B);
+    }
+    {  // tile t+2 (the last iterations re-read their own)
+      const int kn = (t + 2 < ntiles) ? k0 + 2 * KT : k0;
       TILE_LOAD_W(tk, kb + (long long)kn * sh.k_rs, sh.k_rs);
       TILE_LOAD_W(tv, vb + (long long)kn * sh.v_rs, sh.v_rs);
     }
@@ -284,11 +297,6 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_attn_fwd(const __bf16* __restri
       for (int db = 0; db < 4; ++db)
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) acc_o[db] = mfma(tr_operand(vtile, 16 * ks, 32 * db), pf[ks], acc_o[db]);
-    }
-    if (t + 1 < ntiles) {
-      char* nt = smem + (SLOT ^ 1) * 2 * TILE_B;
-      TILE_STORE_W(tk, nt);
-      TILE_STORE_W(tv, nt + TILE_B);
     }
     __syncthreads();
     };
@@ -383,16 +391,26 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_attn_bwd_dq(const __bf16* __res
   TILE_LOAD_W(tv, vb, sh.v_rs);
   TILE_STORE_W(tk, smem);
   TILE_STORE_W(tv, smem + TILE_B);
+  {
+    const int kn = ntiles > 1 ? KT : 0;
+    TILE_LOAD_W(tk, kb + (long long)kn * sh.k_rs, sh.k_rs);
+    TILE_LOAD_W(tv, vb + (long long)kn * sh.v_rs, sh.v_rs);
+  }
   __syncthreads();
-  // unrolled x2 so the LDS ring slot is a compile-time constant: the
-  // lane-dependent LDS addresses stay loop-invariant (immediate offsets)
+  // unrolled x2 (compile-time LDS slot); staging split across the barrier
+  // as in the forward
   auto step_fn = [&](const int t, auto bufc) {
     constexpr int SLOT = decltype(bufc)::value;
     const int k0 = t * KT;
     const char* ktile = smem + SLOT * 2 * TILE_B;
     const char* vtile = ktile + TILE_B;
+    if (t + 1 < ntiles) {
+      char* nt = smem + (SLOT ^ 1) * 2 * TILE_B;
+      TILE_STORE_W(tk, nt);
+      TILE_STORE_W(tv, nt + TILE_B);
+    }
     {
-      const int kn = (t + 1 < ntiles) ? k0 + KT : k0;
+      const int kn = (t + 2 < ntiles) ? k0 + 2 * KT : k0;
       TILE_LOAD_W(tk, kb + (long long)kn * sh.k_rs, sh.k_rs);
       TILE_LOAD_W(tv, vb + (long long)kn * sh.v_rs, sh.v_rs);
     }
@@ -434,11 +452,6 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_attn_bwd_dq(const __bf16* __res
           for (int hs = 0; hs < 2; ++hs)
             acc[db] = mfma(tr_operand(ktile, 32 * kt + 16 * hs, 32 * db), sf[hs], acc[db]);
       }
-    }
-    if (t + 1 < ntiles) {
-      char* nt = smem + (SLOT ^ 1) * 2 * TILE_B;
-      TILE_STORE_W(tk, nt);
-      TILE_STORE_W(tv, nt + TILE_B);
     }
     __syncthreads();
     };
