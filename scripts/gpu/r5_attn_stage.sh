@@ -1,11 +1,13 @@
 #!/bin/bash
 # Attention forward / dQ with the K/V staging split across the barrier
 # (libpto_hip_new.so) vs the committed kernels (libpto_hip_base.so):
-# numerics, then kernel and Llama-3-8B step A/B on one box.
+# numerics, then kernel and Llama-3-8B step A/B on one box.  Build the two
+# libraries first (python -c 'import __graft_entry__ as g; g.build()' on
+# each tree, copied to _lib/libpto_hip_{new,base}.so).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/r5as
+O=gpurun_out/${R5AS_OUT:-r5as}
 mkdir -p $O
 L=pytorch_operator_1_amd/_lib
 cp $L/libpto_hip_new.so $L/libpto_hip.so
