@@ -321,6 +321,16 @@ __global__ __launch_bounds__(NT) void k_swiglu_bwd_t(const uint16_t* __restrict_
   const int f0 = (blockIdx.x % ntf) * SWT;
   const int t = threadIdx.x, fg = t & 7, tq = t >> 3;  // 8 features at 8*fg, tokens 2tq, 2tq+1, 64+2tq, 65+2tq
   const int c = f0 + 8 * fg;
+  // all 12 loads of the thread's 4 tokens in flight before the first use
+  V8 gl[4], ul[4], dl[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long long m = m0 + 64 * (i >> 1) + 2 * tq + (i & 1);
+    const long long mm = m < M ? m : m0;
+    gl[i] = ld8(gu + mm * 2 * F + c);
+    ul[i] = ld8(gu + mm * 2 * F + F + c);
+    dl[i] = ld8(dout + mm * F + c);
+  }
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     V8 dg[2], du[2];
@@ -328,8 +338,9 @@ __global__ __launch_bounds__(NT) void k_swiglu_bwd_t(const uint16_t* __restrict_
     for (int k = 0; k < 2; ++k) {
       const long long m = m0 + 64 * half + 2 * tq + k;
       const bool ok = m < M;
-      const long long mm = ok ? m : m0;
-      const V8 g = ld8(gu + mm * 2 * F + c), u = ld8(gu + mm * 2 * F + F + c), d = ld8(dout + mm * F + c);
+      const V8& g = gl[2 * half + k];
+      const V8& u = ul[2 * half + k];
+      const V8& d = dl[2 * half + k];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float sg = sigmoidf(g.v[e]);  // the same expressions as k_swiglu_bwd
