@@ -40,6 +40,16 @@ __device__ __forceinline__ V8 ld8(const uint16_t* p) {
   }
   return r;
 }
+__device__ __forceinline__ V8 unpack8(const uint4 q) {  // bf16x8 -> 8 floats
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  V8 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    r.v[2 * i] = __uint_as_float(w[i] << 16);
+    r.v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+  return r;
+}
 __device__ __forceinline__ void st8(uint16_t* p, const V8& r) {
   uint32_t w[4];
 #pragma unroll
@@ -148,15 +158,20 @@ __global__ __launch_bounds__(NT) void k_rmsnorm_bwd(const uint16_t* __restrict__
                                                     const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
                                                     float* __restrict__ part, int M, int D) {
   __shared__ float red[4];
-  V8 wv[V], dwacc[V];
+  // the weight row and the prefetched rows stay packed bf16 (4 registers per
+  // 8 columns, unpacked where used): V = 2 fits 128 registers, so all four
+  // 4-wave workgroups of a CU are resident (162 registers and a 768 + 256
+  // block tail before)
+  uint4 wq[V];
+  V8 dwacc[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     const int c = (j * NT + threadIdx.x) * 8;
-    if (c < D) wv[j] = ld8(w + c);
+    wq[j] = c < D ? *reinterpret_cast<const uint4*>(w + c) : uint4{0, 0, 0, 0};
 #pragma unroll
     for (int e = 0; e < 8; ++e) dwacc[j].v[e] = 0.f;
   }
-  V8 hn[V], gn[V], rn[V];
+  uint4 hn[V], gn[V], rn[V];
   float rsn = 0.f;
   auto load = [&](long long row) {
     if (row >= M) return;
@@ -165,21 +180,21 @@ __global__ __launch_bounds__(NT) void k_rmsnorm_bwd(const uint16_t* __restrict__
     for (int j = 0; j < V; ++j) {
       const int c = (j * NT + threadIdx.x) * 8;
       if (c < D) {
-        hn[j] = ld8(h + row * D + c);
-        gn[j] = ld8(dy + row * D + c);
-        if (dres) rn[j] = ld8(dres + row * D + c);
+        hn[j] = *reinterpret_cast<const uint4*>(h + row * D + c);
+        gn[j] = *reinterpret_cast<const uint4*>(dy + row * D + c);
+        if (dres) rn[j] = *reinterpret_cast<const uint4*>(dres + row * D + c);
       }
     }
   };
   load(blockIdx.x);
   for (long long row = blockIdx.x; row < M; row += gridDim.x) {
     const float rs = rsn;
-    V8 hv[V], gv[V], rv[V];
+    uint4 hc[V], gc[V], rc[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      hv[j] = hn[j];
-      gv[j] = gn[j];
-      rv[j] = rn[j];
+      hc[j] = hn[j];
+      gc[j] = gn[j];
+      rc[j] = rn[j];
     }
     load(row + gridDim.x);  // in flight during this row's math and reduction
     float dot = 0.f;
@@ -187,12 +202,12 @@ __global__ __launch_bounds__(NT) void k_rmsnorm_bwd(const uint16_t* __restrict__
     for (int j = 0; j < V; ++j) {
       const int c = (j * NT + threadIdx.x) * 8;
       if (c < D) {
+        const V8 hv = unpack8(hc[j]), gv = unpack8(gc[j]), wv = unpack8(wq[j]);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float n = bf2f(f2bf(hv[j].v[e] * rs));
-          dwacc[j].v[e] += gv[j].v[e] * n;
-          gv[j].v[e] *= wv[j].v[e];  // g = dy * w
-          dot += gv[j].v[e] * hv[j].v[e];
+          const float n = bf2f(f2bf(hv.v[e] * rs));
+          dwacc[j].v[e] += gv.v[e] * n;
+          dot += gv.v[e] * wv.v[e] * hv.v[e];  // g = dy * w
         }
       }
     }
@@ -201,9 +216,13 @@ __global__ __launch_bounds__(NT) void k_rmsnorm_bwd(const uint16_t* __restrict__
     for (int j = 0; j < V; ++j) {
       const int c = (j * NT + threadIdx.x) * 8;
       if (c < D) {
+        const V8 hv = unpack8(hc[j]), gv = unpack8(gc[j]), wv = unpack8(wq[j]);
+        V8 rv;
+        if (dres) rv = unpack8(rc[j]);
         V8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o.v[e] = (dres ? rv[j].v[e] : 0.f) + (rs * gv[j].v[e] - k * hv[j].v[e]);
+        for (int e = 0; e < 8; ++e)
+          o.v[e] = (dres ? rv.v[e] : 0.f) + (rs * (gv.v[e] * wv.v[e]) - k * hv.v[e]);
         st8(dx + row * D + c, o);
       }
     }
