@@ -122,7 +122,13 @@ def test_onfailure_kill_rejoin_every_rank_resumes(cluster, tmp_path):
         assert "[fault-injection]" in log or n.startswith("onfail-master"), n
     pod = cluster.store.get("pods", "default", "onfail-worker-0")
     assert pod["status"]["containerStatuses"][0]["restartCount"] >= 1
-    assert pod["status"]["phase"] == "Succeeded"
+    # the job's Succeeded condition follows the MASTER (reference status.go);
+    # the worker's own exit can reach the store a moment later
+    deadline = time.time() + 30
+    while pod["status"]["phase"] != "Succeeded" and time.time() < deadline:
+        time.sleep(0.2)
+        pod = cluster.store.get("pods", "default", "onfail-worker-0")
+    assert pod["status"]["phase"] == "Succeeded", pod["status"]
 
 
 def test_clean_pod_policy_running_and_delete_cascade(cluster):
