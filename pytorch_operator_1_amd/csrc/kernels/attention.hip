@@ -52,6 +52,7 @@ constexpr int NW = 4;              // waves per block
 constexpr int NT = NW * 64;
 constexpr int TILE_B = KT * HD * 2;  // 16 KiB per K or V tile
 constexpr float LOG2E = 1.4426950408889634f;
+constexpr float ATTN_DEFER = 8.f;  // forward: running-max slack (log2 units) before O is rescaled
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
@@ -264,26 +265,31 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_attn_fwd(const __bf16* __restri
 #pragma unroll
         for (int i = 0; i < 16; ++i) mx = fmaxf(mx, st[kt][i]);
       mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float m_new = fmaxf(m_run, mx * sl);
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      // deferred max: the running max (log2 units) moves only when some row
+      // of the wave grew by more than ATTN_DEFER, so O is rescaled on a few
+      // tiles instead of on most of them (P is then bounded by 2^ATTN_DEFER
+      // instead of 1: the same relative bf16 rounding, l and lse unchanged
+      // in value).  The decision comes before this tile's P exists and after
+      // the previous tile's P.V: nothing at the old scale is pending.
+      float alpha = 1.f;
+      if (__any(mx * sl > m_run + ATTN_DEFER)) {
+        const float m_new = fmaxf(m_run, mx * sl);
+        alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) acc_o[db] *= alpha;
+      }
       float rs = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(st[kt][i], sl, -m_new));
+          const float p = __builtin_amdgcn_exp2f(fmaf(st[kt][i], sl, -m_run));
           st[kt][i] = p;
           rs += p;
         }
       rs += __shfl_xor(rs, 32);
       l_run = l_run * alpha + rs;
-      m_run = m_new;
-      // rescale O only when some row's running max moved (rare after the
-      // first tiles of a causal row)
-      if (__any(alpha != 1.f)) {
-#pragma unroll
-        for (int db = 0; db < 4; ++db) acc_o[db] *= alpha;
-      }
       bf16x8 pf[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {

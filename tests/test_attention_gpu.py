@@ -92,3 +92,34 @@ def test_dkdv_producer_consumer_matches_single_wave_kernel(tmp_path):
         assert r.returncode == 0, r.stderr[-2000:]
         grads.append(torch.load(out, weights_only=True))
     assert torch.equal(grads[0], grads[1])
+
+
+def test_flash_attention_deferred_max_rescales():
+    """The forward moves its running max only when a row's max grows by more
+    than ATTN_DEFER (2^8): random scores rarely do that after the first tile,
+    so here the keys' scores climb along the sequence (every row's max keeps
+    growing by more than the slack, tile after tile) and the output, LSE-based
+    backward and all, must still match the fp32 reference."""
+    from pytorch_operator_1_amd.ops import llm
+
+    B, S, H, Hkv = 1, 512, 8, 2
+    torch.manual_seed(0)
+    x = torch.randn(B * S, H + 2 * Hkv, D, device="cuda")
+    u = torch.nn.functional.normalize(torch.randn(D, device="cuda"), dim=0)
+    x[:, :H] = 0.3 * x[:, :H] + 4.0 * u  # every query leans on u
+    ramp = torch.linspace(0.0, 36.0, S, device="cuda")[:, None, None]
+    x[:, H:H + Hkv] = 0.3 * x[:, H:H + Hkv] + ramp * u  # row 511: ~9 log2 units more per 64-key tile
+    x[:, H:H + Hkv] *= 4.0
+    qkv = x.reshape(B * S, -1).bfloat16()
+    a = qkv.clone().requires_grad_()
+    o = llm.flash_attention(a, B, S, H, Hkv)
+    do = torch.randn_like(o)
+    o.backward(do)
+    r = qkv.float().requires_grad_()
+    orf = reference(r, B, S, H, Hkv)
+    orf.backward(do.float())
+    assert relerr(o, orf) < 1e-2
+    g, gr = a.grad.view(B * S, H + 2 * Hkv, D), r.grad.view(B * S, H + 2 * Hkv, D)
+    assert relerr(g[:, :H], gr[:, :H]) < 2e-2, "dQ"
+    assert relerr(g[:, H:H + Hkv], gr[:, H:H + Hkv]) < 2e-2, "dK"
+    assert relerr(g[:, H + Hkv:], gr[:, H + Hkv:]) < 2e-2, "dV"
