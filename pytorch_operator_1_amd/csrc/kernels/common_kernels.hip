@@ -168,6 +168,22 @@ __global__ __launch_bounds__(1024) void k_gridbar(unsigned* ctr, int rounds, int
   }
 }
 
+// Where each workgroup ran (utils/cu_partition.py): thread 0 records the
+// XCD (HW_REG_XCC_ID) and the HW_ID word (CU / SH / SE / queue fields) of its
+// wave, then the whole group idles `spin` x ~64 cycles so a large grid is
+// spread over every CU the queue may use instead of being drained by the
+// first few.  out[2 * blockIdx.x + {0, 1}] = {xcc id, hw id}.
+__global__ __launch_bounds__(64) void k_cu_id(unsigned* __restrict__ out, int spin) {
+  if (threadIdx.x == 0) {
+    unsigned xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    out[2 * blockIdx.x] = xcc;
+    out[2 * blockIdx.x + 1] = hw;
+  }
+  for (int i = 0; i < spin; ++i) __builtin_amdgcn_s_sleep(1);
+}
+
 // Self-test of the cross-lane helpers of mfma_f32.h (DPP / permlane swaps):
 // one wave, inputs a[64], b[64] -> out[11][64] (tests/test_kernels_gpu.py).
 __global__ __launch_bounds__(64) void k_lane_ops_selftest(const float* __restrict__ a, const float* __restrict__ b,
@@ -253,6 +269,27 @@ PTO_API int pto_gridbar_probe(int blocks, int threads, unsigned* ctr, int rounds
   hipLaunchKernelGGL(k_gridbar, dim3(blocks), dim3(threads), 0, s, ctr, rounds, max_spin);
   return (int)hipGetLastError();
 }
+
+PTO_API int pto_cu_id_probe(int blocks, unsigned* out, int spin, hipStream_t s) {
+  if (blocks < 1 || blocks > 65536 || !out || spin < 0) return -1;
+  hipLaunchKernelGGL(k_cu_id, dim3(blocks), dim3(64), 0, s, out, spin);
+  return (int)hipGetLastError();
+}
+
+// A stream whose hardware queue may only use the CUs set in mask[0..words)
+// (bit i of word w = CU 32 w + i), for ranks that share one GPU
+// (utils/cu_partition.py).  Destroy with pto_stream_destroy.
+PTO_API int pto_stream_create_cu_mask(unsigned words, const unsigned* mask, hipStream_t* out) {
+  if (!words || !mask || !out) return -1;
+  return (int)hipExtStreamCreateWithCUMask(out, words, mask);
+}
+
+PTO_API int pto_stream_get_cu_mask(hipStream_t s, unsigned words, unsigned* mask) {
+  if (!words || !mask) return -1;
+  return (int)hipExtStreamGetCUMask(s, words, mask);
+}
+
+PTO_API int pto_stream_destroy(hipStream_t s) { return (int)hipStreamDestroy(s); }
 
 PTO_API int pto_sgd_block_count(long long n) { return (int)((n + SGD_CHUNK - 1) / SGD_CHUNK); }
 

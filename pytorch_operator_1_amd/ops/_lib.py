@@ -133,6 +133,10 @@ _SIGS = {
     "pto_lane_ops_selftest": [_P, _P, _P, _P],
     "pto_probe_kernel": [_I, _I, _P, _I, _I, _P],
     "pto_gridbar_probe": [_I, _I, _P, _I, _I, _P],
+    "pto_cu_id_probe": [_I, _P, _I, _P],
+    "pto_stream_create_cu_mask": [ctypes.c_uint, _P, ctypes.POINTER(ctypes.c_void_p)],
+    "pto_stream_get_cu_mask": [_P, ctypes.c_uint, _P],
+    "pto_stream_destroy": [_P],
     # fused BatchNorm(+add)(+ReLU), channels-last bf16 (csrc/kernels/bn_kernels.hip)
     "pto_bn_scratch_floats": [_L, _I],
     "pto_bn_fwd": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _I, _P, _P],

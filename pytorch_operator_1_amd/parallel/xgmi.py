@@ -101,7 +101,8 @@ class XgmiAllReduce:
         # (they wait only on roles); a launch whose OTHER workgroups also
         # wait on its roles (the overlapped MNIST forward) does not, so
         # the trainer keeps the exchange in a launch of its own then.
-        self.colocated = False
+        # ``partitioned``: ranks share a GPU but each runs on its own CUs.
+        self.colocated = self.partitioned = False
         if self.world == 1:
             self._opened = []
             self._set_peers(L, [[buf.data_ptr()], [self.tmp.data_ptr()], [self._flags]])
@@ -118,11 +119,28 @@ class XgmiAllReduce:
         # on each other inside one launch (see :attr:`colocated`)
         props = torch.cuda.get_device_properties(self.device)
         me = (props.pci_domain_id, props.pci_bus_id, props.pci_device_id, str(getattr(props, "uuid", "")))
+        # ranks sharing a GPU on DISJOINT CU partitions (utils/cu_partition:
+        # every launch of such a rank goes to a CU-masked queue) cannot hold
+        # each other's CUs: they run the one-rank-per-GPU schedules
+        from ..utils import cu_partition
+
+        part = cu_partition.active(self.device)
+        cus = frozenset(part.bits) if part is not None else None
         allh = [None] * self.world
-        dist.all_gather_object(allh, (mine, me), group=group)
-        devs = [d for _, d in allh]
-        allh = [h for h, _ in allh]
-        self.colocated = len(set(devs)) < self.world
+        dist.all_gather_object(allh, (mine, me, cus), group=group)
+        devs = [d for _, d, _ in allh]
+        masks = [c for _, _, c in allh]
+        allh = [h for h, _, _ in allh]
+        self.colocated = self.partitioned = False
+        for a in range(self.world):
+            for b in range(a + 1, self.world):
+                if devs[a] != devs[b]:
+                    continue
+                if masks[a] is None or masks[b] is None or masks[a] & masks[b]:
+                    self.colocated = True
+                else:
+                    self.partitioned = True
+        self.partitioned = self.partitioned and not self.colocated
         self._opened = []
         ptrs = [[0] * self.world for _ in range(3)]
         ok = 1
@@ -218,16 +236,22 @@ class XgmiAllReduce:
             raise ValueError("XgmiAllReduce: bad range for an all-reduce role")
         return (self.peers.data_ptr(), offset, n, self.rank, self.world, chan, self.epochs.data_ptr(),
                 self.err.data_ptr(), PROTOCOLS[self.protocol],
-                *self.update_args(params, mom, lr_dev, momentum, weight_decay, gscale, nesterov), zero_from)
+                *self.update_args(params, mom, lr_dev, momentum, weight_decay, gscale, nesterov, cover=offset + n),
+                zero_from)
 
     def update_args(self, params: torch.Tensor, mom: torch.Tensor, lr_dev: torch.Tensor, momentum: float,
-                    weight_decay: float, gscale: float, nesterov: bool) -> tuple:
+                    weight_decay: float, gscale: float, nesterov: bool, cover: int | None = None) -> tuple:
         """(params, momentum, lr pointer, momentum, weight decay, grad scale,
         nesterov) of an SGD epilogue, in the gradient layout (the registered
-        buffer may extend past them: e.g. gradient replicas)."""
+        buffer may extend past them: e.g. gradient replicas).  ``cover``: the
+        end (exclusive, in floats) of the furthest range the epilogue will
+        write -- params and momentum must reach it."""
         for t in (params, mom):
             if t.dtype != torch.float32 or t.numel() > self.buf.numel() or t.device != self.device:
                 raise ValueError("XgmiAllReduce: params/momentum must be fp32 in the gradient layout")
+            if cover is not None and t.numel() < cover:
+                raise ValueError(f"XgmiAllReduce: params/momentum ({t.numel()} floats) do not cover the updated "
+                                 f"range (to {cover})")
         return (params.data_ptr(), mom.data_ptr(), lr_dev.data_ptr(), momentum, weight_decay, gscale, int(nesterov))
 
     def exchange_args(self) -> tuple:

@@ -209,8 +209,14 @@ class FusedMnistTrainer:
         # ranks sharing one GPU (rehearsals, the one-GPU test box): the same
         # two roles, but as a launch of their own right after the backward --
         # F12's conv blocks waiting on them could hold the CUs a co-located
-        # peer needs to reach its own roles (XgmiAllReduce.colocated)
+        # peer needs to reach its own roles (XgmiAllReduce.colocated).  Ranks
+        # that share a GPU on disjoint CU partitions (utils/cu_partition)
+        # cannot, and run the inline form like one rank per GPU.
         self._inline = self.overlap and not self._xgmi.colocated
+        if self._xgmi is not None and self._xgmi.partitioned:
+            from ..utils import cu_partition
+
+            self.comm_info["cu_partition"] = dict(cu_partition.active(device).describe(), partitioned=True)
         # every captured graph ends with a hash of this rank's parameters
         # published into every rank's flag page; run() compares them
         # (XgmiAllReduce.check_hashes): a rank whose exchange read a stale
@@ -349,7 +355,8 @@ class FusedMnistTrainer:
             self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
             P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(), self.code1.data_ptr(),
             self.a2p.data_ptr(), self.code2.data_ptr(), B, self.batch_idx.data_ptr(), self.xcur.data_ptr(),
-            *x.exchange_args(), *x.update_args(self._params, self.mom, self.lr_dev, mom, wd, gs, bool(nes)),
+            *x.exchange_args(), *x.update_args(self._params, self.mom, self.lr_dev, mom, wd, gs, bool(nes),
+                                               cover=self.numel),
             0, self._split, FC_CHAN, self.numel,
             self._split, self.numel - self._split, CONV_CHAN,
             self.numel, self.c1_nrep, self.c1_stride, self._c1, self._ready.data_ptr(), self._s()),
@@ -366,7 +373,7 @@ class FusedMnistTrainer:
             return
         L, x = self.L, self._xgmi
         lr, mom, wd, gs, nes = self._opt_args()
-        upd = x.update_args(self._params, self.mom, self.lr_dev, mom, wd, gs, bool(nes))
+        upd = x.update_args(self._params, self.mom, self.lr_dev, mom, wd, gs, bool(nes), cover=self.numel)
         _lib.check(L.pto_ar_oneshot_role_sgd(x.peers.data_ptr(), self._split, self.numel - self._split, x.rank,
                                              x.world, CONV_CHAN, x.epochs.data_ptr(), x.err.data_ptr(),
                                              x.exchange_args()[5], *upd, self.numel, self.c1_nrep, self.c1_stride,
@@ -464,7 +471,9 @@ class FusedMnistTrainer:
         # change the trajectory, then capture
         state = self._state()
         snap = [t.clone() for t in state]
-        s = torch.cuda.Stream(self.device)
+        from ..utils import cu_partition
+
+        s = cu_partition.side_stream(self.device)  # a CU-partitioned rank warms up inside its own CUs
         s.wait_stream(torch.cuda.current_stream(self.device))
         self._align_ranks("warmup")
         with torch.cuda.stream(s):
@@ -802,6 +811,9 @@ def autotune_schedule(cands: list, rc: FusedMnistTrainer, verify_steps: int = 8,
             identical = bool(torch.equal(chk.to(mine.device), mine))
             ok = agree(stalled is None and err <= 1e-4 and identical and xg._xgmi.error_word() == 0)
             out["candidates"][_variant(xg)] = {"param_rel_err": err, "identical": identical, "correct": ok}
+            if xg.overlap:
+                out["candidates"][_variant(xg)]["exchange"] = ("inside the next F12 launch" if xg._inline
+                                                               else "own launch after the backward")
             if stalled:
                 out["candidates"][_variant(xg)]["error"] = stalled
             ok_c.append(ok)
@@ -888,6 +900,40 @@ class RacedTrainer:
         capture, so the timed region runs the kept schedule."""
         self._maybe_race(now=True)
         return self._tr.prepare()
+
+    # Methods a caller may look up ONCE, before the race, and keep calling
+    # (train/mnist.py caches ``loss_async``): defined here so every call
+    # reaches the trainer that is current at call time, not the one that
+    # was current at lookup (ADVICE r5: a twin winning the race must not
+    # leave the logged loss frozen on the abandoned trainer's buffer).
+    def loss_async(self):
+        return self._tr.loss_async()
+
+    def last_loss(self):
+        return self._tr.last_loss()
+
+    def flush(self):
+        return self._tr.flush()
+
+    def check_comm(self, blocking: bool = True):
+        return self._tr.check_comm(blocking)
+
+    def evaluate(self, *a, **k):
+        return self._tr.evaluate(*a, **k)
+
+    def state_dict(self):
+        return self._tr.state_dict()
+
+    def load_state_dict(self, sd):
+        return self._tr.load_state_dict(sd)
+
+    def set_lr(self, lr: float):
+        return self._tr.set_lr(lr)
+
+    @property
+    def needs_host_barrier(self) -> bool:
+        # until the race has run, a twin that needs the barrier may still win
+        return self._kw is not None or self._tr.needs_host_barrier
 
 
 def _race(tr: FusedMnistTrainer, kw: dict) -> FusedMnistTrainer:

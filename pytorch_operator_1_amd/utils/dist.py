@@ -163,6 +163,14 @@ def init_distributed(backend: str | None = None, use_gpu: bool | None = None,
         if store is not None:
             kwargs.update(store=store, rank=env.rank, world_size=env.world_size)
         dist.init_process_group(**kwargs)
+    if use_gpu and env.is_distributed and os.environ.get("PTO_CU_PARTITION") == "1":
+        # ranks that share a GPU (a rehearsal on fewer GPUs than ranks):
+        # each on its own CU partition, so they run the schedules of one
+        # rank per GPU (utils/cu_partition.py)
+        from . import cu_partition
+
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", env.world_size))
+        cu_partition.activate_for_rank(env.local_rank, local_world, device)
     return env, device
 
 

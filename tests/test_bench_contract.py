@@ -120,9 +120,9 @@ def test_params_fingerprint_is_bit_exact():
 
 
 def test_bench_falls_back_to_rccl_when_xgmi_fails():
-    """N > 1: when the peer-memory exchange fails (a bounded spin timing
-    out, or diverged parameter hashes -- both seen by every rank, since the
-    peers wait on / compare each other; injected here on all ranks), the
+    """N > 1: when the peer-memory exchange times out (a bounded spin giving
+    up -- seen by every rank, since the peers wait on each other; injected
+    here on all ranks), the
     ranks agree through the status all-reduces that double as the timing
     barriers, the job is re-measured on the RCCL schedule and the JSON says
     so instead of losing the data point."""
@@ -137,3 +137,16 @@ def test_bench_falls_back_to_rccl_when_xgmi_fails():
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert "injected" in d["config"]["grad_allreduce"]["xgmi_failed_fell_back_to_rccl"]
     assert "re-measuring on the RCCL schedule" in out.stderr
+
+
+def test_bench_fallback_only_on_timeouts():
+    """Only a timed-out exchange is re-measured on the RCCL schedule; diverged
+    replicas (XgmiDivergence) and unrelated errors whose message merely names
+    xGMI are not: they fail the bench."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from pytorch_operator_1_amd.parallel.xgmi import XgmiDivergence, XgmiTimeout
+
+    assert bench._xgmi_failure(XgmiTimeout("barrier timed out"))
+    assert not bench._xgmi_failure(XgmiDivergence("ranks diverged"))
+    assert not bench._xgmi_failure(RuntimeError("xgmi_allreduce failed with hipError 1"))

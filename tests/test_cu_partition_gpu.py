@@ -1,0 +1,59 @@
+"""CU partitions of one GPU (utils/cu_partition.py): the masks a co-located
+rank's streams carry are honoured by the hardware, for eager launches and
+for HIP-graph replays (the trainer's hot path), and disjoint masks give
+disjoint CUs -- the property the inline exchange schedule needs before ranks
+that share a GPU may run it (tests/test_ddp_gpu.py ``*-inline``)."""
+import os
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+
+
+def test_cu_masks_honoured_eager_and_graph_replay():
+    import cu_partition_probe
+
+    # "block" masks only: the hardware honours them (interleaved over the 8
+    # XCDs: partition k of n gets 32/n CUs of every XCD); a "stride" mask
+    # (every n-th bit) is accepted by the runtime but NOT applied -- the probe
+    # finds all 256 CUs in use (profiles/cu_partition_r6.md)
+    res = cu_partition_probe.run(parts_list=(2, 4, 8), layouts=("block",))
+    n = res["unmasked"]["n_cus"]
+    assert n >= res["device_cus"] * 0.9, res["unmasked"]
+    for row in res["partitions"]:
+        if row.get("summary"):
+            assert row["pairwise_overlap_cus"] == 0, row  # disjoint masks -> disjoint CUs
+            assert row["union_cus"] >= 0.9 * n, row
+            continue
+        assert row["outside_unmasked_set"] == 0, row
+        assert row["graph_within_eager"], row  # replay stays inside the mask too
+        # each partition reaches (close to) the CUs its mask grants, no more
+        assert 0.8 * row["mask_cus"] <= row["eager_cus"] <= row["mask_cus"], row
+        assert 0.8 * row["mask_cus"] <= row["graph_cus"] <= row["mask_cus"], row
+        per = row["eager_cus_per_xcc"]
+        assert len(per) == 8 and max(per.values()) - min(per.values()) <= 1, row  # a share of every XCD
+
+
+def test_partition_is_current_stream_and_side_stream_shares_mask():
+    from pytorch_operator_1_amd.utils import cu_partition as cp
+
+    dev = torch.device("cuda", 0)
+    p = cp.Partition(dev, 1, 2)
+    try:
+        assert cp.active(dev) is None
+        p.activate()
+        assert cp.active(dev) is p and torch.cuda.current_stream(dev).cuda_stream == p.stream.cuda_stream
+        s = cp.side_stream(dev)
+        assert p.owns(s) and s.cuda_stream != p.stream.cuda_stream
+        a = set(cp.probe_cus(p.stream)["cus"])
+        b = set(cp.probe_cus(s)["cus"])
+        assert b <= a or len(b - a) == 0
+        x = torch.ones(1000, device=dev) * 3  # ordinary torch work on the masked current stream
+        assert float(x.sum()) == 3000.0
+    finally:
+        p.close()
+    assert cp.active(dev) is None

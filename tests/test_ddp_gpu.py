@@ -31,6 +31,11 @@ def _free_port():
 
 def _worker(rank, world, port, q, comm, steps=STEPS):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    # "-inline": every rank on its own CU partition of the shared GPU
+    # (utils/cu_partition), so the trainer takes the schedule of one rank per
+    # GPU -- the exchange roles inside the next step's F12 launch
+    inline = comm.endswith("-inline")
+    comm = comm[:-len("-inline")] if inline else comm
     if comm == "xgmi-det":  # deterministic backward: per-sample conv1 replicas folded by the all-reduce
         comm = "xgmi"
         os.environ["PTO_DETERMINISTIC"] = "1"
@@ -58,6 +63,11 @@ def _worker(rank, world, port, q, comm, steps=STEPS):
     dist.init_process_group("gloo")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    if inline:
+        from pytorch_operator_1_amd.utils import cu_partition
+
+        part = cu_partition.activate_for_rank(rank, world, dev)
+        assert part is not None and cu_partition.active(dev) is part
     pre = 0
     if race:
         # the schedule race of build_fused_trainer, deferred past the job's
@@ -77,18 +87,25 @@ def _worker(rank, world, port, q, comm, steps=STEPS):
         assert all(c["step_us"] > 0 and c["spread_us"] >= 0 for c in cands.values()), res
         assert res["kept"] == tr.schedule + ("+overlap" if tr.overlap else ""), res
         assert tr.steps_done == 1 and int(tr.batch_idx.item()) == 1
+        if inline:  # the overlapped candidate that raced was the inline form
+            assert cands["ddp-xgmi+overlap"]["exchange"] == "inside the next F12 launch", res
+            assert cands["ddp-xgmi+overlap"]["correct"], res
     else:
         tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=N, seed=1, rank=rank, comm=comm)
     if race:
         pass
     elif comm == "xgmi":
         assert tr.comm_info["transport"] == "xgmi" and tr.graph_mode == "full" and tr.schedule == "ddp-xgmi"
+        assert tr._inline == inline and tr._xgmi.partitioned == inline and tr._xgmi.colocated != inline
+        if inline:
+            assert "next step's F12 launch" in tr.comm_info["overlap"], tr.comm_info
+            assert tr.comm_info["cu_partition"]["parts"] == world, tr.comm_info
     else:
         assert tr.comm_info["transport"] == "host-allreduce (gloo)" and tr.graph_mode == "split"
         assert tr.schedule == "ddp-rccl"
     if verify_fail:
         assert tr.comm_info["correct"] is False and tr.comm_info["use_xgmi"] is False, tr.comm_info
-    assert tr.comm_info["world_size"] == 2
+    assert tr.comm_info["world_size"] == world
     if steps == STEPS:
         for _ in range(steps - pre):
             tr.step()
@@ -108,12 +125,12 @@ def _worker(rank, world, port, q, comm, steps=STEPS):
 
 
 @pytest.mark.parametrize("comm", ["host-allreduce", "xgmi", "xgmi-fenced", "xgmi-det", "xgmi-verify-fail",
-                                  "auto-race"])
+                                  "auto-race", "xgmi-inline", "auto-race-inline"])
 def test_fused_ddp_two_ranks_matches_reference(comm):
     _run_and_compare(comm, STEPS, 1e-4)
 
 
-@pytest.mark.parametrize("comm", ["host-allreduce", "xgmi"])
+@pytest.mark.parametrize("comm", ["host-allreduce", "xgmi", "xgmi-inline"])
 def test_fused_ddp_two_ranks_200_steps(comm):
     """Long horizon: 200 steps of the 2-rank xGMI and
     host-allreduce schedules, replayed from the 32-step graphs, against the
@@ -121,7 +138,15 @@ def test_fused_ddp_two_ranks_200_steps(comm):
     _run_and_compare(comm, 200, 2e-3)
 
 
-def _run_and_compare(comm, steps, tol):
+@pytest.mark.parametrize("world", [4, 8])
+def test_fused_ddp_inline_more_ranks(world):
+    """The inline exchange (roles inside the next F12 launch) at world 4 and
+    8, each rank on its own 1/world of the GPU's CUs, 40 steps through the
+    captured graphs, against the stock-PyTorch reference."""
+    _run_and_compare("xgmi-inline", 40, 1e-3, world=world)
+
+
+def _run_and_compare(comm, steps, tol, world=2):
     """host-allreduce: grads-only step, gloo all-reduce between split graphs,
     SGD launch; xgmi: one peer-memory all-reduce of the whole buffer with the
     SGD epilogue inside the whole-step graph (no optimizer launch); xgmi-det:
@@ -132,14 +157,15 @@ def _run_and_compare(comm, steps, tol):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, comm, steps)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, comm, steps)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(collect(q, procs, 2))
+    res = dict(collect(q, procs, world))
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    assert torch.equal(res[0], res[1]), "ranks diverged"
+    for r in range(1, world):
+        assert torch.equal(res[0], res[r]), f"ranks 0 and {r} diverged"
 
     from pytorch_operator_1_amd.models.mnist import MnistNet, param_offsets, synthetic_mnist
 
@@ -147,7 +173,7 @@ def _run_and_compare(comm, steps, tol):
     torch.manual_seed(1)
     m = MnistNet().to(dev)
     opt = torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.5)
-    data = [synthetic_mnist(N, dev, seed=1 + 1000 * r) for r in range(2)]
+    data = [synthetic_mnist(N, dev, seed=1 + 1000 * r) for r in range(world)]
     for i in range(steps):
         bi = i % (N // 64)
         opt.zero_grad()
@@ -158,7 +184,7 @@ def _run_and_compare(comm, steps, tol):
             g = [p.grad.clone() for p in m.parameters()]
             grads = g if grads is None else [a + b for a, b in zip(grads, g)]
         for p, g in zip(m.parameters(), grads):
-            p.grad = g / 2
+            p.grad = g / world
         opt.step()
     offs, _ = param_offsets()
     flat = res[0]
@@ -169,7 +195,7 @@ def _run_and_compare(comm, steps, tol):
         assert err < tol, (name, err)
 
 
-def _diverge_worker(rank, world, port, q, flip):
+def _diverge_worker(rank, world, port, q, flip, inline=False):
     """Self-verifying multi-GPU run: every captured graph
     ends with a hash of the rank's parameters published into every rank's
     flag page; run() compares them.  ``flip``: after two clean chunks rank 1
@@ -186,8 +212,13 @@ def _diverge_worker(rank, world, port, q, flip):
         dist.init_process_group("gloo")
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
+        if inline:
+            from pytorch_operator_1_amd.utils import cu_partition
+
+            cu_partition.activate_for_rank(rank, world, dev)
         tr = FusedMnistTrainer(dev, batch_size=64, dataset_size=N, seed=1, rank=rank, comm="xgmi", unroll=8)
         assert tr._hash and "consistency" in tr.comm_info
+        assert tr._inline == inline
         for _ in range(2):
             tr.run(8)
         compared = tr._xgmi.hashes_compared
@@ -221,12 +252,13 @@ def _diverge_worker(rank, world, port, q, flip):
         raise
 
 
+@pytest.mark.parametrize("inline", [False, True])
 @pytest.mark.parametrize("flip", [False, True])
-def test_xgmi_ranks_self_verify_parameter_hash(flip):
+def test_xgmi_ranks_self_verify_parameter_hash(flip, inline):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_diverge_worker, args=(r, 2, port, q, flip)) for r in range(2)]
+    ps = [ctx.Process(target=_diverge_worker, args=(r, 2, port, q, flip, inline)) for r in range(2)]
     for p in ps:
         p.start()
     res = collect(q, ps, 2, timeout=110)
