@@ -45,9 +45,19 @@ _CL = torch.channels_last
 
 class GradStash:
     """One gradient handed from a later backward node to an earlier one of
-    the same bottleneck (bn3's residual gradient -> conv1's input GEMM)."""
+    the same bottleneck (bn3's residual gradient -> conv1's input GEMM).
+
+    Constraint (merge mode, a downsample block's two sibling 1x1 convs):
+    BOTH siblings must run their backward in the same pass.  The first one
+    parks its input gradient here and returns None; the second adds its own
+    part and returns the sum.  If autograd prunes one branch (e.g.
+    ``torch.autograd.grad`` restricted to one branch's inputs, or a detached
+    downsample) the parked gradient would be lost, so every parked gradient
+    is counted (:attr:`parked`) and :meth:`assert_drained` -- called by the
+    ResNet trainer after each backward -- raises if one was never taken."""
 
     __slots__ = ("g",)
+    parked = 0  # gradients put and not yet taken, over every stash
 
     def __init__(self):
         self.g = None
@@ -56,10 +66,22 @@ class GradStash:
         if self.g is not None:
             raise RuntimeError("GradStash: gradient already stashed (backward ran twice without a forward?)")
         self.g = g
+        GradStash.parked += 1
 
     def take(self):
         g, self.g = self.g, None
+        if g is not None:
+            GradStash.parked -= 1
         return g
+
+    @classmethod
+    def assert_drained(cls):
+        """Raise if a parked gradient was never consumed (a pruned sibling
+        branch: its input gradient would silently be missing)."""
+        if cls.parked:
+            n, cls.parked = cls.parked, 0
+            raise RuntimeError(f"GradStash: {n} parked input gradient(s) never consumed -- a conv1x1 merge pair "
+                               "whose sibling branch did not run backward (pruned / detached branch)")
 
 
 def gemm_supported(x: torch.Tensor, conv: nn.Conv2d, stride1: bool = False) -> bool:

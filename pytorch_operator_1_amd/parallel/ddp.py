@@ -26,16 +26,43 @@ and relies on its bucketing.  This is the MI355X-first replacement:
 * Comm hook: when the whole gradient buffer is small
   (<= ``PTO_XGMI_MAX_MB``, 512 MB), it is registered with the xGMI peer
   all-reduce kernel (:mod:`.xgmi`, fp32 or bf16), verified against the
-  group's all-reduce, and every bucket is timed both ways at startup; a
+  group's all-reduce, and buckets are timed both ways at startup; a
   bucket goes to the kernel if it was faster there (the decision is
-  recorded in :attr:`GradBucketer.comm_info`).
+  recorded in :attr:`GradBucketer.comm_info`).  The timing is bounded: one
+  bucket per power-of-two size class is timed, at most
+  ``PTO_XGMI_TUNE_CLASSES`` (4) classes, and every other bucket takes the
+  decision of the nearest timed class (:func:`plan_bucket_timing`), so the
+  startup cost does not grow with the bucket count; the seconds spent are
+  recorded (``comm_info["xgmi_tune_s"]``).
 """
 from __future__ import annotations
 
 import os
+import time
 
 import torch
 import torch.distributed as dist
+
+
+def plan_bucket_timing(sizes: list[int], max_classes: int = 4) -> list[int]:
+    """Which bucket's timing decides each bucket: ``plan[i] = j`` means
+    bucket ``i`` takes the xGMI-vs-RCCL decision measured on bucket ``j``
+    (``plan[j] == j`` for the timed ones).  Buckets are grouped by
+    power-of-two size class; the first bucket of each class is timed, for at
+    most ``max_classes`` classes chosen largest first (the large buckets
+    carry the bytes); a bucket of an untimed class follows the timed class
+    nearest in size.  Deterministic in ``sizes``, so every rank makes the
+    same plan (the timing itself is a collective)."""
+    cls = [max(1, int(n)).bit_length() for n in sizes]
+    first: dict[int, int] = {}
+    for i, c in enumerate(cls):
+        first.setdefault(c, i)
+    timed = sorted(first, reverse=True)[:max(1, max_classes)]
+    plan = []
+    for c in cls:
+        best = min(timed, key=lambda t: (abs(t - c), -t))
+        plan.append(first[best])
+    return plan
 
 
 class GradBucketer:
@@ -154,14 +181,23 @@ class GradBucketer:
                 self.comm_info["xgmi"] = {k: v for k, v in res.items() if k != "verify_log"}
                 return
             used = False
-            for (i, b), rng in zip(mine, ranges):
-                tx, tr, ok = ar.time_vs_collective([rng], iters=10, stream=self.comm_stream)
+            plan = plan_bucket_timing([n for _, n in ranges], int(os.environ.get("PTO_XGMI_TUNE_CLASSES", "4")))
+            timings: dict[int, tuple] = {}
+            t0 = time.perf_counter()
+            for k, ((i, b), rng) in enumerate(zip(mine, ranges)):
+                j = plan[k]
+                if j not in timings:
+                    timings[j] = ar.time_vs_collective([ranges[j]], iters=10, stream=self.comm_stream)
+                tx, tr, ok = timings[j]
                 take = ok and (comm == "xgmi" or tx < tr)
                 b["transport"] = "xgmi" if take else "rccl"
                 b["chan"] = i % 2
                 used |= take
                 decisions.append({"bucket": i, "mb": round((b["hi"] - b["lo"]) * buf.element_size() / 2**20, 2),
-                                  "xgmi_us": round(tx, 1), "rccl_us": round(tr, 1), "use": b["transport"]})
+                                  "xgmi_us": round(tx, 1), "rccl_us": round(tr, 1), "use": b["transport"],
+                                  "timed_on": mine[j][0]})
+            self.comm_info["xgmi_tune_s"] = round(self.comm_info.get("xgmi_tune_s", 0.0) + time.perf_counter() - t0, 3)
+            self.comm_info["xgmi_timed_buckets"] = self.comm_info.get("xgmi_timed_buckets", 0) + len(timings)
             if used:
                 self._xgmi[dt] = ar
             else:

@@ -20,6 +20,7 @@ import os
 import torch
 import torch.nn.functional as F
 
+from ..ops.conv1x1 import GradStash
 from ..ops.optim import FusedAdamW, FusedSGD
 from ..parallel.ddp import GradBucketer
 from ..utils.profiling import StepTimer
@@ -162,6 +163,7 @@ class ResNetTrainer(CheckpointMixin):
                 out = self.model(self.x)
             loss = F.cross_entropy(out.float(), self.y)
             loss.backward()
+            GradStash.assert_drained()
             self.bucketer.finish()
             self.opt.step(grad_scale=self.bucketer.grad_scale, zero_grad=self.bucketer.optimizer_zeroes_grads)
         self.opt.finish_capture()  # the launch table of the graph's gradients
@@ -176,6 +178,7 @@ class ResNetTrainer(CheckpointMixin):
             loss = F.cross_entropy(out.float(), self.y)
         with t.phase("backward"):
             loss.backward()
+            GradStash.assert_drained()  # host counter: no sibling conv1x1 gradient left parked
         with t.phase("allreduce_wait"):
             self.bucketer.finish()
         with t.phase("optimizer"):

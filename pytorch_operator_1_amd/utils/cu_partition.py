@@ -208,17 +208,23 @@ def active(device=None) -> Partition | None:
 
 
 def side_stream(device):
-    """A stream for work that must run beside the current one: a second
-    stream with the same CU mask when a partition is active, a plain pool
-    stream otherwise."""
+    """A stream for work that runs beside the current one (e.g. a graph
+    warm-up): a pool stream normally; the partition's OWN stream when a
+    partition is active.  Every extra hardware queue of co-located ranks
+    competes for the scheduler's queue slots, and once those are
+    oversubscribed the firmware time-slices the queues (a rank spinning on
+    a peer whose queue is unmapped waits a whole quantum), so a partitioned
+    rank keeps to one queue; work on it is simply serialised."""
     import torch
 
     p = active(device)
     if p is None:
         return torch.cuda.Stream(device)
-    if len(p._streams) < 2:
-        p.new_stream()
-    return p._streams[1]
+    if os.environ.get("PTO_CU_SIDE_STREAM", "main") == "own":  # A/B knob: a second masked queue
+        if len(p._streams) < 2:
+            p.new_stream()
+        return p._streams[1]
+    return p.stream
 
 
 def share_of(local_rank: int, local_world: int, n_gpus: int) -> tuple[int, int, int]:

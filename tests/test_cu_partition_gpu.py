@@ -47,11 +47,12 @@ def test_partition_is_current_stream_and_side_stream_shares_mask():
         assert cp.active(dev) is None
         p.activate()
         assert cp.active(dev) is p and torch.cuda.current_stream(dev).cuda_stream == p.stream.cuda_stream
-        s = cp.side_stream(dev)
+        assert cp.side_stream(dev).cuda_stream == p.stream.cuda_stream  # one queue per partitioned rank
+        s = p.new_stream()
         assert p.owns(s) and s.cuda_stream != p.stream.cuda_stream
         a = set(cp.probe_cus(p.stream)["cus"])
         b = set(cp.probe_cus(s)["cus"])
-        assert b <= a or len(b - a) == 0
+        assert b == a  # a second stream with the same mask reaches the same CUs
         x = torch.ones(1000, device=dev) * 3  # ordinary torch work on the masked current stream
         assert float(x.sum()) == 3000.0
     finally:

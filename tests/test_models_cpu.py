@@ -174,3 +174,23 @@ def test_grad_bucketer_copy_mode_takes_fresh_grads_each_step():
             assert p.grad.untyped_storage().data_ptr() == flat.untyped_storage().data_ptr()
         bk.release()
         assert all(p.grad is None for p in m.parameters())
+
+
+def test_grad_stash_counts_parked_gradients():
+    """A merge-mode GradStash whose sibling never ran backward leaves a
+    parked gradient: assert_drained raises instead of losing it."""
+    import pytest
+    import torch
+
+    from pytorch_operator_1_amd.ops.conv1x1 import GradStash
+
+    GradStash.assert_drained()
+    s = GradStash()
+    s.put(torch.ones(2))
+    with pytest.raises(RuntimeError, match="never consumed"):
+        GradStash.assert_drained()
+    GradStash.assert_drained()  # the count was reset by the raise
+    s2 = GradStash()
+    s2.put(torch.ones(2))
+    assert s2.take() is not None and s2.take() is None
+    GradStash.assert_drained()
