@@ -620,6 +620,25 @@ PTO_API int pto_bn_fwd(const void* x, const void* res, void* y, long long M, int
   return (int)hipGetLastError();
 }
 
+// Forward whose statistics pass already happened elsewhere: part holds
+// nblk rows of [2][C] partial sums / sums of squares of x (the 3x3 conv's
+// epilogue, conv3x3.hip), so only finalize + apply run.
+PTO_API int pto_bn_fwd_part(const float* part, int nblk, const void* x, const void* res, void* y, long long M, int C,
+                            const float* gamma, const float* beta, float eps, float momentum, float* run_mean,
+                            float* run_var, long long* nbt, float* stat, int relu, void* mask, hipStream_t s) {
+  if (!bn_shape_ok(M, C) || !part || nblk < 1) return -1;
+  if ((((uintptr_t)x) | ((uintptr_t)y) | ((uintptr_t)res)) & 15) return -1;
+  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 31) / 32), dim3(BN_FT), 0, s, part, nblk, M, C, gamma, beta, eps,
+                     momentum, run_mean, run_var, nbt, stat);
+  const long long n8 = M * C / 8;
+  auto* ka = res ? (relu ? k_bn_apply<true, true> : k_bn_apply<true, false>)
+                 : (relu ? k_bn_apply<false, true> : k_bn_apply<false, false>);
+  hipLaunchKernelGGL(ka, dim3(elementwise_blocks(n8)), dim3(BN_T), 0, s, reinterpret_cast<const uint16_t*>(x),
+                     reinterpret_cast<const uint16_t*>(res), reinterpret_cast<uint16_t*>(y), n8, C, stat,
+                     reinterpret_cast<uint8_t*>(mask));
+  return (int)hipGetLastError();
+}
+
 // Backward.  mode 0/1/2 as k_bn_bwd_reduce; ymask (the forward's ReLU
 // bitmask, M*C/8 bytes) needed for mode 2, where g_out (= d residual) is
 // also written.  coef: 3*C floats scratch.

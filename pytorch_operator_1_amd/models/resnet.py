@@ -16,6 +16,7 @@ import torch.nn as nn
 
 from ..ops.bn import BatchNormAct
 from ..ops.conv1x1 import GradStash, conv1x1, conv1x1_res, gemm_supported
+from ..ops.conv3x3 import ConvStats, conv3x3
 from ..ops.pool import MaxPool2d
 from ..ops.stem import stem_conv
 
@@ -35,6 +36,12 @@ class Bottleneck(nn.Module):
         self.downsample = (nn.Sequential(nn.Conv2d(cin, cout, 1, stride=stride, bias=False), BatchNormAct(cout))
                            if down else None)
 
+    def _c2(self, y):
+        """The 3x3 conv + bn2 + ReLU: the MFMA implicit-GEMM kernel, whose
+        epilogue hands bn2 its batch statistics (ops/conv3x3.py)."""
+        st = ConvStats()
+        return self.bn2(conv3x3(y, self.conv2, st), relu=True, stats=st)
+
     @staticmethod
     def _c1(conv, x):
         """1x1 convs (the downsample ones strided): backward on hipBLASLt
@@ -49,7 +56,7 @@ class Bottleneck(nn.Module):
         if self.downsample is None and gemm_supported(x, self.conv1, stride1=True) and self.bn3.can_fuse(x):
             stash = GradStash()
             y = self.bn1(conv1x1_res(x, self.conv1, stash), relu=True)
-            y = self.bn2(self.conv2(y), relu=True)
+            y = self._c2(y)
             return self.bn3(self._c1(self.conv3, y), residual=x, relu=True, stash=stash)
         if (self.downsample is not None and gemm_supported(x, self.downsample[0])
                 and gemm_supported(x, self.conv1)):
@@ -58,11 +65,11 @@ class Bottleneck(nn.Module):
             merge = GradStash()
             idt = self.downsample[1](conv1x1(x, self.downsample[0], merge))
             y = self.bn1(conv1x1(x, self.conv1, merge), relu=True)
-            y = self.bn2(self.conv2(y), relu=True)
+            y = self._c2(y)
             return self.bn3(self._c1(self.conv3, y), residual=idt, relu=True)
         idt = x if self.downsample is None else self.downsample[1](self._c1(self.downsample[0], x))
         y = self.bn1(self._c1(self.conv1, x), relu=True)
-        y = self.bn2(self.conv2(y), relu=True)
+        y = self._c2(y)
         return self.bn3(self._c1(self.conv3, y), residual=idt, relu=True)
 
 

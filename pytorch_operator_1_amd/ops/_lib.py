@@ -29,7 +29,7 @@ ARCH = os.environ.get("PTO_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 
 HIP_SOURCES = ("kernels/mnist_kernels.hip", "kernels/common_kernels.hip", "kernels/optim_kernels.hip",
-               "kernels/llm_kernels.hip", "kernels/attention.hip", "kernels/bn_kernels.hip",
+               "kernels/llm_kernels.hip", "kernels/attention.hip", "kernels/bn_kernels.hip", "kernels/conv3x3.hip",
                "comm/xgmi_allreduce.hip")
 
 _lock = threading.Lock()
@@ -141,6 +141,13 @@ _SIGS = {
     "pto_bn_scratch_floats": [_L, _I],
     "pto_bn_fwd": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _I, _P, _P],
     "pto_bn_bwd": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _I, _P],
+    "pto_bn_fwd_part": [_P, _I, _P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _I, _P, _P],
+    # ResNet-50 3x3 convs (csrc/kernels/conv3x3.hip)
+    "pto_conv3x3_tile_m": [_I],
+    "pto_conv3x3_set_variant": [_I, _I],
+    "pto_conv3x3_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "pto_conv3x3_wcast": [_P, _P, _L, _P],
+    "pto_conv3x3_wflip": [_P, _P, _P, _I, _I, _P],
     "pto_maxpool_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
     "pto_stem_fwd": [_P, _P, _L, _L, _L, _L, _P, _P, _I, _P],
     "pto_maxpool_bwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],

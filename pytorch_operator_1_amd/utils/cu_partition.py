@@ -209,22 +209,23 @@ def active(device=None) -> Partition | None:
 
 def side_stream(device):
     """A stream for work that runs beside the current one (e.g. a graph
-    warm-up): a pool stream normally; the partition's OWN stream when a
-    partition is active.  Every extra hardware queue of co-located ranks
-    competes for the scheduler's queue slots, and once those are
-    oversubscribed the firmware time-slices the queues (a rank spinning on
-    a peer whose queue is unmapped waits a whole quantum), so a partitioned
-    rank keeps to one queue; work on it is simply serialised."""
+    warm-up): a pool stream normally; with a partition active, a SECOND
+    stream carrying the partition's mask (cached on the partition).
+    Measured on the 2-rank rehearsal (profiles/cu_partition_r6.md): warming
+    up on the partition's own stream instead (``PTO_CU_SIDE_STREAM=main``)
+    made every later replay of the inline schedule ~11x slower (728-750 vs
+    66 us/step, interleaved on one box), so the warm-up gets its own
+    masked queue."""
     import torch
 
     p = active(device)
     if p is None:
         return torch.cuda.Stream(device)
-    if os.environ.get("PTO_CU_SIDE_STREAM", "main") == "own":  # A/B knob: a second masked queue
-        if len(p._streams) < 2:
-            p.new_stream()
-        return p._streams[1]
-    return p.stream
+    if os.environ.get("PTO_CU_SIDE_STREAM", "own") == "main":  # the measured-slower variant, for A/B runs
+        return p.stream
+    if len(p._streams) < 2:
+        p.new_stream()
+    return p._streams[1]
 
 
 def share_of(local_rank: int, local_world: int, n_gpus: int) -> tuple[int, int, int]:

@@ -47,9 +47,8 @@ def test_partition_is_current_stream_and_side_stream_shares_mask():
         assert cp.active(dev) is None
         p.activate()
         assert cp.active(dev) is p and torch.cuda.current_stream(dev).cuda_stream == p.stream.cuda_stream
-        assert cp.side_stream(dev).cuda_stream == p.stream.cuda_stream  # one queue per partitioned rank
-        s = p.new_stream()
-        assert p.owns(s) and s.cuda_stream != p.stream.cuda_stream
+        s = cp.side_stream(dev)  # a second masked stream, cached
+        assert p.owns(s) and s.cuda_stream != p.stream.cuda_stream and cp.side_stream(dev) is s
         a = set(cp.probe_cus(p.stream)["cus"])
         b = set(cp.probe_cus(s)["cus"])
         assert b == a  # a second stream with the same mask reaches the same CUs

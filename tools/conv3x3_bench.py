@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""ResNet-50's 3x3 convs at batch 256: the MFMA implicit-GEMM kernel
+(ops/conv3x3.py) against MIOpen (F.conv2d / aten.convolution_backward,
+cudnn.benchmark on), forward and stride-1 data gradient, median of HIP-event
+timed repeats.  One JSON line per shape.
+
+    python tools/conv3x3_bench.py [--batch 256] [--reps 20]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+SHAPES = [(64, 56, 1), (128, 56, 2), (128, 28, 1), (256, 28, 2), (256, 14, 1), (512, 14, 2), (512, 7, 1)]
+
+
+def timed(fn, reps):
+    import torch
+
+    for _ in range(3):
+        fn()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    import torch
+    import torch.nn as nn
+    import torch.nn.functional as F
+
+    from pytorch_operator_1_amd.ops import _lib
+    from pytorch_operator_1_amd.ops import conv3x3 as c3
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--shapes", default="", help="only these C:H:stride shapes, comma-separated")
+    ap.add_argument("--no-dgrad", action="store_true")
+    ap.add_argument("--variants", default="64:2", help="kernel variants bk:pf to time, comma-separated "
+                                                       "(bk = K-step channels 32|64, pf = prefetch steps 1|2)")
+    a = ap.parse_args()
+    torch.backends.cudnn.benchmark = True
+    dev = torch.device("cuda", 0)
+    L = _lib.lib()
+    tot = {"ours_fwd": 0.0, "lib_fwd": 0.0, "ours_dgrad": 0.0, "lib_dgrad": 0.0}
+    want = {tuple(int(u) for u in v.split(":")) for v in a.shapes.split(",") if v}
+    for C, H, s in SHAPES:
+        if want and (C, H, s) not in want:
+            continue
+        N = a.batch
+        conv = nn.Conv2d(C, C, 3, stride=s, padding=1, bias=False).to(dev, memory_format=torch.channels_last)
+        x = torch.randn(N, C, H, H, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        wb = conv.weight.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        OH = (H + 2 - 3) // s + 1
+        part = torch.empty(c3.stats_tiles(N, OH, OH, C) * 2 * C, device=dev)
+        flops = 2.0 * N * OH * OH * C * C * 9
+        lib = timed(lambda: F.conv2d(x, wb, stride=s, padding=1), a.reps)
+        row = {"C": C, "H": H, "stride": s, "batch": N, "miopen_fwd_us": round(lib, 1),
+               "miopen_tflops": round(flops / lib / 1e6, 1)}
+        best = None
+        variants = [tuple(int(u) for u in v.split(":")) for v in a.variants.split(",")]
+        for bk, pf in variants:
+            _lib.check(L.pto_conv3x3_set_variant(bk, pf), "set_variant")
+            t = timed(lambda: c3._fwd(L, x, wb, s, part), a.reps)
+            row[f"fwd_us_{bk}_{pf}"] = round(t, 1)
+            row[f"fwd_tflops_{bk}_{pf}"] = round(flops / t / 1e6, 1)
+            tot[f"ours_fwd_{bk}_{pf}"] = tot.get(f"ours_fwd_{bk}_{pf}", 0.0) + t
+            best = t if best is None else min(best, t)
+        _lib.check(L.pto_conv3x3_set_variant(*variants[0]), "set_variant")
+        ours = best
+        tot["ours_fwd"] += ours
+        tot["lib_fwd"] += lib
+        if s == 1 and not a.no_dgrad:
+            dy = torch.randn(N, C, OH, OH, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            wf = torch.empty_like(wb)
+
+            def ours_dgrad():
+                _lib.check(L.pto_conv3x3_wflip(None, wb.data_ptr(), wf.data_ptr(), C, C,
+                                               torch.cuda.current_stream().cuda_stream), "wflip")
+                return c3._fwd(L, dy, wf, 1)
+
+            def lib_dgrad():
+                return torch.ops.aten.convolution_backward(dy, x, wb, None, [1, 1], [1, 1], [1, 1], False, [0, 0],
+                                                           1, [True, False, False])
+
+            od, ld = timed(ours_dgrad, a.reps), timed(lib_dgrad, a.reps)
+            row.update(dgrad_us=round(od, 1), miopen_dgrad_us=round(ld, 1))
+            tot["ours_dgrad"] += od
+            tot["lib_dgrad"] += ld
+        print(json.dumps(row), flush=True)
+    print(json.dumps({"total_us": {k: round(v, 1) for k, v in tot.items()}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
