@@ -36,6 +36,11 @@ def _worker(rank, world, port, q, comm, steps=STEPS):
     # GPU -- the exchange roles inside the next step's F12 launch
     inline = comm.endswith("-inline")
     comm = comm[:-len("-inline")] if inline else comm
+    if inline and world > 2:
+        # 4+ processes stacked on one GPU: one pooled hardware queue each, or
+        # the scheduler time-slices the oversubscribed queues (set before the
+        # HIP runtime starts in this process; profiles/cu_partition_r6.md)
+        os.environ["GPU_MAX_HW_QUEUES"] = "1"
     if comm == "xgmi-det":  # deterministic backward: per-sample conv1 replicas folded by the all-reduce
         comm = "xgmi"
         os.environ["PTO_DETERMINISTIC"] = "1"
