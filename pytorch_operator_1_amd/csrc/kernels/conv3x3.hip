@@ -267,6 +267,204 @@ __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) vo
   }
 }
 
+// ---------------------------------------------------------------------------
+// The same convolution with LDS-DMA staging (buffer_load ... lds): operand
+// tiles go straight from memory into a 4-stage LDS ring, BK = 32 channels
+// per K step (64-byte rows, 16 KB per stage at 128 x 128), three steps in
+// flight ahead of the one being multiplied, each step retired by a counted
+// vmcnt + a raw barrier (cdna_hip_programming.md §5 "Pipelining across
+// barriers"; every VMEM op in the loop is an LDS-DMA, so the counts are
+// exact).  Register staging (above) keeps one step in flight and paid the
+// load latency on every step.  The DMA writes lane-linear LDS (wave base +
+// 16 * lane), so the XOR swizzle is applied to the SOURCE chunk; padding
+// taps read an out-of-range offset, which the DMA lands as zeros.
+constexpr int C3D_NBUF = 4, C3D_AHEAD = 3;  // stages in the ring, steps in flight beyond the current
+
+typedef __attribute__((address_space(3))) void* c3_lds_ptr;
+
+// One 16-byte-per-lane LDS-DMA (wrapped: the target builtin used directly in
+// the kernel body made host-side compilation drop the kernel's launch stub)
+__device__ __forceinline__ void c3_dma16(__amdgpu_buffer_rsrc_t r, unsigned char* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (c3_lds_ptr)lds, 16, voff, soff, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void c3_wait_vm() {
+  if constexpr (N >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int WM, int WN, int S>
+__global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_conv3x3_fwd_dma(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, float* __restrict__ part,
+    int N, int H, int W, int C, int OH, int OW, int K) {
+  constexpr int BM = 64 * WM, BN = 64 * WN, BK = 32, RB = 64, CPR = 4;
+  constexpr int ROWS_PER_OP = 64 / CPR;              // rows one wave instruction lands (1 KB)
+  constexpr int AOPS = BM / (4 * ROWS_PER_OP);       // DMA instructions per wave for A per step
+  constexpr int BOPS = BN / (4 * ROWS_PER_OP);
+  constexpr int LPS = AOPS + BOPS;                   // VMEM ops per thread per step
+  constexpr int STAGE = (BM + BN) * RB;
+  static_assert(AOPS >= 1 && BOPS >= 1 && C3D_NBUF * STAGE <= 81920, "ring: two blocks per CU");
+  extern __shared__ __attribute__((aligned(16))) unsigned char c3_smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wv / WN, wn = wv % WN;
+  const int M = N * OH * OW;
+  const int ntn = K / BN;
+  const int lb = c3_xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = lb / ntn, nt = lb - mt * ntn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(x), 0, N * H * W * C * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(w), 0, K * 9 * C * 2, 0x00020000);
+  constexpr int C3_OOB = 0x7ffffff0;
+
+  // the lane's row within each of its DMA ops, and the source chunk that
+  // lands at its (linear) LDS slot: slot (lane & 3) of row r holds logical
+  // chunk (lane & 3) ^ key(r)
+  const int lrow = lane / CPR, lslot = lane % CPR;
+  int a_off[AOPS], a_ok[AOPS];
+#pragma unroll
+  for (int i = 0; i < AOPS; ++i) {
+    const int r = (i * 4 + wv) * ROWS_PER_OP + lrow;  // tile row
+    const int ch = lslot ^ ((r >> 2) & 3);
+    const int m = m0 + r;
+    a_off[i] = 0;
+    a_ok[i] = 0;
+    if (m < M) {
+      const int n = m / (OH * OW), rem = m - n * (OH * OW);
+      const int oh = rem / OW, ow = rem - oh * OW;
+      const int ih = oh * S - 1, iw = ow * S - 1;
+      a_off[i] = (((n * H + ih) * W + iw) * C + ch * 8) * 2;
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp)
+        if ((unsigned)(ih + tp / 3) < (unsigned)H && (unsigned)(iw + tp % 3) < (unsigned)W) a_ok[i] |= 1 << tp;
+    }
+  }
+  int b_off[BOPS];
+#pragma unroll
+  for (int i = 0; i < BOPS; ++i) {
+    const int r = (i * 4 + wv) * ROWS_PER_OP + lrow;
+    b_off[i] = ((n0 + r) * 9 * C + (lslot ^ ((r >> 2) & 3)) * 8) * 2;
+  }
+  const int csteps = C / BK, T = 9 * csteps;
+
+  // issue step t's DMA into ring stage t % NBUF (a macro, not a lambda: a
+  // lambda holding these builtins lost the kernel's host-side launch stub)
+#define C3D_ISSUE(t_)                                                                                    \
+  {                                                                                                      \
+    const int st_ = (t_) % C3D_NBUF;                                                                     \
+    const int tap_ = (t_) / csteps, c0_ = ((t_) - tap_ * csteps) * BK;                                  \
+    const int r_ = tap_ / 3, s_ = tap_ - r_ * 3;                                                         \
+    const int toff_ = ((r_ * W + s_) * C + c0_) * 2;                                                     \
+    unsigned char* base_ = c3_smem + st_ * STAGE;                                                        \
+    _Pragma("unroll") for (int i = 0; i < AOPS; ++i)                                                     \
+        c3_dma16(xr, base_ + (i * 4 + wv) * ROWS_PER_OP * RB,                                            \
+                 ((a_ok[i] >> tap_) & 1) ? a_off[i] + toff_ : C3_OOB, 0);                                \
+    _Pragma("unroll") for (int i = 0; i < BOPS; ++i)                                                     \
+        c3_dma16(wr, base_ + BM * RB + (i * 4 + wv) * ROWS_PER_OP * RB, b_off[i], (tap_ * C + c0_) * 2);  \
+  }
+
+  c3_f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = c3_f32x16{};
+  const int fr = lane & 31, fh = lane >> 5;
+
+#pragma unroll
+  for (int t = 0; t < C3D_AHEAD; ++t)
+    if (t < T) C3D_ISSUE(t)
+  for (int t = 0; t < T; ++t) {
+    const int after = T - 1 - t;  // steps issued beyond t (capped at the ring's look-ahead)
+    if (after >= C3D_AHEAD - 1) c3_wait_vm<(C3D_AHEAD - 1) * LPS>();
+    else if (after == 1) c3_wait_vm<LPS>();
+    else c3_wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the stage refilled below are done
+    __builtin_amdgcn_s_barrier();
+    if (t + C3D_AHEAD < T) C3D_ISSUE(t + C3D_AHEAD)  // into the stage step t-1 read, which every wave has left
+    const unsigned char* A = c3_smem + (t % C3D_NBUF) * STAGE;
+    const unsigned char* B = A + BM * RB;
+    c3_bf16x8 af[BK / 16][2], bf[BK / 16][2];
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        af[kk][i] = *reinterpret_cast<const c3_bf16x8*>(A + c3_swz<RB>(wm * 64 + i * 32 + fr, 2 * kk + fh));
+        bf[kk][i] = *reinterpret_cast<const c3_bf16x8*>(B + c3_swz<RB>(wn * 64 + i * 32 + fr, 2 * kk + fh));
+      }
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk][i], bf[kk][j], acc[i][j], 0, 0, 0);
+  }
+#undef C3D_ISSUE
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // every wave is done with the ring: the epilogue reuses it
+
+  constexpr int OLD = BN * 2 + 16;
+  unsigned char* O = c3_smem;
+  float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh;
+        const int col = wn * 64 + j * 32 + fr;
+        const bool valid = m0 + row < M;
+        const uint16_t b = c3_f2bf(acc[i][j][e]);
+        *reinterpret_cast<uint16_t*>(O + row * OLD + col * 2) = b;
+        const float v = valid ? c3_bf2f(b) : 0.f;
+        ssum[j] += v;
+        ssq[j] = fmaf(v, v, ssq[j]);
+      }
+  float* red = reinterpret_cast<float*>(c3_smem + BM * OLD);
+  if (part) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      ssum[j] += __shfl_xor(ssum[j], 32);
+      ssq[j] += __shfl_xor(ssq[j], 32);
+    }
+    if (fh == 0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        red[(wm * 2 + 0) * BN + wn * 64 + j * 32 + fr] = ssum[j];
+        red[(wm * 2 + 1) * BN + wn * 64 + j * 32 + fr] = ssq[j];
+      }
+    }
+  }
+  __syncthreads();
+  if (part) {
+    for (int c = tid; c < 2 * BN; c += C3_T) {
+      const int which = c / BN, col = c - which * BN;
+      float v = 0.f;
+#pragma unroll
+      for (int g = 0; g < WM; ++g) v += red[(g * 2 + which) * BN + col];
+      part[(long long)mt * 2 * K + which * K + n0 + col] = v;
+    }
+  }
+  constexpr int RC = BN / 8;
+#pragma unroll
+  for (int i = 0; i < BM * RC / C3_T; ++i) {
+    const int e = tid + i * C3_T, row = e / RC, ch = e - row * RC;
+    if (m0 + row < M)
+      *reinterpret_cast<c3_u32x4*>(y + (long long)(m0 + row) * K + n0 + ch * 8) =
+          *reinterpret_cast<const c3_u32x4*>(O + row * OLD + ch * 16);
+  }
+}
+
 // w'[c][2-r][2-s][k] = w[k][r][s][c] (bf16, channels-last filters): the
 // stride-1 data gradient as a forward convolution of dY.  Also casts the fp32
 // master filter when src32 is given (one launch for cast + flip).
@@ -310,6 +508,21 @@ int launch_fwd(const void* x, const void* w, void* y, float* part, int N, int H,
   return (int)hipGetLastError();
 }
 
+template <int WM, int WN, int S>
+int launch_dma(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int OH, int OW, int K,
+               hipStream_t s) {
+  constexpr int BM = 64 * WM, BN = 64 * WN;
+  const long long M = (long long)N * OH * OW;
+  const long long blocks = ((M + BM - 1) / BM) * (K / BN);
+  if (blocks > 0x7fffffffLL || C % 32) return -1;
+  const size_t stage = C3D_NBUF * (BM + BN) * 64, epi = BM * (BN * 2 + 16) + WM * 2 * BN * 4;
+  const size_t lds = stage > epi ? stage : epi;
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3x3_fwd_dma<WM, WN, S>), dim3((unsigned)blocks), dim3(C3_T), lds, s,
+                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w),
+                     reinterpret_cast<uint16_t*>(y), part, N, H, W, C, OH, OW, K);
+  return (int)hipGetLastError();
+}
+
 // channel depth of a K step: 64 (128-byte rows, 64 KB of staging per
 // 128 x 128 block) or 32 (half the LDS, twice the steps); the default and
 // the per-variant timings: profiles/resnet50_r6.md
@@ -318,6 +531,7 @@ int g_c3_bk = 64, g_c3_pf = 1;
 template <int WM, int WN, int S>
 int launch_bk(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int OH, int OW, int K,
               hipStream_t s) {
+  if (g_c3_pf == 3) return launch_dma<WM, WN, S>(x, w, y, part, N, H, W, C, OH, OW, K, s);
   if (g_c3_pf == 1)
     return g_c3_bk == 32 ? launch_fwd<WM, WN, S, 32, 1>(x, w, y, part, N, H, W, C, OH, OW, K, s)
                          : launch_fwd<WM, WN, S, 64, 1>(x, w, y, part, N, H, W, C, OH, OW, K, s);
@@ -332,9 +546,10 @@ int launch_bk(const void* x, const void* w, void* y, float* part, int N, int H, 
 // Tile shape for K output channels: 256 x 64 at K = 64, 128 x 128 up to
 // K = 256, 64 x 256 above (fewer, wider column tiles where M is small).
 // Variant knobs for the timing tool (tools/conv3x3_bench.py): K-step depth
-// (32 / 64 channels) and register prefetch depth (1 / 2 steps).
+// (32 / 64 channels) and register prefetch depth (1 / 2 steps); pf = 3: the
+// LDS-DMA ring (k_conv3x3_fwd_dma, BK 32 whatever bk says).
 PTO_API int pto_conv3x3_set_variant(int bk, int pf) {
-  if ((bk != 32 && bk != 64) || (pf != 1 && pf != 2)) return -1;
+  if ((bk != 32 && bk != 64) || pf < 1 || pf > 3) return -1;
   g_c3_bk = bk;
   g_c3_pf = pf;
   return 0;

@@ -71,8 +71,11 @@ def main():
                "miopen_tflops": round(flops / lib / 1e6, 1)}
         best = None
         variants = [tuple(int(u) for u in v.split(":")) for v in a.variants.split(",")]
+        ref = F.conv2d(x.float(), wb.float(), stride=s, padding=1)
         for bk, pf in variants:
             _lib.check(L.pto_conv3x3_set_variant(bk, pf), "set_variant")
+            yv = c3._fwd(L, x, wb, s, part)
+            row[f"relerr_{bk}_{pf}"] = float((yv.float() - ref).abs().max() / ref.abs().max())
             t = timed(lambda: c3._fwd(L, x, wb, s, part), a.reps)
             row[f"fwd_us_{bk}_{pf}"] = round(t, 1)
             row[f"fwd_tflops_{bk}_{pf}"] = round(flops / t / 1e6, 1)
