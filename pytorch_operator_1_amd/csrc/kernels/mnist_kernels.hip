@@ -1743,6 +1743,32 @@ __global__ __launch_bounds__(256) void k_conv1_bwd(const float* __restrict__ g1,
 //   D  dW1 = dh1^T a2p tiles consumed by SGD on fc1.weight.
 //   F  dW2 (fc2) tiles, db1, db2 with SGD epilogues.
 // Block 0 advances the batch cursor and marks conv1's update as owed.
+// dW1 tiles (16 x 16 of fc1.weight's gradient) per wave of a k_bwd_all D
+// block.  A grid of 256-thread blocks starts at ~3.6 ns per block
+// (tools/dispatch_ramp_probe.py: 1422 blocks take 4.6-5.4 us just to all be
+// running, 711 x 512 threads 2.4 us), and k_bwd_all's 1,422 blocks also
+// exceed its 1,280 resident slots, so its D blocks -- last in the grid --
+// both start last and wait for slots; fewer, longer D blocks shrink the grid
+// (profiles/mnist_step_pmc_r6.md).
+#ifndef PTO_BWD_DTPW  // probe builds (tools/bwd_roles_probe.py --dtpw) sweep it
+#define PTO_BWD_DTPW 1  // 2-4 measured slower (profiles/mnist_step_pmc_r6.md)
+#endif
+constexpr int BWD_DTPW = PTO_BWD_DTPW;
+// Role order of k_bwd_all's grid (role ids C 0, F 1, A 2, B 3, D 4).  Order
+// 0: the short independent ranges first, then conv2 wgrad, conv2 dgrad,
+// dW1 (dgrad-first and dW1-before-dgrad measured 0.9 and 1.4 us slower in
+// round 2, profiles/bwd_all_r2.md; re-swept in round 6 with the probe's
+// PTO_BWD_ORDER builds, profiles/mnist_step_pmc_r6.md).
+#ifndef PTO_BWD_ORDER
+#define PTO_BWD_ORDER 0
+#endif
+__host__ __device__ constexpr int bwd_order(int i) {
+  constexpr int o[6][5] = {{0, 1, 2, 3, 4}, {3, 2, 4, 0, 1}, {3, 2, 0, 1, 4}, {2, 3, 0, 1, 4},
+                           {3, 4, 2, 0, 1}, {0, 1, 3, 2, 4}};
+  return o[PTO_BWD_ORDER][i];
+}
+constexpr int bwd_n_dw1_blocks() { return ((((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4 + BWD_DTPW - 1) / BWD_DTPW; }
+
 struct BwdAllArgs {
   const float* g2;         // d(a2p) [B][800]
   const uint8_t* code2;
@@ -1808,11 +1834,23 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
     if (A.bidx) *A.bidx = (*A.bidx + 1) % A.nbatches;
     if (A.pending) *A.pending = 1;
   }
-  // block order: the short independent ranges first (they must not queue
-  // behind the LDS-heavy conv2 blocks for a CU slot), then conv2 wgrad,
-  // conv2 dgrad, dW1 (dgrad-first and dW1-before-dgrad measured 0.9 and
-  // 1.4 us slower, profiles/bwd_all_r2.md)
-  if (bid < A.nC) {
+  // block order (role ranges of the grid): bwd_order(); a grid of
+  // 1,422 blocks takes ~5 us just to start (tools/dispatch_ramp_probe.py),
+  // so the order decides which roles start late
+  int role = 4;
+  {
+    const int cnt[5] = {A.nC, A.nF, A.nA, A.nB, A.nD};  // role ids: C F A B D
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int r = bwd_order(i);
+      if (bid < cnt[r]) {
+        role = r;
+        break;
+      }
+      bid -= cnt[r];
+    }
+  }
+  if (role == 0) {  // C
     const int oc = bid * 4 + wv;
     if (oc >= C2) return;
     const float g = c2_bias_sum(oc, A.g2, A.code2, A.B);
@@ -1825,8 +1863,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
     }
     return;
   }
-  bid -= A.nC;
-  if (bid < A.nF) {
+  if (role == 1) {  // F
     const float lr = *A.a.lr;
     constexpr int NWF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4;
     if (A.grads_only) {
@@ -1849,8 +1886,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
     else block_colsum64_epi(A.dl, NCLS, A.B, NCLS, 0, smem, EpiSgd{A.pfb, A.mfb, 0, lr, &A.a});
     return;
   }
-  bid -= A.nF;
-  if (bid < A.nA) {
+  if (role == 2) {  // A
     const bool det = A.wpart != nullptr;
     c2_wgrad_block<CH, NTW>(bid, smem, A.g2, A.code2, A.a1p, A.g2w, A.B, A.wpart);
     if (A.grads_only && !det) return;
@@ -1913,8 +1949,7 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
       }
     return;
   }
-  bid -= A.nA;
-  if (bid < A.nB) {
+  if (role == 3) {  // B
     const int r = (bid / B2_ICG) % A.nrep;
     float* gw1 = r == 0 ? A.gw1 : A.c1rep + (r - 1) * A.rep_stride;
     float* gb1 = r == 0 ? A.gb1 : A.c1rep + (r - 1) * A.rep_stride + A.bias_off;
@@ -1922,13 +1957,17 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
                    A.wpart != nullptr);
     return;
   }
-  bid -= A.nB;
-  if (bid < A.nD) {
-    if (A.grads_only)
-      block_gemm_4tiles<LAY_KROW, LAY_KROW, EpiStore, 4>(A.dh1, F1OUT, A.a2p, F1IN, F1OUT, F1IN, A.B, bid,
-                                                        EpiStore{A.g1w, F1IN});
-    else
-      dw1_sgd_tile(bid * 4 + wv, A.dh1, A.a2p, A.p1w, A.m1w, A.B, A.a);
+  if (role == 4) {  // D
+    // BWD_DTPW dW1 tiles per wave, one after the other (no barriers in this role)
+#pragma unroll
+    for (int j = 0; j < BWD_DTPW; ++j) {
+      const int vb = bid * BWD_DTPW + j;
+      if (A.grads_only)
+        block_gemm_4tiles<LAY_KROW, LAY_KROW, EpiStore, 4>(A.dh1, F1OUT, A.a2p, F1IN, F1OUT, F1IN, A.B, vb,
+                                                          EpiStore{A.g1w, F1IN});
+      else
+        dw1_sgd_tile(vb * 4 + wv, A.dh1, A.a2p, A.p1w, A.m1w, A.B, A.a);
+    }
     return;
   }
 }
@@ -2309,7 +2348,7 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   A.nA = ((B + BWD_WCHUNK - 1) / BWD_WCHUNK) * (32 / BWD_WNTW);
   A.nB = B * B2_ICG;
   A.nC = (C2 + 3) / 4;
-  A.nD = (((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4;
+  A.nD = bwd_n_dw1_blocks();
   A.nF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9;
   A.wpart = wpart;
   const size_t ldsA = wgrad_lds_floats<BWD_WCHUNK, BWD_WNTW>() * sizeof(float);

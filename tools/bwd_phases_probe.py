@@ -27,7 +27,9 @@ MARKS = {"A": [0, 1, 2, 3, 4, 7], "B": [0, 1, 3, 4, 5, 7]}
 
 def build():
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                           "-I", os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "kernels"), "-I", os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "comm"), "-o", SO, SRC])
+                           "-I", os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "kernels"), "-I", os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "comm"), "-o", SO, SRC,
+                           # mnist_kernels.hip calls pto_ar_timeout_ticks (the exchange roles)
+                           os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "comm", "xgmi_allreduce.hip")])
     print("built", SO)
 
 

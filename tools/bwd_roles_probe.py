@@ -20,17 +20,25 @@ SO = os.path.join(ROOT, "tools", "probes", "libbwd_roles.so")
 ROLES = {1: "C conv2-bias", 2: "F fc2/bias", 4: "A conv2-wgrad", 8: "B dgrad+conv1-wgrad", 16: "D dW1", 32: "-c1 (B without its conv1 wgrad)"}
 
 
-def so_path(chunk):
-    return SO if chunk is None else SO.replace(".so", f"_c{chunk}.so")
+def so_path(chunk, dtpw=None, order=None):
+    p = SO if chunk is None else SO.replace(".so", f"_c{chunk}.so")
+    p = p if dtpw is None else p.replace(".so", f"_d{dtpw}.so")
+    return p if order is None else p.replace(".so", f"_o{order}.so")
 
 
-def build(chunk=None):
+def build(chunk=None, dtpw=None, order=None):
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "kernels"), "-I", os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "comm"), "-o", so_path(chunk), SRC]
+           "-I", os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "kernels"), "-I", os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "comm"), "-o", so_path(chunk, dtpw, order), SRC,
+           # mnist_kernels.hip calls pto_ar_timeout_ticks (the exchange roles)
+           os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "comm", "xgmi_allreduce.hip")]
     if chunk is not None:
         cmd.insert(1, f"-DPTO_BWD_WCHUNK={chunk}")
+    if dtpw is not None:
+        cmd.insert(1, f"-DPTO_BWD_DTPW={dtpw}")
+    if order is not None:
+        cmd.insert(1, f"-DPTO_BWD_ORDER={order}")
     subprocess.check_call(cmd)
-    print("built", so_path(chunk))
+    print("built", so_path(chunk, dtpw, order))
 
 
 def main():
@@ -39,13 +47,29 @@ def main():
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--chunk", type=int, nargs="*", default=None,
                     help="conv2-wgrad samples per block to sweep (each its own probe build)")
+    ap.add_argument("--dtpw", type=int, nargs="*", default=None,
+                    help="dW1 tiles per wave of the D blocks to sweep (each its own probe build)")
+    ap.add_argument("--order", type=int, nargs="*", default=None,
+                    help="k_bwd_all role orders (mnist_kernels.hip bwd_order) to sweep (each its own probe build)")
     ap.add_argument("--pmc-mask", type=int, default=None,
                     help="no timing: 30 eager launches of this role mask, for a rocprofv3 --pmc run "
                          "(pmc_summary.py --skip 3 drops the trainer's own 3 warm-up dispatches)")
     a = ap.parse_args()
     if a.build:
         for c in (a.chunk or [None]):
-            build(c)
+            for d in (a.dtpw or [None]):
+                for o in (a.order or [None]):
+                    build(c, d, o)
+        return
+    if a.order:
+        for o in a.order:
+            print(f"== role order {o}")
+            run_one(so_path(None, None, o), a.reps, masks=[31])
+        return
+    if a.dtpw:
+        for d in a.dtpw:
+            print(f"== dW1 tiles per wave {d}")
+            run_one(so_path(None, d), a.reps, masks=[31, 16, 31 & ~16])
         return
     if a.chunk:
         for c in a.chunk:
