@@ -278,7 +278,6 @@ __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) vo
 // load latency on every step.  The DMA writes lane-linear LDS (wave base +
 // 16 * lane), so the XOR swizzle is applied to the SOURCE chunk; padding
 // taps read an out-of-range offset, which the DMA lands as zeros.
-constexpr int C3D_NBUF = 4, C3D_AHEAD = 3;  // stages in the ring, steps in flight beyond the current
 
 typedef __attribute__((address_space(3))) void* c3_lds_ptr;
 
@@ -290,16 +289,11 @@ __device__ __forceinline__ void c3_dma16(__amdgpu_buffer_rsrc_t r, unsigned char
 
 template <int N>
 __device__ __forceinline__ void c3_wait_vm() {
-  if constexpr (N >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int WM, int WN, int S>
+template <int WM, int WN, int S, int NBUF, int AHEAD>
 __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_conv3x3_fwd_dma(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, float* __restrict__ part,
     int N, int H, int W, int C, int OH, int OW, int K) {
@@ -309,7 +303,7 @@ __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) vo
   constexpr int BOPS = BN / (4 * ROWS_PER_OP);
   constexpr int LPS = AOPS + BOPS;                   // VMEM ops per thread per step
   constexpr int STAGE = (BM + BN) * RB;
-  static_assert(AOPS >= 1 && BOPS >= 1 && C3D_NBUF * STAGE <= 81920, "ring: two blocks per CU");
+  static_assert(AOPS >= 1 && BOPS >= 1 && NBUF * STAGE <= 163840 && AHEAD < NBUF && AHEAD >= 1, "ring");
   extern __shared__ __attribute__((aligned(16))) unsigned char c3_smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -360,7 +354,7 @@ __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) vo
   // lambda holding these builtins lost the kernel's host-side launch stub)
 #define C3D_ISSUE(t_)                                                                                    \
   {                                                                                                      \
-    const int st_ = (t_) % C3D_NBUF;                                                                     \
+    const int st_ = (t_) % NBUF;                                                                     \
     const int tap_ = (t_) / csteps, c0_ = ((t_) - tap_ * csteps) * BK;                                  \
     const int r_ = tap_ / 3, s_ = tap_ - r_ * 3;                                                         \
     const int toff_ = ((r_ * W + s_) * C + c0_) * 2;                                                     \
@@ -380,17 +374,27 @@ __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) vo
   const int fr = lane & 31, fh = lane >> 5;
 
 #pragma unroll
-  for (int t = 0; t < C3D_AHEAD; ++t)
+  for (int t = 0; t < AHEAD; ++t)
     if (t < T) C3D_ISSUE(t)
   for (int t = 0; t < T; ++t) {
-    const int after = T - 1 - t;  // steps issued beyond t (capped at the ring's look-ahead)
-    if (after >= C3D_AHEAD - 1) c3_wait_vm<(C3D_AHEAD - 1) * LPS>();
-    else if (after == 1) c3_wait_vm<LPS>();
-    else c3_wait_vm<0>();
+    // steps issued beyond t: min(AHEAD - 1, T - 1 - t); wait until only theirs are in flight
+    const int after = T - 1 - t;
+    if (after >= AHEAD - 1) c3_wait_vm<(AHEAD - 1) * LPS>();
+    else if constexpr (AHEAD > 2) {
+      if (after == 1) c3_wait_vm<LPS>();
+      else if (after == 2) c3_wait_vm<2 * LPS>();
+      else if (after == 3) c3_wait_vm<(AHEAD > 4 ? 3 : 0) * LPS>();
+      else if (after == 4) c3_wait_vm<(AHEAD > 5 ? 4 : 0) * LPS>();
+      else if (after == 5) c3_wait_vm<(AHEAD > 6 ? 5 : 0) * LPS>();
+      else if (after == 6) c3_wait_vm<(AHEAD > 7 ? 6 : 0) * LPS>();
+      else c3_wait_vm<0>();
+    } else {
+      c3_wait_vm<0>();
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the stage refilled below are done
     __builtin_amdgcn_s_barrier();
-    if (t + C3D_AHEAD < T) C3D_ISSUE(t + C3D_AHEAD)  // into the stage step t-1 read, which every wave has left
-    const unsigned char* A = c3_smem + (t % C3D_NBUF) * STAGE;
+    if (t + AHEAD < T) C3D_ISSUE(t + AHEAD)  // into stage (t + AHEAD) % NBUF, last read at step t + AHEAD - NBUF <= t - 1
+    const unsigned char* A = c3_smem + (t % NBUF) * STAGE;
     const unsigned char* B = A + BM * RB;
     c3_bf16x8 af[BK / 16][2], bf[BK / 16][2];
 #pragma unroll
@@ -508,16 +512,22 @@ int launch_fwd(const void* x, const void* w, void* y, float* part, int N, int H,
   return (int)hipGetLastError();
 }
 
-template <int WM, int WN, int S>
+template <int WM, int WN, int S, int NBUF, int AHEAD>
 int launch_dma(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int OH, int OW, int K,
                hipStream_t s) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
   const long long M = (long long)N * OH * OW;
   const long long blocks = ((M + BM - 1) / BM) * (K / BN);
   if (blocks > 0x7fffffffLL || C % 32) return -1;
-  const size_t stage = C3D_NBUF * (BM + BN) * 64, epi = BM * (BN * 2 + 16) + WM * 2 * BN * 4;
+  const size_t stage = NBUF * (BM + BN) * 64, epi = BM * (BN * 2 + 16) + WM * 2 * BN * 4;
   const size_t lds = stage > epi ? stage : epi;
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3x3_fwd_dma<WM, WN, S>), dim3((unsigned)blocks), dim3(C3_T), lds, s,
+  static bool attr = false;
+  if (!attr) {  // rings above 64 KB
+    (void)hipFuncSetAttribute((const void*)k_conv3x3_fwd_dma<WM, WN, S, NBUF, AHEAD>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    attr = true;
+  }
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3x3_fwd_dma<WM, WN, S, NBUF, AHEAD>), dim3((unsigned)blocks), dim3(C3_T), lds, s,
                      reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w),
                      reinterpret_cast<uint16_t*>(y), part, N, H, W, C, OH, OW, K);
   return (int)hipGetLastError();
@@ -531,7 +541,9 @@ int g_c3_bk = 64, g_c3_pf = 1;
 template <int WM, int WN, int S>
 int launch_bk(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int OH, int OW, int K,
               hipStream_t s) {
-  if (g_c3_pf == 3) return launch_dma<WM, WN, S>(x, w, y, part, N, H, W, C, OH, OW, K, s);
+  if (g_c3_pf == 3) return launch_dma<WM, WN, S, 4, 3>(x, w, y, part, N, H, W, C, OH, OW, K, s);
+  if (g_c3_pf == 4) return launch_dma<WM, WN, S, 6, 5>(x, w, y, part, N, H, W, C, OH, OW, K, s);
+  if (g_c3_pf == 5) return launch_dma<WM, WN, S, 8, 7>(x, w, y, part, N, H, W, C, OH, OW, K, s);
   if (g_c3_pf == 1)
     return g_c3_bk == 32 ? launch_fwd<WM, WN, S, 32, 1>(x, w, y, part, N, H, W, C, OH, OW, K, s)
                          : launch_fwd<WM, WN, S, 64, 1>(x, w, y, part, N, H, W, C, OH, OW, K, s);
@@ -546,10 +558,11 @@ int launch_bk(const void* x, const void* w, void* y, float* part, int N, int H, 
 // Tile shape for K output channels: 256 x 64 at K = 64, 128 x 128 up to
 // K = 256, 64 x 256 above (fewer, wider column tiles where M is small).
 // Variant knobs for the timing tool (tools/conv3x3_bench.py): K-step depth
-// (32 / 64 channels) and register prefetch depth (1 / 2 steps); pf = 3: the
-// LDS-DMA ring (k_conv3x3_fwd_dma, BK 32 whatever bk says).
+// (32 / 64 channels) and register prefetch depth (1 / 2 steps); pf = 3 / 4 / 5:
+// the LDS-DMA ring (k_conv3x3_fwd_dma, BK 32 whatever bk says) with 4 / 6 / 8
+// stages, 3 / 5 / 7 steps in flight.
 PTO_API int pto_conv3x3_set_variant(int bk, int pf) {
-  if ((bk != 32 && bk != 64) || pf < 1 || pf > 3) return -1;
+  if ((bk != 32 && bk != 64) || pf < 1 || pf > 5) return -1;
   g_c3_bk = bk;
   g_c3_pf = pf;
   return 0;

@@ -10,6 +10,6 @@ timeout -k 10 300 python -u -m pytest tests/test_conv3x3_gpu.py -v -x --timeout 
 rc=$?
 grep -E "PASSED|FAILED|passed|failed|Error" $O/pytest.log | tail -16
 case $rc in 0) ;; 1) tail -40 $O/pytest.log;; *) echo "pytest rc=$rc"; exit $rc;; esac
-timeout -k 10 300 python -u tools/conv3x3_bench.py --variants 64:1,32:3 > $O/bench.jsonl 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+timeout -k 10 300 python -u tools/conv3x3_bench.py --variants 64:1,32:3,32:4,32:5 > $O/bench.jsonl 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 cat $O/bench.jsonl
 exit $rc
