@@ -31,6 +31,8 @@
 // kernels that read x / labels take a device pointer to the current batch
 // index (`bidx`, advanced by the SGD launch), so a captured HIP graph walks
 // the dataset without any copy kernels.
+#include <stdlib.h>
+
 #include "mfma_f32.h"
 #include "sgd_f32.h"
 #include "xgmi_ar.h"
@@ -1646,6 +1648,70 @@ PTO_DEV void dw1_sgd_tile(int tile, const float* __restrict__ dh1, const float* 
   }
 }
 
+// One wave: the two dW1 tiles (mt, 2j) and (mt, 2j+1) side by side -- they
+// share the dh1 operand (16 loads per lane instead of 32 for two tiles) and
+// their four MFMA chains interleave, so a wave holds two tiles for about
+// the latency of one (the serial form, PTO_BWD_DTPW 2, measured 2.4 us
+// slower).  Each tile's accumulation order is wave_tile_16x16's (chains
+// acc0/acc1 over k, summed at the end), so the results are bitwise those of
+// dw1_sgd_tile / the grads-only store.  SGD: sgd_elem on fc1.weight;
+// grads-only (gout != nullptr): the gradient is stored instead.
+PTO_DEV void dw1_tile_pair(int pair, const float* __restrict__ dh1, const float* __restrict__ a2p,
+                           float* __restrict__ pw, float* __restrict__ mw, float* __restrict__ gout, int B,
+                           const SgdArgs& a) {
+  constexpr int MT = (F1OUT + 15) / 16, NT = (F1IN + 15) / 16;
+  static_assert(NT % 2 == 0 && F1IN % 16 == 0, "dW1 column tiles pair up with no column tail");
+  if (pair >= MT * NT / 2) return;
+  const int mt = pair % MT, nt0 = 2 * (pair / MT), lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  float pv[2][4], mv[2][4];
+  if (!gout) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = mt * 16 + g * 4 + rr, n = (nt0 + t) * 16 + r;
+        const bool ok = row < F1OUT;
+        pv[t][rr] = ok ? pw[row * F1IN + n] : 0.f;
+        mv[t][rr] = ok ? mw[row * F1IN + n] : 0.f;
+      }
+  }
+  f32x4 acc[2][2] = {{zero4(), zero4()}, {zero4(), zero4()}};
+  constexpr int NG = 4;
+  for (int k = 0; k < B; k += 16 * NG) {
+    float av[NG][4], bv[2][NG][4];
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      load4<LAY_KROW>(dh1, F1OUT, mt * 16 + r, F1OUT, k + 16 * q + 4 * g, B, av[q]);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) load4<LAY_KROW>(a2p, F1IN, (nt0 + t) * 16 + r, F1IN, k + 16 * q + 4 * g, B, bv[t][q]);
+    }
+#pragma unroll
+    for (int q = 0; q < NG; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[t][j & 1] = mfma16x16x4(av[q][j], bv[t][q][j], acc[t][j & 1]);
+  }
+  const float lr = gout ? 0.f : *a.lr;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const f32x4 s = acc[t][0] + acc[t][1];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = mt * 16 + g * 4 + rr, n = (nt0 + t) * 16 + r;
+      if (row >= F1OUT) continue;
+      if (gout) {
+        gout[row * F1IN + n] = s[rr];
+      } else {
+        sgd_elem(pv[t][rr], s[rr], mv[t][rr], lr, a.mom, a.wd, a.gscale, a.nesterov);
+        pw[row * F1IN + n] = pv[t][rr];
+        mw[row * F1IN + n] = mv[t][rr];
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- B1 ----
 // conv1 weight+bias grad.  Block = (out channel, chunk of 4 samples = 576
 // pooled pixels); a thread owns up to 3 pooled pixels: their (grad, code)
@@ -1754,6 +1820,20 @@ __global__ __launch_bounds__(256) void k_conv1_bwd(const float* __restrict__ g1,
 #define PTO_BWD_DTPW 1  // 2-4 measured slower (profiles/mnist_step_pmc_r6.md)
 #endif
 constexpr int BWD_DTPW = PTO_BWD_DTPW;
+// BwdAllArgs::dpair = 1: every D wave holds a PAIR of dW1 tiles side by
+// side (dw1_tile_pair: shared dh1 operand, interleaved chains), 200 D blocks
+// instead of 400, so the whole 1,222-block grid is resident at once (5 x 256
+// slots).  Bitwise equal, but not faster: D alone 5.4 -> 6.7 us, k_bwd_all
+// 13.83-13.93 vs 13.96-13.97 us, step 35.99-36.06 vs 36.19-36.25 us
+// (profiles/mnist_step_pmc_r6.md).  Host switch PTO_BWD_DPAIR (default 0).
+static int bwd_dpair() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PTO_BWD_DPAIR");
+    v = (e && BWD_DTPW == 1) ? (atoi(e) != 0) : 0;
+  }
+  return v;
+}
 // Role order of k_bwd_all's grid (role ids C 0, F 1, A 2, B 3, D 4).  Order
 // 0: the short independent ranges first, then conv2 wgrad, conv2 dgrad,
 // dW1 (dgrad-first and dW1-before-dgrad measured 0.9 and 1.4 us slower in
@@ -1767,7 +1847,10 @@ __host__ __device__ constexpr int bwd_order(int i) {
                            {3, 4, 2, 0, 1}, {0, 1, 3, 2, 4}};
   return o[PTO_BWD_ORDER][i];
 }
-constexpr int bwd_n_dw1_blocks() { return ((((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4 + BWD_DTPW - 1) / BWD_DTPW; }
+constexpr int bwd_n_dw1_blocks(bool pair) {
+  return pair ? ((((F1OUT + 15) / 16) * ((F1IN + 15) / 16) / 2) + 3) / 4
+              : ((((F1OUT + 15) / 16) * ((F1IN + 15) / 16) + 3) / 4 + BWD_DTPW - 1) / BWD_DTPW;
+}
 
 struct BwdAllArgs {
   const float* g2;         // d(a2p) [B][800]
@@ -1791,6 +1874,7 @@ struct BwdAllArgs {
   long long nbatches;
   int* pending;
   int B, nA, nB, nC, nD, nF;
+  int dpair;               // D role: dW1 tile pairs per wave (bwd_dpair())
   // deterministic mode (wpart != nullptr): no floating-point atomics.  The
   // conv2 wgrad chunks store partial tiles into wpart[chunk] and the last
   // arriver per tile sums them in chunk order; conv1 grads go to one
@@ -1958,6 +2042,10 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
     return;
   }
   if (role == 4) {  // D
+    if (A.dpair) {  // two dW1 tiles per wave, side by side
+      dw1_tile_pair(bid * 4 + wv, A.dh1, A.a2p, A.p1w, A.m1w, A.grads_only ? A.g1w : nullptr, A.B, A.a);
+      return;
+    }
     // BWD_DTPW dW1 tiles per wave, one after the other (no barriers in this role)
 #pragma unroll
     for (int j = 0; j < BWD_DTPW; ++j) {
@@ -2348,7 +2436,8 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   A.nA = ((B + BWD_WCHUNK - 1) / BWD_WCHUNK) * (32 / BWD_WNTW);
   A.nB = B * B2_ICG;
   A.nC = (C2 + 3) / 4;
-  A.nD = bwd_n_dw1_blocks();
+  A.dpair = bwd_dpair();
+  A.nD = bwd_n_dw1_blocks(A.dpair);
   A.nF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9;
   A.wpart = wpart;
   const size_t ldsA = wgrad_lds_floats<BWD_WCHUNK, BWD_WNTW>() * sizeof(float);

@@ -33,7 +33,7 @@ def build(chunk=None, dtpw=None, order=None):
            os.path.join(ROOT, "pytorch_operator_1_amd", "csrc", "comm", "xgmi_allreduce.hip")]
     if chunk is not None:
         cmd.insert(1, f"-DPTO_BWD_WCHUNK={chunk}")
-    if dtpw is not None:
+    if dtpw is not None:  # the serial tiles-per-wave form (PTO_BWD_DPAIR is then off)
         cmd.insert(1, f"-DPTO_BWD_DTPW={dtpw}")
     if order is not None:
         cmd.insert(1, f"-DPTO_BWD_ORDER={order}")
@@ -49,6 +49,9 @@ def main():
                     help="conv2-wgrad samples per block to sweep (each its own probe build)")
     ap.add_argument("--dtpw", type=int, nargs="*", default=None,
                     help="dW1 tiles per wave of the D blocks to sweep (each its own probe build)")
+    ap.add_argument("--dpair", type=int, nargs="*", default=None,
+                    help="PTO_BWD_DPAIR values (0: one dW1 tile per wave, 1: a pair side by side) to "
+                         "compare, interleaved (a host switch of the same build)")
     ap.add_argument("--order", type=int, nargs="*", default=None,
                     help="k_bwd_all role orders (mnist_kernels.hip bwd_order) to sweep (each its own probe build)")
     ap.add_argument("--pmc-mask", type=int, default=None,
@@ -60,6 +63,12 @@ def main():
             for d in (a.dtpw or [None]):
                 for o in (a.order or [None]):
                     build(c, d, o)
+        return
+    if a.dpair:
+        for rep in range(2):  # interleaved A/B
+            for pr in a.dpair:
+                print(f"== dW1 tile pairs {pr} (pass {rep})")
+                run_one(SO, a.reps, masks=[31, 16, 31 & ~16], dpair=pr)
         return
     if a.order:
         for o in a.order:
@@ -79,13 +88,20 @@ def main():
     run_one(SO, a.reps, pmc_mask=a.pmc_mask)
 
 
-def run_one(so, reps, masks=None, pmc_mask=None):
+def run_one(so, reps, masks=None, pmc_mask=None, dpair=None):
     import torch
 
     from pytorch_operator_1_amd.ops import _lib
     from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
 
     P_, I_, L_ = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong
+    if dpair is not None:  # read once per process by bwd_dpair(): one CDLL copy per setting
+        os.environ["PTO_BWD_DPAIR"] = str(dpair)
+        so_copy = so.replace(".so", f"_dp{dpair}.so")
+        if not os.path.exists(so_copy):
+            import shutil
+            shutil.copy(so, so_copy)
+        so = so_copy
     lib = ctypes.CDLL(so)
     fn = lib.probe_bwd_all
     fn.argtypes = [P_] * 13 + [L_] * 8 + [P_, P_, L_, P_, I_, P_, P_, I_, I_, I_, P_]

@@ -37,7 +37,8 @@ extern "C" __attribute__((visibility("default"))) int probe_bwd_all(
     A.gw1 = nullptr;
     A.nrep = 1;
   }
-  A.nD = (mask & 16) ? bwd_n_dw1_blocks() : 0;
+  A.dpair = bwd_dpair();
+  A.nD = (mask & 16) ? bwd_n_dw1_blocks(A.dpair) : 0;
   A.wpart = nullptr;
   const size_t ldsA = wgrad_lds_floats<BWD_WCHUNK, BWD_WNTW>() * sizeof(float);
   const size_t ldsB = B2_LDS_FLOATS * sizeof(float);
