@@ -659,6 +659,13 @@ constexpr int PC_TB = QT * 256;  // one 32 x 128 bf16 tile (bytes)
 constexpr int PC_OPB = NW * 4 * 64 * 16;  // operands of one step: 4 waves x 4 frags x 64 lanes x 16 B
 constexpr int PC_LDS = 3 * 2 * PC_TB + 3 * 2 * QT * 4 + 2 * PC_OPB;
 
+// KVW: complete the producers' K/V fragment loads before the loop (an
+// explicit vmcnt(0) the waitcnt pass sees).  Without it hipcc's loop-header
+// merge still counts those 16 loads as pending inside the loop and emits
+// vmcnt(7) .. vmcnt(0) between the S/dP MFMAs -- in steady state that waits
+// for the NEXT slice's Q/dO/row-constant loads issued at the top of the same
+// step, i.e. one global-load latency on the producers' chain every step.
+template <bool KVW>
 __global__ __launch_bounds__(2 * NT) void k_attn_bwd_dkdv_pc(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                              const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                              const float* __restrict__ lse, const float* __restrict__ delta,
@@ -688,8 +695,10 @@ __global__ __launch_bounds__(2 * NT) void k_attn_bwd_dkdv_pc(const __bf16* __res
 
   uint4 rq, rd;
   float rc = 0.f;
-  auto stage = [&](int s) {
-    const int g = s / nqt, qt = s % nqt, h = kvh * G + g;
+  // slices are walked with incremental (head, query tile) counters: no
+  // integer division per step (it was ~20 SALU instructions per use)
+  auto stage = [&](int g, int qt) {
+    const int h = kvh * G + g;
     const long long tok = tok0 + kb0 + (long long)qt * QT;
     rq = tile_piece_load<NTH>(q + tok * sh.q_rs + (long long)h * HD, sh.q_rs, 0);
     rd = tile_piece_load<NTH>(dout + tok * sh.o_rs + (long long)h * HD, sh.o_rs, 0);
@@ -706,8 +715,7 @@ __global__ __launch_bounds__(2 * NT) void k_attn_bwd_dkdv_pc(const __bf16* __res
   auto active = [&](int qt) { return kb0 + qt * QT + QT - 1 >= kb0 + 32 * kw; };
   auto diagonal = [&](int qt) { return kb0 + qt * QT < kb0 + 32 * kw + 31; };
 
-  auto produce = [&](int t, int tslot, int oslot, const bf16x8* kf, const bf16x8* vf) {
-    const int qt = t % nqt;
+  auto produce = [&](int qt, int tslot, int oslot, const bf16x8* kf, const bf16x8* vf) {
     if (!active(qt)) return;
     const char* qtile = smem + tslot * 2 * PC_TB;
     const char* dtile = qtile + PC_TB;
@@ -753,8 +761,7 @@ __global__ __launch_bounds__(2 * NT) void k_attn_bwd_dkdv_pc(const __bf16* __res
       o[64 * (2 + qs)] = acc_to_operand(t1);  // dS fragments 2, 3
     }
   };
-  auto consume = [&](int t, int tslot, int oslot, f32x16* dka, f32x16* dva) {
-    const int qt = t % nqt;
+  auto consume = [&](int qt, int tslot, int oslot, f32x16* dka, f32x16* dva) {
     if (!active(qt)) return;
     const char* qtile = smem + tslot * 2 * PC_TB;
     const char* dtile = qtile + PC_TB;
@@ -774,9 +781,17 @@ __global__ __launch_bounds__(2 * NT) void k_attn_bwd_dkdv_pc(const __bf16* __res
       }
   };
 
-  stage(0);
+  auto next = [&](int& g, int& qt) {
+    if (++qt == nqt) {
+      qt = 0;
+      ++g;
+    }
+  };
+  stage(0, 0);
   commit(0);
   __syncthreads();
+  int ng = 0, nq = 0;  // (head, query tile) of slice t + 1
+  next(ng, nq);
   // iteration t: stage step t+1, producers step t, consumers step t-1.  The
   // two roles run separate loops with the same barrier count (nsteps + 1),
   // so the K/V fragments (producers) and the dK/dV accumulators (consumers)
@@ -792,14 +807,21 @@ __global__ __launch_bounds__(2 * NT) void k_attn_bwd_dkdv_pc(const __bf16* __res
         vf[ks] = *reinterpret_cast<const bf16x8*>(vr + 16 * ks);
       }
     }
+    if constexpr (KVW) {  // a use of every fragment register: hipcc waits for the loads here
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) asm volatile("" ::"v"(kf[ks]), "v"(vf[ks]));
+    }
     int ts = 0;  // tile slot of step t (t mod 3)
+    int tq = 0;  // query tile of step t (t mod nqt)
     for (int t = 0; t <= nsteps; ++t) {
       const int tn = ts == 2 ? 0 : ts + 1;
-      if (t + 1 < nsteps) stage(t + 1);
-      if (t < nsteps) produce(t, ts, t & 1, kf, vf);
+      if (t + 1 < nsteps) stage(ng, nq);
+      if (t < nsteps) produce(tq, ts, t & 1, kf, vf);
       if (t + 1 < nsteps) commit(tn);
       __syncthreads();
       ts = tn;
+      tq = tq + 1 == nqt ? 0 : tq + 1;
+      next(ng, nq);
     }
     return;
   }
@@ -810,16 +832,233 @@ __global__ __launch_bounds__(2 * NT) void k_attn_bwd_dkdv_pc(const __bf16* __res
     dva[db] = (f32x16){};
   }
   int ts = 0;
+  int cq = 0;  // query tile of step t - 1
   for (int t = 0; t <= nsteps; ++t) {
     const int tn = ts == 2 ? 0 : ts + 1;
     const int tp = ts == 0 ? 2 : ts - 1;
-    if (t + 1 < nsteps) stage(t + 1);
-    if (t >= 1) consume(t - 1, tp, (t - 1) & 1, dka, dva);
+    if (t + 1 < nsteps) stage(ng, nq);
+    if (t >= 1) {
+      consume(cq, tp, (t - 1) & 1, dka, dva);
+      cq = cq + 1 == nqt ? 0 : cq + 1;
+    }
     if (t + 1 < nsteps) commit(tn);
     __syncthreads();
     ts = tn;
+    next(ng, nq);
   }
   // consumers: dK^T / dV^T, lane = key, registers = d (32db + 8g + 4hi + 0..3)
+  __bf16* dkr = dk + (tok0 + key) * dkv_rs + (long long)kvh * HD + 4 * hi;
+  __bf16* dvr = dv + (tok0 + key) * dkv_rs + (long long)kvh * HD + 4 * hi;
+  const float c = sh.scale;
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      u32x2 pk = {pack2(dka[db][4 * g] * c, dka[db][4 * g + 1] * c), pack2(dka[db][4 * g + 2] * c, dka[db][4 * g + 3] * c)};
+      *reinterpret_cast<u32x2*>(dkr + 32 * db + 8 * g) = pk;
+      u32x2 pv = {pack2(dva[db][4 * g], dva[db][4 * g + 1]), pack2(dva[db][4 * g + 2], dva[db][4 * g + 3])};
+      *reinterpret_cast<u32x2*>(dvr + 32 * db + 8 * g) = pv;
+    }
+}
+
+// ------------------------------- dK/dV kernel, two producers per consumer
+// Same block (batch, kv head, 128 keys), query sweep and products as
+// k_attn_bwd_dkdv_pc, but 12 waves: per SIMD (waves w, w + 4, w + 8 share
+// one, keys kb0 + 32 (w & 3) ..) two producers and one consumer.  A
+// producer's slice is split over two barrier intervals:
+//   interval s     S = Q K^T, dP = dO V^T (16 MFMAs, accumulators kept),
+//   interval s + 1 mask, P = exp2(c S'), dS = P dP', bf16 operands -> LDS,
+// and the two producers are half a slice apart (A takes even slices, B odd),
+// so in every interval one producer's softmax VALU issues beside the other
+// producer's and the consumer's MFMAs (consumer: slice s in interval s + 2).
+// In the one-producer kernel the softmax sat between the S/dP MFMAs and the
+// barrier with only the consumer's MFMAs to cover it.  Producers also stage
+// the Q / dO tiles and row constants two slices ahead (one 16-byte chunk
+// of each tile per producer thread).  LDS: 4 tile slots (slice s mod 4: read
+// by the producer in s, kept for the consumer in s + 2, refilled at the end
+// of s + 3), 2 operand slots, 4 row-constant slots: 97 KB, one block per CU.
+constexpr int P3_NSLOT = 4;
+constexpr int P3_ROWC = 2 * QT;  // floats per slot: -lse / sl (32), -delta (32)
+constexpr int P3_LDS = P3_NSLOT * 2 * PC_TB + P3_NSLOT * P3_ROWC * 4 + 2 * PC_OPB;
+
+__global__ __launch_bounds__(3 * NT) void k_attn_bwd_dkdv_p3(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                             const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
+                                                             const float* __restrict__ lse, const float* __restrict__ delta,
+                                                             __bf16* __restrict__ dk, __bf16* __restrict__ dv,
+                                                             long long dkv_rs, AttnShape sh) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* rowc = reinterpret_cast<float*>(smem + P3_NSLOT * 2 * PC_TB);
+  char* opnd = smem + P3_NSLOT * 2 * PC_TB + P3_NSLOT * P3_ROWC * 4;
+  const int G = sh.H / sh.Hkv;
+  const int nkb = sh.S / KB;
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  int lin = bid;
+  if ((nblk & 7) == 0) lin = (bid & 7) * (nblk >> 3) + (bid >> 3);
+  const int pair = lin / nkb, kbi = lin % nkb;
+  const int b = pair / sh.Hkv, kvh = pair % sh.Hkv;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, hi = lane >> 5, kl = lane & 31;
+  const int role = w >> 2;  // 0 producer A (even slices), 1 producer B (odd slices), 2 consumer
+  const int kw = w & (NW - 1);
+  const int kb0 = kbi * KB, key = kb0 + 32 * kw + kl;
+  const long long tok0 = (long long)b * sh.S;
+  const float sl = sh.scale * LOG2E;
+  const float inv_sl = 1.f / sl;
+  const int nqt = (sh.S - kb0) / QT;
+  const int nsteps = G * nqt;
+  const int tp = threadIdx.x & (2 * NT - 1);  // producer thread 0..511 (staging)
+
+  // staging (producers): slice s -> one Q and one dO chunk per thread, and
+  // the transformed row constant for threads < 64; two register sets
+  uint4 q0r, d0r, q1r, d1r;
+  float c0r = 0.f, c1r = 0.f;
+  auto ld = [&](int s, uint4& qr, uint4& dr, float& cr) {
+    const int g = s / nqt, qt = s - g * nqt, h = kvh * G + g;
+    const long long tok = tok0 + kb0 + (long long)qt * QT;
+    qr = tile_piece_load<2 * NT>(q + tok * sh.q_rs + (long long)h * HD, sh.q_rs, 0);
+    dr = tile_piece_load<2 * NT>(dout + tok * sh.o_rs + (long long)h * HD, sh.o_rs, 0);
+    const long long li = ((long long)b * sh.H + h) * sh.S + kb0 + (long long)qt * QT;
+    // every thread issues exactly three loads (threads >= 64 re-read a delta
+    // entry): no branch around a load, so hipcc's vmcnt before a register
+    // set's LDS write counts only the younger set's three loads
+    const float x = (tp < QT ? lse : delta)[li + (tp & (QT - 1))];
+    cr = tp < QT ? -x * inv_sl : -x;
+  };
+  auto st = [&](int s, const uint4& qr, const uint4& dr, float cr) {
+    const int slot = s & (P3_NSLOT - 1);
+    char* qtile = smem + slot * 2 * PC_TB;
+    tile_piece_store<2 * NT>(qtile, 0, qr);
+    tile_piece_store<2 * NT>(qtile + PC_TB, 0, dr);
+    if (tp < 2 * QT) rowc[slot * P3_ROWC + tp] = cr;
+  };
+  auto active = [&](int s) { return s % nqt >= kw; };    // some query >= some key of this wave
+  auto diagonal = [&](int s) { return s % nqt == kw; };  // causal mask needed
+
+  if (role < 2) {
+    const int p = role;
+    bf16x8 kf[8], vf[8];
+    {
+      const __bf16* kr = k + (tok0 + key) * sh.k_rs + (long long)kvh * HD + 8 * hi;
+      const __bf16* vr = v + (tok0 + key) * sh.v_rs + (long long)kvh * HD + 8 * hi;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        kf[ks] = *reinterpret_cast<const bf16x8*>(kr + 16 * ks);
+        vf[ks] = *reinterpret_cast<const bf16x8*>(vr + 16 * ks);
+      }
+    }
+    ld(0, q0r, d0r, c0r);
+    ld(nsteps > 1 ? 1 : 0, q1r, d1r, c1r);
+    st(0, q0r, d0r, c0r);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) asm volatile("" ::"v"(kf[ks]), "v"(vf[ks]));  // see KVW above
+    __syncthreads();
+    f32x16 sa, pa;  // S' and dP' of this producer's current slice, live across one barrier
+    auto mfma_phase = [&](int s) {
+      if (!active(s)) return;
+      const int slot = s & (P3_NSLOT - 1);
+      const char* qtile = smem + slot * 2 * PC_TB;
+      const char* dtile = qtile + PC_TB;
+      const float* lrow = rowc + slot * P3_ROWC;
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const float4 l4 = *reinterpret_cast<const float4*>(lrow + 8 * gg + 4 * hi);
+        const float4 d4 = *reinterpret_cast<const float4*>(lrow + QT + 8 * gg + 4 * hi);
+        sa[4 * gg] = l4.x; sa[4 * gg + 1] = l4.y; sa[4 * gg + 2] = l4.z; sa[4 * gg + 3] = l4.w;
+        pa[4 * gg] = d4.x; pa[4 * gg + 1] = d4.y; pa[4 * gg + 2] = d4.z; pa[4 * gg + 3] = d4.w;
+      }
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        sa = mfma(row_operand(qtile, 0, ks), kf[ks], sa);
+        pa = mfma(row_operand(dtile, 0, ks), vf[ks], pa);
+      }
+    };
+    auto valu_phase = [&](int s) {
+      if (!active(s)) return;
+      if (diagonal(s)) {
+        const int q0 = kb0 + (s % nqt) * QT;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int qr = q0 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+          if (key > qr) sa[i] = -INFINITY;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float pv = __builtin_amdgcn_exp2f(sa[i] * sl);
+        sa[i] = pv;
+        pa[i] = pv * pa[i];  // dS
+      }
+      bf16x8* o = reinterpret_cast<bf16x8*>(opnd + (s & 1) * PC_OPB + kw * (4 * 64 * 16)) + lane;
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        float t0[8], t1[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          t0[j] = sa[8 * qs + j];
+          t1[j] = pa[8 * qs + j];
+        }
+        o[64 * qs] = acc_to_operand(t0);        // P fragments 0, 1
+        o[64 * (2 + qs)] = acc_to_operand(t1);  // dS fragments 2, 3
+      }
+    };
+    // interval t: stage slice t+2 (register set t&1), S/dP of slice t
+    // (producer t&1) or softmax of slice t-1 (the other producer), write
+    // slice t+1 (set (t+1)&1) into its slot, barrier.  Unrolled x2 so the
+    // register set and this producer's phase are compile-time.
+    auto interval = [&](int t, auto par) {
+      constexpr int PAR = decltype(par)::value;
+      {  // unconditional (past the end: re-read the last slice, never stored)
+        const int sn = t + 2 < nsteps ? t + 2 : nsteps - 1;
+        if constexpr (PAR == 0) ld(sn, q0r, d0r, c0r);
+        else ld(sn, q1r, d1r, c1r);
+      }
+      if (p == PAR) {
+        if (t < nsteps) mfma_phase(t);
+      } else {
+        if (t >= 1 && t - 1 < nsteps) valu_phase(t - 1);
+      }
+      if (t + 1 < nsteps) {
+        if constexpr (PAR == 0) st(t + 1, q1r, d1r, c1r);
+        else st(t + 1, q0r, d0r, c0r);
+      }
+      __syncthreads();
+    };
+    for (int t = 0; t < nsteps + 2; t += 2) {
+      interval(t, std::integral_constant<int, 0>{});
+      if (t + 1 < nsteps + 2) interval(t + 1, std::integral_constant<int, 1>{});
+    }
+    return;
+  }
+  // consumer: slice s in interval s + 2 (same barrier count: prologue + nsteps + 2)
+  __syncthreads();
+  f32x16 dka[4], dva[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    dka[db] = (f32x16){};
+    dva[db] = (f32x16){};
+  }
+  for (int t = 0; t < nsteps + 2; ++t) {
+    const int s = t - 2;
+    if (s >= 0 && active(s)) {
+      const int slot = s & (P3_NSLOT - 1);
+      const char* qtile = smem + slot * 2 * PC_TB;
+      const char* dtile = qtile + PC_TB;
+      const bf16x8* o = reinterpret_cast<const bf16x8*>(opnd + (s & 1) * PC_OPB + kw * (4 * 64 * 16)) + lane;
+      bf16x8 pf[2], sf[2];
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        pf[qs] = o[64 * qs];
+        sf[qs] = o[64 * (2 + qs)];
+      }
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int qs = 0; qs < 2; ++qs) {
+          dva[db] = mfma(tr_operand(dtile, 16 * qs, 32 * db), pf[qs], dva[db]);
+          dka[db] = mfma(tr_operand(qtile, 16 * qs, 32 * db), sf[qs], dka[db]);
+        }
+    }
+    __syncthreads();
+  }
   __bf16* dkr = dk + (tok0 + key) * dkv_rs + (long long)kvh * HD + 4 * hi;
   __bf16* dvr = dv + (tok0 + key) * dkv_rs + (long long)kvh * HD + 4 * hi;
   const float c = sh.scale;
@@ -889,15 +1128,42 @@ static void launch_attn_dq(const void* q, const void* k, const void* v, const vo
                      (__bf16*)dq, dqkv_rs, sh);
 }
 
-// dK/dV kernel: PTO_ATTN_DKDV_PC=1 -> k_attn_bwd_dkdv_pc (8 waves, producer /
-// consumer roles), 0 -> k_attn_bwd_dkdv (4 waves, one wave per SIMD).
-static bool attn_dkdv_pc() {
+// dK/dV kernel: PTO_ATTN_DKDV_PC=2 -> k_attn_bwd_dkdv_p3 (12 waves, two
+// producers + one consumer per SIMD), 1 -> k_attn_bwd_dkdv_pc (8 waves,
+// producer / consumer), 0 -> k_attn_bwd_dkdv (4 waves, one wave per SIMD).
+static int attn_dkdv_pc() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("PTO_ATTN_DKDV_PC");
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+
+// PTO_ATTN_PC_KVWAIT=0 restores the producer loop without the explicit
+// K/V-fragment wait (for A/B runs); default on.
+static bool attn_pc_kvwait() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PTO_ATTN_PC_KVWAIT");
     v = e ? (atoi(e) != 0) : 1;
   }
   return v != 0;
+}
+
+template <bool KVW>
+static void launch_attn_dkdv_pc(const void* q, const void* k, const void* v, const void* dout, const float* lse,
+                                const float* delta, void* dk, void* dv, long long dqkv_rs, const AttnShape& sh,
+                                hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_attn_bwd_dkdv_pc<KVW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              PC_LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_attn_bwd_dkdv_pc<KVW>, dim3(sh.B * sh.Hkv * (sh.S / KB)), dim3(2 * NT), PC_LDS, s,
+                     (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta,
+                     (__bf16*)dk, (__bf16*)dv, dqkv_rs, sh);
 }
 
 PTO_API int pto_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H,
@@ -929,15 +1195,20 @@ PTO_API int pto_attn_bwd(const void* q, const void* k, const void* v, const void
   const long long rows = (long long)B * S * H;
   hipLaunchKernelGGL(k_attn_bwd_delta, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, (const __bf16*)o,
                      (const __bf16*)dout, delta, sh);
-  if (attn_dkdv_pc()) {
-    static bool attr2 = false;
-    if (!attr2) {
-      (void)hipFuncSetAttribute((const void*)k_attn_bwd_dkdv_pc, hipFuncAttributeMaxDynamicSharedMemorySize, PC_LDS);
-      attr2 = true;
+  if (attn_dkdv_pc() == 2) {
+    static bool attr3 = false;
+    if (!attr3) {
+      (void)hipFuncSetAttribute((const void*)k_attn_bwd_dkdv_p3, hipFuncAttributeMaxDynamicSharedMemorySize, P3_LDS);
+      attr3 = true;
     }
-    hipLaunchKernelGGL(k_attn_bwd_dkdv_pc, dim3(B * Hkv * (S / KB)), dim3(2 * NT), PC_LDS, s, (const __bf16*)q,
+    hipLaunchKernelGGL(k_attn_bwd_dkdv_p3, dim3(B * Hkv * (S / KB)), dim3(3 * NT), P3_LDS, s, (const __bf16*)q,
                        (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dk,
                        (__bf16*)dv, dqkv_rs, sh);
+  } else if (attn_dkdv_pc()) {
+    if (attn_pc_kvwait())
+      launch_attn_dkdv_pc<true>(q, k, v, dout, lse, delta, dk, dv, dqkv_rs, sh, s);
+    else
+      launch_attn_dkdv_pc<false>(q, k, v, dout, lse, delta, dk, dv, dqkv_rs, sh, s);
   } else {
     hipLaunchKernelGGL(k_attn_bwd_dkdv, dim3(B * Hkv * (S / KB)), dim3(NT), 4 * QTB + 2 * 128 * 4, s,
                        (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta,

@@ -186,6 +186,20 @@ _SIGS = {
 }
 
 
+def _current_library() -> str:
+    # build() is a no-op when the stamp matches the current sources, and
+    # recompiles a stale library (e.g. sources edited after a build).
+    try:
+        return build(force=os.environ.get("PTO_REBUILD") == "1")
+    except (OSError, subprocess.CalledProcessError):
+        # Only a library built from exactly these sources may stand in
+        # (e.g. hipcc missing on a run host): a stale one has launchers
+        # whose argument lists no longer match _SIGS.
+        if not is_current():
+            raise
+        return LIB_PATH
+
+
 def lib():
     """Return the loaded ctypes library, building it on first use."""
     global _lib
@@ -194,17 +208,10 @@ def lib():
     with _lock:
         if _lib is not None:
             return _lib
-        # build() is a no-op when the stamp matches the current sources, and
-        # recompiles a stale library (e.g. sources edited after a build).
-        try:
-            path = build(force=os.environ.get("PTO_REBUILD") == "1")
-        except (OSError, subprocess.CalledProcessError):
-            # Only a library built from exactly these sources may stand in
-            # (e.g. hipcc missing on a run host): a stale one has launchers
-            # whose argument lists no longer match _SIGS.
-            if not is_current():
-                raise
-            path = LIB_PATH
+        # PTO_HIP_LIB: load a library built from OTHER sources (A/B runs of
+        # a kernel change in one GPU call: the baseline build sits next to
+        # the current one); its launchers must match _SIGS.
+        path = os.environ.get("PTO_HIP_LIB") or _current_library()
         L = ctypes.CDLL(path)
         for name, args in _SIGS.items():
             fn = getattr(L, name, None)
@@ -217,7 +224,7 @@ def lib():
 
 
 def loaded_path() -> str | None:
-    return LIB_PATH if _lib is not None else None
+    return getattr(_lib, "_name", None) if _lib is not None else None
 
 
 def check(rc: int, what: str) -> None:

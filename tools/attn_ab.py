@@ -4,7 +4,7 @@ shape (B x 4096 tokens, 32 query / 8 KV heads, head dim 128) and report
 TF/s (causal FLOPs: 4 B H S^2 D / 2 forward, 2.5x that backward).
 
 Kernel variants are chosen by env vars read once per process
-(PTO_ATTN_DKDV_PC), so A/B runs are separate processes:
+(PTO_ATTN_DKDV_PC, PTO_ATTN_PC_KVWAIT), so A/B runs are separate processes:
     for v in 0 2 4; do PTO_ATTN_DKDV=$v python tools/attn_ab.py; done
 """
 import json
@@ -42,7 +42,8 @@ def main():
     tb = timed(lambda: torch.autograd.grad(o, a, go, retain_graph=True))
     fl = 4.0 * B * H * S * S * 128 / 2
     g = torch.autograd.grad(o, a, go, retain_graph=True)[0]
-    print(json.dumps({"dkdv_pc": os.environ.get("PTO_ATTN_DKDV_PC", "default"), "B": B, "S": S,
+    print(json.dumps({"dkdv_pc": os.environ.get("PTO_ATTN_DKDV_PC", "default"),
+                      "pc_kvwait": os.environ.get("PTO_ATTN_PC_KVWAIT", "default"), "B": B, "S": S,
                       "fwd_ms": round(tf, 4), "bwd_ms": round(tb, 4), "fwd_tflops": round(fl / tf / 1e9, 1),
                       "bwd_tflops": round(2.5 * fl / tb / 1e9, 1),
                       "grad_checksum": float(g.float().abs().sum().item())}), flush=True)
