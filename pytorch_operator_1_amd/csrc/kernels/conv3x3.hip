@@ -70,7 +70,9 @@ __device__ __forceinline__ int c3_xcd_remap(int b, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
 }
 
-template <int WM, int WN, int S, int BK, int PF>
+// R: filter size, 3 (pad 1) or 1 (pad 0: the 1x1 convolutions are the same
+// GEMM with one tap, so they share the kernel and its statistics epilogue).
+template <int WM, int WN, int S, int BK, int PF, int R = 3>
 __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_conv3x3_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                       uint16_t* __restrict__ y, float* __restrict__ part, int N, int H,
                                                       int W, int C, int OH, int OW, int K) {
@@ -99,11 +101,12 @@ __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) vo
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(x), 0, N * H * W * C * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(w), 0, K * 9 * C * 2, 0x00020000);
+      const_cast<uint16_t*>(w), 0, K * R * R * C * 2, 0x00020000);
   constexpr int C3_OOB = 0x7ffffff0;
+  constexpr int P = R / 2;  // padding
   // per staged A chunk: byte offset of its row's window origin (pixel
-  // (oh S - 1, ow S - 1), possibly in the padding) and the 9-bit mask of the
-  // taps that land inside the image
+  // (oh S - P, ow S - P), possibly in the padding) and the R*R-bit mask of
+  // the taps that land inside the image
   const int q = tid % CPR, rsub = tid / CPR;
   int a_off[AQ], a_ok[AQ];
 #pragma unroll
@@ -114,17 +117,17 @@ __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) vo
     if (m < M) {
       const int n = m / (OH * OW), rem = m - n * (OH * OW);
       const int oh = rem / OW, ow = rem - oh * OW;
-      const int ih = oh * S - 1, iw = ow * S - 1;
+      const int ih = oh * S - P, iw = ow * S - P;
       a_off[i] = (((n * H + ih) * W + iw) * C + q * 8) * 2;
 #pragma unroll
-      for (int tp = 0; tp < 9; ++tp)
-        if ((unsigned)(ih + tp / 3) < (unsigned)H && (unsigned)(iw + tp % 3) < (unsigned)W) a_ok[i] |= 1 << tp;
+      for (int tp = 0; tp < R * R; ++tp)
+        if ((unsigned)(ih + tp / R) < (unsigned)H && (unsigned)(iw + tp % R) < (unsigned)W) a_ok[i] |= 1 << tp;
     }
   }
   int b_off[BQ];
 #pragma unroll
-  for (int i = 0; i < BQ; ++i) b_off[i] = ((n0 + rsub + i * RPI) * 9 * C + q * 8) * 2;
-  const int csteps = C / BK, T = 9 * csteps;
+  for (int i = 0; i < BQ; ++i) b_off[i] = ((n0 + rsub + i * RPI) * R * R * C + q * 8) * 2;
+  const int csteps = C / BK, T = R * R * csteps;
 
   // Two register sets (P0, P1): with PF = 2 the loads of step t+2 are
   // issued while step t computes, so each tile has two steps' MFMA time to
@@ -134,7 +137,7 @@ __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) vo
 #define C3_LOAD(t_, RA, RBV)                                                                            \
   {                                                                                                     \
     const int tap_ = (t_) / csteps, c0_ = ((t_) - tap_ * csteps) * BK;                                 \
-    const int r_ = tap_ / 3, s_ = tap_ - r_ * 3;                                                        \
+    const int r_ = tap_ / R, s_ = tap_ - r_ * R;                                                        \
     const int toff_ = ((r_ * W + s_) * C + c0_) * 2;                                                    \
     _Pragma("unroll") for (int i = 0; i < AQ; ++i) RA[i] = __builtin_bit_cast(                          \
         c3_u32x4, __builtin_amdgcn_raw_buffer_load_b128(                                                \
@@ -217,20 +220,32 @@ __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) vo
   constexpr int OLD = BN * 2 + 16;
   unsigned char* O = c3_smem;
   float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};  // per lane's column j (= wn*64 + j*32 + fr)
+  // Tile writes as 4-byte column pairs: registers e, e+1 hold rows r, r+1 of
+  // this lane's column; lane pairs (fr even, fr+1) swap one value (DPP
+  // quad_perm [1,0,3,2]) so the even lane writes row r, columns (c, c+1) and
+  // the odd lane row r+1, columns (c-1, c): 32 ds_write_b32 per lane instead
+  // of 64 ds_write_b16 (the 1x1 convs, one K step, spent most of their time
+  // in this epilogue).
+  const bool odd = fr & 1;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh;
+      for (int e = 0; e < 16; e += 2) {
+        const int row = wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh;  // rows row, row + 1
         const int col = wn * 64 + j * 32 + fr;
-        const bool valid = m0 + row < M;
-        const uint16_t b = c3_f2bf(acc[i][j][e]);
-        *reinterpret_cast<uint16_t*>(O + row * OLD + col * 2) = b;
-        const float v = valid ? c3_bf2f(b) : 0.f;
-        ssum[j] += v;
-        ssq[j] = fmaf(v, v, ssq[j]);
+        const uint16_t b0 = c3_f2bf(acc[i][j][e]), b1 = c3_f2bf(acc[i][j][e + 1]);
+        const uint32_t send = odd ? b0 : b1;
+        const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xF, 0xF, false);
+        const uint32_t pk = odd ? (recv | ((uint32_t)b1 << 16)) : ((uint32_t)b0 | (recv << 16));
+        *reinterpret_cast<uint32_t*>(O + (row + (odd ? 1 : 0)) * OLD + (col - (odd ? 1 : 0)) * 2) = pk;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float v = m0 + row + h < M ? c3_bf2f(h ? b1 : b0) : 0.f;
+          ssum[j] += v;
+          ssq[j] = fmaf(v, v, ssq[j]);
+        }
       }
   float* red = reinterpret_cast<float*>(c3_smem + BM * OLD);  // [WM][2][BN]
   if (part) {
@@ -497,7 +512,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_wcast(const float* __restrict__
   *reinterpret_cast<uint2*>(dst + i) = o;
 }
 
-template <int WM, int WN, int S, int BK, int PF>
+template <int WM, int WN, int S, int BK, int PF, int R = 3>
 int launch_fwd(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int OH, int OW, int K,
                hipStream_t s) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
@@ -506,7 +521,7 @@ int launch_fwd(const void* x, const void* w, void* y, float* part, int N, int H,
   if (blocks > 0x7fffffffLL || C % BK) return -1;
   const size_t stage = 2 * (BM + BN) * (2 * BK), epi = BM * (BN * 2 + 16) + WM * 2 * BN * 4;
   const size_t lds = stage > epi ? stage : epi;
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3x3_fwd<WM, WN, S, BK, PF>), dim3((unsigned)blocks), dim3(C3_T), lds, s,
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3x3_fwd<WM, WN, S, BK, PF, R>), dim3((unsigned)blocks), dim3(C3_T), lds, s,
                      reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w),
                      reinterpret_cast<uint16_t*>(y), part, N, H, W, C, OH, OW, K);
   return (int)hipGetLastError();
@@ -551,6 +566,14 @@ int launch_bk(const void* x, const void* w, void* y, float* part, int N, int H, 
                        : launch_fwd<WM, WN, S, 64, 2>(x, w, y, part, N, H, W, C, OH, OW, K, s);
 }
 
+// 1x1: register staging, BK 64, one step in flight (a 1x1 conv has C / 64
+// K steps -- one to 32 -- so there is little to pipeline)
+template <int WM, int WN, int S>
+int launch_1x1(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int OH, int OW, int K,
+               hipStream_t s) {
+  return launch_fwd<WM, WN, S, 64, 1, 1>(x, w, y, part, N, H, W, C, OH, OW, K, s);
+}
+
 }  // namespace
 
 #define PTO_API extern "C" __attribute__((visibility("default")))
@@ -590,6 +613,28 @@ PTO_API int pto_conv3x3_fwd(const void* x, const void* w, void* y, float* part, 
   if (K % 256) return -1;
   return stride == 1 ? launch_bk<1, 4, 1>(x, w, y, part, N, H, W, C, OH, OW, K, s)
                      : launch_bk<1, 4, 2>(x, w, y, part, N, H, W, C, OH, OW, K, s);
+}
+
+// y[N][OH][OW][K] = conv1x1(x[N][H][W][C], w[K][C]), stride 1 or 2 (pixel
+// (oh S, ow S)), bf16 channels-last; part as for pto_conv3x3_fwd (same tile
+// rows: pto_conv3x3_tile_m(K)).
+PTO_API int pto_conv1x1_fwd(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int K,
+                            int stride, hipStream_t s) {
+  if (N < 1 || H < 1 || W < 1 || C < 64 || C % 64 || K < 64 || K % 64 || (stride != 1 && stride != 2)) return -1;
+  if ((((uintptr_t)x) | ((uintptr_t)w) | ((uintptr_t)y)) & 15) return -1;
+  const int OH = (H - 1) / stride + 1, OW = (W - 1) / stride + 1;
+  if ((long long)N * H * W * C >= (1LL << 31) || (long long)N * OH * OW * K >= (1LL << 31)) return -1;
+  const int tm = pto_conv3x3_tile_m(K);
+  if (tm == 256) return stride == 1 ? launch_1x1<4, 1, 1>(x, w, y, part, N, H, W, C, OH, OW, K, s)
+                                    : launch_1x1<4, 1, 2>(x, w, y, part, N, H, W, C, OH, OW, K, s);
+  if (tm == 128) {
+    if (K % 128) return -1;
+    return stride == 1 ? launch_1x1<2, 2, 1>(x, w, y, part, N, H, W, C, OH, OW, K, s)
+                       : launch_1x1<2, 2, 2>(x, w, y, part, N, H, W, C, OH, OW, K, s);
+  }
+  if (K % 256) return -1;
+  return stride == 1 ? launch_1x1<1, 4, 1>(x, w, y, part, N, H, W, C, OH, OW, K, s)
+                     : launch_1x1<1, 4, 2>(x, w, y, part, N, H, W, C, OH, OW, K, s);
 }
 
 // bf16 copy of an fp32 channels-last filter (n = K * 9 * C, n % 4 == 0).

@@ -43,30 +43,33 @@ class Bottleneck(nn.Module):
         return self.bn2(conv3x3(y, self.conv2, st), relu=True, stats=st)
 
     @staticmethod
-    def _c1(conv, x):
-        """1x1 convs (the downsample ones strided): backward on hipBLASLt
+    def _c1(conv, x, st=None):
+        """1x1 convs (the downsample ones strided): MFMA forward handing the
+        next BN its statistics (``st``), backward on hipBLASLt
         (ops/conv1x1.py)."""
-        return conv1x1(x, conv) if gemm_supported(x, conv) else conv(x)
+        return conv1x1(x, conv, stats=st) if gemm_supported(x, conv) else conv(x)
 
     def forward(self, x):
         # BN + ReLU (+ the residual add) are one fused pass each way on the
-        # GPU (ops/bn.py); in an identity block the residual's gradient is
+        # GPU (ops/bn.py), with the batch statistics from the producing
+        # conv's epilogue; in an identity block the residual's gradient is
         # folded into conv1's input-gradient GEMM instead of an autograd add
         # (ops/conv1x1.py); state-dict keys are the stock ones
+        s1, s3 = ConvStats(), ConvStats()
         if self.downsample is None and gemm_supported(x, self.conv1, stride1=True) and self.bn3.can_fuse(x):
             stash = GradStash()
-            y = self.bn1(conv1x1_res(x, self.conv1, stash), relu=True)
+            y = self.bn1(conv1x1_res(x, self.conv1, stash, stats=s1), relu=True, stats=s1)
             y = self._c2(y)
-            return self.bn3(self._c1(self.conv3, y), residual=x, relu=True, stash=stash)
+            return self.bn3(self._c1(self.conv3, y, s3), residual=x, relu=True, stash=stash, stats=s3)
         if (self.downsample is not None and gemm_supported(x, self.downsample[0])
                 and gemm_supported(x, self.conv1)):
             # both 1x1 convs read x: one input gradient, the second GEMM
             # accumulating onto the first (no autograd add)
-            merge = GradStash()
-            idt = self.downsample[1](conv1x1(x, self.downsample[0], merge))
-            y = self.bn1(conv1x1(x, self.conv1, merge), relu=True)
+            merge, sd = GradStash(), ConvStats()
+            idt = self.downsample[1](conv1x1(x, self.downsample[0], merge, stats=sd), stats=sd)
+            y = self.bn1(conv1x1(x, self.conv1, merge, stats=s1), relu=True, stats=s1)
             y = self._c2(y)
-            return self.bn3(self._c1(self.conv3, y), residual=idt, relu=True)
+            return self.bn3(self._c1(self.conv3, y, s3), residual=idt, relu=True, stats=s3)
         idt = x if self.downsample is None else self.downsample[1](self._c1(self.downsample[0], x))
         y = self.bn1(self._c1(self.conv1, x), relu=True)
         y = self._c2(y)

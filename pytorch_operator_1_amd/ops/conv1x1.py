@@ -30,7 +30,12 @@ that a captured graph does not replay (from the second replay on, the stale
 contents of the graph's pool leaked into the gradients of layer 1 and the
 stem: tools/probes/graph_alias_probe.py).
 
-The forward stays MIOpen's (faster than the GEMM on most shapes).
+Forward: the 3x3 implicit-GEMM kernel of ``csrc/kernels/conv3x3.hip``
+instantiated with one tap (``pto_conv1x1_fwd``; hipBLASLt's ``mm`` was
+slower than MIOpen on most of these shapes, profiles/raw/r5/conv1x1_bench.jsonl),
+so the next BatchNorm's batch statistics come out of its epilogue as for
+the 3x3 convs (``stats``) and the BN skips its full statistics read of the
+output.  Opt-in (``PTO_CONV1X1_FWD=1``); MIOpen's forward is the default.
 """
 from __future__ import annotations
 
@@ -39,6 +44,9 @@ import os
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from . import _lib
+from .conv3x3 import stats_tiles
 
 _CL = torch.channels_last
 
@@ -112,21 +120,54 @@ def weight_grad_1x1(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     return part.sum(0)
 
 
+def owned_fwd_supported(x: torch.Tensor, weight: torch.Tensor, dtype) -> bool:
+    """The package's MFMA kernel (``pto_conv1x1_fwd``: the 3x3 implicit GEMM
+    with one tap) takes the forward: bf16 compute, channel counts on its
+    tiles, an fp32 filter, and ``PTO_CONV1X1_FWD=1`` (default off: measured
+    slower than MIOpen's on the expanding shapes, profiles/resnet50_r6.md)."""
+    C, K = weight.shape[1], weight.shape[0]
+    return (dtype == torch.bfloat16 and weight.dtype == torch.float32 and x.dim() == 4 and C % 64 == 0
+            and K % 64 == 0 and (K <= 64 or K % 128 == 0) and (K <= 256 or K % 256 == 0)
+            and weight.is_contiguous() and os.environ.get("PTO_CONV1X1_FWD", "0") == "1")
+
+
 class _Conv1x1(torch.autograd.Function):
-    """A 1x1 bias-free convolution (stride s): MIOpen forward, GEMM input
-    gradient (accumulating a stashed residual gradient, if any; at s > 1
-    scattered into a zeroed full-size gradient), split-K GEMM weight
+    """A 1x1 bias-free convolution (stride s): forward on the package's MFMA
+    kernel where :func:`owned_fwd_supported` (with the next BatchNorm's
+    statistics from its epilogue when ``stats`` is given) else MIOpen; GEMM
+    input gradient (accumulating a stashed residual gradient, if any; at
+    s > 1 scattered into a zeroed full-size gradient), split-K GEMM weight
     gradient in fp32 (from the strided sub-grid of x at s > 1)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stash, dtype, stride=1, merge=None):
+    def forward(ctx, x, weight, stash, dtype, stride=1, merge=None, stats=None, wbuf=None):
         x = x.to(dtype).contiguous(memory_format=_CL)
+        ctx.stash, ctx.wdtype, ctx.stride, ctx.merge = stash, weight.dtype, stride, merge
+        ctx.wshape, ctx.wstride = weight.shape, weight.stride()
+        if wbuf is not None:
+            # bf16 image of the fp32 master filter in the module's persistent
+            # buffer (one cast launch), then the MFMA kernel
+            L = _lib.lib()
+            dev = _lib.stream_ptr(x.device)
+            _lib.check(L.pto_conv3x3_wcast(weight.data_ptr(), wbuf.data_ptr(), wbuf.numel(), dev), "conv1x1 wcast")
+            N, C, H, W = x.shape
+            K = weight.shape[0]
+            OH, OW = (H - 1) // stride + 1, (W - 1) // stride + 1
+            part = None
+            if stats is not None:
+                nblk = stats_tiles(N, OH, OW, K)
+                part = torch.empty(nblk * 2 * K, device=x.device, dtype=torch.float32)
+                stats.part, stats.nblk = part, nblk
+            y = torch.empty(N, K, OH, OW, device=x.device, dtype=torch.bfloat16, memory_format=_CL)
+            _lib.check(L.pto_conv1x1_fwd(x.data_ptr(), wbuf.data_ptr(), y.data_ptr(),
+                                         None if part is None else part.data_ptr(), N, H, W, C, K, stride, dev),
+                       "conv1x1_fwd")
+            ctx.save_for_backward(x, wbuf)
+            return y
         wb = weight.to(dtype)
         if wb.dim() == 4 and not wb.is_contiguous(memory_format=_CL):
             wb = wb.contiguous(memory_format=_CL)
         ctx.save_for_backward(x, wb)
-        ctx.stash, ctx.wdtype, ctx.stride, ctx.merge = stash, weight.dtype, stride, merge
-        ctx.wshape, ctx.wstride = weight.shape, weight.stride()
         return F.conv2d(x, wb, stride=stride)
 
     @staticmethod
@@ -175,33 +216,50 @@ class _Conv1x1(torch.autograd.Function):
                 dx = None
         elif ctx.stash is not None:
             ctx.stash.take()
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None, None
 
 
 def _dtype(x):
     return torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
 
 
-def conv1x1(x: torch.Tensor, conv: nn.Conv2d, merge: GradStash | None = None) -> torch.Tensor:
+def _wbuf(conv: nn.Conv2d, x: torch.Tensor, dtype):
+    """The module's persistent bf16 filter image for the owned forward, or
+    None when that forward does not apply."""
+    if not owned_fwd_supported(x, conv.weight, dtype):
+        return None
+    wb = getattr(conv, "_pto_c1_wb", None)
+    if wb is None or wb.device != x.device or wb.shape != conv.weight.shape:
+        wb = torch.empty(conv.weight.shape, device=x.device, dtype=torch.bfloat16, memory_format=_CL)
+        conv._pto_c1_wb = wb
+    return wb
+
+
+def conv1x1(x: torch.Tensor, conv: nn.Conv2d, merge: GradStash | None = None, stats=None) -> torch.Tensor:
     """``conv(x)`` for a 1x1 bias-free conv, any equal stride (see
     :class:`_Conv1x1`).  ``merge``: shared with the one other conv1x1 that
     reads the same ``x`` (a downsample block's conv1 and downsample conv):
     whichever backward runs second accumulates its input gradient onto the
     first one's (GEMM beta = 1, or a strided in-place add) instead of
-    autograd adding the two.  Dtype: the autocast dtype when autocast is on,
-    else x's."""
+    autograd adding the two.  ``stats``: an ``ops.conv3x3.ConvStats`` the
+    owned forward fills with the next BatchNorm's statistics partials (left
+    empty on the MIOpen path).  Dtype: the autocast dtype when autocast is
+    on, else x's."""
     if not gemm_supported(x, conv):
         raise ValueError("conv1x1: needs a 1x1 bias-free conv on a HIP tensor")
     dtype = _dtype(x)
+    wb = _wbuf(conv, x, dtype)
     with torch.autocast("cuda", enabled=False):
-        return _Conv1x1.apply(x, conv.weight, None, dtype, conv.stride[0], merge)
+        return _Conv1x1.apply(x, conv.weight, None, dtype, conv.stride[0], merge, stats if wb is not None else None,
+                              wb)
 
 
-def conv1x1_res(x: torch.Tensor, conv: nn.Conv2d, stash: GradStash) -> torch.Tensor:
+def conv1x1_res(x: torch.Tensor, conv: nn.Conv2d, stash: GradStash, stats=None) -> torch.Tensor:
     """:func:`conv1x1` whose input gradient also receives ``stash``'s
     residual gradient."""
     if not gemm_supported(x, conv, stride1=True):
         raise ValueError("conv1x1_res: needs a 1x1 stride-1 bias-free conv on a HIP tensor")
     dtype = _dtype(x)
+    wb = _wbuf(conv, x, dtype)
     with torch.autocast("cuda", enabled=False):
-        return _Conv1x1.apply(x, conv.weight, stash, dtype, 1, None)
+        return _Conv1x1.apply(x, conv.weight, stash, dtype, 1, None, stats if wb is not None else None, wb)

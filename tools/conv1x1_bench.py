@@ -10,6 +10,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
+from pytorch_operator_1_amd.ops import _lib  # noqa: E402
+
 SHAPES = [  # (N, H, Ci, Co)
     (256, 56, 64, 64), (256, 56, 256, 64), (256, 56, 64, 256),
     (256, 28, 512, 128), (256, 28, 128, 512),
@@ -50,6 +52,16 @@ def main():
         r = {"shape": [N, H, ci, co]}
         r["miopen_fwd"] = timeit(lambda: F.conv2d(x, w))
         r["gemm_fwd"] = timeit(lambda: torch.mm(x2, w2.t()))
+        # the owned MFMA forward (pto_conv1x1_fwd), without / with the BN
+        # statistics partials
+        L, st = _lib.lib(), _lib.stream_ptr(dev)
+        yo = torch.empty(N, co, H, H, device=dev, dtype=bf, memory_format=torch.channels_last)
+        part = torch.empty(((N * H * H + 255) // 64) * 2 * co, device=dev, dtype=torch.float32)
+        r["owned_fwd"] = timeit(lambda: L.pto_conv1x1_fwd(x.data_ptr(), w.data_ptr(), yo.data_ptr(), None,
+                                                          N, H, H, ci, co, 1, st))
+        r["owned_fwd_stats"] = timeit(lambda: L.pto_conv1x1_fwd(x.data_ptr(), w.data_ptr(), yo.data_ptr(),
+                                                                part.data_ptr(), N, H, H, ci, co, 1, st))
+        r["owned_err"] = float((yo.float() - F.conv2d(x, w).float()).abs().max() / F.conv2d(x, w).float().abs().max())
         r["miopen_dgrad"] = timeit(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False]))
         r["gemm_dgrad"] = timeit(lambda: torch.mm(dy2, w2))
