@@ -220,32 +220,20 @@ __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) vo
   constexpr int OLD = BN * 2 + 16;
   unsigned char* O = c3_smem;
   float ssum[2] = {0.f, 0.f}, ssq[2] = {0.f, 0.f};  // per lane's column j (= wn*64 + j*32 + fr)
-  // Tile writes as 4-byte column pairs: registers e, e+1 hold rows r, r+1 of
-  // this lane's column; lane pairs (fr even, fr+1) swap one value (DPP
-  // quad_perm [1,0,3,2]) so the even lane writes row r, columns (c, c+1) and
-  // the odd lane row r+1, columns (c-1, c): 32 ds_write_b32 per lane instead
-  // of 64 ds_write_b16 (the 1x1 convs, one K step, spent most of their time
-  // in this epilogue).
-  const bool odd = fr & 1;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int e = 0; e < 16; e += 2) {
-        const int row = wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh;  // rows row, row + 1
+      for (int e = 0; e < 16; ++e) {
+        const int row = wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh;
         const int col = wn * 64 + j * 32 + fr;
-        const uint16_t b0 = c3_f2bf(acc[i][j][e]), b1 = c3_f2bf(acc[i][j][e + 1]);
-        const uint32_t send = odd ? b0 : b1;
-        const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xF, 0xF, false);
-        const uint32_t pk = odd ? (recv | ((uint32_t)b1 << 16)) : ((uint32_t)b0 | (recv << 16));
-        *reinterpret_cast<uint32_t*>(O + (row + (odd ? 1 : 0)) * OLD + (col - (odd ? 1 : 0)) * 2) = pk;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const float v = m0 + row + h < M ? c3_bf2f(h ? b1 : b0) : 0.f;
-          ssum[j] += v;
-          ssq[j] = fmaf(v, v, ssq[j]);
-        }
+        const bool valid = m0 + row < M;
+        const uint16_t b = c3_f2bf(acc[i][j][e]);
+        *reinterpret_cast<uint16_t*>(O + row * OLD + col * 2) = b;
+        const float v = valid ? c3_bf2f(b) : 0.f;
+        ssum[j] += v;
+        ssq[j] = fmaf(v, v, ssq[j]);
       }
   float* red = reinterpret_cast<float*>(c3_smem + BM * OLD);  // [WM][2][BN]
   if (part) {
