@@ -298,10 +298,15 @@ def test_xgmi_timeout_fails_fast_without_updates():
     assert res[0][1] < 1.2, res[0]
 
 
-def test_trainer_exits_retryable_when_xgmi_peer_killed(tmp_path):
+@pytest.mark.parametrize("partitioned", [False, True])
+def test_trainer_exits_retryable_when_xgmi_peer_killed(tmp_path, partitioned):
     """Two fused-trainer ranks on the one GPU (gloo for rendezvous, xGMI
     kernel for the gradients); rank 1 SIGKILLs itself at step 100.  Rank 0
-    must exit 138 (retryable) within 5 s of the kill."""
+    must exit 138 (retryable) within 5 s of the kill.  ``partitioned``: each
+    rank on its own CU partition (utils/cu_partition.py), so the ranks run
+    the schedule of one rank per GPU -- the exchange as roles INSIDE the next
+    step's F12 launch, whose conv workgroups wait on those roles -- and the
+    dead peer must surface through that in-launch wait's bounded spin."""
     import subprocess
     import sys
     import time
@@ -312,6 +317,8 @@ def test_trainer_exits_retryable_when_xgmi_peer_killed(tmp_path):
     for r in range(2):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), PTO_XGMI_TIMEOUT_MS="500", PYTHONPATH=root)
+        if partitioned:
+            env.update(PTO_CU_PARTITION="1", LOCAL_RANK=str(r), LOCAL_WORLD_SIZE="2")
         cmd = [sys.executable, "-m", "pytorch_operator_1_amd.train.mnist", "--backend", "gloo", "--impl", "fused",
                "--comm", "xgmi", "--max-steps", "2000", "--log-interval", "50", "--no-test", "--train-size", "8192",
                "--fail-at-step", "100", "--fail-rank", "1", "--dir", ""]
@@ -336,6 +343,8 @@ def test_trainer_exits_retryable_when_xgmi_peer_killed(tmp_path):
     assert procs[0].returncode == 138, log0[-3000:]
     assert "timed out" in log0
     assert t_kill is not None and t_exit - t_kill < 5.0, (t_exit - t_kill, log0[-2000:])
+    if partitioned:  # the run took the one-rank-per-GPU (inline) schedule
+        assert "next step's F12 launch" in log0 and "'partitioned': True" in log0, log0[-3000:]
 
 
 def _bucket_worker(rank, world, port, q, dtype_name):
