@@ -72,8 +72,12 @@ __device__ __forceinline__ int c3_xcd_remap(int b, int nwg) {
 
 // R: filter size, 3 (pad 1) or 1 (pad 0: the 1x1 convolutions are the same
 // GEMM with one tap, so they share the kernel and its statistics epilogue).
-template <int WM, int WN, int S, int BK, int PF, int R = 3>
-__global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_conv3x3_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+// NB: LDS staging buffers.  2 (the 3x3 convs: 9 C / 64 K steps, the next
+// step's tile staged while this one multiplies); 1 for the 1x1 convs (1-8
+// K steps: half the LDS, so twice the workgroups per CU keep loads in
+// flight, at the price of a second barrier per step).
+template <int WM, int WN, int S, int BK, int PF, int R = 3, int NB = 2>
+__global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, NB == 1 ? 4 : 2))) void k_conv3x3_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                       uint16_t* __restrict__ y, float* __restrict__ part, int N, int H,
                                                       int W, int C, int OH, int OW, int K) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
@@ -83,7 +87,7 @@ __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) vo
   static_assert(AQ >= 1 && BQ >= 1 && BM % RPI == 0 && BN % RPI == 0, "tile / thread mismatch");
   extern __shared__ __attribute__((aligned(16))) unsigned char c3_smem[];
   // buffer b: A rows at c3_smem + b * BM * RB, B rows at Bs0 + b * BN * RB
-  unsigned char* const Bs0 = c3_smem + 2 * BM * RB;
+  unsigned char* const Bs0 = c3_smem + NB * BM * RB;
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = wv / WN, wn = wv % WN;
@@ -179,7 +183,20 @@ __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, 2))) vo
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk][i], bf[kk][j], acc[i][j], 0, 0, 0); \
   }
 
-  if (PF == 1) {
+  if (NB == 1) {
+    C3_LOAD(0, ra0, rb0)
+    C3_STAGE(0, ra0, rb0)
+    __syncthreads();
+    for (int t = 0; t < T; ++t) {
+      if (t + 1 < T) C3_LOAD(t + 1, ra0, rb0)  // in flight under this step's MFMAs
+      C3_MATH(0)
+      if (t + 1 < T) {
+        __syncthreads();  // every wave's fragment reads of the one buffer are done
+        C3_STAGE(0, ra0, rb0)
+      }
+      __syncthreads();
+    }
+  } else if (PF == 1) {
     C3_LOAD(0, ra0, rb0)
     C3_STAGE(0, ra0, rb0)
     __syncthreads();
@@ -500,16 +517,16 @@ __global__ __launch_bounds__(256) void k_conv3x3_wcast(const float* __restrict__
   *reinterpret_cast<uint2*>(dst + i) = o;
 }
 
-template <int WM, int WN, int S, int BK, int PF, int R = 3>
+template <int WM, int WN, int S, int BK, int PF, int R = 3, int NB = 2>
 int launch_fwd(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int OH, int OW, int K,
                hipStream_t s) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
   const long long M = (long long)N * OH * OW;
   const long long blocks = ((M + BM - 1) / BM) * (K / BN);
   if (blocks > 0x7fffffffLL || C % BK) return -1;
-  const size_t stage = 2 * (BM + BN) * (2 * BK), epi = BM * (BN * 2 + 16) + WM * 2 * BN * 4;
+  const size_t stage = NB * (BM + BN) * (2 * BK), epi = BM * (BN * 2 + 16) + WM * 2 * BN * 4;
   const size_t lds = stage > epi ? stage : epi;
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3x3_fwd<WM, WN, S, BK, PF, R>), dim3((unsigned)blocks), dim3(C3_T), lds, s,
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3x3_fwd<WM, WN, S, BK, PF, R, NB>), dim3((unsigned)blocks), dim3(C3_T), lds, s,
                      reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w),
                      reinterpret_cast<uint16_t*>(y), part, N, H, W, C, OH, OW, K);
   return (int)hipGetLastError();
@@ -555,11 +572,14 @@ int launch_bk(const void* x, const void* w, void* y, float* part, int N, int H, 
 }
 
 // 1x1: register staging, BK 64, one step in flight (a 1x1 conv has C / 64
-// K steps -- one to 32 -- so there is little to pipeline)
+// K steps -- one to 32 -- so there is little to pipeline); g_c1_nb LDS
+// buffers (pto_conv1x1_set_variant, the timing tool's knob)
+int g_c1_nb = 1;
 template <int WM, int WN, int S>
 int launch_1x1(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int OH, int OW, int K,
                hipStream_t s) {
-  return launch_fwd<WM, WN, S, 64, 1, 1>(x, w, y, part, N, H, W, C, OH, OW, K, s);
+  return g_c1_nb == 1 ? launch_fwd<WM, WN, S, 64, 1, 1, 1>(x, w, y, part, N, H, W, C, OH, OW, K, s)
+                      : launch_fwd<WM, WN, S, 64, 1, 1, 2>(x, w, y, part, N, H, W, C, OH, OW, K, s);
 }
 
 }  // namespace
@@ -601,6 +621,12 @@ PTO_API int pto_conv3x3_fwd(const void* x, const void* w, void* y, float* part, 
   if (K % 256) return -1;
   return stride == 1 ? launch_bk<1, 4, 1>(x, w, y, part, N, H, W, C, OH, OW, K, s)
                      : launch_bk<1, 4, 2>(x, w, y, part, N, H, W, C, OH, OW, K, s);
+}
+
+PTO_API int pto_conv1x1_set_variant(int nb) {
+  if (nb != 1 && nb != 2) return -1;
+  g_c1_nb = nb;
+  return 0;
 }
 
 // y[N][OH][OW][K] = conv1x1(x[N][H][W][C], w[K][C]), stride 1 or 2 (pixel

@@ -147,6 +147,7 @@ _SIGS = {
     "pto_conv3x3_set_variant": [_I, _I],
     "pto_conv3x3_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "pto_conv1x1_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "pto_conv1x1_set_variant": [_I],
     "pto_conv3x3_wcast": [_P, _P, _L, _P],
     "pto_conv3x3_wflip": [_P, _P, _P, _I, _I, _P],
     "pto_maxpool_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
