@@ -76,7 +76,11 @@ __device__ __forceinline__ int c3_xcd_remap(int b, int nwg) {
 // step's tile staged while this one multiplies); 1 for the 1x1 convs (1-8
 // K steps: half the LDS, so twice the workgroups per CU keep loads in
 // flight, at the price of a second barrier per step).
-template <int WM, int WN, int S, int BK, int PF, int R = 3, int NB = 2>
+// PERSIST: a grid of resident workgroups walks the tiles (tile = block +
+// i * grid); otherwise one tile per workgroup (XCD-remapped).  A 1x1 conv's
+// grid is 3k-12k short workgroups, whose dispatch alone (~3.5 ns each,
+// profiles/mnist_step_pmc_r6.md) is a large share of its time.
+template <int WM, int WN, int S, int BK, int PF, int R = 3, int NB = 2, bool PERSIST = false>
 __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, NB == 1 ? 4 : 2))) void k_conv3x3_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                       uint16_t* __restrict__ y, float* __restrict__ part, int N, int H,
                                                       int W, int C, int OH, int OW, int K) {
@@ -95,7 +99,10 @@ __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, NB == 1
   // logical block -> (m tile, n tile), n fastest: the channel tiles of one
   // pixel tile are adjacent logical ids, i.e. on one XCD (c3_xcd_remap)
   const int ntn = K / BN;
-  const int lb = c3_xcd_remap(blockIdx.x, gridDim.x);
+  const int ntiles = ((M + BM - 1) / BM) * ntn;
+  for (int lb = PERSIST ? (int)blockIdx.x : c3_xcd_remap(blockIdx.x, gridDim.x); lb < ntiles;
+       lb = PERSIST ? lb + (int)gridDim.x : ntiles) {
+  if (PERSIST) __syncthreads();  // the previous tile's epilogue reads of the LDS image are done
   const int mt = lb / ntn, nt = lb - mt * ntn;
   const int m0 = mt * BM, n0 = nt * BN;
 
@@ -285,6 +292,7 @@ __global__ __launch_bounds__(C3_T) __attribute__((amdgpu_waves_per_eu(1, NB == 1
       *reinterpret_cast<c3_u32x4*>(y + (long long)(m0 + row) * K + n0 + ch * 8) =
           *reinterpret_cast<const c3_u32x4*>(O + row * OLD + ch * 16);
   }
+  }  // tile loop
 }
 
 // ---------------------------------------------------------------------------
@@ -517,16 +525,28 @@ __global__ __launch_bounds__(256) void k_conv3x3_wcast(const float* __restrict__
   *reinterpret_cast<uint2*>(dst + i) = o;
 }
 
-template <int WM, int WN, int S, int BK, int PF, int R = 3, int NB = 2>
+template <int WM, int WN, int S, int BK, int PF, int R = 3, int NB = 2, bool PERSIST = false>
 int launch_fwd(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int OH, int OW, int K,
                hipStream_t s) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
   const long long M = (long long)N * OH * OW;
-  const long long blocks = ((M + BM - 1) / BM) * (K / BN);
+  long long blocks = ((M + BM - 1) / BM) * (K / BN);
   if (blocks > 0x7fffffffLL || C % BK) return -1;
   const size_t stage = NB * (BM + BN) * (2 * BK), epi = BM * (BN * 2 + 16) + WM * 2 * BN * 4;
   const size_t lds = stage > epi ? stage : epi;
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3x3_fwd<WM, WN, S, BK, PF, R, NB>), dim3((unsigned)blocks), dim3(C3_T), lds, s,
+  if (PERSIST) {  // resident grid: CUs x workgroups per CU
+    static int resident = 0;
+    if (!resident) {
+      int per_cu = 0, dev = 0, cus = 0;
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per_cu, (const void*)k_conv3x3_fwd<WM, WN, S, BK, PF, R, NB, PERSIST>, C3_T, lds);
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      resident = (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 256);
+    }
+    if (blocks > resident) blocks = resident;
+  }
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_conv3x3_fwd<WM, WN, S, BK, PF, R, NB, PERSIST>), dim3((unsigned)blocks), dim3(C3_T), lds, s,
                      reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w),
                      reinterpret_cast<uint16_t*>(y), part, N, H, W, C, OH, OW, K);
   return (int)hipGetLastError();
@@ -578,6 +598,7 @@ int g_c1_nb = 1;
 template <int WM, int WN, int S>
 int launch_1x1(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int OH, int OW, int K,
                hipStream_t s) {
+  if (g_c1_nb == 3) return launch_fwd<WM, WN, S, 64, 1, 1, 1, true>(x, w, y, part, N, H, W, C, OH, OW, K, s);
   return g_c1_nb == 1 ? launch_fwd<WM, WN, S, 64, 1, 1, 1>(x, w, y, part, N, H, W, C, OH, OW, K, s)
                       : launch_fwd<WM, WN, S, 64, 1, 1, 2>(x, w, y, part, N, H, W, C, OH, OW, K, s);
 }
@@ -623,8 +644,10 @@ PTO_API int pto_conv3x3_fwd(const void* x, const void* w, void* y, float* part, 
                      : launch_bk<1, 4, 2>(x, w, y, part, N, H, W, C, OH, OW, K, s);
 }
 
+// 1 / 2: LDS staging buffers, one tile per workgroup; 3: one buffer and a
+// resident grid walking the tiles
 PTO_API int pto_conv1x1_set_variant(int nb) {
-  if (nb != 1 && nb != 2) return -1;
+  if (nb < 1 || nb > 3) return -1;
   g_c1_nb = nb;
   return 0;
 }

@@ -13,7 +13,7 @@ timeout -k 10 300 python tools/conv1x1_bench.py > $O/bench.jsonl 2> $O/bench.err
 python -c "
 import json
 for l in open('$O/bench.jsonl'):
-    d=json.loads(l); print(d['shape'], 'miopen', d['miopen_fwd'], 'nb2+stats', d['owned_fwd_stats_nb2'], 'nb1', d['owned_fwd'], 'nb1+stats', d['owned_fwd_stats'])
+    d=json.loads(l); print(d['shape'], 'miopen', d['miopen_fwd'], 'nb2+stats', d['owned_fwd_stats_nb2'], 'persist+stats', d['owned_fwd_stats_nb3'], 'nb1', d['owned_fwd'], 'nb1+stats', d['owned_fwd_stats'], 'err nb2/3/1', round(d['owned_err_nb2'],4), round(d['owned_err_nb3'],4), round(d['owned_err'],4))
 "
 for v in 1 0; do
   PTO_CONV1X1_FWD=$v timeout -k 10 300 python bench.py --model resnet50 --steps 20 --warmup 5 --no-latency > $O/resnet_$v.json 2> $O/resnet_err || { tail -20 $O/resnet_err; exit 1; }

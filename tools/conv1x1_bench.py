@@ -57,13 +57,17 @@ def main():
         L, st = _lib.lib(), _lib.stream_ptr(dev)
         yo = torch.empty(N, co, H, H, device=dev, dtype=bf, memory_format=torch.channels_last)
         part = torch.empty(((N * H * H + 255) // 64) * 2 * co, device=dev, dtype=torch.float32)
-        for nb in (2, 1):  # LDS staging buffers (pto_conv1x1_set_variant); 1 = the default
+        for nb in (2, 3, 1):  # pto_conv1x1_set_variant: LDS buffers (1 = the default), 3 = resident grid
             _lib.check(L.pto_conv1x1_set_variant(nb), "set_variant")
             sfx = "" if nb == 1 else f"_nb{nb}"
             r["owned_fwd" + sfx] = timeit(lambda: L.pto_conv1x1_fwd(x.data_ptr(), w.data_ptr(), yo.data_ptr(), None,
                                                                     N, H, H, ci, co, 1, st))
             r["owned_fwd_stats" + sfx] = timeit(lambda: L.pto_conv1x1_fwd(x.data_ptr(), w.data_ptr(), yo.data_ptr(),
                                                                           part.data_ptr(), N, H, H, ci, co, 1, st))
+            yo.zero_()
+            L.pto_conv1x1_fwd(x.data_ptr(), w.data_ptr(), yo.data_ptr(), None, N, H, H, ci, co, 1, st)
+            ref = F.conv2d(x, w).float()
+            r["owned_err" + sfx] = float((yo.float() - ref).abs().max() / ref.abs().max())
         r["owned_err"] = float((yo.float() - F.conv2d(x, w).float()).abs().max() / F.conv2d(x, w).float().abs().max())
         r["miopen_dgrad"] = timeit(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False]))
