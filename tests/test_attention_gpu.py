@@ -74,24 +74,27 @@ torch.save(qkv.grad.cpu(), sys.argv[1])
 
 
 def test_dkdv_producer_consumer_matches_single_wave_kernel(tmp_path):
-    """The producer/consumer dK/dV kernel (default) and the one-wave-per-SIMD
-    kernel (PTO_ATTN_DKDV_PC=0) accumulate in the same MFMA order: the QKV
-    gradients must be bitwise equal.  The switch is read once per process,
-    hence one child process per kernel."""
+    """Every dK/dV kernel accumulates in the same MFMA order, so the QKV
+    gradients must be bitwise equal: the producer/consumer kernel (default,
+    with and without the K/V-fragment wait, PTO_ATTN_PC_KVWAIT), the 12-wave
+    two-producer kernel (PTO_ATTN_DKDV_PC=2) and the one-wave-per-SIMD kernel
+    (PTO_ATTN_DKDV_PC=0).  The switches are read once per process, hence one
+    child process per kernel."""
     import os
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     grads = []
-    for pc in ("1", "0"):
-        out = str(tmp_path / f"g{pc}.pt")
-        env = dict(os.environ, PTO_ATTN_DKDV_PC=pc)
+    for pc, kvw in (("1", "1"), ("0", "1"), ("2", "1"), ("1", "0")):
+        out = str(tmp_path / f"g{pc}{kvw}.pt")
+        env = dict(os.environ, PTO_ATTN_DKDV_PC=pc, PTO_ATTN_PC_KVWAIT=kvw)
         r = subprocess.run([sys.executable, "-c", _DKDV_CHILD, out, root], capture_output=True, text=True,
                            timeout=300, env=env)
         assert r.returncode == 0, r.stderr[-2000:]
         grads.append(torch.load(out, weights_only=True))
-    assert torch.equal(grads[0], grads[1])
+    for g in grads[1:]:
+        assert torch.equal(grads[0], g)
 
 
 def test_flash_attention_deferred_max_rescales():

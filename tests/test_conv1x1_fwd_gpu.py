@@ -118,3 +118,29 @@ def test_bottleneck_owned_1x1_matches_miopen_forward(monkeypatch, cin, width, st
     assert hasattr(blocks[0].conv1, "_pto_c1_wb") and not hasattr(blocks[1].conv1, "_pto_c1_wb")
     for a, b in zip(*outs):
         assert relerr(a, b) < 2e-2, relerr(a, b)
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("ci,co,H,stride", [(64, 256, 56, 1), (1024, 2048, 14, 2), (2048, 512, 7, 1)])
+def test_conv1x1_kernel_variants_agree(variant, ci, co, H, stride):
+    """Every launch variant of pto_conv1x1_fwd (one / two LDS buffers, the
+    resident grid walking the tiles) computes the same output and the same
+    statistics partials (same MFMA order per tile)."""
+    from pytorch_operator_1_amd.ops import _lib
+    from pytorch_operator_1_amd.ops import conv1x1 as c1
+    from pytorch_operator_1_amd.ops.conv3x3 import ConvStats
+
+    torch.manual_seed(ci + co)
+    conv = _conv(ci, co, stride)
+    x = _x(4 if H >= 28 else 8, ci, H)
+    L = _lib.lib()
+    outs = []
+    for v in (1, variant):
+        _lib.check(L.pto_conv1x1_set_variant(v), "set_variant")
+        st = ConvStats()
+        with torch.no_grad():
+            y = c1.conv1x1(x, conv, stats=st)
+        part, _ = st.take()
+        outs.append((y.clone(), part.clone()))
+    _lib.check(L.pto_conv1x1_set_variant(1), "set_variant")
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
