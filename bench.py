@@ -99,12 +99,14 @@ def _launch_ranks(args, argv) -> int | None:
     s.close()
     argv = list(sys.argv[1:] if argv is None else argv)
     env = None
-    if host_ranks and os.environ.get("PTO_CU_PARTITION") == "1" and "GPU_MAX_HW_QUEUES" not in os.environ:
+    if host_ranks and os.environ.get("PTO_CU_PARTITION") == "1":
         # several ranks stacked on one GPU, each on its own CU partition: one
         # pooled hardware queue per rank, or with 4+ ranks the queues outnumber
         # what the scheduler maps at once and it time-slices them (~22 ms/step
-        # at 4 ranks vs 0.10 ms, profiles/cu_partition_r6.md)
-        env = dict(os.environ, GPU_MAX_HW_QUEUES="1")
+        # at 4 ranks vs 0.10 ms, profiles/cu_partition_r6.md).  Overrides an
+        # inherited GPU_MAX_HW_QUEUES (GPU boxes export HIP's default, 4);
+        # PTO_CU_HW_QUEUES picks another count
+        env = dict(os.environ, GPU_MAX_HW_QUEUES=os.environ.get("PTO_CU_HW_QUEUES", "1"))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + argv
     print(f"[bench] starting {args.gpus} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)

@@ -150,3 +150,30 @@ def test_bench_fallback_only_on_timeouts():
     assert bench._xgmi_failure(XgmiTimeout("barrier timed out"))
     assert not bench._xgmi_failure(XgmiDivergence("ranks diverged"))
     assert not bench._xgmi_failure(RuntimeError("xgmi_allreduce failed with hipError 1"))
+
+
+def test_partitioned_rehearsal_overrides_inherited_hw_queues(monkeypatch):
+    """Stacked CU-partitioned ranks (PTO_CU_PARTITION=1, host backend) get one
+    pooled hardware queue each even when the environment already exports
+    GPU_MAX_HW_QUEUES (GPU boxes export HIP's default, 4: the world-4
+    rehearsal then ran ~200x slower); PTO_CU_HW_QUEUES picks another count.
+    One-rank-per-GPU launches leave the environment alone."""
+    import importlib.util
+    import subprocess as sp
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    seen = []
+    monkeypatch.setattr(sp, "call", lambda cmd, env=None: seen.append(env) or 0)
+    for k in ("WORLD_SIZE", "RANK", "PTO_CU_HW_QUEUES"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    monkeypatch.setenv("PTO_BACKEND", "gloo")
+    args = bench.parse_args(["--gpus", "4"])
+    monkeypatch.setenv("PTO_CU_PARTITION", "1")
+    assert bench._launch_ranks(args, []) == 0 and seen[-1]["GPU_MAX_HW_QUEUES"] == "1"
+    monkeypatch.setenv("PTO_CU_HW_QUEUES", "2")
+    assert bench._launch_ranks(args, []) == 0 and seen[-1]["GPU_MAX_HW_QUEUES"] == "2"
+    monkeypatch.setenv("PTO_CU_PARTITION", "0")
+    assert bench._launch_ranks(args, []) == 0 and seen[-1] is None
