@@ -857,11 +857,29 @@ constexpr int DLS_LD = 20;
 // dh1 overwrites the h1 tile in place (each element is read for its ReLU
 // mask and written by the same lane), then the d(a2p) tile is as before.
 // Requires 16-byte aligned h1 and W2 (checked by the launcher).
+// The NEXT step's images, staged by F4dx's last STAGE_BLOCKS workgroups
+// into a buffer at a fixed address (xnext), which the next F12 reads with no
+// batch cursor: F12 had to load the cursor (written by the previous
+// backward) before it could even address its images -- two dependent
+// memory round trips at the head of the step.  With F12 reading a fixed
+// address the step measured 34.91-34.98 vs 35.96-36.00 us
+// (profiles/mnist_step_pmc_r6.md); a plain prefetch of the next batch into
+// the caches did not help, the dependent cursor load was the cost.  The
+// copy takes batch (cursor + 1) % nb: every schedule advances the cursor
+// after F4dx (k_bwd_all, k_ddp_sgd or the exchange epilogue).
+struct BatchStage {
+  const float* x;  // [nb][n4 * 4] images (nullptr: no staging)
+  float* xnext;    // [n4 * 4]
+  long long nb;
+  int n4;
+};
+constexpr int STAGE_BLOCKS = 4;
+
 __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     const float* __restrict__ h1, const float* __restrict__ w2, const float* __restrict__ b2,
     const int64_t* __restrict__ labels, const float* __restrict__ w1, float* __restrict__ loss_rows,
     float* __restrict__ dlogits, float* __restrict__ dh1, float* __restrict__ da2p, int B, float inv_b,
-    const long long* __restrict__ bidx, Conv1Commit cm) {
+    const long long* __restrict__ bidx, Conv1Commit cm, BatchStage st) {
   // LDS row stride.  500 keeps the dh1 phase's scalar accesses (rows r and
   // r + 4 in one 32-lane group, 4*500 = 16 mod 32 banks apart) conflict-free;
   // 504 would make the float4 operand reads conflict-free instead but the
@@ -874,6 +892,27 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
   const int mtiles = (B + 15) >> 4, ntiles = (F1IN + 15) >> 4;
   const int t = threadIdx.x;
   PTO_STAMP_SCOPE();
+  if (blockIdx.x > (unsigned)(mtiles * ntiles)) {  // next-batch staging (launcher: st.xnext && bidx)
+    const long long nb = (*bidx + 1) % st.nb;
+    const float4* src = reinterpret_cast<const float4*>(st.x) + nb * st.n4;
+    float4* dst = reinterpret_cast<float4*>(st.xnext);
+    const int j0 = (blockIdx.x - mtiles * ntiles - 1) * (FDX_WAVES * 64) + t;
+    constexpr int NQ = 4, STRIDE = STAGE_BLOCKS * FDX_WAVES * 64;  // 4 x 4096 float4 >= B = 64's 12,544
+    for (int i0 = j0; i0 < st.n4; i0 += NQ * STRIDE) {
+      float4 v[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int i = i0 + q * STRIDE;
+        v[q] = src[i < st.n4 ? i : 0];
+      }
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int i = i0 + q * STRIDE;
+        if (i < st.n4) dst[i] = v[q];
+      }
+    }
+    return;
+  }
   if (blockIdx.x == (unsigned)(mtiles * ntiles)) {
     if (cm.zero_word && t == 0) *cm.zero_word = 0;  // every waiter of the previous launch has finished
     if (cm.pending) {
@@ -2349,20 +2388,25 @@ PTO_API int pto_conv2_bwd(const float* g2, const uint8_t* code2, const float* a1
 // F4dx (k_fc2_ce_dx_mf) + one extra block committing conv1's owed update
 // (pending != nullptr; flat range p1/g1/m1 of n1 floats + replicas) and
 // resetting *zero_word (non-null: the overlapped step's conv-role counter,
-// which the previous F12 launch's conv blocks waited on).
+// which the previous F12 launch's conv blocks waited on) + STAGE_BLOCKS
+// blocks copying the next batch's images (st_x [st_nb][B * 784], batch
+// (*bidx + 1) % st_nb) into st_xnext, the next F12's input (optional).
 PTO_API int pto_fc2_ce_dx(const float* h1, const float* w2, const float* b2, const int64_t* labels, const float* w1,
                           float* loss_rows, float* dlogits, float* dh1, float* da2p, int B, float inv_b,
                           const long long* bidx, float* p1, float* g1, float* m1, int n1, const int* pending,
                           const float* lr, float mom, float wd, float gscale, int nesterov, float* rep, int nrep,
-                          int rep_stride, int* zero_word, hipStream_t s) {
+                          int rep_stride, int* zero_word, const float* st_x, float* st_xnext, long long st_nb,
+                          hipStream_t s) {
   if (n1 % 4 || rep_stride % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1) | ((uintptr_t)rep)) & 15))
     return -1;
   if ((((uintptr_t)h1) | ((uintptr_t)w2)) & 15) return -1;  // float4 staging of the h1 tile and W2
   if (nrep < 1 || nrep > C1_MAXREP || (nrep > 1 && !rep)) return -1;
+  if (st_xnext && (!st_x || !bidx || st_nb < 1 || ((((uintptr_t)st_x) | ((uintptr_t)st_xnext)) & 15))) return -1;
   Conv1Commit cm{p1, g1, m1, n1, pending, sgd_args(lr, mom, wd, gscale, nesterov), rep, nrep, rep_stride, zero_word};
+  const BatchStage st{st_x, st_xnext, st_nb, B * 784 / 4};
   const int nblk = ((B + 15) / 16) * ((F1IN + 15) / 16);
-  hipLaunchKernelGGL(k_fc2_ce_dx_mf, dim3(nblk + 1), dim3(FDX_WAVES * 64), 0, s, h1, w2, b2, labels, w1, loss_rows,
-                     dlogits, dh1, da2p, B, inv_b, bidx, cm);
+  hipLaunchKernelGGL(k_fc2_ce_dx_mf, dim3(nblk + 1 + (st_xnext ? STAGE_BLOCKS : 0)), dim3(FDX_WAVES * 64), 0, s, h1,
+                     w2, b2, labels, w1, loss_rows, dlogits, dh1, da2p, B, inv_b, bidx, cm, st);
   LAUNCH_CHECK();
 }
 

@@ -174,6 +174,12 @@ class FusedMnistTrainer:
         self.data = data[: self.n_batches * B].reshape(self.n_batches, B * 784).contiguous()
         self.target = target[: self.n_batches * B].reshape(self.n_batches, B).contiguous()
         self.batch_idx = torch.zeros(1, device=device, dtype=torch.int64)
+        # F12's input at a fixed address: F4dx's extra workgroups copy the
+        # next step's batch here, so F12 loads its images without first
+        # loading the cursor (~1 us/step, profiles/mnist_step_pmc_r6.md);
+        # PTO_XSTAGE=0 reads dataset[cursor] in F12 as before
+        self.xnext = (torch.empty(B * 784, **f32) if os.environ.get("PTO_XSTAGE", "1") == "1" else None)
+        self._stage_batch()
 
         self.lr_dev = torch.tensor([self.lr], **f32)
         self.steps_done = 0
@@ -312,18 +318,36 @@ class FusedMnistTrainer:
         if only in (None, 0) and owed:
             self._exchange_launch(B)
         elif only in (None, 0):
-            self._call("conv12_fwd_lazy_x", self.data.data_ptr(), P["conv1.weight"].data_ptr(),
+            fx, fb = self._f12_input()
+            self._call("conv12_fwd_lazy_x", fx, P["conv1.weight"].data_ptr(),
                        P["conv1.bias"].data_ptr(), P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(),
-                       self.a1p.data_ptr(), self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B, bi,
-                       *lazy, self.xcur.data_ptr(), w2out, *rep)
+                       self.a1p.data_ptr(), self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B,
+                       fb, *lazy, self.xcur.data_ptr(), w2out, *rep)
         if only in (None, 1):
             self._call("linear_fwd", self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
                        self.h1.data_ptr(), B, 500, 800, 1)
         if only in (None, 2):
+            stage = ((self.data.data_ptr(), self.xnext.data_ptr(), self.n_batches) if self.xnext is not None
+                     else (None, None, 0))
             self._call("fc2_ce_dx", self.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
                        self.target.data_ptr(), P["fc1.weight"].data_ptr(), self.loss_rows.data_ptr(),
                        self.dlogits.data_ptr(), self.dh1.data_ptr(), self.da2p.data_ptr(), B, 1.0 / B, bi, *conv1,
-                       pending, *o, *rep, self._ready.data_ptr() if self.overlap else None)
+                       pending, *o, *rep, self._ready.data_ptr() if self.overlap else None, *stage)
+
+    def _f12_input(self):
+        """(images, cursor) arguments of F12: the staged batch and no cursor,
+        or the dataset indexed by the device cursor."""
+        if self.xnext is not None:
+            return self.xnext.data_ptr(), None
+        return self.data.data_ptr(), self.batch_idx.data_ptr()
+
+    def _stage_batch(self):
+        """Copy the cursor's batch into the staging buffer (stream-ordered, no
+        host sync): needed whenever the host sets the cursor; F4dx keeps it
+        current from then on."""
+        if self.xnext is not None:
+            with torch.no_grad():
+                self.xnext.copy_(self.data.index_select(0, self.batch_idx).view(-1))
 
     def _backward(self):
         """``k_bwd_all``: the whole backward in one launch.  Fused-opt: every
@@ -351,10 +375,11 @@ class FusedMnistTrainer:
         L, P = self.L, self._p
         lr, mom, wd, gs, nes = self._opt_args()
         x = self._xgmi
+        fx, fb = self._f12_input()
         _lib.check(L.pto_conv12_fwd_ar(
-            self.data.data_ptr(), P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
+            fx, P["conv1.weight"].data_ptr(), P["conv1.bias"].data_ptr(),
             P["conv2.weight"].data_ptr(), P["conv2.bias"].data_ptr(), self.a1p.data_ptr(), self.code1.data_ptr(),
-            self.a2p.data_ptr(), self.code2.data_ptr(), B, self.batch_idx.data_ptr(), self.xcur.data_ptr(),
+            self.a2p.data_ptr(), self.code2.data_ptr(), B, fb, self.xcur.data_ptr(),
             *x.exchange_args(), *x.update_args(self._params, self.mom, self.lr_dev, mom, wd, gs, bool(nes),
                                                cover=self.numel),
             0, self._split, FC_CHAN, self.numel,
@@ -454,7 +479,9 @@ class FusedMnistTrainer:
             pdist.host_barrier(tag=f"xgmi-{tag}")
 
     def _state(self):
-        return (self._params, self.mom, self.grads, self.batch_idx, self.pending, self.c1rep, self._ready)
+        # the staged batch goes with the cursor it belongs to
+        st = (self._params, self.mom, self.grads, self.batch_idx, self.pending, self.c1rep, self._ready)
+        return st + ((self.xnext,) if self.xnext is not None else ())
 
     def _graph_sizes(self) -> list[int]:
         if self.fused_opt:
@@ -703,6 +730,7 @@ class FusedMnistTrainer:
             self._params.copy_(other._params)
             self.mom.copy_(other.mom)
             self.batch_idx.copy_(other.batch_idx)
+        self._stage_batch()
         self.steps_done = other.steps_done
         self._eager_first = other._eager_first
         self.set_lr(other.lr)
@@ -732,6 +760,7 @@ class FusedMnistTrainer:
                 off, shape = offs[name]
                 self.mom[off:off + math.prod(shape)].copy_(t.reshape(-1).to(self.device))
         self.batch_idx.fill_(int(sd.get("batch_idx", 0)) % self.n_batches)
+        self._stage_batch()
         self.steps_done = int(sd.get("steps_done", 0))
         self.set_lr(float(sd.get("lr", self.lr)))
 
