@@ -61,6 +61,25 @@ def main():
         seq.append(ts)
         del tr
     out["bench_like_run20_us"] = seq
+    # an idle GPU before the region: run(20) after the host sleeps (warm-up
+    # steps then region, as bench.py does), per idle time
+    tr = make()
+    tr.run(a.warmup)
+    tr.prepare() if hasattr(tr, "prepare") else None
+    idle = {}
+    for rep in range(3):
+        for ms in (0, 2, 20, 200, 1000):
+            sync()
+            time.sleep(ms / 1e3)
+            tr.run(a.warmup)
+            sync()
+            t0 = time.perf_counter()
+            tr.run(20)
+            tr.flush()
+            sync()
+            idle.setdefault(ms, []).append(round((time.perf_counter() - t0) * 1e6, 1))
+    out["after_idle_ms_run20_us"] = idle
+    del tr
     tr = make()
     tr.run(1)
     tr.run(5)
