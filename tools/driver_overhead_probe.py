@@ -79,6 +79,31 @@ def main():
             sync()
             idle.setdefault(ms, []).append(round((time.perf_counter() - t0) * 1e6, 1))
     out["after_idle_ms_run20_us"] = idle
+    # what the replay just before the region does to it
+    x = torch.zeros(1, device=dev)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        x.add_(1)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=s):
+            x.add_(1)
+    g.replay()
+    sync()
+    before = {"run20": lambda: tr.run(20), "run5": lambda: tr.run(5), "run1": lambda: tr.run(1),
+              "run32": lambda: tr.run(32), "tiny_graph": g.replay, "tiny_kernel": lambda: x.add_(1),
+              "nothing": lambda: None}
+    prev = {}
+    for rep in range(4):
+        for name, f in before.items():
+            sync()
+            f()
+            sync()
+            t0 = time.perf_counter()
+            tr.run(20)
+            sync()
+            prev.setdefault(name, []).append(round((time.perf_counter() - t0) * 1e6, 1))
+    out["run20_after_us"] = prev
     del tr
     tr = make()
     tr.run(1)
