@@ -897,19 +897,20 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     const float4* src = reinterpret_cast<const float4*>(st.x) + nb * st.n4;
     float4* dst = reinterpret_cast<float4*>(st.xnext);
     const int j0 = (blockIdx.x - mtiles * ntiles - 1) * (FDX_WAVES * 64) + t;
-    constexpr int NQ = 4, STRIDE = STAGE_BLOCKS * FDX_WAVES * 64;  // 4 x 4096 float4 >= B = 64's 12,544
-    for (int i0 = j0; i0 < st.n4; i0 += NQ * STRIDE) {
-      float4 v[NQ];
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int i = i0 + q * STRIDE;
-        v[q] = src[i < st.n4 ? i : 0];
-      }
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int i = i0 + q * STRIDE;
-        if (i < st.n4) dst[i] = v[q];
-      }
+    constexpr int STRIDE = STAGE_BLOCKS * FDX_WAVES * 64;  // 4 x 4096 float4 >= B = 64's 12,544
+    // four named float4s, not an array: with `float4 v[4]` and the guarded
+    // stores the compiler kept v in scratch, which gave the whole kernel a
+    // private segment (80 bytes per lane)
+    for (int i0 = j0; i0 < st.n4; i0 += 4 * STRIDE) {
+      const int i1 = i0 + STRIDE, i2 = i0 + 2 * STRIDE, i3 = i0 + 3 * STRIDE;
+      const float4 v0 = src[i0];
+      const float4 v1 = src[i1 < st.n4 ? i1 : i0];
+      const float4 v2 = src[i2 < st.n4 ? i2 : i0];
+      const float4 v3 = src[i3 < st.n4 ? i3 : i0];
+      dst[i0] = v0;
+      if (i1 < st.n4) dst[i1] = v1;
+      if (i2 < st.n4) dst[i2] = v2;
+      if (i3 < st.n4) dst[i3] = v3;
     }
     return;
   }
