@@ -137,6 +137,8 @@ def fwd_phases(lib, rd, tr, dev, reps):
     tr.L = lib  # trainer launches through the probe library
 
     kernels = {"F12": (lambda: tr._forward_part(0), 256, ["staged", "conv1", "conv2+reduce", "exit"], [0, 1, 2, 3, 7]),
+               "F3": (lambda: tr._forward_part(1), 256 if getattr(tr, "h1a", None) is not None else 128,
+                      ["w0 loads+MFMA", "barrier", "reduce+store"], [0, 1, 2, 7]),
                "F4dx": (lambda: tr._forward_part(2), 201 + 0, ["staged", "Z gemm", "softmax", "dh1", "da2p", "exit"],
                         [0, 1, 2, 3, 4, 5, 7])}
     out = {}
