@@ -704,20 +704,22 @@ __global__ __launch_bounds__(1024) void k_linear_fwd_vec16(const float* __restri
 // trip each) at B = 64 instead of 128 of 16, so every CU holds one tile-half
 // and pulls half the operand bytes through its L1 (F3 spent ~3 us of its
 // ~4.5 us span getting its 128 KB per CU of operands in:
-// profiles/mnist_step_pmc_r6.md).  The halves go to two buffers; F4dx, the
-// only reader, forms relu(ha + hb + b1) while staging them and writes h1
-// out for the backward.  XCD-aware: XCD x runs n-tiles 4x..4x+3 (its W1 rows
-// fetched into one L2), all m-tiles, both halves.
+// profiles/mnist_step_pmc_r6.md).  Both halves are added into h (zero on
+// entry: k_bwd_all re-zeroes it) by hardware fp32 atomics -- exactly two
+// addends onto +0, so the sum is the same in either arrival order; F4dx,
+// the only reader, applies bias + ReLU while staging it and writes h1 out for
+// the backward.  XCD-aware: XCD x runs n-tiles 4x..4x+3 (its W1 rows fetched
+// into one L2), all m-tiles, both halves.
 __global__ __launch_bounds__(512) void k_fc1_fwd_split2(const float* __restrict__ x, const float* __restrict__ w,
-                                                        float* __restrict__ ha, float* __restrict__ hb, int M) {
+                                                        float* __restrict__ h, int M) {
   __shared__ float red[8 * RED_W];
   PTO_STAMP_SCOPE();
   const int mtiles = (M + 15) >> 4;
   const int i = blockIdx.x, xcd = i & 7, j = i >> 3;
-  const int nt = 4 * xcd + j / (2 * mtiles), mt = (j >> 1) % mtiles, h = j & 1;
+  const int nt = 4 * xcd + j / (2 * mtiles), mt = (j >> 1) % mtiles, half = j & 1;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   constexpr int KH = F1IN / 2;
-  const int kb = h * KH + wv * 64, ke = min(kb + 64, (h + 1) * KH);
+  const int kb = half * KH + wv * 64, ke = min(kb + 64, (half + 1) * KH);
   const f32x4 acc = wave_tile_16x16<LAY_ROWK, LAY_ROWK, 4, true, true>(x, F1IN, w, F1IN, M, F1OUT, F1IN, mt * 16,
                                                                        nt * 16, kb, ke);
 #pragma unroll
@@ -731,7 +733,7 @@ __global__ __launch_bounds__(512) void k_fc1_fwd_split2(const float* __restrict_
 #pragma unroll
     for (int q = 0; q < 8; ++q) v += red[q * RED_W + red_slot(t)];
     const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
-    if (m < M && n < F1OUT) (h ? hb : ha)[m * F1OUT + n] = v;
+    if (m < M && n < F1OUT) atomicAdd(h + m * F1OUT + n, v);
   }
 }
 
@@ -918,8 +920,8 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     const float* __restrict__ h1, const float* __restrict__ w2, const float* __restrict__ b2,
     const int64_t* __restrict__ labels, const float* __restrict__ w1, float* __restrict__ loss_rows,
     float* __restrict__ dlogits, float* __restrict__ dh1, float* __restrict__ da2p, int B, float inv_b,
-    const long long* __restrict__ bidx, Conv1Commit cm, BatchStage st, const float* __restrict__ h1b,
-    const float* __restrict__ b1, float* __restrict__ h1out) {
+    const long long* __restrict__ bidx, Conv1Commit cm, BatchStage st, const float* __restrict__ b1,
+    float* __restrict__ h1out) {
   // LDS row stride.  500 keeps the dh1 phase's scalar accesses (rows r and
   // r + 4 in one 32-lane group, 4*500 = 16 mod 32 banks apart) conflict-free;
   // 504 would make the float4 operand reads conflict-free instead but the
@@ -985,15 +987,12 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
   const int h4n = nrow * (F1OUT / 4);
   float4 hv0 = t < h4n ? hg[t] : float4(z4);
   float4 hv1 = (t + NT < H4 && t + NT < h4n) ? hg[t + NT] : float4(z4);
-  // split fc1 (h1b != nullptr): h1 = relu(ha + hb + b1), formed here; the
-  // second half and the bias are loaded in the same round as the first
-  float4 hb0 = z4, hb1 = z4, bb0 = z4, bb1 = z4;
-  if (h1b) {
-    const float4* hgb = reinterpret_cast<const float4*>(h1b + (size_t)mt * 16 * F1OUT);
+  // split fc1 (b1 != nullptr): h1 holds the raw split-K sum; relu(h + b1)
+  // is formed here, the bias loaded in the same round
+  float4 bb0 = z4, bb1 = z4;
+  if (b1) {
     const float4* b4 = reinterpret_cast<const float4*>(b1);
     constexpr int RB = F1OUT / 4;
-    hb0 = t < h4n ? hgb[t] : float4(z4);
-    hb1 = (t + NT < H4 && t + NT < h4n) ? hgb[t + NT] : float4(z4);
     bb0 = b4[t % RB];
     bb1 = b4[(t + NT) % RB];
   }
@@ -1010,13 +1009,12 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
     if (grow < B && labels) y = (int)labels[(bidx ? (size_t)(*bidx) * B : 0) + grow];
     if (hn < NCLS) bias = b2[hn];
   }
-  if (h1b) {
-    auto act = [](float4 a, float4 b, float4 c) {
-      return make_float4(fmaxf((a.x + b.x) + c.x, 0.f), fmaxf((a.y + b.y) + c.y, 0.f),
-                         fmaxf((a.z + b.z) + c.z, 0.f), fmaxf((a.w + b.w) + c.w, 0.f));
+  if (b1) {
+    auto act = [](float4 a, float4 c) {
+      return make_float4(fmaxf(a.x + c.x, 0.f), fmaxf(a.y + c.y, 0.f), fmaxf(a.z + c.z, 0.f), fmaxf(a.w + c.w, 0.f));
     };
-    hv0 = t < h4n ? act(hv0, hb0, bb0) : float4(z4);
-    hv1 = (t + NT < H4 && t + NT < h4n) ? act(hv1, hb1, bb1) : float4(z4);
+    hv0 = t < h4n ? act(hv0, bb0) : float4(z4);
+    hv1 = (t + NT < H4 && t + NT < h4n) ? act(hv1, bb1) : float4(z4);
     if (nt == 0) {  // h1 for the backward's fc2 weight gradient, one writer per row
       float4* ho = reinterpret_cast<float4*>(h1out + (size_t)mt * 16 * F1OUT);
       if (t < h4n) ho[t] = hv0;
@@ -1999,6 +1997,8 @@ struct BwdAllArgs {
   // whose exchange runs inside the next forward)
   int grads_only;
   float* g2b; float* g1w; float* g1b; float* gfw; float* gfb;  // grad slots of conv2.bias, fc1.w/b, fc2.w/b
+  float* hz;  // split fc1's accumulation buffer, re-zeroed here for the next F3 (nz floats, or nullptr)
+  int nz;
 };
 
 struct EpiSgd {
@@ -2022,6 +2022,10 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
   if (bid == 0 && threadIdx.x == 0) {  // no block of this launch reads the cursor
     if (A.bidx) *A.bidx = (*A.bidx + 1) % A.nbatches;
     if (A.pending) *A.pending = 1;
+  }
+  if (A.hz) {  // F4dx, its only reader, has finished with it
+    const int i = bid * 256 + (int)threadIdx.x;
+    if (i < A.nz) A.hz[i] = 0.f;
   }
   // block order (role ranges of the grid): bwd_order(); a grid of
   // 1,422 blocks takes ~5 us just to start (tools/dispatch_ramp_probe.py),
@@ -2381,10 +2385,11 @@ PTO_API int pto_linear_fwd(const float* x, const float* w, const float* b, float
 }
 
 // fc1 forward of the training step, split-K over two workgroups per tile
-// (k_fc1_fwd_split2): ha + hb = x W^T, no bias / ReLU (F4dx applies them).
-PTO_API int pto_fc1_fwd_split(const float* x, const float* w, float* ha, float* hb, int M, hipStream_t s) {
-  if (M < 1 || !x || !w || !ha || !hb || ((((uintptr_t)x) | ((uintptr_t)w)) & 15)) return -1;
-  hipLaunchKernelGGL(k_fc1_fwd_split2, dim3(((M + 15) / 16) * 64), dim3(512), 0, s, x, w, ha, hb, M);
+// (k_fc1_fwd_split2): h += x W^T (h zero on entry), no bias / ReLU (F4dx
+// applies them, k_bwd_all re-zeroes h).
+PTO_API int pto_fc1_fwd_split(const float* x, const float* w, float* h, int M, hipStream_t s) {
+  if (M < 1 || !x || !w || !h || ((((uintptr_t)x) | ((uintptr_t)w)) & 15)) return -1;
+  hipLaunchKernelGGL(k_fc1_fwd_split2, dim3(((M + 15) / 16) * 64), dim3(512), 0, s, x, w, h, M);
   LAUNCH_CHECK();
 }
 
@@ -2470,8 +2475,8 @@ PTO_API int pto_fc2_ce_dx(const float* h1, const float* w2, const float* b2, con
                           const long long* bidx, float* p1, float* g1, float* m1, int n1, const int* pending,
                           const float* lr, float mom, float wd, float gscale, int nesterov, float* rep, int nrep,
                           int rep_stride, int* zero_word, const float* st_x, float* st_xnext, long long st_nb,
-                          const float* h1b, const float* b1, float* h1out, hipStream_t s) {
-  if (h1b && (!b1 || !h1out || ((((uintptr_t)h1b) | ((uintptr_t)b1) | ((uintptr_t)h1out)) & 15))) return -1;
+                          const float* b1, float* h1out, hipStream_t s) {
+  if (b1 && (!h1out || ((((uintptr_t)b1) | ((uintptr_t)h1out)) & 15))) return -1;
   if (n1 % 4 || rep_stride % 4 || ((((uintptr_t)p1) | ((uintptr_t)g1) | ((uintptr_t)m1) | ((uintptr_t)rep)) & 15))
     return -1;
   if ((((uintptr_t)h1) | ((uintptr_t)w2)) & 15) return -1;  // float4 staging of the h1 tile and W2
@@ -2481,7 +2486,7 @@ PTO_API int pto_fc2_ce_dx(const float* h1, const float* w2, const float* b2, con
   const BatchStage st{st_x, st_xnext, st_nb, B * 784 / 4};
   const int nblk = ((B + 15) / 16) * ((F1IN + 15) / 16);
   hipLaunchKernelGGL(k_fc2_ce_dx_mf, dim3(nblk + 1 + (st_xnext ? STAGE_BLOCKS : 0)), dim3(FDX_WAVES * 64), 0, s, h1,
-                     w2, b2, labels, w1, loss_rows, dlogits, dh1, da2p, B, inv_b, bidx, cm, st, h1b, b1, h1out);
+                     w2, b2, labels, w1, loss_rows, dlogits, dh1, da2p, B, inv_b, bidx, cm, st, b1, h1out);
   LAUNCH_CHECK();
 }
 
@@ -2526,7 +2531,7 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
                         long long off_fc1b, long long off_c2w, long long off_c2b, long long off_c1w,
                         long long off_c1b, int* ctr, long long* bidx, long long nbatches, int* pending, int B,
                         const float* lr, float mom, float wd, float gscale, int nesterov, float* c1rep, int nrep,
-                        int rep_stride, int grads_only, float* wpart, hipStream_t s) {
+                        int rep_stride, int grads_only, float* wpart, float* hz, int nz, hipStream_t s) {
   if (!ctr) return -1;
   if (((uintptr_t)(grads_only ? p + off_c2w : w2f)) & 7) return -1;  // float2 staging of the W2 slice
   if (!grads_only && (!bidx || !pending || !w2f)) return -1;
@@ -2559,6 +2564,9 @@ PTO_API int pto_bwd_all(const float* g2, const uint8_t* code2, const float* a1p,
   A.nD = bwd_n_dw1_blocks(A.dpair);
   A.nF = (((NCLS + 15) / 16) * ((F1OUT + 15) / 16) + 3) / 4 + 9;
   A.wpart = wpart;
+  A.hz = hz;
+  A.nz = hz ? nz : 0;
+  if ((long long)A.nz > (long long)(A.nA + A.nB + A.nC + A.nD + A.nF) * 256) return -1;  // one element per thread
   const size_t ldsA = wgrad_lds_floats<BWD_WCHUNK, BWD_WNTW>() * sizeof(float);
   const size_t ldsB = B2_LDS_FLOATS * sizeof(float);
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;

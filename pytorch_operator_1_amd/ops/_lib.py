@@ -102,12 +102,13 @@ _SIGS = {
     "pto_conv12_fwd_ar": [_P] * 9 + [_I, _P, _P, _P, _I, _I, _P, _P, _I, _P, _P, _P, _F, _F, _F, _I,
                                      _L, _L, _I, _L, _L, _L, _I, _L, _I, _I, _L, _P, _P],
     "pto_synth_mnist": [_P, _P, _L, ctypes.c_ulonglong, _P],
-    "pto_bwd_all": [_P] * 13 + [_L] * 8 + [_P, _P, _L, _P, _I, _P, _F, _F, _F, _I, _P, _I, _I, _I, _P, _P],
+    "pto_bwd_all": [_P] * 13 + [_L] * 8 + [_P, _P, _L, _P, _I, _P, _F, _F, _F, _I, _P, _I, _I, _I, _P, _P, _I,
+                                          _P],
     "pto_conv1_commit": [_P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _P, _I, _I, _P],
     "pto_mnist_ddp_sgd": [_P, _P, _P, _I, _I, _I, _P, _I, _P, _F, _F, _F, _I, _P, _L, _P],
     "pto_fc2_ce_dx": [_P] * 9 + [_I, _F, _P, _P, _P, _P, _I, _P, _P, _F, _F, _F, _I, _P, _I, _I, _P, _P, _P, _L,
-                                  _P, _P, _P, _P],
-    "pto_fc1_fwd_split": [_P, _P, _P, _P, _I, _P],
+                                  _P, _P, _P],
+    "pto_fc1_fwd_split": [_P, _P, _P, _I, _P],
     "pto_eval_head": [_P, _P, _P, _I, _P],
     "pto_sgd_block_count": [_L],
     "pto_sgd_multi": [_P, _P, _I, _I, _P, _F, _F, _F, _F, _I, _I, _P, _L, _P],

@@ -156,11 +156,11 @@ class FusedMnistTrainer:
         self.a2p = torch.empty(B * 800, **f32)
         self.code2 = torch.empty(B * 800, device=device, dtype=torch.uint8)
         self.h1 = torch.empty(B * 500, **f32)
-        # fc1 forward split over two workgroups per tile (PTO_FC1_SPLIT=0: one
-        # 16-wave workgroup per tile with the bias / ReLU epilogue)
+        # fc1 forward split over two workgroups per tile, accumulated into h1a
+        # (zero between steps: k_bwd_all re-zeroes it); PTO_FC1_SPLIT=0: one
+        # 16-wave workgroup per tile with the bias / ReLU epilogue
         split = os.environ.get("PTO_FC1_SPLIT", "1") == "1"
-        self.h1a = torch.empty(B * 500, **f32) if split else None
-        self.h1b = torch.empty(B * 500, **f32) if split else None
+        self.h1a = torch.zeros(B * 500, **f32) if split else None
         self.loss_rows = torch.zeros(B, **f32)
         self.dlogits = torch.empty(B * 10, **f32)
         self.dh1 = torch.empty(B * 500, **f32)
@@ -329,17 +329,15 @@ class FusedMnistTrainer:
                        self.a1p.data_ptr(), self.code1.data_ptr(), self.a2p.data_ptr(), self.code2.data_ptr(), B,
                        fb, *lazy, self.xcur.data_ptr(), w2out, *rep)
         if only in (None, 1):
-            if self.h1a is not None:  # split-K halves; F4dx forms relu(h1a + h1b + b1) and writes h1
-                self._call("fc1_fwd_split", self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), self.h1a.data_ptr(),
-                           self.h1b.data_ptr(), B)
+            if self.h1a is not None:  # split-K sum into h1a; F4dx forms relu(h1a + b1) and writes h1
+                self._call("fc1_fwd_split", self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), self.h1a.data_ptr(), B)
             else:
                 self._call("linear_fwd", self.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(),
                            self.h1.data_ptr(), B, 500, 800, 1)
         if only in (None, 2):
             stage = ((self.data.data_ptr(), self.xnext.data_ptr(), self.n_batches) if self.xnext is not None
                      else (None, None, 0))
-            split = ((self.h1b.data_ptr(), P["fc1.bias"].data_ptr(), self.h1.data_ptr()) if self.h1a is not None
-                     else (None, None, None))
+            split = ((P["fc1.bias"].data_ptr(), self.h1.data_ptr()) if self.h1a is not None else (None, None))
             h1in = self.h1a if self.h1a is not None else self.h1
             self._call("fc2_ce_dx", h1in.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
                        self.target.data_ptr(), P["fc1.weight"].data_ptr(), self.loss_rows.data_ptr(),
@@ -374,7 +372,7 @@ class FusedMnistTrainer:
                    self.mom.data_ptr(), *self._offs, self.c2_ctr.data_ptr(),
                    self.batch_idx.data_ptr() if cursor else None, self.n_batches,
                    None if go else self.pending.data_ptr(), self.B, *self._opt_args(), self.c1rep.data_ptr(),
-                   self.c1_nrep, self.c1_stride, int(go), _lib.ptr(self.wpart))
+                   self.c1_nrep, self.c1_stride, int(go), _lib.ptr(self.wpart), _lib.ptr(self.h1a), self.B * 500)
 
     def _exchange_launch(self, B: int):
         """ddp-xgmi overlap: the previous step's exchange as the two roles of

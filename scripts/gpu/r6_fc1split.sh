@@ -1,12 +1,12 @@
 #!/bin/bash
 # fc1 forward split-K over two workgroups per tile with F4dx forming
-# relu(ha + hb + b1) (PTO_FC1_SPLIT=1, default) vs one 16-wave workgroup per
+# relu(h + b1) from the atomically summed halves (PTO_FC1_SPLIT=1, default) vs one 16-wave workgroup per
 # tile with the bias/ReLU epilogue (0), interleaved; F3 phase stamps both
 # ways; then every MNIST GPU test on the split path.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/r6_fc1split
+O=gpurun_out/r6_fc1split${TAG:-}
 mkdir -p $O
 for v in 1 0; do
 PTO_FC1_SPLIT=$v timeout -k 10 300 python tools/bwd_phases_probe.py --fwd --reps 30 > $O/fwd_phases_$v.txt 2>&1 || { tail -20 $O/fwd_phases_$v.txt; exit 1; }

@@ -53,7 +53,7 @@ def main():
             tr.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(), tr.target.data_ptr(),
             P["fc1.weight"].data_ptr(), tr.loss_rows.data_ptr(), tr.dlogits.data_ptr(), tr.dh1.data_ptr(),
             tr.da2p.data_ptr(), B, 1.0 / B, bi, tr._params[tr._c1:].data_ptr(), tr.grads[tr._c1:].data_ptr(),
-            tr.mom[tr._c1:].data_ptr(), tr.numel - tr._c1, None, *o, None, 1, 0, None, None, None, 0, None, None, None, s),
+            tr.mom[tr._c1:].data_ptr(), tr.numel - tr._c1, None, *o, None, 1, 0, None, None, None, 0, None, None, s),
         "B bwd_all(grads)": lambda: tr._backward(),
         "fc2_ce": lambda: L.pto_fc2_ce(tr.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(),
                                        tr.target.data_ptr(), None, tr.loss_rows.data_ptr(), tr.dlogits.data_ptr(),

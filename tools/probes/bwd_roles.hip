@@ -40,6 +40,8 @@ extern "C" __attribute__((visibility("default"))) int probe_bwd_all(
   A.dpair = bwd_dpair();
   A.nD = (mask & 16) ? bwd_n_dw1_blocks(A.dpair) : 0;
   A.wpart = nullptr;
+  A.hz = nullptr;
+  A.nz = 0;
   const size_t ldsA = wgrad_lds_floats<BWD_WCHUNK, BWD_WNTW>() * sizeof(float);
   const size_t ldsB = B2_LDS_FLOATS * sizeof(float);
   const size_t lds = ldsA > ldsB ? ldsA : ldsB;
