@@ -43,11 +43,16 @@ knobs):
       collective runs between two captured graphs ("split").
   deterministic (``PTO_DETERMINISTIC=1``): ``k_bwd_all`` without floating-
       point atomics (conv2 wgrad partial tiles summed in chunk order, one
-      conv1 gradient replica per sample); bitwise reproducible runs.
+      conv1 gradient replica per sample); bitwise reproducible runs.  (The
+      split fc1 forward's two atomic adds per element land on +0, so their
+      sum does not depend on arrival order: reproducible in every mode.)
 
 Env knobs: ``PTO_COMM`` (auto|xgmi|rccl), ``PTO_GRAPH_UNROLL``,
 ``PTO_DETERMINISTIC``, ``PTO_CAPTURE_COMM`` (0: collectives between graphs),
-``PTO_XGMI_OVERLAP`` (0: one whole-buffer xGMI all-reduce per step).
+``PTO_XGMI_OVERLAP`` (0: one whole-buffer xGMI all-reduce per step),
+``PTO_XSTAGE`` / ``PTO_FC1_SPLIT`` (0: F12 reads the dataset through the
+cursor / fc1 forward as one workgroup per tile), ``PTO_C1_REPLICAS``
+(conv1 gradient replicas, 8).
 """
 from __future__ import annotations
 
@@ -65,7 +70,7 @@ from ..ops import _lib
 # each address sees B/R same-address fp32 atomics instead of B (19.5 vs 21.6
 # us for R = 8 vs 1, profiles/bwd_all_r2.md); the readers (F12's lazy
 # update, the commit, the xGMI fold) sum them in replica order
-C1_REPLICAS = 8
+C1_REPLICAS = int(os.environ.get("PTO_C1_REPLICAS", "8"))  # conv1 gradient replicas (k_bwd_all atomics spread)
 
 # xGMI channels of the overlapped step's two exchange roles (xgmi_ar.h)
 FC_CHAN, CONV_CHAN = 1, 2
