@@ -125,6 +125,52 @@ def test_linear(M, N, K, relu):
         assert rel_err(a, r) < 1e-5
 
 
+@pytest.mark.parametrize("M", [64, 7, 100])
+def test_fc1_forward_split_k(M):
+    """pto_fc1_fwd_split (two workgroups per 16x16 tile, halves added by fp32
+    atomics onto a zeroed buffer) against fp32 x W^T; two addends onto +0
+    make the sum independent of arrival order, so repeats are bitwise equal."""
+    from pytorch_operator_1_amd.ops import _lib
+
+    torch.manual_seed(3)
+    L = _lib.lib()
+    x = torch.randn(M, 800, device=DEV)
+    w = torch.randn(500, 800, device=DEV) / 800 ** 0.5
+    outs = []
+    for _ in range(3):
+        h = torch.zeros(M * 500, device=DEV)
+        _lib.check(L.pto_fc1_fwd_split(x.data_ptr(), w.data_ptr(), h.data_ptr(), M, _lib.stream_ptr()), "fc1 split")
+        outs.append(h.view(M, 500).clone())
+    torch.cuda.synchronize()
+    ref = x.double() @ w.double().t()
+    assert rel_err(outs[0].double(), ref) < 1e-5
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_fused_trainer_fc1_forms_match_eager(monkeypatch, split):
+    """Both fc1 forward forms of the fused step (split-K with bias/ReLU in F4dx,
+    and one workgroup per tile) against the stock PyTorch step, graphs on."""
+    from pytorch_operator_1_amd.train.fused_step import FusedMnistTrainer
+    from pytorch_operator_1_amd.train.runner import EagerMnistTrainer
+
+    monkeypatch.setenv("PTO_FC1_SPLIT", split)
+    dev = torch.device(DEV)
+    fused = FusedMnistTrainer(dev, batch_size=64, dataset_size=640, seed=1, graph="full")
+    assert (fused.h1a is not None) == (split == "1")
+    eager = EagerMnistTrainer(dev, batch_size=64, dataset_size=640, seed=1)
+    fused.run(1)
+    fused.run(7)
+    for _ in range(8):
+        eager.step()
+    torch.cuda.synchronize()
+    assert abs(fused.last_loss() - eager.last_loss()) < 1e-4
+    for name, t in eager.model.state_dict().items():
+        assert rel_err(fused.p[name], t) < 1e-4, name
+    if split == "1":  # k_bwd_all leaves the accumulation buffer zeroed for the next F3
+        assert not fused.h1a.any()
+
+
 def test_log_softmax_and_ce():
     from pytorch_operator_1_amd import ops
 
