@@ -700,8 +700,8 @@ __global__ __launch_bounds__(1024) void k_linear_fwd_vec16(const float* __restri
 }
 
 // fc1 forward WITHOUT bias / ReLU, K split over two workgroups per 16x16
-// tile: 2 x 128 workgroups of 8 waves (64-deep K slices, one memory round
-// trip each) at B = 64 instead of 128 of 16, so every CU holds one tile-half
+// tile: 2 x 128 workgroups (16 waves of 32-deep K slices by default, one
+// memory round trip each) at B = 64 instead of 128 of 16, so every CU holds one tile-half
 // and pulls half the operand bytes through its L1 (F3 spent ~3 us of its
 // ~4.5 us span getting its 128 KB per CU of operands in:
 // profiles/mnist_step_pmc_r6.md).  Both halves are added into h (zero on
@@ -710,18 +710,22 @@ __global__ __launch_bounds__(1024) void k_linear_fwd_vec16(const float* __restri
 // the only reader, applies bias + ReLU while staging it and writes h1 out for
 // the backward.  XCD-aware: XCD x runs n-tiles 4x..4x+3 (its W1 rows fetched
 // into one L2), all m-tiles, both halves.
-__global__ __launch_bounds__(512) void k_fc1_fwd_split2(const float* __restrict__ x, const float* __restrict__ w,
-                                                        float* __restrict__ h, int M) {
-  __shared__ float red[8 * RED_W];
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_fc1_fwd_split2(const float* __restrict__ x, const float* __restrict__ w,
+                                                          float* __restrict__ h, int M) {
+  // NW waves per workgroup, each a KW-deep slice of the 400-deep K half in
+  // one memory round (KW / 16 k-groups of loads in flight)
+  constexpr int KW = ((F1IN / 2 + NW - 1) / NW + 15) / 16 * 16;
+  __shared__ float red[NW * RED_W];
   PTO_STAMP_SCOPE();
   const int mtiles = (M + 15) >> 4;
   const int i = blockIdx.x, xcd = i & 7, j = i >> 3;
   const int nt = 4 * xcd + j / (2 * mtiles), mt = (j >> 1) % mtiles, half = j & 1;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   constexpr int KH = F1IN / 2;
-  const int kb = half * KH + wv * 64, ke = min(kb + 64, (half + 1) * KH);
-  const f32x4 acc = wave_tile_16x16<LAY_ROWK, LAY_ROWK, 4, true, true>(x, F1IN, w, F1IN, M, F1OUT, F1IN, mt * 16,
-                                                                       nt * 16, kb, ke);
+  const int kb = half * KH + wv * KW, ke = min(kb + KW, (half + 1) * KH);
+  const f32x4 acc = wave_tile_16x16<LAY_ROWK, LAY_ROWK, KW / 16, true, true>(x, F1IN, w, F1IN, M, F1OUT, F1IN,
+                                                                             mt * 16, nt * 16, kb, ke);
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) red[wv * RED_W + rr * RED_RR + lane] = acc[rr];
   PTO_STAMP(1);
@@ -731,7 +735,7 @@ __global__ __launch_bounds__(512) void k_fc1_fwd_split2(const float* __restrict_
   if (t < 256) {
     float v = 0.f;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v += red[q * RED_W + red_slot(t)];
+    for (int q = 0; q < NW; ++q) v += red[q * RED_W + red_slot(t)];
     const int m = mt * 16 + (t >> 4), n = nt * 16 + (t & 15);
     if (m < M && n < F1OUT) atomicAdd(h + m * F1OUT + n, v);
   }
@@ -2389,7 +2393,18 @@ PTO_API int pto_linear_fwd(const float* x, const float* w, const float* b, float
 // applies them, k_bwd_all re-zeroes h).
 PTO_API int pto_fc1_fwd_split(const float* x, const float* w, float* h, int M, hipStream_t s) {
   if (M < 1 || !x || !w || !h || ((((uintptr_t)x) | ((uintptr_t)w)) & 15)) return -1;
-  hipLaunchKernelGGL(k_fc1_fwd_split2, dim3(((M + 15) / 16) * 64), dim3(512), 0, s, x, w, h, M);
+  static const int nw = [] {
+    const char* e = getenv("PTO_FC1_NW");
+    const int v = e ? atoi(e) : 16;  // 16 waves of 32-deep slices: 34.13-34.19 vs 34.34-34.40 us/step with 8
+    return (v == 4 || v == 8) ? v : 16;
+  }();
+  const dim3 g(((M + 15) / 16) * 64);
+  if (nw == 4)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fc1_fwd_split2<4>), g, dim3(256), 0, s, x, w, h, M);
+  else if (nw == 16)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fc1_fwd_split2<16>), g, dim3(1024), 0, s, x, w, h, M);
+  else
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fc1_fwd_split2<8>), g, dim3(512), 0, s, x, w, h, M);
   LAUNCH_CHECK();
 }
 
