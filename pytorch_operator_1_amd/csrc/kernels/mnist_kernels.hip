@@ -110,6 +110,11 @@ PTO_DEV void commit4(const Conv1Commit& cm, int i, float lr) {
     sgd_flat4(cm.p, cm.g, cm.m, i, lr, cm.a);
     return;
   }
+  // the parameter / momentum loads first: in flight with the gradient and
+  // replica loads (after the replica zeroing stores they were a second
+  // round trip -- the compiler cannot move them above possibly aliasing stores)
+  float4 pv = *reinterpret_cast<float4*>(cm.p + i);
+  float4 mv = *reinterpret_cast<float4*>(cm.m + i);
   float4 gs = *reinterpret_cast<const float4*>(cm.g + i);
   for (int r0 = 0; r0 < cm.nrep - 1; r0 += REP_CHUNK) {
     float4 v[REP_CHUNK];  // a chunk of replica loads in flight before the first add
@@ -123,8 +128,6 @@ PTO_DEV void commit4(const Conv1Commit& cm, int i, float lr) {
       *reinterpret_cast<float4*>(cm.rep + (size_t)(r0 + r) * cm.rep_stride + i) = float4{0.f, 0.f, 0.f, 0.f};
     }
   }
-  float4 pv = *reinterpret_cast<float4*>(cm.p + i);
-  float4 mv = *reinterpret_cast<float4*>(cm.m + i);
   sgd_elem(pv.x, gs.x, mv.x, lr, cm.a.mom, cm.a.wd, cm.a.gscale, cm.a.nesterov);
   sgd_elem(pv.y, gs.y, mv.y, lr, cm.a.mom, cm.a.wd, cm.a.gscale, cm.a.nesterov);
   sgd_elem(pv.z, gs.z, mv.z, lr, cm.a.mom, cm.a.wd, cm.a.gscale, cm.a.nesterov);
@@ -963,10 +966,10 @@ __global__ __launch_bounds__(FDX_WAVES * 64) void k_fc2_ce_dx_mf(
   if (blockIdx.x == (unsigned)(mtiles * ntiles)) {
     if (cm.zero_word && t == 0) *cm.zero_word = 0;  // every waiter of the previous launch has finished
     if (cm.pending) {
-      if (*cm.pending) {
-        const float lr = *cm.a.lr;
+      const int pend = *cm.pending;
+      const float lr = *cm.a.lr;  // in flight with the flag
+      if (pend)
         for (int i = 4 * t; i < cm.n; i += 4 * FDX_WAVES * 64) commit4(cm, i, lr);
-      }
     }
     return;
   }
@@ -2176,8 +2179,9 @@ __global__ __launch_bounds__(256) void k_bwd_all(BwdAllArgs A) {
 // Host-side flush of an owed conv1 update (before the parameters are read
 // or replaced): commit it and clear `pending`.  One block.
 __global__ __launch_bounds__(256) void k_conv1_commit(Conv1Commit cm, int* __restrict__ pending) {
-  if (!*cm.pending) return;
-  const float lr = *cm.a.lr;
+  const int pend = *cm.pending;
+  const float lr = *cm.a.lr;  // in flight with the flag (one round trip, not two)
+  if (!pend) return;
   for (int i = 4 * threadIdx.x; i < cm.n; i += 1024) commit4(cm, i, lr);
   __syncthreads();
   if (threadIdx.x == 0) *pending = 0;
