@@ -35,6 +35,7 @@ def main():
     s = _lib.stream_ptr(dev)
     bi = tr.batch_idx.data_ptr()
     da1p = torch.empty(B * 2880, device=dev)
+    f3acc = torch.zeros(B * 500, device=dev)
     o = tr._opt_args()
     launches = {
         "conv1_fwd": lambda: L.pto_conv1_fwd(tr.data.data_ptr(), P["conv1.weight"].data_ptr(),
@@ -47,8 +48,12 @@ def main():
             P["conv2.bias"].data_ptr(), tr.a1p.data_ptr(), tr.code1.data_ptr(), tr.a2p.data_ptr(),
             tr.code2.data_ptr(), B, bi, None, None, 0, None, None, 0.0, 0.0, 1.0, 0, tr.xcur.data_ptr(), None, None,
             1, 0, s),
-        "F3 fc1_fwd": lambda: L.pto_linear_fwd(tr.a2p.data_ptr(), P["fc1.weight"].data_ptr(),
-                                               P["fc1.bias"].data_ptr(), tr.h1.data_ptr(), B, 500, 800, 1, s),
+        "F3 fc1_fwd (one workgroup per tile)": lambda: L.pto_linear_fwd(
+            tr.a2p.data_ptr(), P["fc1.weight"].data_ptr(), P["fc1.bias"].data_ptr(), tr.h1.data_ptr(), B, 500, 800,
+            1, s),
+        # the step's form; accumulates into a scratch buffer (timing only)
+        "F3 fc1_fwd_split": lambda: L.pto_fc1_fwd_split(tr.a2p.data_ptr(), P["fc1.weight"].data_ptr(),
+                                                        f3acc.data_ptr(), B, s),
         "F4dx fc2_ce_dx": lambda: L.pto_fc2_ce_dx(
             tr.h1.data_ptr(), P["fc2.weight"].data_ptr(), P["fc2.bias"].data_ptr(), tr.target.data_ptr(),
             P["fc1.weight"].data_ptr(), tr.loss_rows.data_ptr(), tr.dlogits.data_ptr(), tr.dh1.data_ptr(),
